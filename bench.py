@@ -1,0 +1,227 @@
+#!/usr/bin/env python3
+"""bench.py -- canonical k-mer counting throughput on MI355X.
+
+Metric (BASELINE.json): canonical k-mers/s inserted (+ achieved HBM GB/s).
+Workload at N=1: BASELINE.json configs[1] = "C2": synthetic 10M x 150 bp reads
+(seeded generator, SURVEY.md 8d: uniform 50 Mbp genome, 50 % reverse complement,
+0.1 % substitutions, single-line FASTA), k = 31, Kaarme table (-m 2 -s 200000000).
+
+One step = one full counting job over the resident input: table re-initialised
+(kc_reset, the table constructor), reference chunking of the FASTA image, gather
+into the chunk stage, tokenize, canonicalise + insert every window.  The FASTA image
+is generated directly in HBM before timing (inputs resident, as the contract asks).
+
+N > 1 (torch.distributed over RCCL): weak scaling, every rank owns its own 10M-read
+slice of one dataset; canonical keys are routed to their hash-prefix owner with one
+all-to-all per step (see kaarme_amd/sharded.py) and counted there.
+
+Extra JSON keys: roofline (dominant kernel k_count vs 8 TB/s HBM), cpu_baseline (the
+reference CLI oracle/_ref/kaarme on a bounded sample of the same workload, rank 0,
+N=1 only).
+"""
+import argparse
+import json
+import math
+import os
+import re
+import subprocess
+import sys
+import tempfile
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "canonical-k-mer-hash-table_amd")
+sys.path.insert(0, PKG)
+
+METRIC = "k-mers/s inserted (canonical) + achieved HBM GB/s, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(args, slots_per_read):
+    """Time the reference CLI (or, if it was not built, the C oracle) on a bounded sample."""
+    ref = os.path.join(REPO, "oracle", "_ref", "kaarme")
+    orc = os.path.join(REPO, "oracle", "_ref", "kc_oracle")
+    gen = os.path.join(PKG, "bin", "kc_gen")
+    if not os.path.exists(gen):
+        return None
+    kind = "reference" if os.path.exists(ref) else ("port" if os.path.exists(orc) else None)
+    if kind is None:
+        return None
+    n = args.cpu_sample_reads if kind == "reference" else max(1, args.cpu_sample_reads // 20)
+    threads = max(3, min(args.cpu_threads, os.cpu_count() or 3, 64))
+    with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
+        fa = os.path.join(td, "sample.fasta")
+        subprocess.run([gen, fa, str(n), str(args.read_len), str(args.genome), "-s", str(args.seed),
+                        "-e", str(args.err)], check=True)
+        with open(fa, "rb") as f:  # pre-warm the page cache
+            while f.read(1 << 24):
+                pass
+        windows = n * (args.read_len - args.k + 1)
+        slots = max(1000, int(slots_per_read * n))
+        if kind == "reference":
+            cmd = [ref, fa, str(args.k), "-m", "2", "-s", str(slots), "-t", str(threads), "-a", "0"]
+            p = subprocess.run(cmd, capture_output=True, text=True, timeout=1800)
+            m = re.search(r"Time used to build hash table: (\d+) microseconds", p.stdout)
+            if p.returncode != 0 or not m:
+                log("cpu baseline failed:", p.stdout[-500:], p.stderr[-500:])
+                return None
+            secs = int(m.group(1)) / 1e6
+            cores = threads - 1  # t-2 hashing workers + 1 IO thread (main.cpp:383)
+        else:
+            t0 = time.perf_counter()
+            subprocess.run([orc, "count", fa, str(args.k), "-a", "0"], check=True, capture_output=True)
+            secs = time.perf_counter() - t0
+            cores = 1
+    return {"value": windows / secs, "unit": "k-mers/s", "cores": cores, "kind": kind,
+            "sample": f"first {n} reads of the same generator ({windows} windows, k={args.k}, "
+                      f"-m 2 -s {slots} -t {threads}, {secs:.2f} s counting time)"}
+
+
+def load_traffic(workload):
+    """HBM bytes per k_count launch from the committed rocprofv3 PMC summary, if any."""
+    p = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        if d.get("workload") == workload:
+            return d.get("bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--reads", type=int, default=10_000_000, help="reads per GPU")
+    ap.add_argument("--read-len", type=int, default=150)
+    ap.add_argument("--genome", type=int, default=50_000_000)
+    ap.add_argument("--k", type=int, default=31)
+    ap.add_argument("--slots", type=int, default=200_000_000, help="-s per GPU (C2: 200000000)")
+    ap.add_argument("--err", type=float, default=0.001)
+    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--cpu-sample-reads", type=int, default=2_000_000)
+    ap.add_argument("--cpu-threads", type=int, default=18)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import kaarme_amd as ka
+
+    lib = ka.load_library()
+    L, k, N = args.read_len, args.k, args.reads
+    first = rank * N
+    stream = torch.cuda.current_stream()
+    nbytes = lib.kc_synth_bytes(first, N, L, 0)
+    image = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    rc = lib.kc_synth_device(image.data_ptr(), first, N, args.seed, args.genome, L, 0, args.err, 0.0,
+                             stream.cuda_stream)
+    assert rc == 0, "kc_synth_device failed"
+    torch.cuda.synchronize()
+    host = image.cpu().numpy().tobytes()  # setup only: the host chunker reads boundary bytes
+    chunks = ka.plan_chunks(host, k, ka.FMT_FASTA)
+    del host
+    batch = (nbytes + len(chunks) * 4096 + (1 << 20)) // 4096 * 4096
+    windows_expected = N * (L - k + 1)
+    workload = f"C2: synthetic {N} x {L} bp reads/GPU, k={k}, -m 2 -s {args.slots}"
+
+    if world > 1:
+        from kaarme_amd.sharded import ShardedCounter
+        counter = ShardedCounter(ka.Config(k=k, mode=2, table_slots=args.slots, min_abundance=2,
+                                           batch_bytes=batch, device=local), dist)
+    else:
+        counter = ka.KmerCounter(ka.Config(k=k, mode=2, table_slots=args.slots, min_abundance=2,
+                                           batch_bytes=batch, device=local))
+
+    def step():
+        counter.reset()
+        counter.count_device(image.data_ptr(), chunks, ka.FMT_FASTA, stream.cuda_stream)
+        counter.sync()
+
+    for _ in range(args.warmup):
+        step()
+    counter.profile(True)
+    counter.timing()  # drop warmup events
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    counter.profile(False)
+    tm = counter.timing()
+    st = counter.finish()  # raises on table overflow
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    windows_step = st["windows"]
+    assert windows_step == windows_expected, (windows_step, windows_expected)
+    total_windows = windows_step * world * args.steps
+    value = total_windows / elapsed
+
+    # --- roofline of the dominant kernel (k_count), SURVEY.md 8d:
+    # A = sym_B + (1+u)*K + 8 bytes per window (K = 8*ceil(2k/64) key bytes, u = distinct/W,
+    # 8 = 4-byte count read + write), times the windows of one launch.
+    K = 8 * math.ceil(2 * k / 64)
+    u = st["distinct"] / max(1, windows_step)
+    launches = max(1, tm["launches"])
+    sym_per_launch = tm["symbols"] if tm["symbols"] else nbytes
+    win_per_launch = windows_step / (launches / args.steps)
+    bytes_per_launch = sym_per_launch + win_per_launch * ((1 + u) * K + 8)
+    count_ms = tm["count_ms"] / launches
+    achieved = bytes_per_launch / (count_ms * 1e-3) / 1e9
+    traffic = load_traffic(workload)
+    roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                "kernel": "k_count<1,0>", "kernel_ms": round(count_ms, 4),
+                "algorithmic_bytes_per_launch": int(bytes_per_launch)}
+    step_ms = elapsed / args.steps * 1e3
+    out = {
+        "metric": METRIC, "value": value, "unit": "k-mers/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": step_ms, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u64", "data": "synthetic (seeded generator, SURVEY.md 8d)",
+        "config": {"workload": workload, "reads_per_gpu": N, "read_len": L, "k": k, "genome": args.genome,
+                   "table": f"-m 2 -s {args.slots}",
+                   "parallelism": f"hash-prefix shard x{world}" if world > 1 else "single"},
+        "roofline": roofline,
+        "hbm_gbs_step": round(bytes_per_launch * (launches / args.steps) / (step_ms * 1e-3) / 1e9, 2),
+        "kernel_ms": {"gather": round(tm["gather_ms"] / launches, 4), "tokenize": round(tm["tokenize_ms"] / launches, 4),
+                      "count": round(count_ms, 4)},
+        "windows_per_step_per_gpu": windows_step, "distinct_per_gpu": st["distinct"],
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args, args.slots / N)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,648 @@
+// kc_api.cpp -- host side of the C ABI (include/kc_api.h): context, staging,
+// batch scheduling, table/Bloom sizing and result extraction.  Compiled by hipcc
+// into libkc.so together with kc_device.hip.
+//
+// Data flow per batch (the reference's io_worker -> in_queue -> string_worker,
+// parallel_parser.hpp:1230-1519, re-shaped for one device):
+//   host chunk -> pinned stage image (chunk at a 4 KiB-aligned offset)
+//   -> one async H2D per batch -> tokenize (3 kernels) -> count/bloom kernel.
+// Two pinned stage buffers alternate so the host fills one while the device
+// consumes the other.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/kc_api.h"
+#include "kc_internal.h"
+#include "kc_synth.h"
+
+using namespace kc;
+
+namespace {
+
+thread_local std::string g_create_error;
+
+constexpr uint64_t kDefaultBatch = 256ull << 20;
+
+uint64_t round_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
+
+}  // namespace
+
+struct kc_ctx {
+    kc_config cfg{};
+    int W = 1, S = 8;
+    hipStream_t stream = nullptr;
+    std::string err;
+
+    // staging
+    uint64_t batch_bytes = 0;
+    uint64_t max_chunks = 0;
+    uint8_t* h_stage[2] = {nullptr, nullptr};
+    ChunkDesc* h_desc[2] = {nullptr, nullptr};
+    hipEvent_t h_free[2] = {nullptr, nullptr};  // recorded after the H2D reading buffer i
+    hipEvent_t xev = nullptr;                   // orders the context stream with a caller stream
+    int cur = 0;
+    uint64_t cur_used = 0;                      // stage bytes used in h_stage[cur]
+    uint64_t cur_n = 0;                         // chunks in h_stage[cur]
+    int cur_fmt = -1;
+    int cur_pass = -1;                          // 0 count, 1 bloom
+
+    uint8_t* d_stage = nullptr;
+    uint8_t* d_sym = nullptr;
+    TileInfo* d_tiles = nullptr;
+    TileOut* d_touts = nullptr;
+    ChunkDesc* d_chunks = nullptr;
+    DevCounters* d_ctr = nullptr;
+
+    // table
+    uint64_t* d_table = nullptr;
+    uint64_t nbuckets = 0;
+
+    // bloom
+    uint32_t* d_bloom = nullptr;
+    uint64_t bf_bits = 0;
+    int nh = 0, nh_gate = 0;
+    bool bloom_final = false;
+
+    uint64_t n_chunks = 0, n_bytes = 0;
+
+    // profiling: event quadruples {start, after gather, after tokenize, after count}
+    bool profiling = false;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::array<hipEvent_t, 4>> ev_pending;
+    kc_timing timing{};
+    uint64_t* d_stream_len_probe = nullptr;
+    std::vector<uint64_t> pending_symbols_bound;
+
+    hipEvent_t get_event() {
+        if (!ev_pool.empty()) {
+            hipEvent_t e = ev_pool.back();
+            ev_pool.pop_back();
+            return e;
+        }
+        hipEvent_t e = nullptr;
+        (void)hipEventCreate(&e);
+        return e;
+    }
+
+    int fail(int code, const std::string& m) {
+        err = m;
+        return code;
+    }
+    int hipfail(hipError_t e, const char* what) {
+        err = std::string(what) + ": " + hipGetErrorString(e);
+        return KC_ERR_HIP;
+    }
+};
+
+#define HIPCHK(ctx, expr)                                  \
+    do {                                                   \
+        hipError_t _e = (expr);                            \
+        if (_e != hipSuccess) return (ctx)->hipfail(_e, #expr); \
+    } while (0)
+
+// ------------------------------------------------------------------------------
+// sizing helpers
+// ------------------------------------------------------------------------------
+static void bloom_sizes(uint64_t U, double fpr, uint64_t* bits, int* nh, int* nh_gate) {
+    // main.cpp:402-418: bits = next pow2 >= -U ln f / ln^2 2 (compared as uint64),
+    // hf = bits_min / U * ln 2; pass 1 uses ceil(hf) (main.cpp:417), the pass-2 gate
+    // receives hf through a uint64_t parameter, i.e. trunc(hf) (parallel_parser.hpp:2397).
+    double bits_min = (-double(U) * std::log(fpr)) / std::pow(std::log(2), 2);
+    double hf = (bits_min / double(U)) * std::log(2);
+    uint64_t b = 2;
+    while (b < uint64_t(bits_min)) b *= 2;
+    *bits = b;
+    *nh = int(std::ceil(hf));
+    *nh_gate = int(uint64_t(hf));
+}
+
+static int alloc_table(kc_ctx* c, uint64_t min_slots) {
+    // Kaarme's table holds exactly next_prime3mod4(min_slots) slots and dies when
+    // full; open addressing on the GPU keeps 25 % headroom over that.
+    uint64_t want = std::max<uint64_t>(min_slots, 64);
+    want = want + want / 4;
+    c->nbuckets = (want + c->S - 1) / c->S;
+    const size_t bytes = c->nbuckets * BUCKET_WORDS * sizeof(uint64_t);
+    hipError_t e = hipMalloc(&c->d_table, bytes);
+    if (e != hipSuccess) return c->fail(KC_ERR_NOMEM, "table allocation failed (" + std::to_string(bytes) + " bytes)");
+    HIPCHK(c, hipMemsetAsync(c->d_table, 0, bytes, c->stream));
+    return KC_OK;
+}
+
+static hipStream_t pick_stream(kc_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
+
+// ------------------------------------------------------------------------------
+// batch execution
+// ------------------------------------------------------------------------------
+static int run_batch(kc_ctx* c, uint64_t used, uint64_t nchunks, int fmt, int pass, hipStream_t s,
+                     hipEvent_t ev_start = nullptr, hipEvent_t ev_gather = nullptr) {
+    const uint64_t ntiles = used / TILE;
+    if (ntiles == 0) return KC_OK;
+    std::array<hipEvent_t, 4> ev{ev_start, ev_gather, nullptr, nullptr};
+    if (c->profiling) {
+        if (!ev[0]) {
+            ev[0] = c->get_event();
+            ev[1] = c->get_event();
+            HIPCHK(c, hipEventRecord(ev[0], s));
+            HIPCHK(c, hipEventRecord(ev[1], s));
+        }
+        ev[2] = c->get_event();
+        ev[3] = c->get_event();
+    }
+    HIPCHK(c, launch_tokenize(c->d_stage, ntiles, c->d_chunks, (int)nchunks, fmt, c->d_tiles, c->d_touts, c->d_sym,
+                              c->batch_bytes + c->max_chunks, c->d_ctr, s));
+    if (c->profiling) HIPCHK(c, hipEventRecord(ev[2], s));
+    TableView tv{c->d_table, c->nbuckets, c->W, c->S};
+    BloomView bv{c->d_bloom, c->bf_bits ? c->bf_bits - 1 : 0, c->nh, c->nh_gate};
+    int mode;
+    if (pass == 1) mode = 1;
+    else mode = (c->cfg.bf_enable && c->cfg.mode != 1) ? 2 : 0;  // -m 1 -b ignores the filter (main.cpp:482-489)
+    HIPCHK(c, launch_count(c->d_sym, used + nchunks, c->cfg.k, mode, tv, bv, c->d_ctr, s));
+    if (c->profiling) {
+        HIPCHK(c, hipEventRecord(ev[3], s));
+        c->ev_pending.push_back(ev);
+        c->pending_symbols_bound.push_back(used + nchunks);
+    }
+    return KC_OK;
+}
+
+static int flush_host(kc_ctx* c) {
+    if (c->cur_n == 0) return KC_OK;
+    const int b = c->cur;
+    HIPCHK(c, hipMemcpyAsync(c->d_stage, c->h_stage[b], c->cur_used, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_chunks, c->h_desc[b], c->cur_n * sizeof(ChunkDesc), hipMemcpyHostToDevice,
+                             c->stream));
+    HIPCHK(c, hipEventRecord(c->h_free[b], c->stream));
+    int rc = run_batch(c, c->cur_used, c->cur_n, c->cur_fmt, c->cur_pass, c->stream);
+    if (rc) return rc;
+    c->cur ^= 1;
+    c->cur_used = 0;
+    c->cur_n = 0;
+    HIPCHK(c, hipEventSynchronize(c->h_free[c->cur]));  // buffer we fill next is no longer read
+    return KC_OK;
+}
+
+static int add_host_chunk(kc_ctx* c, const uint8_t* buf, size_t len, int fmt, int bh, int pass) {
+    if (!buf && len) return c->fail(KC_ERR_ARG, "null buffer");
+    if (fmt == KC_FMT_FASTQ) return c->fail(KC_ERR_UNSUPPORTED, "Input file format not supported.");
+    if (fmt != KC_FMT_FASTA && fmt != KC_FMT_PLAIN) return c->fail(KC_ERR_ARG, "unknown format");
+    if (len == 0) return KC_OK;
+    const uint64_t need = round_up(len, TILE);
+    if (need > c->batch_bytes) return c->fail(KC_ERR_ARG, "chunk larger than the staging batch");
+    if (c->cur_n && (c->cur_fmt != fmt || c->cur_pass != pass || c->cur_used + need > c->batch_bytes ||
+                     c->cur_n + 1 > c->max_chunks)) {
+        int rc = flush_host(c);
+        if (rc) return rc;
+    }
+    ChunkDesc d;
+    d.src_off = 0;
+    d.stage_off = c->cur_used;
+    d.len = len;
+    d.bh = bh ? 1 : 0;
+    d.pad = 0;
+    std::memcpy(c->h_stage[c->cur] + c->cur_used, buf, len);
+    c->h_desc[c->cur][c->cur_n++] = d;
+    c->cur_used += need;
+    c->cur_fmt = fmt;
+    c->cur_pass = pass;
+    if (pass == 0) { c->n_chunks++; c->n_bytes += len; }
+    return KC_OK;
+}
+
+static int device_pass(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, size_t n, int fmt, int pass,
+                       hipStream_t s) {
+    if (fmt == KC_FMT_FASTQ) return c->fail(KC_ERR_UNSUPPORTED, "Input file format not supported.");
+    if (fmt != KC_FMT_FASTA && fmt != KC_FMT_PLAIN) return c->fail(KC_ERR_ARG, "unknown format");
+    int rc = flush_host(c);  // keep order with staged host chunks
+    if (rc) return rc;
+    if (s != c->stream) {
+        HIPCHK(c, hipEventRecord(c->xev, c->stream));
+        HIPCHK(c, hipStreamWaitEvent(s, c->xev, 0));
+    }
+    std::vector<ChunkDesc> batch;
+    uint64_t used = 0;
+    auto launch = [&]() -> int {
+        if (batch.empty()) return KC_OK;
+        // descriptors go through the (idle) pinned desc buffer of the current slot
+        std::memcpy(c->h_desc[c->cur], batch.data(), batch.size() * sizeof(ChunkDesc));
+        HIPCHK(c, hipMemcpyAsync(c->d_chunks, c->h_desc[c->cur], batch.size() * sizeof(ChunkDesc),
+                                 hipMemcpyHostToDevice, s));
+        HIPCHK(c, hipEventRecord(c->h_free[c->cur], s));
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (c->profiling) {
+            e0 = c->get_event();
+            e1 = c->get_event();
+            HIPCHK(c, hipEventRecord(e0, s));
+        }
+        HIPCHK(c, launch_gather(img, c->d_stage, c->d_chunks, (int)batch.size(), batch.data(), s));
+        if (c->profiling) HIPCHK(c, hipEventRecord(e1, s));
+        int r = run_batch(c, used, batch.size(), fmt, pass, s, e0, e1);
+        if (r) return r;
+        HIPCHK(c, hipEventSynchronize(c->h_free[c->cur]));
+        batch.clear();
+        used = 0;
+        return KC_OK;
+    };
+    for (size_t i = 0; i < n; i++) {
+        const uint64_t need = round_up(chunks[i].len, TILE);
+        if (chunks[i].len == 0) continue;
+        if (need > c->batch_bytes) return c->fail(KC_ERR_ARG, "chunk larger than the staging batch");
+        if (used + need > c->batch_bytes || batch.size() + 1 > c->max_chunks) {
+            rc = launch();
+            if (rc) return rc;
+        }
+        ChunkDesc d;
+        d.src_off = chunks[i].off;
+        d.stage_off = used;
+        d.len = chunks[i].len;
+        d.bh = chunks[i].broken_header ? 1 : 0;
+        d.pad = 0;
+        batch.push_back(d);
+        used += need;
+        if (pass == 0) { c->n_chunks++; c->n_bytes += chunks[i].len; }
+    }
+    rc = launch();
+    if (rc) return rc;
+    if (s != c->stream) {
+        HIPCHK(c, hipEventRecord(c->xev, s));
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->xev, 0));
+    }
+    return KC_OK;
+}
+
+// ------------------------------------------------------------------------------
+// C ABI
+// ------------------------------------------------------------------------------
+extern "C" {
+
+const char* kc_last_error(const kc_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
+
+int kc_create(const kc_config* cfg, kc_ctx** out) {
+    if (!cfg || !out) { g_create_error = "null argument"; return KC_ERR_ARG; }
+    *out = nullptr;
+    if (cfg->k < 1 || cfg->k > 127) { g_create_error = "k must be in 1..127"; return KC_ERR_ARG; }
+    if (cfg->mode < 0 || cfg->mode > 2) { g_create_error = "mode must be 0, 1 or 2"; return KC_ERR_ARG; }
+    if (cfg->bf_enable && (cfg->est_unique == 0 || !(cfg->fpr >= 0.001 && cfg->fpr <= 0.999))) {
+        g_create_error = "bloom filter needs est_unique > 0 and 0.001 <= fpr <= 0.999";
+        return KC_ERR_ARG;
+    }
+    kc_ctx* c = new kc_ctx();
+    c->cfg = *cfg;
+    c->W = words_for_k(cfg->k);
+    c->S = slots_per_bucket(c->W);
+    c->batch_bytes = round_up(cfg->batch_bytes ? cfg->batch_bytes : kDefaultBatch, TILE);
+    c->max_chunks = c->batch_bytes / TILE;
+    auto bail = [&](int code, const std::string& m) {
+        g_create_error = m.empty() ? c->err : m;
+        kc_destroy(c);
+        return code;
+    };
+    hipError_t e = hipSetDevice(cfg->device);
+    if (e != hipSuccess) return bail(KC_ERR_HIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
+    if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
+        return bail(KC_ERR_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+    for (int i = 0; i < 2; i++) {
+        if (hipHostMalloc(&c->h_stage[i], c->batch_bytes, hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc(&c->h_desc[i], c->max_chunks * sizeof(ChunkDesc), hipHostMallocDefault) != hipSuccess)
+            return bail(KC_ERR_NOMEM, "pinned staging allocation failed");
+        if (hipEventCreateWithFlags(&c->h_free[i], hipEventDisableTiming) != hipSuccess)
+            return bail(KC_ERR_HIP, "event creation failed");
+    }
+    if (hipEventCreateWithFlags(&c->xev, hipEventDisableTiming) != hipSuccess)
+        return bail(KC_ERR_HIP, "event creation failed");
+    const uint64_t ntiles = c->batch_bytes / TILE;
+    if (hipMalloc(&c->d_stage, c->batch_bytes) != hipSuccess ||
+        hipMalloc(&c->d_sym, c->batch_bytes + c->max_chunks + 64) != hipSuccess ||
+        hipMalloc(&c->d_tiles, ntiles * sizeof(TileInfo)) != hipSuccess ||
+        hipMalloc(&c->d_touts, ntiles * sizeof(TileOut)) != hipSuccess ||
+        hipMalloc(&c->d_chunks, c->max_chunks * sizeof(ChunkDesc)) != hipSuccess ||
+        hipMalloc(&c->d_ctr, sizeof(DevCounters)) != hipSuccess)
+        return bail(KC_ERR_NOMEM, "device staging allocation failed");
+    if (hipMemsetAsync(c->d_ctr, 0, sizeof(DevCounters), c->stream) != hipSuccess)
+        return bail(KC_ERR_HIP, "memset failed");
+    if (cfg->bf_enable) {
+        bloom_sizes(cfg->est_unique, cfg->fpr, &c->bf_bits, &c->nh, &c->nh_gate);
+        if (c->nh > MAX_NH) return bail(KC_ERR_ARG, "too many Bloom hash functions");
+        const uint64_t words = std::max<uint64_t>(1, (2 * c->bf_bits + 31) / 32);
+        if (hipMalloc(&c->d_bloom, words * 4) != hipSuccess)
+            return bail(KC_ERR_NOMEM, "Bloom filter allocation failed");
+        if (hipMemsetAsync(c->d_bloom, 0, words * 4, c->stream) != hipSuccess) return bail(KC_ERR_HIP, "memset");
+    } else {
+        int rc = alloc_table(c, cfg->table_slots);
+        if (rc) return bail(rc, "");
+    }
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return bail(KC_ERR_HIP, "stream sync failed");
+    *out = c;
+    return KC_OK;
+}
+
+void kc_destroy(kc_ctx* c) {
+    if (!c) return;
+    if (c->stream) hipStreamSynchronize(c->stream);
+    for (int i = 0; i < 2; i++) {
+        if (c->h_stage[i]) hipHostFree(c->h_stage[i]);
+        if (c->h_desc[i]) hipHostFree(c->h_desc[i]);
+        if (c->h_free[i]) hipEventDestroy(c->h_free[i]);
+    }
+    hipFree(c->d_stage);
+    hipFree(c->d_sym);
+    hipFree(c->d_tiles);
+    hipFree(c->d_touts);
+    hipFree(c->d_chunks);
+    hipFree(c->d_ctr);
+    hipFree(c->d_table);
+    hipFree(c->d_bloom);
+    if (c->xev) hipEventDestroy(c->xev);
+    for (auto e : c->ev_pool) hipEventDestroy(e);
+    for (auto& ev : c->ev_pending)
+        for (auto e : ev) hipEventDestroy(e);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int kc_bloom_chunk(kc_ctx* c, const uint8_t* buf, size_t len, int fmt, int bh) {
+    if (!c) return KC_ERR_ARG;
+    if (!c->cfg.bf_enable || c->bloom_final) return c->fail(KC_ERR_STATE, "bloom pass not active");
+    return add_host_chunk(c, buf, len, fmt, bh, 1);
+}
+
+int kc_bloom_device(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, size_t n, int fmt, void* s) {
+    if (!c || (!img && n) || (!chunks && n)) return KC_ERR_ARG;
+    if (!c->cfg.bf_enable || c->bloom_final) return c->fail(KC_ERR_STATE, "bloom pass not active");
+    return device_pass(c, img, chunks, n, fmt, 1, pick_stream(c, s));
+}
+
+int kc_bloom_finalize(kc_ctx* c, uint64_t* new_in_second) {
+    if (!c) return KC_ERR_ARG;
+    if (!c->cfg.bf_enable || c->bloom_final) return c->fail(KC_ERR_STATE, "bloom pass not active");
+    int rc = flush_host(c);
+    if (rc) return rc;
+    HIPCHK(c, hipDeviceSynchronize());
+    DevCounters h;
+    HIPCHK(c, hipMemcpy(&h, c->d_ctr, sizeof(h), hipMemcpyDeviceToHost));
+    if (new_in_second) *new_in_second = h.new_in_second;
+    c->bloom_final = true;
+    rc = alloc_table(c, 2 * h.new_in_second);  // main.cpp:454
+    if (rc) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return KC_OK;
+}
+
+int kc_count_chunk(kc_ctx* c, const uint8_t* buf, size_t len, int fmt, int bh) {
+    if (!c) return KC_ERR_ARG;
+    if (!c->d_table) return c->fail(KC_ERR_STATE, "kc_bloom_finalize must precede the counting pass");
+    return add_host_chunk(c, buf, len, fmt, bh, 0);
+}
+
+int kc_count_device(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, size_t n, int fmt, void* s) {
+    if (!c || (!img && n) || (!chunks && n)) return KC_ERR_ARG;
+    if (!c->d_table) return c->fail(KC_ERR_STATE, "kc_bloom_finalize must precede the counting pass");
+    return device_pass(c, img, chunks, n, fmt, 0, pick_stream(c, s));
+}
+
+int kc_sync(kc_ctx* c) {
+    if (!c) return KC_ERR_ARG;
+    int rc = flush_host(c);
+    if (rc) return rc;
+    HIPCHK(c, hipDeviceSynchronize());
+    return KC_OK;
+}
+
+int kc_finish(kc_ctx* c, kc_stats* st) {
+    int rc = kc_sync(c);
+    if (rc) return rc;
+    DevCounters h;
+    HIPCHK(c, hipMemcpy(&h, c->d_ctr, sizeof(h), hipMemcpyDeviceToHost));
+    if (st) {
+        std::memset(st, 0, sizeof(*st));
+        st->windows = h.windows;
+        st->bf_windows = h.bf_windows;
+        st->inserted = h.inserted;
+        st->table_slots = c->nbuckets * c->S;
+        st->bf_bits = c->bf_bits;
+        st->new_in_first = h.new_in_first;
+        st->new_in_second = h.new_in_second;
+        st->failed_in_first = h.failed_in_first;
+        st->chunks = c->n_chunks;
+        st->bytes = c->n_bytes;
+        // occupied slots
+        if (c->d_table) {
+            HIPCHK(c, hipMemsetAsync(&c->d_ctr->occupied, 0, 8, c->stream));
+            HIPCHK(c, hipMemsetAsync(&c->d_ctr->dump_n, 0, 8, c->stream));
+            TableView tv{c->d_table, c->nbuckets, c->W, c->S};
+            HIPCHK(c, launch_dump(tv, c->cfg.mode == 0 ? 0 : 1, ~0ULL, nullptr, c->d_ctr, c->stream));
+            unsigned long long occ = 0;
+            HIPCHK(c, hipMemcpyAsync(&occ, &c->d_ctr->occupied, 8, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            st->distinct = occ;
+        }
+    }
+    if (h.overflow) return c->fail(KC_ERR_TABLE_FULL, "Hash table is full (" + std::to_string(h.overflow) +
+                                                           " k-mers could not be inserted)");
+    return KC_OK;
+}
+
+int kc_reset(kc_ctx* c) {
+    if (!c) return KC_ERR_ARG;
+    int rc = kc_sync(c);
+    if (rc) return rc;
+    if (c->d_table) HIPCHK(c, hipMemsetAsync(c->d_table, 0, c->nbuckets * BUCKET_WORDS * sizeof(uint64_t), c->stream));
+    if (c->d_bloom) {
+        const uint64_t words = std::max<uint64_t>(1, (2 * c->bf_bits + 31) / 32);
+        HIPCHK(c, hipMemsetAsync(c->d_bloom, 0, words * 4, c->stream));
+        if (c->bloom_final) {  // back to the Bloom pass: the table is sized again after it
+            hipFree(c->d_table);
+            c->d_table = nullptr;
+            c->nbuckets = 0;
+            c->bloom_final = false;
+        }
+    }
+    HIPCHK(c, hipMemsetAsync(c->d_ctr, 0, sizeof(DevCounters), c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->n_chunks = c->n_bytes = 0;
+    return KC_OK;
+}
+
+int kc_profile(kc_ctx* c, int enable) {
+    if (!c) return KC_ERR_ARG;
+    c->profiling = enable != 0;
+    return KC_OK;
+}
+
+int kc_get_timing(kc_ctx* c, kc_timing* t) {
+    if (!c || !t) return KC_ERR_ARG;
+    int rc = kc_sync(c);
+    if (rc) return rc;
+    for (auto& ev : c->ev_pending) {
+        float a = 0, b = 0, d = 0;
+        HIPCHK(c, hipEventElapsedTime(&a, ev[0], ev[1]));
+        HIPCHK(c, hipEventElapsedTime(&b, ev[1], ev[2]));
+        HIPCHK(c, hipEventElapsedTime(&d, ev[2], ev[3]));
+        c->timing.gather_ms += a;
+        c->timing.tokenize_ms += b;
+        c->timing.count_ms += d;
+        c->timing.launches++;
+        for (auto e : ev) c->ev_pool.push_back(e);
+    }
+    c->ev_pending.clear();
+    unsigned long long sl = 0;
+    HIPCHK(c, hipMemcpy(&sl, &c->d_ctr->stream_len, 8, hipMemcpyDeviceToHost));
+    c->timing.symbols = sl;  // symbols of the LAST batch (exact for single-batch steps)
+    *t = c->timing;
+    c->timing = kc_timing{};
+    return KC_OK;
+}
+
+int kc_key_words(const kc_ctx* c) { return c ? c->W : 0; }
+void kc_free(void* p) { std::free(p); }
+
+int kc_dump(kc_ctx* c, uint64_t** records, uint64_t* n_records) {
+    if (!c || !records || !n_records) return KC_ERR_ARG;
+    *records = nullptr;
+    *n_records = 0;
+    int rc = kc_sync(c);
+    if (rc) return rc;
+    if (!c->d_table) return c->fail(KC_ERR_STATE, "no table");
+    TableView tv{c->d_table, c->nbuckets, c->W, c->S};
+    const int cm = c->cfg.mode == 0 ? 0 : 1;
+    const uint64_t a = c->cfg.min_abundance;
+    HIPCHK(c, hipMemsetAsync(&c->d_ctr->dump_n, 0, 16 * 8 * 2, c->stream));  // dump_n + occupied lines
+    HIPCHK(c, launch_dump(tv, cm, a, nullptr, c->d_ctr, c->stream));
+    unsigned long long n = 0;
+    HIPCHK(c, hipMemcpyAsync(&n, &c->d_ctr->dump_n, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const size_t rec = (size_t)(c->W + 1) * sizeof(uint64_t);
+    uint64_t* h = (uint64_t*)std::malloc(std::max<size_t>(1, n * rec));
+    if (!h) return c->fail(KC_ERR_NOMEM, "host allocation failed");
+    if (n) {
+        uint64_t* d = nullptr;
+        hipError_t e = hipMalloc(&d, n * rec);
+        if (e != hipSuccess) { std::free(h); return c->fail(KC_ERR_NOMEM, "dump buffer allocation failed"); }
+        HIPCHK(c, hipMemsetAsync(&c->d_ctr->dump_n, 0, 16 * 8 * 2, c->stream));
+        HIPCHK(c, launch_dump(tv, cm, a, d, c->d_ctr, c->stream));
+        HIPCHK(c, hipMemcpyAsync(h, d, n * rec, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        hipFree(d);
+    }
+    *records = h;
+    *n_records = n;
+    return KC_OK;
+}
+
+int kc_write(kc_ctx* c, const char* path) {
+    if (!c || !path) return KC_ERR_ARG;
+    if (c->cfg.min_abundance == 0) return KC_OK;  // parallel_parser.hpp:1536 / 858
+    uint64_t* rec = nullptr;
+    uint64_t n = 0;
+    int rc = kc_dump(c, &rec, &n);
+    if (rc) return rc;
+    FILE* f = std::fopen(path, "wb");
+    if (!f) { kc_free(rec); return c->fail(KC_ERR_IO, std::string("cannot open ") + path); }
+    const int k = c->cfg.k, W = c->W;
+    const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const uint64_t block = 1 << 16;
+    std::vector<std::string> bufs(nt);
+    static const char sym[4] = {'A', 'C', 'G', 'T'};
+    for (uint64_t b0 = 0; b0 < n; b0 += block * nt) {
+        std::vector<std::thread> th;
+        for (unsigned t = 0; t < nt; t++) {
+            th.emplace_back([&, t]() {
+                std::string& s = bufs[t];
+                s.clear();
+                const uint64_t lo = b0 + t * block, hi = std::min(n, lo + block);
+                if (lo >= hi) return;
+                s.reserve((hi - lo) * (k + 8));
+                char line[160];
+                for (uint64_t i = lo; i < hi; i++) {
+                    const uint64_t* r = rec + i * (W + 1);
+                    for (int j = 0; j < k; j++) {
+                        const int bit = 2 * (k - 1 - j);
+                        line[j] = sym[(r[W - 1 - bit / 64] >> (bit % 64)) & 3];
+                    }
+                    int len = k + std::snprintf(line + k, sizeof(line) - k, " %llu\n", (unsigned long long)r[W]);
+                    s.append(line, len);
+                }
+            });
+        }
+        for (auto& x : th) x.join();
+        for (unsigned t = 0; t < nt; t++)
+            if (!bufs[t].empty() && std::fwrite(bufs[t].data(), 1, bufs[t].size(), f) != bufs[t].size()) {
+                std::fclose(f);
+                kc_free(rec);
+                return c->fail(KC_ERR_IO, "write failed");
+            }
+    }
+    std::fclose(f);
+    kc_free(rec);
+    return KC_OK;
+}
+
+int kc_plan_chunks(const uint8_t* image, uint64_t size, int k, uint64_t chunk_size, int fmt, kc_chunk** out,
+                   uint64_t* n_out) {
+    if (!out || !n_out || k < 1 || (!image && size)) return KC_ERR_ARG;
+    if (chunk_size == 0) chunk_size = 10ull << 20;  // main.cpp:387
+    const unsigned char start = fmt == KC_FMT_FASTA ? '>' : fmt == KC_FMT_FASTQ ? '@' : 0;
+    std::vector<kc_chunk> v;
+    // io_worker: loop while rem >= k, each chunk min(chunk_size, rem) bytes, then
+    // read_chunk_from_file with its k = k-1 (parallel_parser.hpp:1246-1285).
+    const int64_t back = (int64_t)k - 1;
+    int64_t rem = (int64_t)size;
+    uint64_t pos = 0;
+    bool bh = false;
+    while (rem >= (int64_t)k) {
+        const int64_t n = std::min<int64_t>((int64_t)chunk_size, rem);
+        const uint8_t* b = image + pos;
+        kc_chunk ck{pos, (uint64_t)n, bh ? 1 : 0, 0};
+        v.push_back(ck);
+        int64_t fake = 0;
+        if (start) {
+            int64_t real = 0, si = n - 1;
+            if (start == '>')
+                for (; real < back && si >= 0; si--) (b[si] != '\n') ? real++ : fake++;  // text_reader.h:143-150
+            if (real != back) break;                                                 // text_reader.h:156-160
+            // broken header of the NEXT chunk: scan back from the byte before its start
+            bh = true;
+            for (int64_t i = n - 1 - back - fake; i >= 0; i--) {  // text_reader.h:164-184
+                if (b[i] == start) break;
+                if (b[i] == '\n') { bh = false; break; }
+            }
+        }
+        if (rem == n) break;                 // text_reader.h:201-204
+        const int64_t adv = n - back - fake;  // seek back (k-1) + fake (text_reader.h:210-220)
+        if (adv == 0) break;
+        rem -= adv;
+        pos += (uint64_t)adv;
+    }
+    kc_chunk* r = (kc_chunk*)std::malloc(std::max<size_t>(1, v.size()) * sizeof(kc_chunk));
+    if (!r) return KC_ERR_NOMEM;
+    if (!v.empty()) std::memcpy(r, v.data(), v.size() * sizeof(kc_chunk));
+    *out = r;
+    *n_out = v.size();
+    return KC_OK;
+}
+
+uint64_t kc_synth_bytes(uint64_t first_read, uint64_t n_reads, uint32_t read_len, uint32_t wrap) {
+    kc_synth_params p{};
+    p.read_len = read_len;
+    p.wrap = wrap;
+    return kcs_record_offset(&p, first_read + n_reads) - kcs_record_offset(&p, first_read);
+}
+
+int kc_synth_device(uint8_t* dst, uint64_t first_read, uint64_t n_reads, uint64_t seed, uint64_t genome_len,
+                    uint32_t read_len, uint32_t wrap, double err_rate, double n_rate, void* s) {
+    if (!dst || genome_len < read_len || read_len == 0) return KC_ERR_ARG;
+    hipError_t e = launch_synth(dst, first_read, n_reads, seed, genome_len, read_len, wrap, err_rate, n_rate,
+                                (hipStream_t)s);
+    return e == hipSuccess ? KC_OK : KC_ERR_HIP;
+}
+
+}  // extern "C"

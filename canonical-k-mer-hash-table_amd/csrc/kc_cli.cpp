@@ -1,0 +1,342 @@
+// kc_cli.cpp -- `kaarme` drop-in command line on top of libkc.so.
+//
+// Same interface as the reference's main.cpp:127-156 (CLI11 options, exactly one
+// of -s/-u, -u needs -b, -f needs -b), the same input format detection
+// (main.cpp:19-68), the same chunking (kc_plan_chunks == io_worker +
+// read_chunk_from_file) and the same output text ("<CANONICAL_KMER> <count>\n" for
+// T(c) >= a, default file "<input stem>.kaarme_counts", main.cpp:189-191).
+// Exit codes of option errors follow CLI11's ExitCodes (CLI11.hpp).
+//
+// Deliberate differences (documented in DESIGN.md): -t defaults to 3 (the reference
+// crashes without it); gzip input is decompressed completely (the reference
+// truncates it); the work runs on one MI355X.
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+#include <zlib.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <iostream>
+#include <string>
+#include <vector>
+
+#include "../../include/kc_api.h"
+
+namespace {
+
+enum CliExit { kConversion = 104, kValidation = 105, kRequired = 106, kRequires = 107, kExtras = 109 };
+
+struct Args {
+    std::string input, output;
+    long long k = 0;
+    int mode = 2;
+    unsigned long long min_abundance = 2;
+    int threads = 3;
+    bool use_bf = false;
+    double fpr = 0.01;
+    bool fpr_set = false;
+    bool have_s = false, have_u = false;
+    unsigned long long slots = 0, unique = 0;
+    int device = 0;
+};
+
+void usage(const char* prog) {
+    std::cout << "Space-efficient k-mer counter\n"
+                 "Usage: " << prog << " [OPTIONS] INPUT KLEN\n\n"
+                 "Positionals:\n"
+                 "  INPUT TEXT:FILE REQUIRED    Input file (automatic format detection)\n"
+                 "  KLEN INT REQUIRED           k-mer length\n\n"
+                 "Options:\n"
+                 "  -h,--help                   Print this help message and exit\n"
+                 "  -m,--hash-table-type INT    Hash table type: 0 for plain and 2 for kaarme (def. 2)\n"
+                 "  -a,--min-k-abu UINT         Minimum abundance threshold for the output k-mers (def. 2)\n"
+                 "  -t,--threads UINT           Number of working threads (def. 3)\n"
+                 "  -o,--output-file TEXT       Output file where the k-mer counts will be stored\n"
+                 "  -b,--use-bfilter            Use bloom filters to discard unique k-mers\n"
+                 "  -f,--bfilter-fpr FLOAT      Bloom filter false positive rate (def. 0.01)\n"
+                 "  --device INT                HIP device ordinal (def. 0)\n\n"
+                 "Mandatory params:\n"
+                 "  -s,--hash-tab-size UINT     Hash table size\n"
+                 "  -u,--unq-kmers UINT         Estimated number of unique k-mers\n";
+}
+
+int cli_error(int code, const std::string& msg) {
+    std::cerr << msg << "\nRun with --help for more information.\n";
+    return code;
+}
+
+bool parse_uint(const std::string& s, unsigned long long* v) {
+    if (s.empty() || s[0] == '-' || s[0] == '+') return false;
+    char* end = nullptr;
+    errno = 0;
+    *v = std::strtoull(s.c_str(), &end, 10);
+    return errno == 0 && end && *end == 0;
+}
+bool parse_int(const std::string& s, long long* v) {
+    if (s.empty()) return false;
+    char* end = nullptr;
+    errno = 0;
+    *v = std::strtoll(s.c_str(), &end, 10);
+    return errno == 0 && end && *end == 0;
+}
+bool parse_double(const std::string& s, double* v) {
+    if (s.empty()) return false;
+    char* end = nullptr;
+    *v = std::strtod(s.c_str(), &end);
+    return end && *end == 0;
+}
+
+// returns -1 on success, else exit code
+int parse(int argc, char** argv, Args* a) {
+    std::vector<std::string> pos;
+    for (int i = 1; i < argc; i++) {
+        std::string o = argv[i];
+        std::string val;
+        bool has_inline = false;
+        if (o.rfind("--", 0) == 0 && o.find('=') != std::string::npos) {
+            val = o.substr(o.find('=') + 1);
+            o = o.substr(0, o.find('='));
+            has_inline = true;
+        }
+        auto next = [&](std::string* out) -> bool {
+            if (has_inline) { *out = val; return true; }
+            if (i + 1 >= argc) return false;
+            *out = argv[++i];
+            return true;
+        };
+        if (o == "-h" || o == "--help") { usage(argv[0]); return 0; }
+        if (o == "-b" || o == "--use-bfilter") { a->use_bf = true; continue; }
+        if (o.size() > 1 && o[0] == '-' && !(o.size() > 1 && std::isdigit((unsigned char)o[1]))) {
+            std::string v;
+            if (!next(&v)) return cli_error(kRequired, o + " requires an argument");
+            unsigned long long u;
+            long long si;
+            double d;
+            if (o == "-m" || o == "--hash-table-type") {
+                if (!parse_int(v, &si)) return cli_error(kConversion, "Could not convert: " + o + " = " + v);
+                if (si < 0 || si > 2) return cli_error(kValidation, o + ": Value " + v + " not in range 0 to 2");
+                a->mode = (int)si;
+            } else if (o == "-a" || o == "--min-k-abu") {
+                if (!parse_uint(v, &u)) return cli_error(kConversion, "Could not convert: " + o + " = " + v);
+                a->min_abundance = u;
+            } else if (o == "-t" || o == "--threads") {
+                if (!parse_int(v, &si)) return cli_error(kConversion, "Could not convert: " + o + " = " + v);
+                if (si < 3 || si > 64) return cli_error(kValidation, o + ": Value " + v + " not in range 3 to 64");
+                a->threads = (int)si;
+            } else if (o == "-o" || o == "--output-file") {
+                a->output = v;
+            } else if (o == "-f" || o == "--bfilter-fpr") {
+                if (!parse_double(v, &d)) return cli_error(kConversion, "Could not convert: " + o + " = " + v);
+                if (!(d >= 0.001 && d <= 0.999))
+                    return cli_error(kValidation, o + ": Value " + v + " not in range 0.001 to 0.999");
+                a->fpr = d;
+                a->fpr_set = true;
+            } else if (o == "-s" || o == "--hash-tab-size") {
+                if (!parse_uint(v, &u)) return cli_error(kConversion, "Could not convert: " + o + " = " + v);
+                a->slots = u;
+                a->have_s = true;
+            } else if (o == "-u" || o == "--unq-kmers") {
+                if (!parse_uint(v, &u)) return cli_error(kConversion, "Could not convert: " + o + " = " + v);
+                a->unique = u;
+                a->have_u = true;
+            } else if (o == "--device") {
+                if (!parse_int(v, &si) || si < 0) return cli_error(kConversion, "Could not convert: " + o + " = " + v);
+                a->device = (int)si;
+            } else {
+                return cli_error(kExtras, "The following argument was not expected: " + o);
+            }
+            continue;
+        }
+        pos.push_back(o);
+    }
+    if (pos.size() > 2) return cli_error(kExtras, "The following arguments were not expected: " + pos[2]);
+    if (pos.size() < 1) return cli_error(kRequired, "INPUT is required");
+    if (pos.size() < 2) return cli_error(kRequired, "KLEN is required");
+    a->input = pos[0];
+    struct stat st;
+    if (stat(a->input.c_str(), &st) != 0 || S_ISDIR(st.st_mode))
+        return cli_error(kValidation, "INPUT: File does not exist: " + a->input);
+    if (!parse_int(pos[1], &a->k)) return cli_error(kConversion, "Could not convert: KLEN = " + pos[1]);
+    if (a->k <= 0) return cli_error(kValidation, "KLEN: Value " + pos[1] + " not in range 0 to inf");
+    if (a->have_s == a->have_u)
+        return cli_error(kRequired, "[Option Group: dummy group2] Exactly 1 option from [-s,--hash-tab-size,-u,--unq-kmers] is required");
+    if (a->use_bf && !a->have_u) return cli_error(kRequires, "--use-bfilter requires --unq-kmers");
+    if (a->have_u && !a->use_bf) return cli_error(kRequires, "--unq-kmers requires --use-bfilter");
+    if (a->fpr_set && !a->use_bf) return cli_error(kRequires, "--bfilter-fpr requires --use-bfilter");
+    return -1;
+}
+
+std::string ext_of(const std::string& p) {  // std::filesystem::path::extension()
+    size_t slash = p.find_last_of('/');
+    std::string fn = slash == std::string::npos ? p : p.substr(slash + 1);
+    size_t dot = fn.find_last_of('.');
+    if (dot == std::string::npos || dot == 0 || fn == "..") return "";
+    return fn.substr(dot);
+}
+std::string stem_of(const std::string& p) {
+    size_t slash = p.find_last_of('/');
+    std::string fn = slash == std::string::npos ? p : p.substr(slash + 1);
+    size_t dot = fn.find_last_of('.');
+    if (dot == std::string::npos || dot == 0) return fn;
+    return fn.substr(0, dot);
+}
+std::string filename_of(const std::string& p) {
+    size_t slash = p.find_last_of('/');
+    return slash == std::string::npos ? p : p.substr(slash + 1);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    Args a;
+    int prc = parse(argc, argv, &a);
+    if (prc >= 0) return prc;
+
+    // ---- format detection (main.cpp:19-68)
+    int fd = open(a.input.c_str(), O_RDONLY);
+    if (fd < 0) { std::cerr << "cannot open " << a.input << "\n"; return 1; }
+    struct stat st;
+    fstat(fd, &st);
+    const uint64_t fsize = (uint64_t)st.st_size;
+    unsigned char magic[2] = {0, 0};
+    if (fsize >= 2) { ssize_t r = pread(fd, magic, 2, 0); (void)r; }
+    const bool gz = magic[0] == 0x1f && magic[1] == 0x8b;
+    std::string ext_path = a.input;
+    if (gz) {
+        while (ext_of(ext_path) == ".gz") ext_path = ext_path.substr(0, ext_path.size() - 3);
+    }
+    const std::string ext = ext_of(ext_path);
+
+    // ---- load the image (mmap, or a full gunzip)
+    const uint8_t* image = nullptr;
+    uint64_t isize = 0;
+    std::vector<uint8_t> gzbuf;
+    void* map = nullptr;
+    if (gz) {
+        gzFile g = gzdopen(dup(fd), "r");
+        std::vector<uint8_t> tmp(1 << 22);
+        int n;
+        while ((n = gzread(g, tmp.data(), (unsigned)tmp.size())) > 0) gzbuf.insert(gzbuf.end(), tmp.begin(), tmp.begin() + n);
+        gzclose(g);
+        image = gzbuf.data();
+        isize = gzbuf.size();
+    } else if (fsize) {
+        map = mmap(nullptr, fsize, PROT_READ, MAP_PRIVATE, fd, 0);
+        if (map == MAP_FAILED) { std::cerr << "mmap failed\n"; return 1; }
+        madvise(map, fsize, MADV_SEQUENTIAL);
+        image = (const uint8_t*)map;
+        isize = fsize;
+    }
+    const unsigned char sym = isize ? image[0] : 0;
+    int fmt;
+    bool ill = false;
+    if (ext == ".fasta" || ext == ".fa") { fmt = KC_FMT_FASTA; ill = sym != '>'; }
+    else if (ext == ".fastq" || ext == ".fq") { fmt = KC_FMT_FASTQ; ill = sym != '@'; }
+    else { fmt = KC_FMT_PLAIN; ill = !(sym && std::strchr("actgACGT", sym)); }
+    if (ill) {
+        std::cerr << "Input file " << a.input << " is ill-formed" << std::endl;
+        return 1;
+    }
+    if (a.output.empty()) a.output = stem_of(a.input) + ".kaarme_counts";
+
+    std::cout << "Running settings: " << std::endl;
+    std::cout << "  input file:               " << filename_of(a.input) << std::endl;
+    std::cout << "  input format:             " << (fmt == KC_FMT_FASTA ? "FASTA" : fmt == KC_FMT_FASTQ ? "FASTQ" : "ONE-STR-PER-LINE") << std::endl;
+    std::cout << "  gzip compressed:          " << (gz ? "yes" : "no") << std::endl;
+    std::cout << "  k-mer length:             " << a.k << std::endl;
+    std::cout << "  min. abundance threshold: " << a.min_abundance << std::endl;
+    std::cout << "  hash table type:          " << (a.mode == 0 ? "plain" : "kaarme") << std::endl;
+    std::cout << "  using bloom filers:       " << (a.use_bf ? "yes" : "no") << std::endl;
+    if (a.use_bf) {
+        std::cout << "    est. unique k-mers:     " << a.unique << std::endl;
+        std::cout << "    false positive rate:    " << a.fpr << std::endl;
+    } else {
+        std::cout << "    est. hash table size:   " << a.slots << std::endl;
+    }
+    std::cout << "  working threads:          " << a.threads << std::endl;
+    std::cout << "  output file:              " << a.output << std::endl;
+    std::cout << "  device:                   MI355X (HIP device " << a.device << ")" << std::endl;
+
+    if (fmt == KC_FMT_FASTQ) {  // parallel_parser.hpp:1216-1225
+        std::cout << "Input file format not supported.";
+        return 0;
+    }
+    if (a.k > 127) {
+        std::cerr << "k-mer length above 127 is not supported by this build" << std::endl;
+        return 1;
+    }
+
+    kc_chunk* chunks = nullptr;
+    uint64_t nch = 0;
+    if (kc_plan_chunks(image, isize, (int)a.k, 0, fmt, &chunks, &nch) != KC_OK) {
+        std::cerr << "chunk planning failed" << std::endl;
+        return 1;
+    }
+
+    kc_config cfg;
+    std::memset(&cfg, 0, sizeof(cfg));
+    cfg.k = (int)a.k;
+    cfg.mode = a.mode;
+    cfg.bf_enable = a.use_bf;
+    cfg.device = a.device;
+    cfg.table_slots = a.slots;
+    cfg.est_unique = a.unique;
+    cfg.fpr = a.fpr;
+    cfg.min_abundance = a.min_abundance;
+    kc_ctx* ctx = nullptr;
+    if (kc_create(&cfg, &ctx) != KC_OK) {
+        std::cerr << "kc_create: " << kc_last_error(nullptr) << std::endl;
+        return 1;
+    }
+    auto die = [&](const char* what) {
+        std::cerr << what << ": " << kc_last_error(ctx) << std::endl;
+        kc_destroy(ctx);
+        std::exit(1);
+    };
+    using clk = std::chrono::high_resolution_clock;
+    if (a.use_bf) {
+        std::cout << "Starting parallel bloom filtering\n";
+        auto t0 = clk::now();
+        for (uint64_t i = 0; i < nch; i++)
+            if (kc_bloom_chunk(ctx, image + chunks[i].off, chunks[i].len, fmt, chunks[i].broken_header) != KC_OK)
+                die("bloom pass");
+        uint64_t nis = 0;
+        if (kc_bloom_finalize(ctx, &nis) != KC_OK) die("bloom finalize");
+        auto t1 = clk::now();
+        std::cout << "New k-mers in second bloom filter " << nis << "\n";
+        std::cout << "Time used to bloom filter k-mers: "
+                  << std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0).count() << " microseconds\n";
+    }
+    std::cout << "Starting " << (a.mode == 0 ? "atomic flag basic" : "atomic variable pointer") << " hash table\n";
+    auto t0 = clk::now();
+    for (uint64_t i = 0; i < nch; i++)
+        if (kc_count_chunk(ctx, image + chunks[i].off, chunks[i].len, fmt, chunks[i].broken_header) != KC_OK)
+            die("counting pass");
+    kc_stats stt;
+    if (kc_finish(ctx, &stt) != KC_OK) {
+        std::cout << "Hash table is full... Cannot handle this yet\n";
+        die("counting pass");
+    }
+    auto t1 = clk::now();
+    std::cout << "Hash table size is: " << stt.table_slots << "\n";
+    if (a.min_abundance > 0) {
+        std::cout << "Start writing k-mers in a file\n";
+        if (kc_write(ctx, a.output.c_str()) != KC_OK) die("writing k-mers");
+    }
+    auto t2 = clk::now();
+    std::cout << "Time used to build hash table: " << std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0).count()
+              << " microseconds\n";
+    std::cout << "Time used to write k-mers in a file: "
+              << std::chrono::duration_cast<std::chrono::microseconds>(t2 - t1).count() << " microseconds\n";
+    std::cout << "Processed k-mers: " << stt.windows << " (inserted " << stt.inserted << ")\n";
+    std::cout << "Main array slots used " << stt.distinct << " / " << stt.table_slots << "\n";
+    kc_destroy(ctx);
+    kc_free(chunks);
+    if (map) munmap(map, fsize);
+    close(fd);
+    return 0;
+}

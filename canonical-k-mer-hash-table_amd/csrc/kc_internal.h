@@ -1,0 +1,97 @@
+// kc_internal.h -- declarations shared by the HIP kernels (kc_device.hip) and the
+// host side of the C ABI (kc_api.cpp).  Not part of the public boundary
+// (that is include/kc_api.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace kc {
+
+// Staged-batch geometry.  Each reference chunk (text_reader.h:17-36) is placed at a
+// TILE-aligned offset of the device stage buffer so that no tile straddles two
+// chunks; the tokenizer then works per 4 KiB tile.
+constexpr int TILE = 4096;
+constexpr int TILE_THREADS = 256;          // 16 bytes per thread
+constexpr int COUNT_THREADS = 256;
+constexpr int RUN = 32;                    // consecutive symbols rolled per thread
+constexpr int BUCKET_WORDS = 16;           // 128-byte buckets
+constexpr uint64_t EMPTY = 0;              // empty slot: word 0 of a stored key carries OCC
+constexpr uint64_t OCC = 1ULL << 63;       // word 0 always has spare top bits (W = k/32 + 1)
+constexpr uint64_t READY = 1ULL << 62;     // multi-word slot published flag, in the count word
+constexpr uint64_t CNT_MASK = READY - 1;
+constexpr int MAX_NH = 10;                 // -f >= 0.001  =>  ceil(-ln f / ln 2) <= 10
+constexpr uint8_t SYM_BREAK = 4;
+
+// symbol-stream code for byte b outside a header (functions_strings.cpp:56-70)
+enum Fmt { FMT_FASTA = 0, FMT_FASTQ = 1, FMT_PLAIN = 2 };
+
+struct ChunkDesc {          // one reference chunk inside the stage buffer
+    uint64_t src_off;       // offset in the source image (device-resident path)
+    uint64_t stage_off;     // TILE-aligned offset in the stage buffer
+    uint64_t len;           // bytes
+    uint32_t bh;            // broken_header (text_reader.h:24)
+    uint32_t pad;
+};
+
+struct TileInfo {           // written by k_tile_summary, consumed by k_tile_scan / k_emit
+    uint32_t nl;            // FASTA newlines (removed from the symbol stream)
+    uint32_t valid;         // bytes of the chunk inside this tile
+    uint8_t marker;         // last header marker: 0 none, 1 '\n', 2 '>'
+    uint8_t first;          // tile starts a chunk
+    uint8_t bh;             // chunk's broken_header (only meaningful when first)
+    uint8_t pad;
+    uint32_t pad2;
+};
+
+struct TileOut {            // written by k_tile_scan
+    uint64_t out_off;       // first symbol index of the tile in the stream
+    uint32_t hs_in;         // header state entering the tile
+    uint32_t pad;
+};
+
+// Device-side counters (one 128-byte line each to avoid false sharing).
+struct DevCounters {
+    unsigned long long windows;         uint64_t _p0[15];
+    unsigned long long inserted;        uint64_t _p1[15];
+    unsigned long long overflow;        uint64_t _p2[15];
+    unsigned long long new_in_first;    uint64_t _p3[15];
+    unsigned long long new_in_second;   uint64_t _p4[15];
+    unsigned long long failed_in_first; uint64_t _p5[15];
+    unsigned long long dump_n;          uint64_t _p6[15];
+    unsigned long long occupied;        uint64_t _p7[15];
+    unsigned long long stream_len;      uint64_t _p8[15];
+    unsigned long long bf_windows;      uint64_t _p9[15];
+};
+
+struct TableView {
+    uint64_t* buckets;      // nbuckets * BUCKET_WORDS
+    uint64_t nbuckets;
+    int W;                  // key words
+    int S;                  // slots per bucket
+};
+
+struct BloomView {
+    uint32_t* bits;         // 2 * nbits filter bits, interleaved: bit 2h = filter 1, 2h+1 = filter 2
+    uint64_t mask;          // nbits - 1
+    int nh;                 // ceil(hf): pass-1 hashes
+    int nh_gate;            // trunc(hf): pass-2 gate hashes
+};
+
+inline int words_for_k(int k) { return k / 32 + 1; }          // spare top bit for EMPTY
+inline int slots_per_bucket(int W) { return BUCKET_WORDS / (W + 1); }
+
+// ---- launchers (kc_device.hip) -------------------------------------------------
+hipError_t launch_gather(const uint8_t* src, uint8_t* stage, const ChunkDesc* d_chunks, int n_chunks,
+                         const ChunkDesc* h_chunks, hipStream_t s);
+hipError_t launch_tokenize(const uint8_t* stage, uint64_t ntiles, const ChunkDesc* d_chunks, int n_chunks,
+                           int fmt, TileInfo* tiles, TileOut* touts, uint8_t* sym, uint64_t sym_cap,
+                           DevCounters* ctr, hipStream_t s);
+// mode: 0 count all windows, 1 Bloom pass 1, 2 count windows passing the Bloom gate
+hipError_t launch_count(const uint8_t* sym, uint64_t sym_bound, int k, int mode, TableView t, BloomView bf,
+                        DevCounters* ctr, hipStream_t s);
+hipError_t launch_dump(TableView t, int count_mode, uint64_t min_abundance, uint64_t* out, DevCounters* ctr,
+                       hipStream_t s);
+hipError_t launch_synth(uint8_t* dst, uint64_t first_read, uint64_t n_reads, uint64_t seed, uint64_t genome_len,
+                        uint32_t read_len, uint32_t wrap, double err_rate, double n_rate, hipStream_t s);
+
+}  // namespace kc

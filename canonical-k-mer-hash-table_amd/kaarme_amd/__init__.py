@@ -1,0 +1,319 @@
+"""kaarme_amd -- Python host mirror of the MI355X canonical k-mer counting engine.
+
+Thin ctypes binding over ``lib/libkc.so`` (C ABI in ``include/kc_api.h``).  It mirrors
+the reference's operator interface for the hot path: the ``parse_input_*`` functors
+(``include/parallel_parser.hpp``) become :func:`count_file` / :class:`KmerCounter`,
+``hash_kmers(chunk, format)`` becomes :meth:`KmerCounter.count_chunk`, the Bloom pass
+``bloom_filter_kmers`` becomes :meth:`KmerCounter.bloom_chunk`, and the writers
+(``write_kmers_on_disk_separately_even_faster`` / ``write_kmers``) become
+:meth:`KmerCounter.write`.
+
+There is no CPU fallback: if ``libkc.so`` is missing or no HIP device is usable, the
+calls raise.  PyTorch is optional and only used by ``bench.py`` for device buffers,
+streams and ``torch.distributed``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+from typing import Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libkc.so")
+CLI_PATH = os.path.join(PKG_ROOT, "bin", "kaarme")
+GEN_PATH = os.path.join(PKG_ROOT, "bin", "kc_gen")
+
+KC_OK = 0
+ERRORS = {
+    -1: "KC_ERR_ARG",
+    -2: "KC_ERR_HIP",
+    -3: "KC_ERR_TABLE_FULL",
+    -4: "KC_ERR_STATE",
+    -5: "KC_ERR_IO",
+    -6: "KC_ERR_NOMEM",
+    -7: "KC_ERR_UNSUPPORTED",
+}
+FMT_FASTA, FMT_FASTQ, FMT_PLAIN = 0, 1, 2
+
+# Public C-ABI symbols (include/kc_api.h); tests check every one is exported.
+EXPORTS = (
+    "kc_create", "kc_destroy", "kc_last_error", "kc_bloom_chunk", "kc_bloom_finalize",
+    "kc_count_chunk", "kc_bloom_device", "kc_count_device", "kc_sync", "kc_finish", "kc_dump",
+    "kc_write", "kc_key_words", "kc_free", "kc_plan_chunks", "kc_synth_bytes", "kc_synth_device",
+    "kc_reset", "kc_profile", "kc_get_timing",
+)
+
+
+class KcError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class kc_config(ctypes.Structure):
+    _fields_ = [
+        ("k", ctypes.c_int32), ("mode", ctypes.c_int32), ("bf_enable", ctypes.c_int32),
+        ("device", ctypes.c_int32), ("table_slots", ctypes.c_uint64), ("est_unique", ctypes.c_uint64),
+        ("fpr", ctypes.c_double), ("min_abundance", ctypes.c_uint64), ("batch_bytes", ctypes.c_uint64),
+    ]
+
+
+class kc_chunk(ctypes.Structure):
+    _fields_ = [("off", ctypes.c_uint64), ("len", ctypes.c_uint64),
+                ("broken_header", ctypes.c_int32), ("pad", ctypes.c_int32)]
+
+
+class kc_timing(ctypes.Structure):
+    _fields_ = [("gather_ms", ctypes.c_double), ("tokenize_ms", ctypes.c_double), ("count_ms", ctypes.c_double),
+                ("launches", ctypes.c_uint64), ("symbols", ctypes.c_uint64)]
+
+
+class kc_stats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in (
+        "windows", "inserted", "distinct", "table_slots", "bf_windows", "bf_bits", "new_in_first",
+        "new_in_second", "failed_in_first", "chunks", "bytes")]
+
+    def as_dict(self) -> dict:
+        return {n: int(getattr(self, n)) for n, _ in self._fields_}
+
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libkc.so (raises if it is missing: there is no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise FileNotFoundError(
+            f"{path} not built; run `make -C {PKG_ROOT}` or __graft_entry__.build()")
+    lib = ctypes.CDLL(path)
+    P, U64, I32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
+    sig = {
+        "kc_create": (I32, [ctypes.POINTER(kc_config), ctypes.POINTER(P)]),
+        "kc_destroy": (None, [P]),
+        "kc_last_error": (ctypes.c_char_p, [P]),
+        "kc_bloom_chunk": (I32, [P, P, ctypes.c_size_t, I32, I32]),
+        "kc_bloom_finalize": (I32, [P, ctypes.POINTER(U64)]),
+        "kc_count_chunk": (I32, [P, P, ctypes.c_size_t, I32, I32]),
+        "kc_bloom_device": (I32, [P, P, ctypes.POINTER(kc_chunk), ctypes.c_size_t, I32, P]),
+        "kc_count_device": (I32, [P, P, ctypes.POINTER(kc_chunk), ctypes.c_size_t, I32, P]),
+        "kc_sync": (I32, [P]),
+        "kc_finish": (I32, [P, ctypes.POINTER(kc_stats)]),
+        "kc_dump": (I32, [P, ctypes.POINTER(ctypes.POINTER(U64)), ctypes.POINTER(U64)]),
+        "kc_write": (I32, [P, ctypes.c_char_p]),
+        "kc_key_words": (I32, [P]),
+        "kc_free": (None, [P]),
+        "kc_plan_chunks": (I32, [P, U64, I32, U64, I32, ctypes.POINTER(ctypes.POINTER(kc_chunk)),
+                                 ctypes.POINTER(U64)]),
+        "kc_synth_bytes": (U64, [U64, U64, ctypes.c_uint32, ctypes.c_uint32]),
+        "kc_reset": (I32, [P]),
+        "kc_profile": (I32, [P, I32]),
+        "kc_get_timing": (I32, [P, ctypes.POINTER(kc_timing)]),
+        "kc_synth_device": (I32, [P, U64, U64, U64, U64, ctypes.c_uint32, ctypes.c_uint32,
+                                  ctypes.c_double, ctypes.c_double, P]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def words_for_k(k: int) -> int:
+    return k // 32 + 1
+
+
+def detect_format(path: str, first_byte: int) -> int:
+    """file_format (main.cpp:27-68) on an uncompressed image: returns FMT_* or raises."""
+    ext = os.path.splitext(path)[1]
+    if ext in (".fasta", ".fa"):
+        ok, fmt = first_byte == ord(">"), FMT_FASTA
+    elif ext in (".fastq", ".fq"):
+        ok, fmt = first_byte == ord("@"), FMT_FASTQ
+    else:
+        ok, fmt = first_byte in b"actgACGT", FMT_PLAIN
+    if not ok:
+        raise ValueError(f"Input file {path} is ill-formed")
+    return fmt
+
+
+def plan_chunks(image: bytes, k: int, fmt: int, chunk_size: int = 0) -> List[Tuple[int, int, int]]:
+    """Reference chunk table (off, len, broken_header) of a file image."""
+    lib = load_library()
+    buf = ctypes.create_string_buffer(bytes(image), len(image)) if len(image) else None
+    out = ctypes.POINTER(kc_chunk)()
+    n = ctypes.c_uint64()
+    rc = lib.kc_plan_chunks(buf, len(image), k, chunk_size, fmt, ctypes.byref(out), ctypes.byref(n))
+    if rc:
+        raise KcError(rc, "kc_plan_chunks")
+    res = [(out[i].off, out[i].len, out[i].broken_header) for i in range(n.value)]
+    lib.kc_free(out)
+    return res
+
+
+def decode_records(records: np.ndarray, k: int) -> List[Tuple[str, int]]:
+    """(W+1)-word records -> [(kmer string, T(c))] (test helper, vectorised)."""
+    W = words_for_k(k)
+    recs = records.reshape(-1, W + 1)
+    n = recs.shape[0]
+    chars = np.empty((n, k), dtype=np.uint8)
+    lut = np.frombuffer(b"ACGT", dtype=np.uint8)
+    for j in range(k):
+        bit = 2 * (k - 1 - j)
+        word = W - 1 - bit // 64
+        chars[:, j] = lut[(recs[:, word] >> np.uint64(bit % 64)) & np.uint64(3)]
+    strs = [bytes(r).decode() for r in chars]
+    return list(zip(strs, (int(c) for c in recs[:, W])))
+
+
+@dataclass
+class Config:
+    k: int
+    mode: int = 2
+    table_slots: int = 1 << 20
+    bf_enable: bool = False
+    est_unique: int = 0
+    fpr: float = 0.01
+    min_abundance: int = 2
+    device: int = 0
+    batch_bytes: int = 0
+
+    def to_c(self) -> kc_config:
+        return kc_config(self.k, self.mode, int(self.bf_enable), self.device, self.table_slots,
+                         self.est_unique, self.fpr, self.min_abundance, self.batch_bytes)
+
+
+class KmerCounter:
+    """One device table (+ optional double Bloom filter) behind the C ABI."""
+
+    def __init__(self, cfg: Config):
+        self.lib = load_library()
+        self.cfg = cfg
+        self._ctx = ctypes.c_void_p()
+        c = cfg.to_c()
+        rc = self.lib.kc_create(ctypes.byref(c), ctypes.byref(self._ctx))
+        if rc:
+            raise KcError(rc, self.lib.kc_last_error(None).decode())
+
+    # -- lifecycle
+    def close(self):
+        if self._ctx:
+            self.lib.kc_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc: int, what: str):
+        if rc:
+            raise KcError(rc, f"{what}: {self.lib.kc_last_error(self._ctx).decode()}")
+
+    # -- passes over host chunks
+    def bloom_chunk(self, buf: bytes, fmt: int, broken_header: bool = False):
+        self._chk(self.lib.kc_bloom_chunk(self._ctx, buf, len(buf), fmt, int(broken_header)), "kc_bloom_chunk")
+
+    def bloom_finalize(self) -> int:
+        n = ctypes.c_uint64()
+        self._chk(self.lib.kc_bloom_finalize(self._ctx, ctypes.byref(n)), "kc_bloom_finalize")
+        return n.value
+
+    def count_chunk(self, buf: bytes, fmt: int, broken_header: bool = False):
+        self._chk(self.lib.kc_count_chunk(self._ctx, buf, len(buf), fmt, int(broken_header)), "kc_count_chunk")
+
+    # -- passes over a device-resident image (e.g. a torch uint8 CUDA tensor's data_ptr)
+    @staticmethod
+    def _chunk_array(chunks: Sequence[Tuple[int, int, int]]):
+        arr = (kc_chunk * max(1, len(chunks)))()
+        for i, (o, l, b) in enumerate(chunks):
+            arr[i].off, arr[i].len, arr[i].broken_header = o, l, b
+        return arr
+
+    def bloom_device(self, dev_ptr: int, chunks, fmt: int, stream: int = 0):
+        arr = self._chunk_array(chunks)
+        self._chk(self.lib.kc_bloom_device(self._ctx, ctypes.c_void_p(dev_ptr), arr, len(chunks), fmt,
+                                           ctypes.c_void_p(stream or None)), "kc_bloom_device")
+
+    def count_device(self, dev_ptr: int, chunks, fmt: int, stream: int = 0):
+        arr = self._chunk_array(chunks)
+        self._chk(self.lib.kc_count_device(self._ctx, ctypes.c_void_p(dev_ptr), arr, len(chunks), fmt,
+                                           ctypes.c_void_p(stream or None)), "kc_count_device")
+
+    def sync(self):
+        self._chk(self.lib.kc_sync(self._ctx), "kc_sync")
+
+    def reset(self):
+        self._chk(self.lib.kc_reset(self._ctx), "kc_reset")
+
+    def profile(self, enable: bool = True):
+        self._chk(self.lib.kc_profile(self._ctx, int(enable)), "kc_profile")
+
+    def timing(self) -> dict:
+        t = kc_timing()
+        self._chk(self.lib.kc_get_timing(self._ctx, ctypes.byref(t)), "kc_get_timing")
+        return {n: getattr(t, n) for n, _ in t._fields_}
+
+    def finish(self) -> dict:
+        st = kc_stats()
+        self._chk(self.lib.kc_finish(self._ctx, ctypes.byref(st)), "kc_finish")
+        return st.as_dict()
+
+    # -- results
+    def dump(self) -> np.ndarray:
+        """Records as a uint64 array of shape (n, W+1): key words then T(c)."""
+        p = ctypes.POINTER(ctypes.c_uint64)()
+        n = ctypes.c_uint64()
+        self._chk(self.lib.kc_dump(self._ctx, ctypes.byref(p), ctypes.byref(n)), "kc_dump")
+        W = self.lib.kc_key_words(self._ctx)
+        try:
+            if n.value == 0:
+                return np.zeros((0, W + 1), dtype=np.uint64)
+            arr = np.ctypeslib.as_array(p, shape=(n.value * (W + 1),)).copy()
+        finally:
+            self.lib.kc_free(p)
+        return arr.reshape(-1, W + 1)
+
+    def lines(self) -> List[str]:
+        """Sorted "<KMER> <count>" lines (what sort(kaarme output) yields)."""
+        return sorted(f"{s} {c}" for s, c in decode_records(self.dump(), self.cfg.k))
+
+    def write(self, path: str):
+        self._chk(self.lib.kc_write(self._ctx, path.encode()), "kc_write")
+
+
+def count_file(path: str, k: int, mode: int = 2, min_abundance: int = 2, table_slots: int = 1 << 20,
+               bf_enable: bool = False, est_unique: int = 0, fpr: float = 0.01, chunk_size: int = 0,
+               batch_bytes: int = 0, device: int = 0) -> Tuple[KmerCounter, dict]:
+    """The parse_input_* functor chain (main.cpp:427-543) on one device, host chunks."""
+    with open(path, "rb") as f:
+        image = f.read()
+    fmt = detect_format(path, image[0] if image else 0)
+    if fmt == FMT_FASTQ:
+        raise KcError(-7, "Input file format not supported.")
+    chunks = plan_chunks(image, k, fmt, chunk_size)
+    kc = KmerCounter(Config(k=k, mode=mode, table_slots=table_slots, bf_enable=bf_enable,
+                            est_unique=est_unique, fpr=fpr, min_abundance=min_abundance,
+                            batch_bytes=batch_bytes, device=device))
+    mv = memoryview(image)
+    if bf_enable:
+        for off, ln, bh in chunks:
+            kc.bloom_chunk(bytes(mv[off:off + ln]), fmt, bool(bh))
+        kc.bloom_finalize()
+    for off, ln, bh in chunks:
+        kc.count_chunk(bytes(mv[off:off + ln]), fmt, bool(bh))
+    stats = kc.finish()
+    return kc, stats

@@ -1,0 +1,161 @@
+/*
+ * kc_api.h -- C ABI of the MI355X canonical k-mer counting engine
+ * (canonical-k-mer-hash-table_amd/lib/libkc.so).
+ *
+ * This is the drop-in boundary for the hot path of Kaarme
+ * (Denopia/canonical-k-mer-hash-table): parallel_parser -> kmer_factory ->
+ * kmer_hash_table (+ double_bloomfilter).  The reference has no FFI; its internal
+ * seams are the per-chunk worker call hash_kmers(chunk, format)
+ * (include/parallel_parser.hpp:1302-1479), the per-k-mer table call
+ * process_kmer_MT (include/kmer_hash_table.hpp:308, source/kmer_hash_table.cpp:2207)
+ * and the writers (source/kmer_hash_table.cpp:2013-2050, 4318-4524).  Each entry
+ * point below names the reference interface it replaces.
+ *
+ * Conventions: plain pointers and sizes, no C++ or torch types.  Every call
+ * returns 0 (KC_OK) or a negative KC_ERR_*; the library never exit()s (the
+ * reference does, e.g. kmer_hash_table.cpp:2552-2556) -- kc_last_error() gives
+ * the message.  A context owns all device memory and is used by one host thread
+ * at a time.  Host buffers passed to *_chunk calls are copied before return.
+ */
+#ifndef KC_API_H
+#define KC_API_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KC_OK 0
+#define KC_ERR_ARG (-1)         /* invalid argument */
+#define KC_ERR_HIP (-2)         /* HIP runtime / device error */
+#define KC_ERR_TABLE_FULL (-3)  /* "Hash table is full" (kmer_hash_table.cpp:2552-2556) */
+#define KC_ERR_STATE (-4)       /* call out of order (e.g. count before bloom finalize) */
+#define KC_ERR_IO (-5)          /* file error */
+#define KC_ERR_NOMEM (-6)       /* host or device allocation failed */
+#define KC_ERR_UNSUPPORTED (-7) /* e.g. FASTQ input (parallel_parser.hpp:1216-1225) */
+
+/* input_mode of main.cpp:178-189 */
+#define KC_FMT_FASTA 0
+#define KC_FMT_FASTQ 1
+#define KC_FMT_PLAIN 2
+
+typedef struct kc_ctx kc_ctx;
+
+/* Replaces the CLI-derived arguments struct (main.cpp:70-99) that main() hands to
+ * the parse_input_* functors (main.cpp:468-543). */
+typedef struct {
+    int32_t k;              /* KLEN, 1..127 (the reference is wrong for k % 32 == 0) */
+    int32_t mode;           /* -m: 0 plain table (uint16 counts wrap), 1/2 kaarme (saturate at 16383) */
+    int32_t bf_enable;      /* -b: two-pass double Bloom filter prefilter */
+    int32_t device;         /* HIP device ordinal */
+    uint64_t table_slots;   /* -s: minimum hash table slots (ignored with bf_enable: 2 * new_in_second) */
+    uint64_t est_unique;    /* -u: estimated unique k-mers, sizes the Bloom filter */
+    double fpr;             /* -f: Bloom filter false positive rate (0.001..0.999) */
+    uint64_t min_abundance; /* -a: output threshold on T(c) */
+    uint64_t batch_bytes;   /* staging batch size in bytes (0 = 256 MiB) */
+} kc_config;
+
+/* One reference chunk (text_chunk, include/text_reader.h:17-36): `len` bytes at
+ * `off` of a file image, processed with `broken_header`. */
+typedef struct {
+    uint64_t off;
+    uint64_t len;
+    int32_t broken_header;
+    int32_t pad;
+} kc_chunk;
+
+typedef struct {
+    uint64_t windows;         /* k-mer windows of the counting pass */
+    uint64_t inserted;        /* windows inserted (all windows without BF; gate-passing with BF) */
+    uint64_t distinct;        /* occupied table slots ("Main array slots used", parallel_parser.hpp:1551-1562) */
+    uint64_t table_slots;     /* slot capacity of the device table */
+    uint64_t bf_windows;      /* k-mer windows of Bloom pass 1 */
+    uint64_t bf_bits;         /* bits per Bloom filter (main.cpp:402-418) */
+    uint64_t new_in_first;    /* DoubleAtomicDoubleBloomFilter counters (double_bloomfilter.hpp:233-246) */
+    uint64_t new_in_second;
+    uint64_t failed_in_first;
+    uint64_t chunks;          /* chunks processed by the counting pass */
+    uint64_t bytes;           /* input bytes processed by the counting pass */
+} kc_stats;
+
+/* Creates the device table (PointerHashTableCanonicalAV ctor,
+ * kmer_hash_table.cpp:2128-2150 / BasicAtomicFlagHashTableLong, 1992-2003) and,
+ * with bf_enable, the Bloom filter (DoubleAtomicDoubleBloomFilter ctor,
+ * double_bloomfilter.hpp:255-260 sized as main.cpp:402-431). */
+int kc_create(const kc_config* cfg, kc_ctx** out);
+void kc_destroy(kc_ctx* ctx);
+/* Message of the last failed call on ctx (or of kc_create when ctx == NULL). */
+const char* kc_last_error(const kc_ctx* ctx);
+
+/* Bloom pass 1 over one chunk: bloom_filter_kmers(chunk, format)
+ * (parallel_parser.hpp:2788-2940) -> insertion_process per k-mer. */
+int kc_bloom_chunk(kc_ctx* ctx, const uint8_t* buf, size_t len, int fmt, int broken_header);
+/* End of pass 1: main.cpp:454-461 (min_slots = 2 * new_in_second; resize()).
+ * Sizes and allocates the table. */
+int kc_bloom_finalize(kc_ctx* ctx, uint64_t* new_in_second);
+/* Counting pass over one chunk: hash_kmers(chunk, format) (parallel_parser.hpp:1302-1479)
+ * calling process_kmer_MT per window (kmer_hash_table.cpp:2207) -- behind the Bloom
+ * gate (parallel_parser.hpp:2436-2453) when bf_enable and mode != 1. */
+int kc_count_chunk(kc_ctx* ctx, const uint8_t* buf, size_t len, int fmt, int broken_header);
+
+/* The same two passes over a DEVICE-resident file image and a chunk table
+ * (kc_plan_chunks), enqueued on hip_stream (a hipStream_t, NULL = the context's
+ * stream).  The image must stay valid until the work completes (kc_sync). */
+int kc_bloom_device(kc_ctx* ctx, const uint8_t* dev_image, const kc_chunk* chunks, size_t n_chunks, int fmt,
+                    void* hip_stream);
+int kc_count_device(kc_ctx* ctx, const uint8_t* dev_image, const kc_chunk* chunks, size_t n_chunks, int fmt,
+                    void* hip_stream);
+/* Wait for all work enqueued on the context. */
+int kc_sync(kc_ctx* ctx);
+
+/* Re-initialise the table, the Bloom filter and all counters (the table/filter
+ * constructors again, without reallocating). */
+int kc_reset(kc_ctx* ctx);
+
+/* Per-kernel device time, accumulated while profiling is enabled (HIP events on
+ * the stream each kernel runs on). */
+typedef struct {
+    double gather_ms;      /* k_gather (device-image path only) */
+    double tokenize_ms;    /* k_tile_summary + k_tile_scan + k_emit */
+    double count_ms;       /* k_count (table insert / Bloom pass / gated insert) */
+    uint64_t launches;     /* batches timed */
+    uint64_t symbols;      /* symbol-stream bytes produced by the timed batches */
+} kc_timing;
+int kc_profile(kc_ctx* ctx, int enable);
+int kc_get_timing(kc_ctx* ctx, kc_timing* t);  /* waits for the timed work; resets the accumulators */
+
+/* Flush staged chunks, wait, and report counters (the timers/counters the functors
+ * print, parallel_parser.hpp:1544-1562). stats may be NULL. */
+int kc_finish(kc_ctx* ctx, kc_stats* stats);
+
+/* Records {key words[kc_key_words()], T(c)} for every k-mer with T(c) >= a, in
+ * table order; key word 0 is most significant, character j of the k-mer is bits
+ * 2(k-1-j)..2(k-1-j)+1 of the 64*W-bit integer.  T(c) = c mod 65536 for -m 0,
+ * min(c, 16383) otherwise.  Free with kc_free. */
+int kc_dump(kc_ctx* ctx, uint64_t** records, uint64_t* n_records);
+/* Writes "<CANONICAL_KMER> <T(c)>\n" lines for T(c) >= a (a == 0: nothing written):
+ * write_kmers_on_disk_separately_even_faster (kmer_hash_table.cpp:4318-4524) /
+ * write_kmers (2013-2050).  Line order is unspecified, as in the reference. */
+int kc_write(kc_ctx* ctx, const char* path);
+int kc_key_words(const kc_ctx* ctx);
+void kc_free(void* p);
+
+/* Reference chunking of a file image: io_worker (parallel_parser.hpp:1230-1299) +
+ * read_chunk_from_file (text_reader.h:93-226) with chunk_size (0 = 10 MiB,
+ * main.cpp:387).  *chunks is allocated by the library (kc_free). */
+int kc_plan_chunks(const uint8_t* image, uint64_t size, int k, uint64_t chunk_size, int fmt, kc_chunk** chunks,
+                   uint64_t* n_chunks);
+
+/* Synthetic reads (bench/test input): writes the FASTA records
+ * [first_read, first_read + n_reads) of the seeded generator to device memory
+ * dev_dst (which receives kc_synth_bytes(first_read, n_reads) bytes). */
+uint64_t kc_synth_bytes(uint64_t first_read, uint64_t n_reads, uint32_t read_len, uint32_t wrap);
+int kc_synth_device(uint8_t* dev_dst, uint64_t first_read, uint64_t n_reads, uint64_t seed, uint64_t genome_len,
+                    uint32_t read_len, uint32_t wrap, double err_rate, double n_rate, void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KC_API_H */

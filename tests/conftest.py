@@ -1,0 +1,115 @@
+"""Shared test plumbing.
+
+Markers: ``gpu`` = needs a real MI355X (runs on the GPU box via gpurun); everything
+else runs on CPU.  The oracle under oracle/ is test infrastructure: tests use it
+(and the reference binary oracle/_ref/kaarme when it was built) only as the checker.
+"""
+import hashlib
+import json
+import os
+import shutil
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "canonical-k-mer-hash-table_amd")
+GOLDEN = os.path.join(REPO, "tests", "golden")
+ORACLE_DIR = os.path.join(REPO, "oracle")
+ORACLE = os.path.join(ORACLE_DIR, "_ref", "kc_oracle")
+REF_BIN = os.path.join(ORACLE_DIR, "_ref", "kaarme")
+LIB = os.path.join(PKG, "lib", "libkc.so")
+CLI = os.path.join(PKG, "bin", "kaarme")
+GEN = os.path.join(PKG, "bin", "kc_gen")
+
+sys.path.insert(0, PKG)
+sys.path.insert(0, GOLDEN)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device)")
+    config.addinivalue_line("markers", "slow: larger inputs")
+
+
+def _ensure_built():
+    if not os.path.exists(ORACLE):
+        subprocess.run(["make", "-C", ORACLE_DIR, "oracle"], check=True, capture_output=True)
+    if not (os.path.exists(LIB) and os.path.exists(CLI) and os.path.exists(GEN)):
+        subprocess.run(["make", "-C", PKG, "-j8"], check=True, capture_output=True)
+
+
+_ensure_built()
+
+
+def load_cases():
+    with open(os.path.join(GOLDEN, "cases.json")) as f:
+        return json.load(f)
+
+
+def sha256_file(path):
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for b in iter(lambda: f.read(1 << 20), b""):
+            h.update(b)
+    return h.hexdigest()
+
+
+def sorted_digest_lines(lines):
+    """lines: iterable of str without newline -> (sha256 of sorted text, n)."""
+    data = sorted(l.encode() + b"\n" for l in lines)
+    return hashlib.sha256(b"".join(data)).hexdigest(), len(data)
+
+
+def sorted_digest_file(path):
+    if not os.path.exists(path):
+        return hashlib.sha256(b"").hexdigest(), 0
+    with open(path, "rb") as f:
+        lines = f.read().splitlines(keepends=True)
+    lines.sort()
+    return hashlib.sha256(b"".join(lines)).hexdigest(), len(lines)
+
+
+@pytest.fixture(scope="session")
+def golden_input(tmp_path_factory):
+    """Returns a function name -> path of the (re)generated, sha-checked input."""
+    meta = load_cases()["inputs"]
+    work = tmp_path_factory.mktemp("golden_inputs")
+    cache = {}
+
+    def get(name):
+        if name in cache:
+            return cache[name]
+        m = meta[name]
+        if m["commit"]:
+            path = os.path.join(GOLDEN, name)
+        else:
+            path = str(work / name)
+            if "gen" in m:
+                subprocess.run([GEN, path] + m["gen"], check=True)
+            else:
+                import make_edge
+                seed, n, hdr, seq, polya, plain = m["edge"]
+                make_edge.make(path, seed, n, hdr, seq, polya, plain)
+        assert sha256_file(path) == m["sha256"], f"fixture input {name} does not match its pinned SHA-256"
+        cache[name] = path
+        return path
+
+    return get
+
+
+def oracle_count(path, k, args, out):
+    """Run the C oracle; returns its stats line as a dict."""
+    p = subprocess.run([ORACLE, "count", path, str(k)] + list(args) + ["-o", str(out)],
+                       capture_output=True, text=True, check=True)
+    stats = {}
+    for tok in p.stdout.split():
+        if "=" in tok:
+            a, b = tok.split("=")
+            stats[a] = int(b)
+    return stats
+
+
+def strip_ref_only(args):
+    """Reference CLI args -> oracle args (the oracle ignores -s, takes the rest)."""
+    return [a for a in args]

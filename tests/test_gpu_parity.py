@@ -1,0 +1,185 @@
+"""GPU parity: the MI355X path through the C ABI against the reference fixtures and
+the oracle.  Integer work, so everything is bit-exact on sorted output.
+
+Bloom-filter runs with -a 1 are nondeterministic in the reference itself once more
+than one worker runs: for those the GPU must reproduce every
+k-mer with count >= 2 exactly and may only emit count-1 k-mers that truly occur once.
+"""
+import hashlib
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import CLI, GEN, load_cases, oracle_count, sorted_digest_file, sorted_digest_lines
+import kaarme_amd as ka
+
+pytestmark = pytest.mark.gpu
+
+CASES = load_cases()["cases"]
+
+
+def _case_id(c):
+    return f"{c['input']}-k{c['k']}-" + "".join(a.strip("-") for a in c["args"])
+
+
+def parse_ref_args(args):
+    o = {"mode": 2, "min_abundance": 2, "table_slots": 0, "bf_enable": False, "est_unique": 0, "fpr": 0.01}
+    i = 0
+    while i < len(args):
+        a = args[i]
+        if a == "-b":
+            o["bf_enable"] = True
+            i += 1
+            continue
+        v = args[i + 1]
+        key = {"-m": "mode", "-a": "min_abundance", "-s": "table_slots", "-u": "est_unique", "-f": "fpr"}[a]
+        o[key] = float(v) if key == "fpr" else int(v)
+        i += 2
+    return o
+
+
+def lines_of(kc):
+    return kc.lines()
+
+
+def bf_singleton_check(lines, path, k, mode, tmp_path):
+    """BF with -a 1: counts >= 2 exact, count-1 lines must be true singletons."""
+    full = tmp_path / "nobf.txt"
+    oracle_count(path, k, ["-m", str(mode), "-a", "1"], full)
+    truth = dict(l.rsplit(" ", 1) for l in open(full).read().splitlines())
+    got = dict(l.rsplit(" ", 1) for l in lines)
+    solid_truth = {s: c for s, c in truth.items() if int(c) >= 2}
+    solid_got = {s: c for s, c in got.items() if int(c) >= 2}
+    assert solid_got == solid_truth
+    for s, c in got.items():
+        if c == "1":
+            assert truth.get(s) == "1", s
+
+
+@pytest.mark.parametrize("case", CASES, ids=_case_id)
+def test_golden_case_host_chunks(case, golden_input, tmp_path):
+    path = golden_input(case["input"])
+    o = parse_ref_args(case["args"])
+    kc, st = ka.count_file(path, case["k"], mode=o["mode"], min_abundance=o["min_abundance"],
+                           table_slots=max(o["table_slots"], 1 << 16), bf_enable=o["bf_enable"],
+                           est_unique=o["est_unique"], fpr=o["fpr"])
+    with kc:
+        lines = lines_of(kc)
+        if o["bf_enable"] and o["min_abundance"] == 1:
+            bf_singleton_check(lines, path, case["k"], o["mode"] if o["mode"] != 1 else 2, tmp_path)
+        else:
+            assert sorted_digest_lines(lines) == (case["sorted_sha256"], case["lines"])
+        if case["distinct"] is not None and not o["bf_enable"]:
+            assert st["distinct"] == case["distinct"]
+
+
+@pytest.mark.parametrize("name,k,args", [
+    ("reads_w60.fasta", 31, ["-a", "1"]),
+    ("edge.fasta", 25, ["-m", "0", "-a", "1"]),
+    ("long.fasta", 127, ["-a", "1"]),
+    ("big_edge.fasta", 31, ["-a", "1"]),
+])
+def test_device_image_path_and_small_batches(name, k, args, golden_input, tmp_path):
+    """kc_count_device over a device-resident image with the reference chunk table,
+    with a staging batch far smaller than the input (many batches, chunk splits)."""
+    torch = pytest.importorskip("torch")
+    path = golden_input(name)
+    image = open(path, "rb").read()
+    fmt = ka.detect_format(path, image[0])
+    o = parse_ref_args(args)
+    exp = tmp_path / "exp.txt"
+    oracle_count(path, k, args, exp)
+    for chunk_size, batch in [(0, 0), (5000, 1 << 16), (100003, 1 << 20)]:
+        chunks = ka.plan_chunks(image, k, fmt, chunk_size)
+        dev = torch.frombuffer(bytearray(image), dtype=torch.uint8).cuda()
+        with ka.KmerCounter(ka.Config(k=k, mode=o["mode"], min_abundance=o["min_abundance"],
+                                      table_slots=1 << 22, batch_bytes=batch)) as kc:
+            kc.count_device(dev.data_ptr(), chunks, fmt, torch.cuda.current_stream().cuda_stream)
+            kc.finish()
+            # chunking other than the reference's 10 MiB changes nothing on these inputs
+            # except where a header is cut (then the oracle is re-run with the same chunking)
+            if chunk_size:
+                exp2 = tmp_path / f"exp_{chunk_size}.txt"
+                oracle_count(path, k, args + ["-c", str(chunk_size)], exp2)
+                want = sorted_digest_file(exp2)
+            else:
+                want = sorted_digest_file(exp)
+            assert sorted_digest_lines(kc.lines()) == want, (chunk_size, batch)
+
+
+def test_synth_device_matches_cpu_generator(tmp_path):
+    torch = pytest.importorskip("torch")
+    lib = ka.load_library()
+    for (first, n, L, w, e, nr) in [(0, 3000, 150, 0, 0.001, 0.0), (977, 1500, 151, 60, 0.01, 0.002),
+                                    (0, 20, 10000, 0, 0.001, 0.0)]:
+        nbytes = lib.kc_synth_bytes(first, n, L, w)
+        buf = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+        rc = lib.kc_synth_device(buf.data_ptr(), first, n, 42, 200000, L, w, e, nr,
+                                 torch.cuda.current_stream().cuda_stream)
+        assert rc == 0
+        torch.cuda.synchronize()
+        p = tmp_path / "c.fa"
+        subprocess.run([GEN, str(p), str(first + n), str(L), "200000", "-s", "42", "-e", str(e), "-n", str(nr),
+                        "--first", str(first), "--count", str(n)] + (["-w", str(w)] if w else []), check=True)
+        assert bytes(buf.cpu().numpy()) == open(p, "rb").read()
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c["input"] in ("reads_w60.fasta", "edge.fasta", "big_reads.fasta")
+                                  and not ("-b" in c["args"] and "1" == c["args"][c["args"].index("-a") + 1])],
+                         ids=_case_id)
+def test_cli_end_to_end(case, golden_input, tmp_path):
+    path = golden_input(case["input"])
+    out = tmp_path / "out.kaarme_counts"
+    r = subprocess.run([CLI, path, str(case["k"]), "-t", "3", "-o", str(out)] + case["args"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert sorted_digest_file(out) == (case["sorted_sha256"], case["lines"])
+    assert "Time used to build hash table" in r.stdout
+
+
+def test_cli_default_output_name(golden_input, tmp_path):
+    path = golden_input("reads.txt")
+    r = subprocess.run([CLI, path, "31", "-s", "100000", "-a", "1"], capture_output=True, text=True, cwd=tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert (tmp_path / "reads.kaarme_counts").exists()
+    r = subprocess.run([CLI, path, "31", "-s", "100000", "-a", "0", "-o", "none.txt"], capture_output=True,
+                       text=True, cwd=tmp_path)
+    assert r.returncode == 0 and not (tmp_path / "none.txt").exists()  # -a 0 writes nothing
+
+
+def test_table_full_is_an_error(golden_input):
+    path = golden_input("reads_w60.fasta")
+    with pytest.raises(ka.KcError) as e:
+        ka.count_file(path, 31, table_slots=64, min_abundance=1)
+    assert e.value.code == -3
+
+
+def test_counts_sum_to_windows_at_scale():
+    """Size-independent properties on a larger device-generated input (no N's):
+    windows == N*(L-k+1); sum of counts == windows; counting the input twice doubles
+    every count; distinct k-mers equal the dumped records at -a 1."""
+    torch = pytest.importorskip("torch")
+    lib = ka.load_library()
+    N, L, G, k = 400_000, 150, 5_000_000, 31
+    nbytes = lib.kc_synth_bytes(0, N, L, 0)
+    img = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    assert lib.kc_synth_device(img.data_ptr(), 0, N, 42, G, L, 0, 0.001, 0.0, 0) == 0
+    torch.cuda.synchronize()
+    host = bytes(img.cpu().numpy())
+    chunks = ka.plan_chunks(host, k, ka.FMT_FASTA)
+    with ka.KmerCounter(ka.Config(k=k, min_abundance=1, table_slots=30_000_000)) as kc:
+        kc.count_device(img.data_ptr(), chunks, ka.FMT_FASTA)
+        st = kc.finish()
+        assert st["windows"] == N * (L - k + 1)
+        rec = kc.dump()
+        assert rec.shape[0] == st["distinct"]
+        assert int(rec[:, -1].sum()) == st["windows"]
+        kc.count_device(img.data_ptr(), chunks, ka.FMT_FASTA)
+        kc.finish()
+        rec2 = kc.dump()
+        a = rec[np.lexsort(rec[:, :-1].T[::-1])]
+        b = rec2[np.lexsort(rec2[:, :-1].T[::-1])]
+        assert np.array_equal(a[:, :-1], b[:, :-1])
+        assert np.array_equal(2 * a[:, -1], b[:, -1])

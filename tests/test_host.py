@@ -1,0 +1,121 @@
+"""CPU: the C-ABI library loads and exports the boundary; host logic of the engine
+(reference chunking, format detection, CLI option semantics, generator sizes) --
+nothing here launches a kernel."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import CLI, GEN, LIB, ORACLE, REPO, golden_input  # noqa: F401
+import kaarme_amd as ka
+
+HEADER = os.path.join(REPO, "include", "kc_api.h")
+
+
+def declared_symbols():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(kc_[a-z_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    syms = declared_symbols()
+    assert len(syms) >= 15
+    lib = ctypes.CDLL(LIB)
+    for s in syms:
+        assert hasattr(lib, s), s
+    nm = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True, check=True).stdout
+    exported = set(l.split()[-1] for l in nm.splitlines() if l.strip())
+    assert set(syms) <= exported
+    assert set(ka.EXPORTS) == set(syms)
+
+
+def oracle_chunks(path, k, chunk):
+    out = subprocess.run([ORACLE, "chunks", path, str(k), "-c", str(chunk)], capture_output=True, text=True,
+                         check=True).stdout.split()
+    return [tuple(int(x) for x in out[i:i + 3]) for i in range(0, len(out), 3)]
+
+
+@pytest.mark.parametrize("name", ["reads_w60.fasta", "edge.fasta", "edge.txt", "long.fasta"])
+@pytest.mark.parametrize("k", [1, 2, 31, 51, 127])
+def test_plan_chunks_matches_oracle_small_chunks(name, k, golden_input):
+    """read_chunk_from_file's overlap / fake-symbol / broken_header logic at many
+    boundaries (tiny chunk sizes put boundaries inside headers and wrapped lines)."""
+    path = golden_input(name)
+    image = open(path, "rb").read()
+    fmt = ka.detect_format(path, image[0])
+    for chunk in (k + 1, 97, 1000, 4093, 65536):
+        if chunk <= k:
+            continue
+        got = ka.plan_chunks(image, k, fmt, chunk)
+        assert got == oracle_chunks(path, k, chunk), (chunk,)
+
+
+def test_plan_chunks_big_input_has_broken_headers(golden_input):
+    path = golden_input("big_edge.fasta")
+    image = open(path, "rb").read()
+    got = ka.plan_chunks(image, 31, ka.FMT_FASTA)
+    assert got == oracle_chunks(path, 31, 10 << 20)
+    assert len(got) >= 3 and any(bh for _, _, bh in got)
+
+
+def test_synth_bytes_matches_cpu_generator(tmp_path):
+    lib = ka.load_library()
+    for (n, L, w) in [(1000, 150, 0), (37, 5000, 60), (12345, 100, 0), (1, 31, 7)]:
+        p = tmp_path / "g.fa"
+        args = [GEN, str(p), str(n), str(L), str(max(L, 20000))] + (["-w", str(w)] if w else [])
+        subprocess.run(args, check=True)
+        assert lib.kc_synth_bytes(0, n, L, w) == os.path.getsize(p)
+    # a slice [first, first+count) has the bytes of its records
+    full = tmp_path / "full.fa"
+    part = tmp_path / "part.fa"
+    subprocess.run([GEN, str(full), "2000", "150", "50000"], check=True)
+    subprocess.run([GEN, str(part), "2000", "150", "50000", "--first", "990", "--count", "20"], check=True)
+    data = open(full, "rb").read()
+    off = lib.kc_synth_bytes(0, 990, 150, 0)
+    assert data[off:off + os.path.getsize(part)] == open(part, "rb").read()
+
+
+def test_detect_format():
+    assert ka.detect_format("x.fasta", ord(">")) == ka.FMT_FASTA
+    assert ka.detect_format("x.fa", ord(">")) == ka.FMT_FASTA
+    assert ka.detect_format("x.fq", ord("@")) == ka.FMT_FASTQ
+    assert ka.detect_format("x.txt", ord("a")) == ka.FMT_PLAIN
+    with pytest.raises(ValueError):
+        ka.detect_format("x.fasta", ord("A"))
+    with pytest.raises(ValueError):
+        ka.detect_format("x.txt", ord(">"))
+
+
+def run_cli(*args, cwd=None):
+    return subprocess.run([CLI] + [str(a) for a in args], capture_output=True, text=True, cwd=cwd)
+
+
+def test_cli_option_semantics(golden_input, tmp_path):
+    """CLI11 semantics of main.cpp:127-156 (exit codes = CLI11 ExitCodes)."""
+    fa = golden_input("reads_w60.fasta")
+    assert run_cli(fa, 31).returncode == 106                         # neither -s nor -u
+    assert run_cli(fa, 31, "-s", 10, "-u", 10, "-b").returncode == 106  # both
+    assert run_cli(fa, 31, "-u", 1000).returncode == 107             # -u needs -b
+    assert run_cli(fa, 31, "-s", 1000, "-b").returncode in (106, 107)  # -b needs -u
+    assert run_cli(fa, 31, "-s", 1000, "-f", 0.1).returncode == 107  # -f needs -b
+    assert run_cli(fa, 31, "-b", "-u", "4e8").returncode == 104      # integers only
+    assert run_cli(fa, 31, "-s", 1000, "-t", 2).returncode == 105    # -t in 3..64
+    assert run_cli(fa, 31, "-s", 1000, "-m", 3).returncode == 105    # -m in 0..2
+    assert run_cli(fa, 0, "-s", 1000).returncode == 105              # KLEN > 0
+    assert run_cli(tmp_path / "missing.fa", 31, "-s", 1000).returncode == 105
+    assert run_cli(fa).returncode == 106
+    assert run_cli("-h").returncode == 0
+
+
+def test_cli_format_checks(tmp_path):
+    bad = tmp_path / "bad.fasta"
+    bad.write_bytes(b"ACGT\n")
+    r = run_cli(bad, 5, "-s", 100)
+    assert r.returncode == 1 and "ill-formed" in r.stderr
+    fq = tmp_path / "r.fq"
+    fq.write_bytes(b"@r1\nACGT\n+\nIIII\n")
+    r = run_cli(fq, 3, "-s", 100, "-o", tmp_path / "out.txt")
+    assert r.returncode == 0 and "Input file format not supported." in r.stdout
+    assert not (tmp_path / "out.txt").exists()
