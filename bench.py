@@ -41,7 +41,7 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(args, slots_per_read):
+def cpu_baseline(args):
     """Time the reference CLI (or, if it was not built, the C oracle) on a bounded sample."""
     ref = os.path.join(REPO, "oracle", "_ref", "kaarme")
     orc = os.path.join(REPO, "oracle", "_ref", "kc_oracle")
@@ -52,7 +52,9 @@ def cpu_baseline(args, slots_per_read):
     if kind is None:
         return None
     n = args.cpu_sample_reads if kind == "reference" else max(1, args.cpu_sample_reads // 20)
-    threads = max(3, min(args.cpu_threads, os.cpu_count() or 3, 64))
+    # the box gives this job a 16-core share (nproc); t-2 workers + 1 IO thread
+    ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 3)
+    threads = max(3, min(args.cpu_threads or ncpu + 1, 64))
     with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
         fa = os.path.join(td, "sample.fasta")
         subprocess.run([gen, fa, str(n), str(args.read_len), str(args.genome), "-s", str(args.seed),
@@ -61,7 +63,7 @@ def cpu_baseline(args, slots_per_read):
             while f.read(1 << 24):
                 pass
         windows = n * (args.read_len - args.k + 1)
-        slots = max(1000, int(slots_per_read * n))
+        slots = args.slots  # the sample's distinct k-mers approach the genome size: keep C2's -s
         if kind == "reference":
             cmd = [ref, fa, str(args.k), "-m", "2", "-s", str(slots), "-t", str(threads), "-a", "0"]
             p = subprocess.run(cmd, capture_output=True, text=True, timeout=1800)
@@ -107,7 +109,7 @@ def main():
     ap.add_argument("--err", type=float, default=0.001)
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--cpu-sample-reads", type=int, default=2_000_000)
-    ap.add_argument("--cpu-threads", type=int, default=18)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="-t of the reference (0 = cores + 1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -215,7 +217,7 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args, args.slots / N)
+        out["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

@@ -91,6 +91,16 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     if not os.path.exists(path):
         raise FileNotFoundError(
             f"{path} not built; run `make -C {PKG_ROOT}` or __graft_entry__.build()")
+    # PyTorch-ROCm wheels ship their own libamdhip64.so.7.  If torch is around, load
+    # it first so that libkc.so binds to that same runtime (one HIP runtime per
+    # process; device pointers and streams are then shared with torch).  Without
+    # torch, libkc.so uses /opt/rocm's runtime through its RUNPATH.
+    try:
+        import torch  # noqa: F401
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except ImportError:
+        pass
     lib = ctypes.CDLL(path)
     P, U64, I32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
     sig = {
