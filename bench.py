@@ -52,9 +52,11 @@ def cpu_baseline(args):
     if kind is None:
         return None
     n = args.cpu_sample_reads if kind == "reference" else max(1, args.cpu_sample_reads // 20)
-    # the box gives this job a 16-core share (nproc); t-2 workers + 1 IO thread
-    ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 3)
-    threads = max(3, min(args.cpu_threads or ncpu + 1, 64))
+    # The box gives one GPU's job a 16-core share of a larger host (OMP_NUM_THREADS is set to
+    # it; the affinity mask still lists every CPU).  -t = share + 2: share hashing workers plus
+    # the IO thread (main.cpp:383).
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    threads = max(3, min(args.cpu_threads or share + 2, 64))
     with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
         fa = os.path.join(td, "sample.fasta")
         subprocess.run([gen, fa, str(n), str(args.read_len), str(args.genome), "-s", str(args.seed),
@@ -72,7 +74,7 @@ def cpu_baseline(args):
                 log("cpu baseline failed:", p.stdout[-500:], p.stderr[-500:])
                 return None
             secs = int(m.group(1)) / 1e6
-            cores = threads - 1  # t-2 hashing workers + 1 IO thread (main.cpp:383)
+            cores = threads - 2  # t-2 hashing workers (+ 1 mostly idle IO thread, main.cpp:383)
         else:
             t0 = time.perf_counter()
             subprocess.run([orc, "count", fa, str(args.k), "-a", "0"], check=True, capture_output=True)
@@ -108,8 +110,8 @@ def main():
     ap.add_argument("--slots", type=int, default=200_000_000, help="-s per GPU (C2: 200000000)")
     ap.add_argument("--err", type=float, default=0.001)
     ap.add_argument("--seed", type=int, default=42)
-    ap.add_argument("--cpu-sample-reads", type=int, default=2_000_000)
-    ap.add_argument("--cpu-threads", type=int, default=0, help="-t of the reference (0 = cores + 1)")
+    ap.add_argument("--cpu-sample-reads", type=int, default=1_000_000)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="-t of the reference (0 = core share + 2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 

@@ -65,6 +65,13 @@ struct kc_ctx {
     // table
     uint64_t* d_table = nullptr;
     uint64_t nbuckets = 0;
+    uint64_t R = 0;
+    uint32_t F1 = 1, F2 = 1;
+
+    // partitioned insert buffers
+    PartBufs pb{};
+    uint32_t pb_nblk1_cap = 0;
+    uint64_t pb_key_cap = 0;
 
     // bloom
     uint32_t* d_bloom = nullptr;
@@ -127,15 +134,86 @@ static void bloom_sizes(uint64_t U, double fpr, uint64_t* bits, int* nh, int* nh
 
 static int alloc_table(kc_ctx* c, uint64_t min_slots) {
     // Kaarme's table holds exactly next_prime3mod4(min_slots) slots and dies when
-    // full; open addressing on the GPU keeps 25 % headroom over that.
+    // full; open addressing on the GPU keeps 25 % headroom over that.  The table is
+    // R = F1 * F2 regions of BPR 128-byte buckets (a region = one LDS-resident table).
     uint64_t want = std::max<uint64_t>(min_slots, 64);
     want = want + want / 4;
-    c->nbuckets = (want + c->S - 1) / c->S;
+    const uint64_t buckets = (want + c->S - 1) / c->S;
+    const uint64_t regions = std::max<uint64_t>(1, (buckets + BPR - 1) / BPR);
+    uint64_t f1 = 1;
+    while (f1 * f1 < regions && f1 < 1024) f1 *= 2;  // F1 ~ sqrt(R), a power of two
+    f1 = std::min<uint64_t>(f1, regions);
+    const uint64_t f2 = (regions + f1 - 1) / f1;
+    c->F1 = (uint32_t)f1;
+    c->F2 = (uint32_t)f2;
+    c->R = f1 * f2;
+    c->nbuckets = c->R * BPR;
     const size_t bytes = c->nbuckets * BUCKET_WORDS * sizeof(uint64_t);
     hipError_t e = hipMalloc(&c->d_table, bytes);
     if (e != hipSuccess) return c->fail(KC_ERR_NOMEM, "table allocation failed (" + std::to_string(bytes) + " bytes)");
     HIPCHK(c, hipMemsetAsync(c->d_table, 0, bytes, c->stream));
     return KC_OK;
+}
+
+static TableView table_view(const kc_ctx* c) {
+    TableView tv;
+    tv.buckets = c->d_table;
+    tv.nbuckets = c->nbuckets;
+    tv.R = c->R;
+    tv.F1 = c->F1;
+    tv.F2 = c->F2;
+    tv.W = c->W;
+    tv.S = c->S;
+    return tv;
+}
+
+// Partition buffers for a batch of up to `syms` symbols (lazily grown).
+static int ensure_part(kc_ctx* c, uint64_t syms) {
+    const uint64_t tile = (uint64_t)COUNT_THREADS * run_width(c->W);
+    const uint32_t nblk1 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(2048, (syms + tile - 1) / tile));
+    const uint32_t B2 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(64, 2048 / c->F1));
+    if (!c->pb.hist1 || nblk1 > c->pb_nblk1_cap) {
+        hipFree(c->pb.hist1);
+        hipFree(c->pb.off1);
+        c->pb.hist1 = nullptr;
+        c->pb.off1 = nullptr;
+        const uint32_t cap = 2048;
+        if (hipMalloc(&c->pb.hist1, (size_t)c->F1 * cap * 4) != hipSuccess ||
+            hipMalloc(&c->pb.off1, ((size_t)c->F1 * cap + 1) * 8) != hipSuccess)
+            return c->fail(KC_ERR_NOMEM, "partition histogram allocation failed");
+        c->pb_nblk1_cap = cap;
+    }
+    if (!c->pb.hist2) {
+        if (hipMalloc(&c->pb.hist2, (size_t)c->R * B2 * 4) != hipSuccess ||
+            hipMalloc(&c->pb.off2, ((size_t)c->R * B2 + 1) * 8) != hipSuccess)
+            return c->fail(KC_ERR_NOMEM, "partition histogram allocation failed");
+    }
+    if (syms > c->pb_key_cap) {
+        hipFree(c->pb.keys1);
+        hipFree(c->pb.keys2);
+        c->pb.keys1 = c->pb.keys2 = nullptr;
+        const size_t bytes = (size_t)syms * c->W * 8;
+        if (hipMalloc(&c->pb.keys1, bytes) != hipSuccess || hipMalloc(&c->pb.keys2, bytes) != hipSuccess) {
+            c->pb_key_cap = 0;
+            return c->fail(KC_ERR_NOMEM, "partition key buffers allocation failed (" + std::to_string(2 * bytes) +
+                                             " bytes)");
+        }
+        c->pb_key_cap = syms;
+    }
+    c->pb.nblk1 = nblk1;
+    c->pb.B2 = B2;
+    return KC_OK;
+}
+
+// Insert path per batch: the partitioned pipeline moves ~(4W+1)*8 bytes per window
+// plus two sweeps of the table; the direct path is bound by scattered device atomics
+// (~20 G/s on MI355X, i.e. ~275 bytes-equivalent per window at ~5.5 TB/s).
+static bool use_partitioned(const kc_ctx* c, uint64_t syms) {
+    const char* env = std::getenv("KC_INSERT_PATH");
+    if (env && !std::strcmp(env, "direct")) return false;
+    if (env && !std::strcmp(env, "partitioned")) return true;
+    const double table_bytes = (double)c->nbuckets * 128.0;
+    return (double)syms * 275.0 > (double)syms * (4.0 * c->W + 1) * 8.0 + 2.0 * table_bytes;
 }
 
 static hipStream_t pick_stream(kc_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
@@ -161,12 +239,19 @@ static int run_batch(kc_ctx* c, uint64_t used, uint64_t nchunks, int fmt, int pa
     HIPCHK(c, launch_tokenize(c->d_stage, ntiles, c->d_chunks, (int)nchunks, fmt, c->d_tiles, c->d_touts, c->d_sym,
                               c->batch_bytes + c->max_chunks, c->d_ctr, s));
     if (c->profiling) HIPCHK(c, hipEventRecord(ev[2], s));
-    TableView tv{c->d_table, c->nbuckets, c->W, c->S};
+    TableView tv = table_view(c);
     BloomView bv{c->d_bloom, c->bf_bits ? c->bf_bits - 1 : 0, c->nh, c->nh_gate};
     int mode;
     if (pass == 1) mode = 1;
     else mode = (c->cfg.bf_enable && c->cfg.mode != 1) ? 2 : 0;  // -m 1 -b ignores the filter (main.cpp:482-489)
-    HIPCHK(c, launch_count(c->d_sym, used + nchunks, c->cfg.k, mode, tv, bv, c->d_ctr, s));
+    const uint64_t syms = used + nchunks;
+    if (mode != 1 && use_partitioned(c, syms)) {
+        int rc = ensure_part(c, syms);
+        if (rc) return rc;
+        HIPCHK(c, launch_count_partitioned(c->d_sym, syms, c->cfg.k, mode, tv, bv, c->d_ctr, c->pb, s));
+    } else {
+        HIPCHK(c, launch_count(c->d_sym, syms, c->cfg.k, mode, tv, bv, c->d_ctr, s));
+    }
     if (c->profiling) {
         HIPCHK(c, hipEventRecord(ev[3], s));
         c->ev_pending.push_back(ev);
@@ -361,6 +446,12 @@ void kc_destroy(kc_ctx* c) {
     hipFree(c->d_ctr);
     hipFree(c->d_table);
     hipFree(c->d_bloom);
+    hipFree(c->pb.hist1);
+    hipFree(c->pb.off1);
+    hipFree(c->pb.hist2);
+    hipFree(c->pb.off2);
+    hipFree(c->pb.keys1);
+    hipFree(c->pb.keys2);
     if (c->xev) hipEventDestroy(c->xev);
     for (auto e : c->ev_pool) hipEventDestroy(e);
     for (auto& ev : c->ev_pending)
@@ -438,7 +529,7 @@ int kc_finish(kc_ctx* c, kc_stats* st) {
         if (c->d_table) {
             HIPCHK(c, hipMemsetAsync(&c->d_ctr->occupied, 0, 8, c->stream));
             HIPCHK(c, hipMemsetAsync(&c->d_ctr->dump_n, 0, 8, c->stream));
-            TableView tv{c->d_table, c->nbuckets, c->W, c->S};
+            TableView tv = table_view(c);
             HIPCHK(c, launch_dump(tv, c->cfg.mode == 0 ? 0 : 1, ~0ULL, nullptr, c->d_ctr, c->stream));
             unsigned long long occ = 0;
             HIPCHK(c, hipMemcpyAsync(&occ, &c->d_ctr->occupied, 8, hipMemcpyDeviceToHost, c->stream));
@@ -461,6 +552,10 @@ int kc_reset(kc_ctx* c) {
         HIPCHK(c, hipMemsetAsync(c->d_bloom, 0, words * 4, c->stream));
         if (c->bloom_final) {  // back to the Bloom pass: the table is sized again after it
             hipFree(c->d_table);
+            hipFree(c->pb.hist2);
+            hipFree(c->pb.off2);
+            c->pb.hist2 = nullptr;
+            c->pb.off2 = nullptr;
             c->d_table = nullptr;
             c->nbuckets = 0;
             c->bloom_final = false;
@@ -512,7 +607,7 @@ int kc_dump(kc_ctx* c, uint64_t** records, uint64_t* n_records) {
     int rc = kc_sync(c);
     if (rc) return rc;
     if (!c->d_table) return c->fail(KC_ERR_STATE, "no table");
-    TableView tv{c->d_table, c->nbuckets, c->W, c->S};
+    TableView tv = table_view(c);
     const int cm = c->cfg.mode == 0 ? 0 : 1;
     const uint64_t a = c->cfg.min_abundance;
     HIPCHK(c, hipMemsetAsync(&c->d_ctr->dump_n, 0, 16 * 8 * 2, c->stream));  // dump_n + occupied lines

@@ -1,0 +1,181 @@
+// kc_common.h -- device helpers shared by the tokenizer (kc_tokenize.hip) and the
+// counting kernels (kc_count.hip): symbol codes, hashing, wave scans, the 2-bit
+// canonical window roller, XXH64 and the table geometry.
+#pragma once
+#include "kc_internal.h"
+
+namespace kc {
+
+#define DEV __device__ __forceinline__
+
+DEV uint8_t char_code(uint8_t c) {  // functions_strings.cpp:56-70
+    switch (c) {
+    case 'A': case 'a': return 0;
+    case 'C': case 'c': return 1;
+    case 'G': case 'g': return 2;
+    case 'T': case 't': return 3;
+    default: return SYM_BREAK;
+    }
+}
+
+DEV uint64_t fmix64(uint64_t k) {
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdULL;
+    k ^= k >> 33;
+    k *= 0xc4ceb9fe1a85ec53ULL;
+    k ^= k >> 33;
+    return k;
+}
+
+// 64-bit hash of a canonical key (word 0 most significant)
+template <int W>
+DEV uint64_t key_hash(const uint64_t (&key)[W]) {
+    uint64_t h = fmix64(key[W - 1] ^ 0x243f6a8885a308d3ULL);
+#pragma unroll
+    for (int i = W - 2; i >= 0; i--) h = fmix64(h ^ key[i]);
+    return h;
+}
+// hash-prefix owner of a key among `parts` shards: independent of the table's bits
+DEV uint32_t owner_of(uint64_t h, uint32_t parts) {
+    return (uint32_t)__umul64hi(fmix64(h ^ 0x13198a2e03707344ULL), parts);
+}
+
+// ---- table geometry -------------------------------------------------------------
+// region = mulhi(h, R); bucket inside the region = mulhi(h * R, BPR); linear probing
+// wraps inside the region, so a region is an independent table that fits in LDS.
+DEV uint64_t region_of(uint64_t h, uint64_t R) { return __umul64hi(h, R); }
+DEV uint32_t bucket_in_region(uint64_t h, uint64_t R) { return (uint32_t)__umul64hi(h * R, (uint64_t)BPR); }
+
+// wave-level inclusive scans (64 lanes)
+DEV uint32_t wave_incl_sum(uint32_t v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t o = __shfl_up(v, d, 64);
+        if (lane >= d) v += o;
+    }
+    return v;
+}
+DEV uint32_t wave_incl_last(uint32_t v) {  // last non-zero value up to this lane
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t o = __shfl_up(v, d, 64);
+        if (lane >= d && v == 0) v = o;
+    }
+    return v;
+}
+
+// ---- XXH64 of one 8-byte value (xxhash.h:3368-3509 / doc/xxhash_spec.md:191-334) ----
+DEV uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+DEV uint64_t xxh64_u64(uint64_t v, uint64_t seed) {
+    const uint64_t P1 = 0x9E3779B185EBCA87ULL, P2 = 0xC2B2AE3D27D4EB4FULL, P3 = 0x165667B19E3779F9ULL,
+                   P4 = 0x85EBCA77C2B2AE63ULL, P5 = 0x27D4EB2F165667C5ULL;
+    uint64_t h = seed + P5 + 8;
+    uint64_t k1 = rotl64(v * P2, 31) * P1;
+    h ^= k1;
+    h = rotl64(h, 27) * P1 + P4;
+    h ^= h >> 33;
+    h *= P2;
+    h ^= h >> 29;
+    h *= P3;
+    h ^= h >> 32;
+    return h;
+}
+
+DEV uint64_t atomic_load_agent(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+DEV void atomic_store_agent(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---- canonical window roller ------------------------------------------------------
+// KMerFactoryCanonical2BC::push_new_integer (kmer_factory.cpp:172-239): forward word
+// grows at the low end, reverse complement at the top; canonical = min as a 2k-bit
+// integer.  With a Bloom filter the Rabin-Karp pair mod 2^54 of RollingHasherDual
+// (hash_functions.cpp:102-192) is rolled alongside and root = min(F, B).
+constexpr uint64_t M54 = (1ULL << 54) - 1;
+constexpr uint64_t INV5_54 = 0xCCCCCCCCCCCCDULL;  // 5 * INV5_54 == 1 (mod 2^54)
+
+struct RollConst {
+    int k;
+    int top;          // bits of the k-mer held by word 0
+    int rc_word;      // word and bit of the oldest character (2k-2)
+    int rc_bit;
+    uint64_t topmask;
+    uint64_t pow5_k, pow5_km1;
+};
+
+template <int W>
+DEV RollConst make_roll(int k, uint64_t pk, uint64_t pkm1) {
+    RollConst r;
+    r.k = k;
+    r.top = 2 * k - 64 * (W - 1);
+    r.topmask = r.top >= 64 ? ~0ULL : ((1ULL << r.top) - 1);
+    r.rc_word = W - 1 - (2 * k - 2) / 64;
+    r.rc_bit = (2 * k - 2) % 64;
+    r.pow5_k = pk;
+    r.pow5_km1 = pkm1;
+    return r;
+}
+
+// Rolls sym[pstart, pend) and calls f(fwd, rc, root) for every complete window whose
+// last symbol is at p >= p0.  ROOT: also roll the mod-2^54 pair (Bloom modes).
+template <int W, bool ROOT, class F>
+DEV void roll_run(const uint8_t* __restrict__ sym, uint64_t pstart, uint64_t p0, uint64_t pend,
+                  const RollConst& rk, F&& f) {
+    uint64_t fwd[W], rc[W];
+#pragma unroll
+    for (int i = 0; i < W; i++) { fwd[i] = 0; rc[i] = 0; }
+    int fill = 0;
+    uint64_t Fh = 0, Bh = 0, p5 = 1;
+    for (uint64_t p = pstart; p < pend; p++) {
+        const uint8_t c = sym[p];
+        if (c > 3) {
+            fill = 0;
+#pragma unroll
+            for (int i = 0; i < W; i++) { fwd[i] = 0; rc[i] = 0; }
+            if constexpr (ROOT) { Fh = 0; Bh = 0; p5 = 1; }
+            continue;
+        }
+        if constexpr (ROOT) {
+            if (fill < rk.k) {
+                Fh = (Fh * 5 + c) & M54;
+                Bh = (Bh + (uint64_t)(3 - c) * p5) & M54;
+                p5 = (p5 * 5) & M54;
+            } else {
+                uint64_t out = 0;
+#pragma unroll
+                for (int i = 0; i < W; i++)
+                    if (i == rk.rc_word) out = (fwd[i] >> rk.rc_bit) & 3;
+                Fh = (Fh * 5 + c - rk.pow5_k * out) & M54;
+                Bh = (((Bh - (3 - out)) & M54) * INV5_54 + (uint64_t)(3 - c) * rk.pow5_km1) & M54;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < W - 1; i++) fwd[i] = (fwd[i] << 2) | (fwd[i + 1] >> 62);
+        fwd[W - 1] = (fwd[W - 1] << 2) | c;
+        fwd[0] &= rk.topmask;
+#pragma unroll
+        for (int i = W - 1; i >= 1; i--) rc[i] = (rc[i] >> 2) | (rc[i - 1] << 62);
+        rc[0] >>= 2;
+#pragma unroll
+        for (int i = 0; i < W; i++)
+            if (i == rk.rc_word) rc[i] |= (uint64_t)(3 - c) << rk.rc_bit;
+        if (fill < rk.k) fill++;
+        if (fill == rk.k && p >= p0) f(fwd, rc, Fh < Bh ? Fh : Bh);
+    }
+}
+
+template <int W>
+DEV void canonical(const uint64_t (&fwd)[W], const uint64_t (&rc)[W], uint64_t (&key)[W]) {
+    bool fwd_le = true;
+#pragma unroll
+    for (int i = W - 1; i >= 0; i--)
+        if (fwd[i] != rc[i]) fwd_le = fwd[i] < rc[i];
+#pragma unroll
+    for (int i = 0; i < W; i++) key[i] = fwd_le ? fwd[i] : rc[i];
+}
+
+}  // namespace kc

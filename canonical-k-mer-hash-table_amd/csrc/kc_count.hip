@@ -1,0 +1,670 @@
+// kc_count.hip -- canonical k-mer insertion, Bloom passes and the table dump.
+//
+// The reference inserts every window with process_kmer_MT (kmer_hash_table.cpp:
+// 2207-2567): a CAS-probed table shared by all threads.  Two MI355X paths produce the
+// same table contents:
+//
+//  direct       k_count<W,MODE>: roll windows, canonicalise, CAS-claim / atomic-add
+//               in HBM.  One scattered device-scope atomic per window, so it runs at
+//               the chip's scattered-atomic rate (~20 G/s measured); used for small
+//               batches and for Bloom pass 1 (bit-array atomics).
+//  partitioned  keys are moved to where they are counted instead:
+//               p1  windows -> F1 coarse bins (hash prefix), LDS counting sort per tile
+//                   so every bin is written as a contiguous run;
+//               p2  each coarse bin -> its F2 regions, same scheme;
+//               p3  one workgroup per region: load the region's 64 KiB of buckets into
+//                   LDS, insert its keys with LDS atomics, write the region back.
+//               Bandwidth-bound (~(4W+1)*8 bytes of key traffic per window plus two
+//               table sweeps) instead of atomic-bound.
+//
+// Table layout (both paths): 128-byte buckets, keys [S][W] u64 then counts [S] u64,
+// S = 16/(W+1).  Word 0 of a stored key carries OCC (bit 63), so 0 is EMPTY.  A key
+// lives in region mulhi(h,R); its probe sequence starts at bucket mulhi(h*R, BPR) of
+// the region and wraps inside it.  W > 1 keys: word 0 claimed by CAS, other words
+// stored, then READY|1 added to the count word; readers matching word 0 wait for READY.
+#include "kc_common.h"
+
+namespace kc {
+
+__constant__ uint64_t c_bf_seeds[MAX_NH] = {2411, 3253, 1061, 1129, 2269, 7309, 3491, 8237, 6359, 8779};
+
+// --------------------------------------------------------------------------------
+// direct insert into the HBM table
+// --------------------------------------------------------------------------------
+template <int W>
+DEV bool table_insert(const TableView& tv, const uint64_t (&key)[W], uint64_t h) {
+    constexpr int S = BUCKET_WORDS / (W + 1);
+    const uint64_t region = region_of(h, tv.R);
+    uint32_t b = bucket_in_region(h, tv.R);
+    const uint64_t k0 = key[0] | OCC;
+    for (int probe = 0; probe < BPR; probe++) {
+        uint64_t* bk = tv.buckets + (region * BPR + b) * BUCKET_WORDS;
+        uint64_t w0[S];
+        if constexpr (W == 1) {
+            const uint4* b4 = reinterpret_cast<const uint4*>(bk);
+#pragma unroll
+            for (int q = 0; q < S / 2; q++) {
+                uint4 v = b4[q];
+                w0[2 * q] = ((uint64_t)v.y << 32) | v.x;
+                w0[2 * q + 1] = ((uint64_t)v.w << 32) | v.z;
+            }
+        } else {
+#pragma unroll
+            for (int s = 0; s < S; s++) w0[s] = bk[s * W];
+        }
+        int s = 0;
+        while (s < S) {
+            uint64_t* kp = bk + s * W;
+            uint64_t* cp = bk + S * W + s;
+            uint64_t v0 = w0[s];
+            if (v0 == EMPTY) {
+                const uint64_t old = atomicCAS((unsigned long long*)kp, (unsigned long long)EMPTY,
+                                               (unsigned long long)k0);
+                if (old == EMPTY) {
+                    if constexpr (W == 1) {
+                        atomicAdd((unsigned long long*)cp, 1ULL);
+                    } else {
+#pragma unroll
+                        for (int i = 1; i < W; i++) atomic_store_agent(kp + i, key[i]);
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // words land before READY
+                        atomicAdd((unsigned long long*)cp, (unsigned long long)(READY + 1));
+                    }
+                    return true;
+                }
+                v0 = old;
+                w0[s] = old;
+            }
+            if (v0 == k0) {
+                if constexpr (W == 1) {
+                    atomicAdd((unsigned long long*)cp, 1ULL);
+                    return true;
+                } else {
+                    const uint64_t c = atomic_load_agent(cp);
+                    if (!(c & READY)) continue;  // claimed, not yet published: retry this slot
+                    asm volatile("" ::: "memory");
+                    bool eq = true;
+#pragma unroll
+                    for (int i = 1; i < W; i++) eq &= atomic_load_agent(kp + i) == key[i];
+                    if (eq) {
+                        atomicAdd((unsigned long long*)cp, 1ULL);
+                        return true;
+                    }
+                }
+            }
+            s++;
+        }
+        b = b + 1 == BPR ? 0 : b + 1;
+    }
+    return false;  // region full
+}
+
+// --------------------------------------------------------------------------------
+// Bloom filter: both filters interleaved in one bit array (filter-1 bit of h = 2h,
+// filter-2 bit = 2h+1, the MyAtomicBitArrayFT layout, mybitarray.hpp:30-125)
+// --------------------------------------------------------------------------------
+struct BloomLocal {
+    uint32_t new_first, new_second, failed;
+};
+
+// insertion_process (double_bloomfilter.hpp:371-413); a "set" counts as ours only if
+// our atomicOr flipped the bit (MyAtomicBitArrayFT::set, mybitarray.hpp:87-125)
+DEV void bloom_insert(const BloomView& bf, uint64_t root, BloomLocal& loc) {
+    uint64_t widx[MAX_NH];
+    uint32_t bpos[MAX_NH];
+    uint32_t view[MAX_NH];
+    int s1 = 0, s2 = 0;
+#pragma unroll
+    for (int j = 0; j < MAX_NH; j++) {
+        if (j < bf.nh) {
+            const uint64_t hv = xxh64_u64(root, c_bf_seeds[j]) & bf.mask;
+            const uint64_t bit = 2 * hv;
+            widx[j] = bit >> 5;
+            bpos[j] = (uint32_t)(bit & 31);
+            view[j] = bf.bits[widx[j]];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < MAX_NH; j++)
+        if (j < bf.nh) {
+            s1 += (view[j] >> bpos[j]) & 1;
+            s2 += (view[j] >> (bpos[j] + 1)) & 1;
+        }
+    if (s2 == bf.nh) return;
+    bool to_second;
+    if (s1 == bf.nh) {
+        to_second = true;
+    } else {
+        int mine = 0;
+#pragma unroll
+        for (int j = 0; j < MAX_NH; j++)
+            if (j < bf.nh) {
+                const uint32_t m = 1u << bpos[j];
+                if (!(view[j] & m)) {
+                    const uint32_t old = atomicOr(bf.bits + widx[j], m);
+                    if (!(old & m)) mine++;
+                    view[j] = old | m;
+                }
+            }
+        if (mine == bf.nh - s1) { loc.new_first++; to_second = false; }
+        else { loc.failed++; to_second = true; }
+    }
+    if (to_second) {
+        int mine = 0;
+#pragma unroll
+        for (int j = 0; j < MAX_NH; j++)
+            if (j < bf.nh) {
+                const uint32_t m = 2u << bpos[j];
+                if (!(view[j] & m)) {
+                    const uint32_t old = atomicOr(bf.bits + widx[j], m);
+                    if (!(old & m)) mine++;
+                }
+            }
+        if (mine == bf.nh - s2) loc.new_second++;
+    }
+}
+
+// pass-2 gate: all of the first trunc(hf) filter-2 bits set (parallel_parser.hpp:2436-2441)
+DEV bool bloom_gate(const BloomView& bf, uint64_t root) {
+    bool all = true;
+#pragma unroll
+    for (int j = 0; j < MAX_NH; j++)
+        if (j < bf.nh_gate) {
+            const uint64_t bit = 2 * (xxh64_u64(root, c_bf_seeds[j]) & bf.mask) + 1;
+            all &= (bf.bits[bit >> 5] >> (bit & 31)) & 1;
+        }
+    return all;
+}
+
+// block reduction of up to 4 counters, one atomic each per block
+DEV void block_add4(unsigned long long v0, unsigned long long v1, unsigned long long v2, unsigned long long v3,
+                    unsigned long long* d0, unsigned long long* d1, unsigned long long* d2,
+                    unsigned long long* d3) {
+    __shared__ unsigned long long s_red[4][4];
+    unsigned long long v[4] = {v0, v1, v2, v3};
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        unsigned long long x = v[q];
+        for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+        if (lane == 0) s_red[q][wid] = x;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        unsigned long long x = 0;
+        for (int w = 0; w < (int)(blockDim.x / 64); w++) x += s_red[threadIdx.x][w];
+        unsigned long long* dst = threadIdx.x == 0 ? d0 : threadIdx.x == 1 ? d1 : threadIdx.x == 2 ? d2 : d3;
+        if (x && dst) atomicAdd(dst, x);
+    }
+}
+
+// --------------------------------------------------------------------------------
+// k_count<W, MODE>: direct path. MODE 0 count, 1 Bloom pass 1, 2 count behind the gate
+// --------------------------------------------------------------------------------
+template <int W, int MODE>
+__global__ __launch_bounds__(COUNT_THREADS) void k_count(const uint8_t* __restrict__ sym, int k, TableView tv,
+                                                         BloomView bf, DevCounters* __restrict__ ctr,
+                                                         uint64_t pow5_k, uint64_t pow5_km1) {
+    const uint64_t M = ctr->stream_len;
+    const uint64_t p0 = ((uint64_t)blockIdx.x * COUNT_THREADS + threadIdx.x) * RUN;
+    uint32_t n_win = 0, n_ins = 0, n_fail = 0;
+    BloomLocal bl = {0, 0, 0};
+    if (p0 < M) {
+        const RollConst rk = make_roll<W>(k, pow5_k, pow5_km1);
+        const uint64_t pstart = p0 >= (uint64_t)(k - 1) ? p0 - (k - 1) : 0;
+        roll_run<W, MODE != 0>(sym, pstart, p0, min(p0 + RUN, M), rk,
+                               [&](const uint64_t (&fwd)[W], const uint64_t (&rc)[W], uint64_t root) {
+            n_win++;
+            if constexpr (MODE == 1) {
+                bloom_insert(bf, root, bl);
+            } else {
+                if constexpr (MODE == 2) {
+                    if (!bloom_gate(bf, root)) return;
+                }
+                uint64_t key[W];
+                canonical<W>(fwd, rc, key);
+                n_ins++;
+                if (!table_insert<W>(tv, key, key_hash<W>(key))) n_fail++;
+            }
+        });
+    }
+    if constexpr (MODE == 1)
+        block_add4(n_win, bl.new_first, bl.new_second, bl.failed, &ctr->bf_windows, &ctr->new_in_first,
+                   &ctr->new_in_second, &ctr->failed_in_first);
+    else
+        block_add4(n_win, n_ins, n_fail, 0, &ctr->windows, &ctr->inserted, &ctr->overflow, nullptr);
+}
+
+// --------------------------------------------------------------------------------
+// partitioned path
+// --------------------------------------------------------------------------------
+template <int W>
+constexpr int run_w() { return W == 1 ? 32 : (W == 2 ? 16 : 8); }
+template <int W>
+constexpr int tile_win() { return COUNT_THREADS * run_w<W>(); }
+template <int W>
+constexpr size_t part_smem(uint32_t F) {  // tilehist, tilestart, tilecur (u32), gbase (u64), keys
+    return ((size_t)F * 3 + 1) * 4 + 4 + (size_t)F * 8 + (size_t)tile_win<W>() * 8 * W;
+}
+
+// exclusive scan of an LDS u32 array of n entries (n <= 4096) by one 256-thread block
+DEV void block_excl_scan_lds(const uint32_t* in, uint32_t* out, uint32_t n) {
+    __shared__ uint32_t s_w[COUNT_THREADS / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint32_t per = (n + COUNT_THREADS - 1) / COUNT_THREADS;
+    const uint32_t lo = min(n, tid * per), hi = min(n, lo + per);
+    uint32_t sum = 0;
+    for (uint32_t i = lo; i < hi; i++) sum += in[i];
+    const uint32_t incl = wave_incl_sum(sum);
+    if (lane == 63) s_w[wid] = incl;
+    __syncthreads();
+    uint32_t base = incl - sum;
+    for (int w = 0; w < wid; w++) base += s_w[w];
+    for (uint32_t i = lo; i < hi; i++) {
+        const uint32_t v = in[i];
+        out[i] = base;
+        base += v;
+    }
+    __syncthreads();
+}
+
+// Level 1: windows of a contiguous symbol range -> coarse bins mulhi(h, F1).
+// SCATTER = false: histogram only ([bin][block] into hist1); true: write the keys.
+template <int W, int MODE, bool SCATTER>
+__global__ __launch_bounds__(COUNT_THREADS) void k_p1(const uint8_t* __restrict__ sym, int k, TableView tv,
+                                                      BloomView bf, DevCounters* __restrict__ ctr, PartBufs pb,
+                                                      uint64_t pow5_k, uint64_t pow5_km1) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int RUNW = run_w<W>(), TW = tile_win<W>();
+    const uint32_t F = tv.F1;
+    uint32_t* tilehist = reinterpret_cast<uint32_t*>(smem);
+    uint32_t* tilestart = tilehist + F;
+    uint32_t* tilecur = tilestart + F;
+    uint64_t* gbase = reinterpret_cast<uint64_t*>(tilecur + F + (F & 1));
+    uint64_t* lkeys = gbase + F;
+    const int tid = threadIdx.x;
+    const uint64_t M = ctr->stream_len;
+    const uint64_t per = (M + pb.nblk1 - 1) / pb.nblk1;
+    const uint64_t lo = min(M, (uint64_t)blockIdx.x * per), hi = min(M, lo + per);
+    for (uint32_t b = tid; b < F; b += COUNT_THREADS) {
+        tilehist[b] = 0;
+        if constexpr (SCATTER) gbase[b] = pb.off1[(uint64_t)b * pb.nblk1 + blockIdx.x];
+    }
+    __syncthreads();
+    const RollConst rk = make_roll<W>(k, pow5_k, pow5_km1);
+    uint32_t n_win = 0, n_ins = 0;
+    for (uint64_t t0 = lo; t0 < hi; t0 += TW) {
+        const uint64_t r0 = t0 + (uint64_t)tid * RUNW, r1 = min(r0 + RUNW, hi);
+        const uint64_t ps = r0 >= (uint64_t)(k - 1) ? r0 - (k - 1) : 0;
+        // (a) histogram of this tile
+        if (r0 < r1)
+            roll_run<W, MODE != 0>(sym, ps, r0, r1, rk,
+                                   [&](const uint64_t (&fwd)[W], const uint64_t (&rc)[W], uint64_t root) {
+                if constexpr (!SCATTER) n_win++;
+                if constexpr (MODE == 2) {
+                    if (!bloom_gate(bf, root)) return;
+                }
+                uint64_t key[W];
+                canonical<W>(fwd, rc, key);
+                if constexpr (!SCATTER) n_ins++;
+                atomicAdd(&tilehist[(uint32_t)__umul64hi(key_hash<W>(key), F)], 1u);
+            });
+        if constexpr (SCATTER) {
+            __syncthreads();
+            block_excl_scan_lds(tilehist, tilestart, F);
+            for (uint32_t b = tid; b < F; b += COUNT_THREADS) tilecur[b] = tilestart[b];
+            __syncthreads();
+            // (b) place keys in bin order in LDS
+            if (r0 < r1)
+                roll_run<W, MODE != 0>(sym, ps, r0, r1, rk,
+                                       [&](const uint64_t (&fwd)[W], const uint64_t (&rc)[W], uint64_t root) {
+                    if constexpr (MODE == 2) {
+                        if (!bloom_gate(bf, root)) return;
+                    }
+                    uint64_t key[W];
+                    canonical<W>(fwd, rc, key);
+                    const uint32_t b = (uint32_t)__umul64hi(key_hash<W>(key), F);
+                    const uint32_t slot = atomicAdd(&tilecur[b], 1u);
+#pragma unroll
+                    for (int i = 0; i < W; i++) lkeys[slot * W + i] = key[i];
+                });
+            __syncthreads();
+            // (c) contiguous runs per bin -> global
+            const uint32_t n = tilestart[F - 1] + tilehist[F - 1];
+            for (uint32_t i = tid; i < n; i += COUNT_THREADS) {
+                uint64_t key[W];
+#pragma unroll
+                for (int w = 0; w < W; w++) key[w] = lkeys[i * W + w];
+                const uint32_t b = (uint32_t)__umul64hi(key_hash<W>(key), F);
+                const uint64_t dst = gbase[b] + (i - tilestart[b]);
+#pragma unroll
+                for (int w = 0; w < W; w++) pb.keys1[dst * W + w] = key[w];
+            }
+            __syncthreads();
+            for (uint32_t b = tid; b < F; b += COUNT_THREADS) {
+                gbase[b] += tilehist[b];
+                tilehist[b] = 0;
+            }
+            __syncthreads();
+        }
+    }
+    if constexpr (!SCATTER) {
+        __syncthreads();
+        for (uint32_t b = tid; b < F; b += COUNT_THREADS) pb.hist1[(uint64_t)b * pb.nblk1 + blockIdx.x] = tilehist[b];
+        block_add4(n_win, n_ins, 0, 0, &ctr->windows, &ctr->inserted, nullptr, nullptr);
+    }
+}
+
+// Level 2: coarse bin c (block = c * B2 + j) -> its F2 regions.
+template <int W, bool SCATTER>
+__global__ __launch_bounds__(COUNT_THREADS) void k_p2(TableView tv, PartBufs pb) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int TW = tile_win<W>();
+    const uint32_t F = tv.F2;
+    uint32_t* tilehist = reinterpret_cast<uint32_t*>(smem);
+    uint32_t* tilestart = tilehist + F;
+    uint32_t* tilecur = tilestart + F;
+    uint64_t* gbase = reinterpret_cast<uint64_t*>(tilecur + F + (F & 1));
+    uint64_t* lkeys = gbase + F;
+    const int tid = threadIdx.x;
+    const uint32_t c = blockIdx.x / pb.B2, j = blockIdx.x % pb.B2;
+    const uint64_t cs = pb.off1[(uint64_t)c * pb.nblk1], ce = pb.off1[(uint64_t)(c + 1) * pb.nblk1];
+    const uint64_t part = (ce - cs + pb.B2 - 1) / pb.B2;
+    const uint64_t lo = min(ce, cs + j * part), hi = min(ce, lo + part);
+    const uint64_t rbase = (uint64_t)c * F;
+    for (uint32_t b = tid; b < F; b += COUNT_THREADS) {
+        tilehist[b] = 0;
+        if constexpr (SCATTER) gbase[b] = pb.off2[(rbase + b) * pb.B2 + j];
+    }
+    __syncthreads();
+    for (uint64_t t0 = lo; t0 < hi; t0 += TW) {
+        const uint32_t n = (uint32_t)min((uint64_t)TW, hi - t0);
+        // (a) histogram of this tile
+        for (uint32_t i = tid; i < n; i += COUNT_THREADS) {
+            uint64_t key[W];
+#pragma unroll
+            for (int w = 0; w < W; w++) key[w] = pb.keys1[(t0 + i) * W + w];
+            atomicAdd(&tilehist[(uint32_t)(region_of(key_hash<W>(key), tv.R) - rbase)], 1u);
+        }
+        if constexpr (SCATTER) {
+            __syncthreads();
+            block_excl_scan_lds(tilehist, tilestart, F);
+            for (uint32_t b = tid; b < F; b += COUNT_THREADS) tilecur[b] = tilestart[b];
+            __syncthreads();
+            // (b) counting sort into LDS (the tile is re-read from L2)
+            for (uint32_t i = tid; i < n; i += COUNT_THREADS) {
+                uint64_t key[W];
+#pragma unroll
+                for (int w = 0; w < W; w++) key[w] = pb.keys1[(t0 + i) * W + w];
+                const uint32_t f = (uint32_t)(region_of(key_hash<W>(key), tv.R) - rbase);
+                const uint32_t slot = atomicAdd(&tilecur[f], 1u);
+#pragma unroll
+                for (int w = 0; w < W; w++) lkeys[slot * W + w] = key[w];
+            }
+            __syncthreads();
+            // (c) contiguous runs per region -> global
+            for (uint32_t i = tid; i < n; i += COUNT_THREADS) {
+                uint64_t key[W];
+#pragma unroll
+                for (int w = 0; w < W; w++) key[w] = lkeys[i * W + w];
+                const uint32_t f = (uint32_t)(region_of(key_hash<W>(key), tv.R) - rbase);
+                const uint64_t dst = gbase[f] + (i - tilestart[f]);
+#pragma unroll
+                for (int w = 0; w < W; w++) pb.keys2[dst * W + w] = key[w];
+            }
+            __syncthreads();
+            for (uint32_t b = tid; b < F; b += COUNT_THREADS) {
+                gbase[b] += tilehist[b];
+                tilehist[b] = 0;
+            }
+            __syncthreads();
+        }
+    }
+    if constexpr (!SCATTER) {
+        __syncthreads();
+        for (uint32_t b = tid; b < F; b += COUNT_THREADS) pb.hist2[(rbase + b) * pb.B2 + j] = tilehist[b];
+    }
+}
+
+// Level 3: one workgroup per region: LDS-resident table
+template <int W>
+__global__ __launch_bounds__(COUNT_THREADS) void k_p3(TableView tv, PartBufs pb, DevCounters* __restrict__ ctr) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int S = BUCKET_WORDS / (W + 1);
+    uint64_t* lt = reinterpret_cast<uint64_t*>(smem);  // BPR * BUCKET_WORDS words
+    const uint64_t r = blockIdx.x;
+    const uint64_t start = pb.off2[r * pb.B2], end = pb.off2[(r + 1) * pb.B2];
+    if (start == end) return;  // nothing to insert: leave the region untouched
+    uint4* g4 = reinterpret_cast<uint4*>(tv.buckets + r * BPR * BUCKET_WORDS);
+    uint4* l4 = reinterpret_cast<uint4*>(lt);
+    constexpr int N4 = BPR * BUCKET_WORDS / 2;
+    for (int i = threadIdx.x; i < N4; i += COUNT_THREADS) l4[i] = g4[i];
+    __syncthreads();
+    uint32_t n_fail = 0;
+    for (uint64_t i = start + threadIdx.x; i < end; i += COUNT_THREADS) {
+        uint64_t key[W];
+#pragma unroll
+        for (int w = 0; w < W; w++) key[w] = pb.keys2[i * W + w];
+        const uint64_t h = key_hash<W>(key);
+        uint32_t b = bucket_in_region(h, tv.R);
+        const uint64_t k0 = key[0] | OCC;
+        bool done = false;
+        for (int probe = 0; probe < BPR && !done; probe++) {
+            uint64_t* bk = lt + b * BUCKET_WORDS;
+            int s = 0;
+            while (s < S) {
+                uint64_t* kp = bk + s * W;
+                unsigned long long* cp = reinterpret_cast<unsigned long long*>(bk + S * W + s);
+                uint64_t v0 = *reinterpret_cast<volatile uint64_t*>(kp);
+                if (v0 == EMPTY) {
+                    const uint64_t old = atomicCAS((unsigned long long*)kp, 0ULL, (unsigned long long)k0);
+                    if (old == EMPTY) {
+                        if constexpr (W == 1) {
+                            atomicAdd(cp, 1ULL);
+                        } else {
+#pragma unroll
+                            for (int w = 1; w < W; w++) *reinterpret_cast<volatile uint64_t*>(kp + w) = key[w];
+                            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                            atomicAdd(cp, (unsigned long long)(READY + 1));
+                        }
+                        done = true;
+                        break;
+                    }
+                    v0 = old;
+                }
+                if (v0 == k0) {
+                    if constexpr (W == 1) {
+                        atomicAdd(cp, 1ULL);
+                        done = true;
+                        break;
+                    } else {
+                        const uint64_t c = __hip_atomic_load(cp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        if (!(c & READY)) continue;
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                        bool eq = true;
+#pragma unroll
+                        for (int w = 1; w < W; w++) eq &= *reinterpret_cast<volatile uint64_t*>(kp + w) == key[w];
+                        if (eq) {
+                            atomicAdd(cp, 1ULL);
+                            done = true;
+                            break;
+                        }
+                    }
+                }
+                s++;
+            }
+            b = b + 1 == BPR ? 0 : b + 1;
+        }
+        if (!done) n_fail++;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < N4; i += COUNT_THREADS) g4[i] = l4[i];
+    if (n_fail) atomicAdd(&ctr->overflow, (unsigned long long)n_fail);
+}
+
+// single-workgroup exclusive scan of n u32 -> u64 (out has n+1 entries)
+constexpr int SCAN_T = 1024;
+__global__ __launch_bounds__(SCAN_T) void k_scan_u32(const uint32_t* __restrict__ in, uint64_t n,
+                                                    uint64_t* __restrict__ out) {
+    __shared__ unsigned long long s_w[SCAN_T / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint64_t per = (n + SCAN_T - 1) / SCAN_T;
+    const uint64_t lo = min(n, (uint64_t)tid * per), hi = min(n, lo + per);
+    unsigned long long sum = 0;
+    for (uint64_t i = lo; i < hi; i++) sum += in[i];
+    unsigned long long incl = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        unsigned long long o = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += o;
+    }
+    if (lane == 63) s_w[wid] = incl;
+    __syncthreads();
+    unsigned long long base = incl - sum;
+    for (int w = 0; w < wid; w++) base += s_w[w];
+    for (uint64_t i = lo; i < hi; i++) {
+        out[i] = base;
+        base += in[i];
+    }
+    if (tid == SCAN_T - 1) out[n] = base;
+}
+
+// --------------------------------------------------------------------------------
+// k_dump<W>: occupied slots with T(c) >= a -> records {W key words, T(c)}
+// count_mode 0: c mod 65536 (-m 0); else min(c, 16383).  out == nullptr: count only.
+// --------------------------------------------------------------------------------
+template <int W>
+__global__ __launch_bounds__(256) void k_dump(TableView tv, int count_mode, uint64_t min_abundance,
+                                              uint64_t* __restrict__ out, DevCounters* __restrict__ ctr) {
+    constexpr int S = BUCKET_WORDS / (W + 1);
+    const uint64_t bkt = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    uint32_t occ = 0, nout = 0;
+    uint64_t tv_c[S];
+    bool emit[S];
+    const uint64_t* b = tv.buckets + bkt * BUCKET_WORDS;
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+        emit[s] = false;
+        tv_c[s] = 0;
+        if (bkt < tv.nbuckets && b[s * W] != EMPTY) {
+            occ++;
+            const uint64_t c = b[S * W + s] & CNT_MASK;
+            const uint64_t t = count_mode == 0 ? (c & 0xFFFF) : (c < 16383 ? c : 16383);
+            if (t >= min_abundance) { emit[s] = true; tv_c[s] = t; nout++; }
+        }
+    }
+    const int lane = threadIdx.x & 63;
+    uint32_t incl = wave_incl_sum(nout);
+    uint32_t wtot = __shfl(incl, 63, 64);
+    unsigned long long base = 0;
+    if (lane == 63 && wtot) base = atomicAdd(&ctr->dump_n, (unsigned long long)wtot);
+    base = __shfl(base, 63, 64);
+    uint64_t idx = base + incl - nout;
+#pragma unroll
+    for (int s = 0; s < S; s++)
+        if (out && emit[s]) {
+            uint64_t* o = out + idx * (W + 1);
+#pragma unroll
+            for (int i = 0; i < W; i++) o[i] = b[s * W + i] & (i == 0 ? ~OCC : ~0ULL);
+            o[W] = tv_c[s];
+            idx++;
+        }
+    uint32_t occ_w = occ;
+    for (int d = 32; d >= 1; d >>= 1) occ_w += __shfl_xor(occ_w, d, 64);
+    if (lane == 0 && occ_w) atomicAdd(&ctr->occupied, (unsigned long long)occ_w);
+}
+
+// ================================================================================
+// launchers
+// ================================================================================
+static uint64_t pow5_mod54(int e) {
+    uint64_t r = 1;
+    for (int i = 0; i < e; i++) r = (r * 5) & M54;
+    return r;
+}
+
+int run_width(int W) { return W == 1 ? 32 : (W == 2 ? 16 : 8); }
+
+template <int W>
+static hipError_t launch_count_w(const uint8_t* sym, uint64_t sym_bound, int k, int mode, TableView t, BloomView bf,
+                                 DevCounters* ctr, hipStream_t s) {
+    const uint64_t threads = (sym_bound + RUN - 1) / RUN;
+    const unsigned grid = (unsigned)((threads + COUNT_THREADS - 1) / COUNT_THREADS);
+    const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
+    if (grid == 0) return hipSuccess;
+    if (mode == 0)
+        hipLaunchKernelGGL((k_count<W, 0>), dim3(grid), dim3(COUNT_THREADS), 0, s, sym, k, t, bf, ctr, pk, pkm1);
+    else if (mode == 1)
+        hipLaunchKernelGGL((k_count<W, 1>), dim3(grid), dim3(COUNT_THREADS), 0, s, sym, k, t, bf, ctr, pk, pkm1);
+    else
+        hipLaunchKernelGGL((k_count<W, 2>), dim3(grid), dim3(COUNT_THREADS), 0, s, sym, k, t, bf, ctr, pk, pkm1);
+    return hipGetLastError();
+}
+
+hipError_t launch_count(const uint8_t* sym, uint64_t sym_bound, int k, int mode, TableView t, BloomView bf,
+                        DevCounters* ctr, hipStream_t s) {
+    switch (t.W) {
+    case 1: return launch_count_w<1>(sym, sym_bound, k, mode, t, bf, ctr, s);
+    case 2: return launch_count_w<2>(sym, sym_bound, k, mode, t, bf, ctr, s);
+    case 3: return launch_count_w<3>(sym, sym_bound, k, mode, t, bf, ctr, s);
+    case 4: return launch_count_w<4>(sym, sym_bound, k, mode, t, bf, ctr, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+template <class K>
+static hipError_t set_smem(K kernel, size_t bytes) {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)bytes);
+}
+
+template <int W, int MODE>
+static hipError_t launch_part_w(const uint8_t* sym, int k, TableView t, BloomView bf, DevCounters* ctr, PartBufs pb,
+                                hipStream_t s) {
+    const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
+    const size_t sm1 = part_smem<W>(t.F1), sm2 = part_smem<W>(t.F2);
+    const size_t sm3 = (size_t)BPR * BUCKET_WORDS * 8;
+    hipError_t e;
+    if ((e = set_smem(k_p1<W, MODE, false>, sm1)) != hipSuccess) return e;
+    if ((e = set_smem(k_p1<W, MODE, true>, sm1)) != hipSuccess) return e;
+    if ((e = set_smem(k_p2<W, false>, sm2)) != hipSuccess) return e;
+    if ((e = set_smem(k_p2<W, true>, sm2)) != hipSuccess) return e;
+    if ((e = set_smem(k_p3<W>, sm3)) != hipSuccess) return e;
+    hipLaunchKernelGGL((k_p1<W, MODE, false>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1, s, sym, k, t, bf, ctr, pb,
+                       pk, pkm1);
+    hipLaunchKernelGGL(k_scan_u32, dim3(1), dim3(SCAN_T), 0, s, pb.hist1, (uint64_t)t.F1 * pb.nblk1, pb.off1);
+    hipLaunchKernelGGL((k_p1<W, MODE, true>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1, s, sym, k, t, bf, ctr, pb,
+                       pk, pkm1);
+    hipLaunchKernelGGL((k_p2<W, false>), dim3(t.F1 * pb.B2), dim3(COUNT_THREADS), sm2, s, t, pb);
+    hipLaunchKernelGGL(k_scan_u32, dim3(1), dim3(SCAN_T), 0, s, pb.hist2, t.R * pb.B2, pb.off2);
+    hipLaunchKernelGGL((k_p2<W, true>), dim3(t.F1 * pb.B2), dim3(COUNT_THREADS), sm2, s, t, pb);
+    hipLaunchKernelGGL((k_p3<W>), dim3((unsigned)t.R), dim3(COUNT_THREADS), sm3, s, t, pb, ctr);
+    return hipGetLastError();
+}
+
+hipError_t launch_count_partitioned(const uint8_t* sym, uint64_t sym_bound, int k, int mode, TableView t,
+                                    BloomView bf, DevCounters* ctr, PartBufs pb, hipStream_t s) {
+    (void)sym_bound;
+    const bool gate = mode == 2;
+    switch (t.W) {
+    case 1: return gate ? launch_part_w<1, 2>(sym, k, t, bf, ctr, pb, s) : launch_part_w<1, 0>(sym, k, t, bf, ctr, pb, s);
+    case 2: return gate ? launch_part_w<2, 2>(sym, k, t, bf, ctr, pb, s) : launch_part_w<2, 0>(sym, k, t, bf, ctr, pb, s);
+    case 3: return gate ? launch_part_w<3, 2>(sym, k, t, bf, ctr, pb, s) : launch_part_w<3, 0>(sym, k, t, bf, ctr, pb, s);
+    case 4: return gate ? launch_part_w<4, 2>(sym, k, t, bf, ctr, pb, s) : launch_part_w<4, 0>(sym, k, t, bf, ctr, pb, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_dump(TableView t, int count_mode, uint64_t min_abundance, uint64_t* out, DevCounters* ctr,
+                       hipStream_t s) {
+    const unsigned grid = (unsigned)((t.nbuckets + 255) / 256);
+    switch (t.W) {
+    case 1: hipLaunchKernelGGL(k_dump<1>, dim3(grid), dim3(256), 0, s, t, count_mode, min_abundance, out, ctr); break;
+    case 2: hipLaunchKernelGGL(k_dump<2>, dim3(grid), dim3(256), 0, s, t, count_mode, min_abundance, out, ctr); break;
+    case 3: hipLaunchKernelGGL(k_dump<3>, dim3(grid), dim3(256), 0, s, t, count_mode, min_abundance, out, ctr); break;
+    case 4: hipLaunchKernelGGL(k_dump<4>, dim3(grid), dim3(256), 0, s, t, count_mode, min_abundance, out, ctr); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace kc

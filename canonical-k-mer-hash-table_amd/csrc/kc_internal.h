@@ -15,6 +15,7 @@ constexpr int TILE_THREADS = 256;          // 16 bytes per thread
 constexpr int COUNT_THREADS = 256;
 constexpr int RUN = 32;                    // consecutive symbols rolled per thread
 constexpr int BUCKET_WORDS = 16;           // 128-byte buckets
+constexpr int BPR = 512;                   // buckets per region: 64 KiB, one LDS-resident table
 constexpr uint64_t EMPTY = 0;              // empty slot: word 0 of a stored key carries OCC
 constexpr uint64_t OCC = 1ULL << 63;       // word 0 always has spare top bits (W = k/32 + 1)
 constexpr uint64_t READY = 1ULL << 62;     // multi-word slot published flag, in the count word
@@ -65,9 +66,23 @@ struct DevCounters {
 
 struct TableView {
     uint64_t* buckets;      // nbuckets * BUCKET_WORDS
-    uint64_t nbuckets;
+    uint64_t nbuckets;      // R * BPR
+    uint64_t R;             // regions = F1 * F2
+    uint32_t F1, F2;        // partition fan-outs of the two scatter levels
     int W;                  // key words
     int S;                  // slots per bucket
+};
+
+// Buffers of the partitioned insert (keys -> coarse bins -> regions -> LDS tables).
+struct PartBufs {
+    uint32_t nblk1;         // level-1 workgroups (each owns a contiguous symbol range)
+    uint32_t B2;            // level-2 workgroups per coarse bin
+    uint32_t* hist1;        // [F1][nblk1]
+    uint64_t* off1;         // F1*nblk1 + 1 exclusive offsets
+    uint32_t* hist2;        // [R][B2]
+    uint64_t* off2;         // R*B2 + 1
+    uint64_t* keys1;        // coarse-binned keys (W words each)
+    uint64_t* keys2;        // region-binned keys
 };
 
 struct BloomView {
@@ -89,6 +104,10 @@ hipError_t launch_tokenize(const uint8_t* stage, uint64_t ntiles, const ChunkDes
 // mode: 0 count all windows, 1 Bloom pass 1, 2 count windows passing the Bloom gate
 hipError_t launch_count(const uint8_t* sym, uint64_t sym_bound, int k, int mode, TableView t, BloomView bf,
                         DevCounters* ctr, hipStream_t s);
+// partitioned insert for modes 0 and 2 (same table, same result as launch_count)
+hipError_t launch_count_partitioned(const uint8_t* sym, uint64_t sym_bound, int k, int mode, TableView t,
+                                    BloomView bf, DevCounters* ctr, PartBufs pb, hipStream_t s);
+int run_width(int W);  // windows rolled per thread in the partitioned kernels
 hipError_t launch_dump(TableView t, int count_mode, uint64_t min_abundance, uint64_t* out, DevCounters* ctr,
                        hipStream_t s);
 hipError_t launch_synth(uint8_t* dst, uint64_t first_read, uint64_t n_reads, uint64_t seed, uint64_t genome_len,

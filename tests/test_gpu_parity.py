@@ -58,8 +58,15 @@ def bf_singleton_check(lines, path, k, mode, tmp_path):
             assert truth.get(s) == "1", s
 
 
+@pytest.fixture(params=["direct", "partitioned"])
+def insert_path(request, monkeypatch):
+    """Both insert paths must give the reference's result (KC_INSERT_PATH forces one)."""
+    monkeypatch.setenv("KC_INSERT_PATH", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("case", CASES, ids=_case_id)
-def test_golden_case_host_chunks(case, golden_input, tmp_path):
+def test_golden_case_host_chunks(case, golden_input, tmp_path, insert_path):
     path = golden_input(case["input"])
     o = parse_ref_args(case["args"])
     kc, st = ka.count_file(path, case["k"], mode=o["mode"], min_abundance=o["min_abundance"],
@@ -81,7 +88,7 @@ def test_golden_case_host_chunks(case, golden_input, tmp_path):
     ("long.fasta", 127, ["-a", "1"]),
     ("big_edge.fasta", 31, ["-a", "1"]),
 ])
-def test_device_image_path_and_small_batches(name, k, args, golden_input, tmp_path):
+def test_device_image_path_and_small_batches(name, k, args, golden_input, tmp_path, insert_path):
     """kc_count_device over a device-resident image with the reference chunk table,
     with a staging batch far smaller than the input (many batches, chunk splits)."""
     torch = pytest.importorskip("torch")
@@ -149,14 +156,14 @@ def test_cli_default_output_name(golden_input, tmp_path):
     assert r.returncode == 0 and not (tmp_path / "none.txt").exists()  # -a 0 writes nothing
 
 
-def test_table_full_is_an_error(golden_input):
+def test_table_full_is_an_error(golden_input, insert_path):
     path = golden_input("reads_w60.fasta")
     with pytest.raises(ka.KcError) as e:
         ka.count_file(path, 31, table_slots=64, min_abundance=1)
     assert e.value.code == -3
 
 
-def test_counts_sum_to_windows_at_scale():
+def test_counts_sum_to_windows_at_scale(insert_path):
     """Size-independent properties on a larger device-generated input (no N's):
     windows == N*(L-k+1); sum of counts == windows; counting the input twice doubles
     every count; distinct k-mers equal the dumped records at -a 1."""
