@@ -56,7 +56,8 @@ struct kc_ctx {
     int cur_pass = -1;                          // 0 count, 1 bloom
 
     uint8_t* d_stage = nullptr;
-    uint8_t* d_sym = nullptr;
+    uint64_t* d_pk = nullptr;  // packed symbol stream
+    uint32_t* d_bk = nullptr;  // break bitmap
     TileInfo* d_tiles = nullptr;
     TileOut* d_touts = nullptr;
     ChunkDesc* d_chunks = nullptr;
@@ -236,8 +237,9 @@ static int run_batch(kc_ctx* c, uint64_t used, uint64_t nchunks, int fmt, int pa
         ev[2] = c->get_event();
         ev[3] = c->get_event();
     }
-    HIPCHK(c, launch_tokenize(c->d_stage, ntiles, c->d_chunks, (int)nchunks, fmt, c->d_tiles, c->d_touts, c->d_sym,
-                              c->batch_bytes + c->max_chunks, c->d_ctr, s));
+    const PackedView sv{c->d_pk, c->d_bk};
+    HIPCHK(c, launch_tokenize(c->d_stage, ntiles, c->d_chunks, (int)nchunks, fmt, c->d_tiles, c->d_touts, sv,
+                              used + nchunks, c->d_ctr, s));
     if (c->profiling) HIPCHK(c, hipEventRecord(ev[2], s));
     TableView tv = table_view(c);
     BloomView bv{c->d_bloom, c->bf_bits ? c->bf_bits - 1 : 0, c->nh, c->nh_gate};
@@ -248,9 +250,9 @@ static int run_batch(kc_ctx* c, uint64_t used, uint64_t nchunks, int fmt, int pa
     if (mode != 1 && use_partitioned(c, syms)) {
         int rc = ensure_part(c, syms);
         if (rc) return rc;
-        HIPCHK(c, launch_count_partitioned(c->d_sym, syms, c->cfg.k, mode, tv, bv, c->d_ctr, c->pb, s));
+        HIPCHK(c, launch_count_partitioned(sv, syms, c->cfg.k, mode, tv, bv, c->d_ctr, c->pb, s));
     } else {
-        HIPCHK(c, launch_count(c->d_sym, syms, c->cfg.k, mode, tv, bv, c->d_ctr, s));
+        HIPCHK(c, launch_count(sv, syms, c->cfg.k, mode, tv, bv, c->d_ctr, s));
     }
     if (c->profiling) {
         HIPCHK(c, hipEventRecord(ev[3], s));
@@ -406,7 +408,8 @@ int kc_create(const kc_config* cfg, kc_ctx** out) {
         return bail(KC_ERR_HIP, "event creation failed");
     const uint64_t ntiles = c->batch_bytes / TILE;
     if (hipMalloc(&c->d_stage, c->batch_bytes) != hipSuccess ||
-        hipMalloc(&c->d_sym, c->batch_bytes + c->max_chunks + 64) != hipSuccess ||
+        hipMalloc(&c->d_pk, ((c->batch_bytes + c->max_chunks) / 32 + 4) * 8) != hipSuccess ||
+        hipMalloc(&c->d_bk, ((c->batch_bytes + c->max_chunks) / 32 + 4) * 4) != hipSuccess ||
         hipMalloc(&c->d_tiles, ntiles * sizeof(TileInfo)) != hipSuccess ||
         hipMalloc(&c->d_touts, ntiles * sizeof(TileOut)) != hipSuccess ||
         hipMalloc(&c->d_chunks, c->max_chunks * sizeof(ChunkDesc)) != hipSuccess ||
@@ -439,7 +442,8 @@ void kc_destroy(kc_ctx* c) {
         if (c->h_free[i]) hipEventDestroy(c->h_free[i]);
     }
     hipFree(c->d_stage);
-    hipFree(c->d_sym);
+    hipFree(c->d_pk);
+    hipFree(c->d_bk);
     hipFree(c->d_tiles);
     hipFree(c->d_touts);
     hipFree(c->d_chunks);

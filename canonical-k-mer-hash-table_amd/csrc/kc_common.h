@@ -120,18 +120,23 @@ DEV RollConst make_roll(int k, uint64_t pk, uint64_t pkm1) {
     return r;
 }
 
-// Rolls sym[pstart, pend) and calls f(fwd, rc, root) for every complete window whose
+// symbol p of the packed stream: 0..3, or 4 for a break
+DEV uint32_t sym_at(const PackedView& sv, uint64_t p) {
+    if ((sv.bk[p >> 5] >> (31 - (p & 31))) & 1) return SYM_BREAK;
+    return (uint32_t)(sv.pk[p >> 5] >> (62 - 2 * (p & 31))) & 3;
+}
+
+// Rolls symbols [pstart, pend) and calls f(fwd, rc, root) for every complete window whose
 // last symbol is at p >= p0.  ROOT: also roll the mod-2^54 pair (Bloom modes).
 template <int W, bool ROOT, class F>
-DEV void roll_run(const uint8_t* __restrict__ sym, uint64_t pstart, uint64_t p0, uint64_t pend,
-                  const RollConst& rk, F&& f) {
+DEV void roll_run(const PackedView& sv, uint64_t pstart, uint64_t p0, uint64_t pend, const RollConst& rk, F&& f) {
     uint64_t fwd[W], rc[W];
 #pragma unroll
     for (int i = 0; i < W; i++) { fwd[i] = 0; rc[i] = 0; }
     int fill = 0;
     uint64_t Fh = 0, Bh = 0, p5 = 1;
     for (uint64_t p = pstart; p < pend; p++) {
-        const uint8_t c = sym[p];
+        const uint32_t c = sym_at(sv, p);
         if (c > 3) {
             fill = 0;
 #pragma unroll
@@ -166,6 +171,57 @@ DEV void roll_run(const uint8_t* __restrict__ sym, uint64_t pstart, uint64_t p0,
         if (fill < rk.k) fill++;
         if (fill == rk.k && p >= p0) f(fwd, rc, Fh < Bh ? Fh : Bh);
     }
+}
+
+// ---- direct window extraction (no rolling) -----------------------------------------
+// The window ending at symbol `last` is the contiguous bit range of the big-endian packed
+// stream: W funnel shifts of adjacent words; valid iff no break bit in [last-k+1, last].
+template <int W>
+DEV bool extract_window(const PackedView& sv, uint64_t last, const RollConst& rk, uint64_t (&fwd)[W]) {
+    if (last + 1 < (uint64_t)rk.k) return false;
+    const uint64_t a = last + 1 - rk.k;
+    const uint64_t wa = a >> 5, wl = last >> 5;
+    for (uint64_t w = wa; w <= wl; w++) {
+        uint32_t m = sv.bk[w];
+        if (w == wa) m &= 0xFFFFFFFFu >> (a & 31);
+        if (w == wl) m &= 0xFFFFFFFFu << (31 - (last & 31));
+        if (m) return false;
+    }
+    const int s = 2 * ((int)(last & 31) + 1);  // 2..64
+    uint64_t lo = sv.pk[wl];
+#pragma unroll
+    for (int i = 0; i < W; i++) {
+        const uint64_t hi = wl >= (uint64_t)(i + 1) ? sv.pk[wl - i - 1] : 0;
+        fwd[W - 1 - i] = s == 64 ? lo : ((hi << s) | (lo >> (64 - s)));
+        lo = hi;
+    }
+    fwd[0] &= rk.topmask;
+    return true;
+}
+
+DEV uint64_t rev2(uint64_t x) {  // reverse the order of the 32 two-bit groups
+    x = ((x >> 2) & 0x3333333333333333ULL) | ((x & 0x3333333333333333ULL) << 2);
+    x = ((x >> 4) & 0x0F0F0F0F0F0F0F0FULL) | ((x & 0x0F0F0F0F0F0F0F0FULL) << 4);
+    return __builtin_bswap64(x);
+}
+
+// reverse complement of the k-mer held in the low 2k bits of the W-word integer
+template <int W>
+DEV void revcomp(const uint64_t (&f)[W], const RollConst& rk, uint64_t (&r)[W]) {
+    uint64_t t[W];
+#pragma unroll
+    for (int i = 0; i < W; i++) t[i] = rev2(~f[W - 1 - i]);
+    const int sh = 64 * W - 2 * rk.k;  // 2..64
+    const int q = sh >> 6, b = sh & 63;
+#pragma unroll
+    for (int i = 0; i < W; i++) {
+        const int src = i - q;
+        uint64_t v = 0;
+        if (src >= 0) v = b ? (t[src] >> b) : t[src];
+        if (b && src - 1 >= 0) v |= t[src - 1] << (64 - b);
+        r[i] = v;
+    }
+    r[0] &= rk.topmask;
 }
 
 template <int W>

@@ -198,21 +198,52 @@ DEV void block_add4(unsigned long long v0, unsigned long long v1, unsigned long 
 }
 
 // --------------------------------------------------------------------------------
+// windows of a tile
+// --------------------------------------------------------------------------------
+template <int W>
+constexpr int run_w() { return W == 1 ? 32 : (W == 2 ? 16 : 8); }
+template <int W>
+constexpr int tile_win() { return COUNT_THREADS * run_w<W>(); }
+
+// Calls f(fwd, rc, root) for every window whose last symbol is in [t0, t1):
+// MODE 0 extracts each window directly from the packed stream (consecutive lanes take
+// consecutive windows); MODE 1/2 roll one contiguous run per thread because the
+// Bloom root (RollingHasherDual mod 2^54) is a rolled quantity.
+template <int W, int MODE, class F>
+DEV void tile_windows(const PackedView& sv, uint64_t t0, uint64_t t1, const RollConst& rk, F&& f) {
+    if constexpr (MODE == 0) {
+        for (uint64_t p = t0 + threadIdx.x; p < t1; p += COUNT_THREADS) {
+            uint64_t fwd[W], rc[W];
+            if (!extract_window<W>(sv, p, rk, fwd)) continue;
+            revcomp<W>(fwd, rk, rc);
+            f(fwd, rc, 0ULL);
+        }
+    } else {
+        constexpr int RUNW = run_w<W>();
+        const uint64_t r0 = t0 + (uint64_t)threadIdx.x * RUNW, r1 = min(r0 + RUNW, t1);
+        if (r0 < r1) {
+            const uint64_t ps = r0 >= (uint64_t)(rk.k - 1) ? r0 - (rk.k - 1) : 0;
+            roll_run<W, true>(sv, ps, r0, r1, rk, f);
+        }
+    }
+}
+
+// --------------------------------------------------------------------------------
 // k_count<W, MODE>: direct path. MODE 0 count, 1 Bloom pass 1, 2 count behind the gate
 // --------------------------------------------------------------------------------
 template <int W, int MODE>
-__global__ __launch_bounds__(COUNT_THREADS) void k_count(const uint8_t* __restrict__ sym, int k, TableView tv,
-                                                         BloomView bf, DevCounters* __restrict__ ctr,
-                                                         uint64_t pow5_k, uint64_t pow5_km1) {
+__global__ __launch_bounds__(COUNT_THREADS) void k_count(PackedView sv, int k, TableView tv, BloomView bf,
+                                                         DevCounters* __restrict__ ctr, uint64_t pow5_k,
+                                                         uint64_t pow5_km1) {
+    constexpr int TW = tile_win<W>();
     const uint64_t M = ctr->stream_len;
-    const uint64_t p0 = ((uint64_t)blockIdx.x * COUNT_THREADS + threadIdx.x) * RUN;
+    const uint64_t t0 = (uint64_t)blockIdx.x * TW;
     uint32_t n_win = 0, n_ins = 0, n_fail = 0;
     BloomLocal bl = {0, 0, 0};
-    if (p0 < M) {
+    if (t0 < M) {
         const RollConst rk = make_roll<W>(k, pow5_k, pow5_km1);
-        const uint64_t pstart = p0 >= (uint64_t)(k - 1) ? p0 - (k - 1) : 0;
-        roll_run<W, MODE != 0>(sym, pstart, p0, min(p0 + RUN, M), rk,
-                               [&](const uint64_t (&fwd)[W], const uint64_t (&rc)[W], uint64_t root) {
+        tile_windows<W, MODE>(sv, t0, min(t0 + TW, M), rk,
+                              [&](const uint64_t (&fwd)[W], const uint64_t (&rc)[W], uint64_t root) {
             n_win++;
             if constexpr (MODE == 1) {
                 bloom_insert(bf, root, bl);
@@ -237,10 +268,7 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_count(const uint8_t* __restri
 // --------------------------------------------------------------------------------
 // partitioned path
 // --------------------------------------------------------------------------------
-template <int W>
-constexpr int run_w() { return W == 1 ? 32 : (W == 2 ? 16 : 8); }
-template <int W>
-constexpr int tile_win() { return COUNT_THREADS * run_w<W>(); }
+constexpr size_t hist_smem(uint32_t F) { return ((size_t)F * 3 + 1) * 4 + 4 + (size_t)F * 8; }
 template <int W>
 constexpr size_t part_smem(uint32_t F) {  // tilehist, tilestart, tilecur (u32), gbase (u64), keys
     return ((size_t)F * 3 + 1) * 4 + 4 + (size_t)F * 8 + (size_t)tile_win<W>() * 8 * W;
@@ -270,11 +298,11 @@ DEV void block_excl_scan_lds(const uint32_t* in, uint32_t* out, uint32_t n) {
 // Level 1: windows of a contiguous symbol range -> coarse bins mulhi(h, F1).
 // SCATTER = false: histogram only ([bin][block] into hist1); true: write the keys.
 template <int W, int MODE, bool SCATTER>
-__global__ __launch_bounds__(COUNT_THREADS) void k_p1(const uint8_t* __restrict__ sym, int k, TableView tv,
-                                                      BloomView bf, DevCounters* __restrict__ ctr, PartBufs pb,
-                                                      uint64_t pow5_k, uint64_t pow5_km1) {
+__global__ __launch_bounds__(COUNT_THREADS) void k_p1(PackedView sv, int k, TableView tv, BloomView bf,
+                                                      DevCounters* __restrict__ ctr, PartBufs pb, uint64_t pow5_k,
+                                                      uint64_t pow5_km1) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    constexpr int RUNW = run_w<W>(), TW = tile_win<W>();
+    constexpr int TW = tile_win<W>();
     const uint32_t F = tv.F1;
     uint32_t* tilehist = reinterpret_cast<uint32_t*>(smem);
     uint32_t* tilestart = tilehist + F;
@@ -293,40 +321,37 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_p1(const uint8_t* __restrict_
     const RollConst rk = make_roll<W>(k, pow5_k, pow5_km1);
     uint32_t n_win = 0, n_ins = 0;
     for (uint64_t t0 = lo; t0 < hi; t0 += TW) {
-        const uint64_t r0 = t0 + (uint64_t)tid * RUNW, r1 = min(r0 + RUNW, hi);
-        const uint64_t ps = r0 >= (uint64_t)(k - 1) ? r0 - (k - 1) : 0;
+        const uint64_t t1 = min(t0 + TW, hi);
         // (a) histogram of this tile
-        if (r0 < r1)
-            roll_run<W, MODE != 0>(sym, ps, r0, r1, rk,
-                                   [&](const uint64_t (&fwd)[W], const uint64_t (&rc)[W], uint64_t root) {
-                if constexpr (!SCATTER) n_win++;
-                if constexpr (MODE == 2) {
-                    if (!bloom_gate(bf, root)) return;
-                }
-                uint64_t key[W];
-                canonical<W>(fwd, rc, key);
-                if constexpr (!SCATTER) n_ins++;
-                atomicAdd(&tilehist[(uint32_t)__umul64hi(key_hash<W>(key), F)], 1u);
-            });
+        tile_windows<W, MODE == 0 ? 0 : 2>(sv, t0, t1, rk,
+                                          [&](const uint64_t (&fwd)[W], const uint64_t (&rc)[W], uint64_t root) {
+            if constexpr (!SCATTER) n_win++;
+            if constexpr (MODE == 2) {
+                if (!bloom_gate(bf, root)) return;
+            }
+            uint64_t key[W];
+            canonical<W>(fwd, rc, key);
+            if constexpr (!SCATTER) n_ins++;
+            atomicAdd(&tilehist[(uint32_t)__umul64hi(key_hash<W>(key), F)], 1u);
+        });
         if constexpr (SCATTER) {
             __syncthreads();
             block_excl_scan_lds(tilehist, tilestart, F);
             for (uint32_t b = tid; b < F; b += COUNT_THREADS) tilecur[b] = tilestart[b];
             __syncthreads();
             // (b) place keys in bin order in LDS
-            if (r0 < r1)
-                roll_run<W, MODE != 0>(sym, ps, r0, r1, rk,
-                                       [&](const uint64_t (&fwd)[W], const uint64_t (&rc)[W], uint64_t root) {
-                    if constexpr (MODE == 2) {
-                        if (!bloom_gate(bf, root)) return;
-                    }
-                    uint64_t key[W];
-                    canonical<W>(fwd, rc, key);
-                    const uint32_t b = (uint32_t)__umul64hi(key_hash<W>(key), F);
-                    const uint32_t slot = atomicAdd(&tilecur[b], 1u);
+            tile_windows<W, MODE == 0 ? 0 : 2>(sv, t0, t1, rk,
+                                              [&](const uint64_t (&fwd)[W], const uint64_t (&rc)[W], uint64_t root) {
+                if constexpr (MODE == 2) {
+                    if (!bloom_gate(bf, root)) return;
+                }
+                uint64_t key[W];
+                canonical<W>(fwd, rc, key);
+                const uint32_t b = (uint32_t)__umul64hi(key_hash<W>(key), F);
+                const uint32_t slot = atomicAdd(&tilecur[b], 1u);
 #pragma unroll
-                    for (int i = 0; i < W; i++) lkeys[slot * W + i] = key[i];
-                });
+                for (int i = 0; i < W; i++) lkeys[slot * W + i] = key[i];
+            });
             __syncthreads();
             // (c) contiguous runs per bin -> global
             const uint32_t n = tilestart[F - 1] + tilehist[F - 1];
@@ -450,11 +475,24 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_p3(TableView tv, PartBufs pb,
         bool done = false;
         for (int probe = 0; probe < BPR && !done; probe++) {
             uint64_t* bk = lt + b * BUCKET_WORDS;
+            uint64_t w0[S];
+            if constexpr (W == 1) {
+                const uint4* b4 = reinterpret_cast<const uint4*>(bk);
+#pragma unroll
+                for (int q = 0; q < S / 2; q++) {
+                    const uint4 v = b4[q];
+                    w0[2 * q] = ((uint64_t)v.y << 32) | v.x;
+                    w0[2 * q + 1] = ((uint64_t)v.w << 32) | v.z;
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < S; q++) w0[q] = bk[q * W];
+            }
             int s = 0;
             while (s < S) {
                 uint64_t* kp = bk + s * W;
                 unsigned long long* cp = reinterpret_cast<unsigned long long*>(bk + S * W + s);
-                uint64_t v0 = *reinterpret_cast<volatile uint64_t*>(kp);
+                uint64_t v0 = w0[s];
                 if (v0 == EMPTY) {
                     const uint64_t old = atomicCAS((unsigned long long*)kp, 0ULL, (unsigned long long)k0);
                     if (old == EMPTY) {
@@ -462,7 +500,8 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_p3(TableView tv, PartBufs pb,
                             atomicAdd(cp, 1ULL);
                         } else {
 #pragma unroll
-                            for (int w = 1; w < W; w++) *reinterpret_cast<volatile uint64_t*>(kp + w) = key[w];
+                            for (int w = 1; w < W; w++)
+                                __hip_atomic_store(kp + w, key[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                             atomicAdd(cp, (unsigned long long)(READY + 1));
                         }
@@ -470,6 +509,7 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_p3(TableView tv, PartBufs pb,
                         break;
                     }
                     v0 = old;
+                    w0[s] = old;
                 }
                 if (v0 == k0) {
                     if constexpr (W == 1) {
@@ -478,11 +518,12 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_p3(TableView tv, PartBufs pb,
                         break;
                     } else {
                         const uint64_t c = __hip_atomic_load(cp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        if (!(c & READY)) continue;
+                        if (!(c & READY)) continue;  // claimed by another lane, words not published yet
                         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                         bool eq = true;
 #pragma unroll
-                        for (int w = 1; w < W; w++) eq &= *reinterpret_cast<volatile uint64_t*>(kp + w) == key[w];
+                        for (int w = 1; w < W; w++)
+                            eq &= __hip_atomic_load(kp + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == key[w];
                         if (eq) {
                             atomicAdd(cp, 1ULL);
                             done = true;
@@ -585,10 +626,9 @@ static uint64_t pow5_mod54(int e) {
 int run_width(int W) { return W == 1 ? 32 : (W == 2 ? 16 : 8); }
 
 template <int W>
-static hipError_t launch_count_w(const uint8_t* sym, uint64_t sym_bound, int k, int mode, TableView t, BloomView bf,
+static hipError_t launch_count_w(PackedView sym, uint64_t sym_bound, int k, int mode, TableView t, BloomView bf,
                                  DevCounters* ctr, hipStream_t s) {
-    const uint64_t threads = (sym_bound + RUN - 1) / RUN;
-    const unsigned grid = (unsigned)((threads + COUNT_THREADS - 1) / COUNT_THREADS);
+    const unsigned grid = (unsigned)((sym_bound + tile_win<W>() - 1) / tile_win<W>());
     const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
     if (grid == 0) return hipSuccess;
     if (mode == 0)
@@ -600,7 +640,7 @@ static hipError_t launch_count_w(const uint8_t* sym, uint64_t sym_bound, int k, 
     return hipGetLastError();
 }
 
-hipError_t launch_count(const uint8_t* sym, uint64_t sym_bound, int k, int mode, TableView t, BloomView bf,
+hipError_t launch_count(PackedView sym, uint64_t sym_bound, int k, int mode, TableView t, BloomView bf,
                         DevCounters* ctr, hipStream_t s) {
     switch (t.W) {
     case 1: return launch_count_w<1>(sym, sym_bound, k, mode, t, bf, ctr, s);
@@ -618,30 +658,31 @@ static hipError_t set_smem(K kernel, size_t bytes) {
 }
 
 template <int W, int MODE>
-static hipError_t launch_part_w(const uint8_t* sym, int k, TableView t, BloomView bf, DevCounters* ctr, PartBufs pb,
+static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf, DevCounters* ctr, PartBufs pb,
                                 hipStream_t s) {
     const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
     const size_t sm1 = part_smem<W>(t.F1), sm2 = part_smem<W>(t.F2);
+    const size_t sm1h = hist_smem(t.F1), sm2h = hist_smem(t.F2);  // histogram passes: no key buffer
     const size_t sm3 = (size_t)BPR * BUCKET_WORDS * 8;
     hipError_t e;
-    if ((e = set_smem(k_p1<W, MODE, false>, sm1)) != hipSuccess) return e;
+    if ((e = set_smem(k_p1<W, MODE, false>, sm1h)) != hipSuccess) return e;
     if ((e = set_smem(k_p1<W, MODE, true>, sm1)) != hipSuccess) return e;
-    if ((e = set_smem(k_p2<W, false>, sm2)) != hipSuccess) return e;
+    if ((e = set_smem(k_p2<W, false>, sm2h)) != hipSuccess) return e;
     if ((e = set_smem(k_p2<W, true>, sm2)) != hipSuccess) return e;
     if ((e = set_smem(k_p3<W>, sm3)) != hipSuccess) return e;
-    hipLaunchKernelGGL((k_p1<W, MODE, false>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1, s, sym, k, t, bf, ctr, pb,
+    hipLaunchKernelGGL((k_p1<W, MODE, false>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1h, s, sym, k, t, bf, ctr, pb,
                        pk, pkm1);
     hipLaunchKernelGGL(k_scan_u32, dim3(1), dim3(SCAN_T), 0, s, pb.hist1, (uint64_t)t.F1 * pb.nblk1, pb.off1);
     hipLaunchKernelGGL((k_p1<W, MODE, true>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1, s, sym, k, t, bf, ctr, pb,
                        pk, pkm1);
-    hipLaunchKernelGGL((k_p2<W, false>), dim3(t.F1 * pb.B2), dim3(COUNT_THREADS), sm2, s, t, pb);
+    hipLaunchKernelGGL((k_p2<W, false>), dim3(t.F1 * pb.B2), dim3(COUNT_THREADS), sm2h, s, t, pb);
     hipLaunchKernelGGL(k_scan_u32, dim3(1), dim3(SCAN_T), 0, s, pb.hist2, t.R * pb.B2, pb.off2);
     hipLaunchKernelGGL((k_p2<W, true>), dim3(t.F1 * pb.B2), dim3(COUNT_THREADS), sm2, s, t, pb);
     hipLaunchKernelGGL((k_p3<W>), dim3((unsigned)t.R), dim3(COUNT_THREADS), sm3, s, t, pb, ctr);
     return hipGetLastError();
 }
 
-hipError_t launch_count_partitioned(const uint8_t* sym, uint64_t sym_bound, int k, int mode, TableView t,
+hipError_t launch_count_partitioned(PackedView sym, uint64_t sym_bound, int k, int mode, TableView t,
                                     BloomView bf, DevCounters* ctr, PartBufs pb, hipStream_t s) {
     (void)sym_bound;
     const bool gate = mode == 2;

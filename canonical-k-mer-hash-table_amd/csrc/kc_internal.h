@@ -64,6 +64,14 @@ struct DevCounters {
     unsigned long long bf_windows;      uint64_t _p9[15];
 };
 
+// The symbol stream: 32 symbols per word, symbol j of word w at bits 62-2j of pk[w]
+// (A=0 C=1 G=2 T=3, big-endian so a window is a contiguous bit range) and break
+// flags at bit 31-j of bk[w] (non-ACGT, header byte, chunk start).
+struct PackedView {
+    uint64_t* pk;
+    uint32_t* bk;
+};
+
 struct TableView {
     uint64_t* buckets;      // nbuckets * BUCKET_WORDS
     uint64_t nbuckets;      // R * BPR
@@ -99,13 +107,13 @@ inline int slots_per_bucket(int W) { return BUCKET_WORDS / (W + 1); }
 hipError_t launch_gather(const uint8_t* src, uint8_t* stage, const ChunkDesc* d_chunks, int n_chunks,
                          const ChunkDesc* h_chunks, hipStream_t s);
 hipError_t launch_tokenize(const uint8_t* stage, uint64_t ntiles, const ChunkDesc* d_chunks, int n_chunks,
-                           int fmt, TileInfo* tiles, TileOut* touts, uint8_t* sym, uint64_t sym_cap,
+                           int fmt, TileInfo* tiles, TileOut* touts, PackedView sv, uint64_t sym_bound,
                            DevCounters* ctr, hipStream_t s);
 // mode: 0 count all windows, 1 Bloom pass 1, 2 count windows passing the Bloom gate
-hipError_t launch_count(const uint8_t* sym, uint64_t sym_bound, int k, int mode, TableView t, BloomView bf,
+hipError_t launch_count(PackedView sv, uint64_t sym_bound, int k, int mode, TableView t, BloomView bf,
                         DevCounters* ctr, hipStream_t s);
 // partitioned insert for modes 0 and 2 (same table, same result as launch_count)
-hipError_t launch_count_partitioned(const uint8_t* sym, uint64_t sym_bound, int k, int mode, TableView t,
+hipError_t launch_count_partitioned(PackedView sv, uint64_t sym_bound, int k, int mode, TableView t,
                                     BloomView bf, DevCounters* ctr, PartBufs pb, hipStream_t s);
 int run_width(int W);  // windows rolled per thread in the partitioned kernels
 hipError_t launch_dump(TableView t, int count_mode, uint64_t min_abundance, uint64_t* out, DevCounters* ctr,

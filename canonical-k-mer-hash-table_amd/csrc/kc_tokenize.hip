@@ -178,7 +178,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_tile_scan(const TileInfo* __re
 __global__ __launch_bounds__(TILE_THREADS) void k_emit(const uint8_t* __restrict__ stage,
                                                        const TileInfo* __restrict__ tiles,
                                                        const TileOut* __restrict__ touts, int fmt,
-                                                       uint8_t* __restrict__ sym) {
+                                                       uint64_t* __restrict__ pk, uint32_t* __restrict__ bk) {
     __shared__ uint8_t s_codes[TILE + 16];
     __shared__ uint32_t s_wsum[TILE_THREADS / 64];
     __shared__ uint32_t s_wmk[TILE_THREADS / 64];
@@ -233,22 +233,44 @@ __global__ __launch_bounds__(TILE_THREADS) void k_emit(const uint8_t* __restrict
     uint32_t incl = wave_incl_sum(kept);
     if (lane == 63) s_wsum[wid] = incl;
     __syncthreads();
-    uint32_t pos = incl - kept;
-    uint32_t total = 0;
+    // a chunk's first tile starts with the chunk-separating break
+    uint32_t pos = incl - kept + ti.first;
+    uint32_t total = ti.first;
     for (int w = 0; w < TILE_THREADS / 64; w++) {
         if (w < wid) pos += s_wsum[w];
         total += s_wsum[w];
     }
+    if (ti.first && tid == 0) s_codes[0] = SYM_BREAK;
 #pragma unroll
     for (int j = 0; j < 16; j++)
         if (codes[j] != 0xff) s_codes[pos++] = codes[j];
     __syncthreads();
-    uint8_t* dst = sym + to.out_off;
-    if (ti.first) {
-        if (tid == 0) dst[0] = SYM_BREAK;
-        dst += 1;
+    if (total == 0) return;
+    // pack: 32 symbols per word, symbol j of word w at bits 62-2j (codes) / 31-j (breaks);
+    // words shared with the neighbouring tiles are OR-ed into the zeroed buffers
+    const uint64_t g0 = to.out_off;
+    const uint64_t w_lo = g0 >> 5, w_hi = (g0 + total - 1) >> 5;
+    for (uint64_t w = w_lo + tid; w <= w_hi; w += TILE_THREADS) {
+        const int64_t l0 = (int64_t)(w << 5) - (int64_t)g0;
+        uint64_t pv = 0;
+        uint32_t bv = 0;
+#pragma unroll 8
+        for (int j = 0; j < 32; j++) {
+            const int64_t l = l0 + j;
+            if (l >= 0 && l < (int64_t)total) {
+                const uint8_t c = s_codes[l];
+                if (c > 3) bv |= 1u << (31 - j);
+                else pv |= (uint64_t)c << (62 - 2 * j);
+            }
+        }
+        if (l0 >= 0 && l0 + 32 <= (int64_t)total) {
+            pk[w] = pv;
+            bk[w] = bv;
+        } else {
+            if (pv) atomicOr((unsigned long long*)(pk + w), (unsigned long long)pv);
+            if (bv) atomicOr(bk + w, bv);
+        }
     }
-    for (uint32_t i = tid; i < total; i += TILE_THREADS) dst[i] = s_codes[i];
 }
 
 
@@ -298,13 +320,16 @@ hipError_t launch_gather(const uint8_t* src, uint8_t* stage, const ChunkDesc* d_
 }
 
 hipError_t launch_tokenize(const uint8_t* stage, uint64_t ntiles, const ChunkDesc* d_chunks, int n_chunks, int fmt,
-                           TileInfo* tiles, TileOut* touts, uint8_t* sym, uint64_t sym_cap, DevCounters* ctr,
+                           TileInfo* tiles, TileOut* touts, PackedView sv, uint64_t sym_bound, DevCounters* ctr,
                            hipStream_t s) {
-    (void)sym_cap;
+    const uint64_t words = sym_bound / 32 + 2;
+    hipError_t e;
+    if ((e = hipMemsetAsync(sv.pk, 0, words * 8, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(sv.bk, 0, words * 4, s)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_tile_summary, dim3((unsigned)ntiles), dim3(TILE_THREADS), 0, s, stage, d_chunks, n_chunks,
                        fmt, tiles);
     hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(SCAN_THREADS), 0, s, tiles, ntiles, fmt, touts, ctr);
-    hipLaunchKernelGGL(k_emit, dim3((unsigned)ntiles), dim3(TILE_THREADS), 0, s, stage, tiles, touts, fmt, sym);
+    hipLaunchKernelGGL(k_emit, dim3((unsigned)ntiles), dim3(TILE_THREADS), 0, s, stage, tiles, touts, fmt, sv.pk, sv.bk);
     return hipGetLastError();
 }
 
