@@ -68,6 +68,7 @@ struct kc_ctx {
     uint64_t nbuckets = 0;
     uint64_t R = 0;
     uint32_t F1 = 1, F2 = 1;
+    int rbits = 0, f1bits = 0;
 
     // partitioned insert buffers
     PartBufs pb{};
@@ -141,13 +142,14 @@ static int alloc_table(kc_ctx* c, uint64_t min_slots) {
     want = want + want / 4;
     const uint64_t buckets = (want + c->S - 1) / c->S;
     const uint64_t regions = std::max<uint64_t>(1, (buckets + BPR - 1) / BPR);
-    uint64_t f1 = 1;
-    while (f1 * f1 < regions && f1 < 1024) f1 *= 2;  // F1 ~ sqrt(R), a power of two
-    f1 = std::min<uint64_t>(f1, regions);
-    const uint64_t f2 = (regions + f1 - 1) / f1;
-    c->F1 = (uint32_t)f1;
-    c->F2 = (uint32_t)f2;
-    c->R = f1 * f2;
+    int rbits = 0;
+    while ((1ULL << rbits) < regions) rbits++;          // R = 2^rbits regions
+    const int f1bits = std::min(10, (rbits + 1) / 2);   // level-1 fan-out ~ sqrt(R), <= 1024
+    c->rbits = rbits;
+    c->f1bits = f1bits;
+    c->F1 = 1u << f1bits;
+    c->F2 = (uint32_t)(1ULL << (rbits - f1bits));
+    c->R = 1ULL << rbits;
     c->nbuckets = c->R * BPR;
     const size_t bytes = c->nbuckets * BUCKET_WORDS * sizeof(uint64_t);
     hipError_t e = hipMalloc(&c->d_table, bytes);
@@ -163,6 +165,8 @@ static TableView table_view(const kc_ctx* c) {
     tv.R = c->R;
     tv.F1 = c->F1;
     tv.F2 = c->F2;
+    tv.rbits = c->rbits;
+    tv.f1bits = c->f1bits;
     tv.W = c->W;
     tv.S = c->S;
     return tv;

@@ -35,16 +35,53 @@ DEV uint64_t key_hash(const uint64_t (&key)[W]) {
     for (int i = W - 2; i >= 0; i--) h = fmix64(h ^ key[i]);
     return h;
 }
-// hash-prefix owner of a key among `parts` shards: independent of the table's bits
-DEV uint32_t owner_of(uint64_t h, uint32_t parts) {
-    return (uint32_t)__umul64hi(fmix64(h ^ 0x13198a2e03707344ULL), parts);
+// ---- table keys -------------------------------------------------------------------
+// The table stores the canonical key through a bijection ("tkey"): word 0 becomes
+// fmix64(key0 ^ MIX_C ^ (g & M62)), g = a hash of the other words; words 1.. are kept.
+// The hash is computed once per window, every later level (bins, regions, buckets,
+// shard owner) is a bit field of tkey word 0, and k_dump inverts the mix.  key0 < 2^62
+// and MIX_C has bit 63 set, so the fmix64 argument is never 0 and neither is tkey word 0
+// (fmix64 is a bijection with fmix64(0) = 0): 0 marks an empty slot.
+constexpr uint64_t MIX_C = 0x9E3779B97F4A7C15ULL;  // bit 63 set
+constexpr uint64_t M62 = (1ULL << 62) - 1;
+
+DEV uint64_t fmix64_inv(uint64_t k) {
+    k ^= k >> 33;
+    k *= 0x9cb4b2f8129337dbULL;  // inverse of 0xc4ceb9fe1a85ec53
+    k ^= k >> 33;
+    k *= 0x4f74430c22a54005ULL;  // inverse of 0xff51afd7ed558ccd
+    k ^= k >> 33;
+    return k;
+}
+template <int W>
+DEV uint64_t side_hash(const uint64_t (&w)[W]) {
+    uint64_t g = 0;
+#pragma unroll
+    for (int i = 1; i < W; i++) g = fmix64(g ^ w[i] ^ (0x243f6a8885a308d3ULL * i));
+    return g & M62;
+}
+template <int W>
+DEV void to_tkey(const uint64_t (&key)[W], uint64_t (&t)[W]) {
+    t[0] = fmix64(key[0] ^ MIX_C ^ side_hash<W>(key));
+#pragma unroll
+    for (int i = 1; i < W; i++) t[i] = key[i];
+}
+template <int W>
+DEV void from_tkey(const uint64_t (&t)[W], uint64_t (&key)[W]) {
+#pragma unroll
+    for (int i = 1; i < W; i++) key[i] = t[i];
+    key[0] = fmix64_inv(t[0]) ^ MIX_C ^ side_hash<W>(t);
 }
 
 // ---- table geometry -------------------------------------------------------------
-// region = mulhi(h, R); bucket inside the region = mulhi(h * R, BPR); linear probing
+// region = top rbits of tkey word 0, bucket = the next BPR_BITS bits; linear probing
 // wraps inside the region, so a region is an independent table that fits in LDS.
-DEV uint64_t region_of(uint64_t h, uint64_t R) { return __umul64hi(h, R); }
-DEV uint32_t bucket_in_region(uint64_t h, uint64_t R) { return (uint32_t)__umul64hi(h * R, (uint64_t)BPR); }
+// The shard owner (multi-GPU) uses the low bits, independent of both.
+DEV uint64_t region_of(uint64_t t0, int rbits) { return rbits ? t0 >> (64 - rbits) : 0; }
+DEV uint32_t bucket_in_region(uint64_t t0, int rbits) {
+    return (uint32_t)(t0 >> (64 - rbits - BPR_BITS)) & (BPR - 1);
+}
+DEV uint32_t owner_of(uint64_t t0, uint32_t parts) { return (uint32_t)(((t0 & 0xFFFFFFFFULL) * parts) >> 32); }
 
 // wave-level inclusive scans (64 lanes)
 DEV uint32_t wave_incl_sum(uint32_t v) {

@@ -18,9 +18,10 @@
 //               table sweeps) instead of atomic-bound.
 //
 // Table layout (both paths): 128-byte buckets, keys [S][W] u64 then counts [S] u64,
-// S = 16/(W+1).  Word 0 of a stored key carries OCC (bit 63), so 0 is EMPTY.  A key
-// lives in region mulhi(h,R); its probe sequence starts at bucket mulhi(h*R, BPR) of
-// the region and wraps inside it.  W > 1 keys: word 0 claimed by CAS, other words
+// S = 16/(W+1).  Keys are stored as table keys (kc_common.h: word 0 = a bijective mix,
+// never 0, so 0 is EMPTY).  A key lives in the region given by the top bits of word 0;
+// its probe sequence starts at the bucket given by the next 9 bits and wraps inside
+// the region.  W > 1 keys: word 0 claimed by CAS, other words
 // stored, then READY|1 added to the count word; readers matching word 0 wait for READY.
 #include "kc_common.h"
 
@@ -29,14 +30,13 @@ namespace kc {
 __constant__ uint64_t c_bf_seeds[MAX_NH] = {2411, 3253, 1061, 1129, 2269, 7309, 3491, 8237, 6359, 8779};
 
 // --------------------------------------------------------------------------------
-// direct insert into the HBM table
+// direct insert of one table key into the HBM table
 // --------------------------------------------------------------------------------
 template <int W>
-DEV bool table_insert(const TableView& tv, const uint64_t (&key)[W], uint64_t h) {
+DEV bool table_insert(const TableView& tv, const uint64_t (&tk)[W]) {
     constexpr int S = BUCKET_WORDS / (W + 1);
-    const uint64_t region = region_of(h, tv.R);
-    uint32_t b = bucket_in_region(h, tv.R);
-    const uint64_t k0 = key[0] | OCC;
+    const uint64_t region = region_of(tk[0], tv.rbits);
+    uint32_t b = bucket_in_region(tk[0], tv.rbits);
     for (int probe = 0; probe < BPR; probe++) {
         uint64_t* bk = tv.buckets + (region * BPR + b) * BUCKET_WORDS;
         uint64_t w0[S];
@@ -59,13 +59,13 @@ DEV bool table_insert(const TableView& tv, const uint64_t (&key)[W], uint64_t h)
             uint64_t v0 = w0[s];
             if (v0 == EMPTY) {
                 const uint64_t old = atomicCAS((unsigned long long*)kp, (unsigned long long)EMPTY,
-                                               (unsigned long long)k0);
+                                               (unsigned long long)tk[0]);
                 if (old == EMPTY) {
                     if constexpr (W == 1) {
                         atomicAdd((unsigned long long*)cp, 1ULL);
                     } else {
 #pragma unroll
-                        for (int i = 1; i < W; i++) atomic_store_agent(kp + i, key[i]);
+                        for (int i = 1; i < W; i++) atomic_store_agent(kp + i, tk[i]);
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // words land before READY
                         atomicAdd((unsigned long long*)cp, (unsigned long long)(READY + 1));
                     }
@@ -74,7 +74,7 @@ DEV bool table_insert(const TableView& tv, const uint64_t (&key)[W], uint64_t h)
                 v0 = old;
                 w0[s] = old;
             }
-            if (v0 == k0) {
+            if (v0 == tk[0]) {
                 if constexpr (W == 1) {
                     atomicAdd((unsigned long long*)cp, 1ULL);
                     return true;
@@ -84,7 +84,7 @@ DEV bool table_insert(const TableView& tv, const uint64_t (&key)[W], uint64_t h)
                     asm volatile("" ::: "memory");
                     bool eq = true;
 #pragma unroll
-                    for (int i = 1; i < W; i++) eq &= atomic_load_agent(kp + i) == key[i];
+                    for (int i = 1; i < W; i++) eq &= atomic_load_agent(kp + i) == tk[i];
                     if (eq) {
                         atomicAdd((unsigned long long*)cp, 1ULL);
                         return true;
@@ -93,7 +93,7 @@ DEV bool table_insert(const TableView& tv, const uint64_t (&key)[W], uint64_t h)
             }
             s++;
         }
-        b = b + 1 == BPR ? 0 : b + 1;
+        b = (b + 1) & (BPR - 1);
     }
     return false;  // region full
 }
@@ -200,31 +200,32 @@ DEV void block_add4(unsigned long long v0, unsigned long long v1, unsigned long 
 // --------------------------------------------------------------------------------
 // windows of a tile
 // --------------------------------------------------------------------------------
+// per-thread windows of one tile (the tile is COUNT_THREADS * run_w windows)
 template <int W>
-constexpr int run_w() { return W == 1 ? 32 : (W == 2 ? 16 : 8); }
+constexpr int run_w() { return W == 1 ? 16 : (W == 2 ? 8 : 4); }
 template <int W>
 constexpr int tile_win() { return COUNT_THREADS * run_w<W>(); }
 
-// Calls f(fwd, rc, root) for every window whose last symbol is in [t0, t1):
-// MODE 0 extracts each window directly from the packed stream (consecutive lanes take
-// consecutive windows); MODE 1/2 roll one contiguous run per thread because the
-// Bloom root (RollingHasherDual mod 2^54) is a rolled quantity.
-template <int W, int MODE, class F>
-DEV void tile_windows(const PackedView& sv, uint64_t t0, uint64_t t1, const RollConst& rk, F&& f) {
-    if constexpr (MODE == 0) {
-        for (uint64_t p = t0 + threadIdx.x; p < t1; p += COUNT_THREADS) {
-            uint64_t fwd[W], rc[W];
-            if (!extract_window<W>(sv, p, rk, fwd)) continue;
-            revcomp<W>(fwd, rk, rc);
-            f(fwd, rc, 0ULL);
-        }
-    } else {
-        constexpr int RUNW = run_w<W>();
-        const uint64_t r0 = t0 + (uint64_t)threadIdx.x * RUNW, r1 = min(r0 + RUNW, t1);
-        if (r0 < r1) {
-            const uint64_t ps = r0 >= (uint64_t)(rk.k - 1) ? r0 - (rk.k - 1) : 0;
-            roll_run<W, true>(sv, ps, r0, r1, rk, f);
-        }
+// table key of the window ending at p (MODE 0 path: direct extraction)
+template <int W>
+DEV bool window_tkey(const PackedView& sv, uint64_t p, const RollConst& rk, uint64_t (&tk)[W]) {
+    uint64_t fwd[W], rc[W], key[W];
+    if (!extract_window<W>(sv, p, rk, fwd)) return false;
+    revcomp<W>(fwd, rk, rc);
+    canonical<W>(fwd, rc, key);
+    to_tkey<W>(key, tk);
+    return true;
+}
+
+// MODE 1/2: the Bloom root (RollingHasherDual mod 2^54) is a rolled quantity, so these
+// modes roll one contiguous run of run_w windows per thread.
+template <int W, class F>
+DEV void tile_rolled(const PackedView& sv, uint64_t t0, uint64_t t1, const RollConst& rk, F&& f) {
+    constexpr int RUNW = run_w<W>();
+    const uint64_t r0 = t0 + (uint64_t)threadIdx.x * RUNW, r1 = min(r0 + RUNW, t1);
+    if (r0 < r1) {
+        const uint64_t ps = r0 >= (uint64_t)(rk.k - 1) ? r0 - (rk.k - 1) : 0;
+        roll_run<W, true>(sv, ps, r0, r1, rk, f);
     }
 }
 
@@ -241,22 +242,31 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_count(PackedView sv, int k, T
     uint32_t n_win = 0, n_ins = 0, n_fail = 0;
     BloomLocal bl = {0, 0, 0};
     if (t0 < M) {
+        const uint64_t t1 = min(t0 + TW, M);
         const RollConst rk = make_roll<W>(k, pow5_k, pow5_km1);
-        tile_windows<W, MODE>(sv, t0, min(t0 + TW, M), rk,
-                              [&](const uint64_t (&fwd)[W], const uint64_t (&rc)[W], uint64_t root) {
-            n_win++;
-            if constexpr (MODE == 1) {
-                bloom_insert(bf, root, bl);
-            } else {
-                if constexpr (MODE == 2) {
-                    if (!bloom_gate(bf, root)) return;
-                }
-                uint64_t key[W];
-                canonical<W>(fwd, rc, key);
+        if constexpr (MODE == 0) {
+            for (uint64_t p = t0 + threadIdx.x; p < t1; p += COUNT_THREADS) {
+                uint64_t tk[W];
+                if (!window_tkey<W>(sv, p, rk, tk)) continue;
+                n_win++;
                 n_ins++;
-                if (!table_insert<W>(tv, key, key_hash<W>(key))) n_fail++;
+                if (!table_insert<W>(tv, tk)) n_fail++;
             }
-        });
+        } else {
+            tile_rolled<W>(sv, t0, t1, rk, [&](const uint64_t (&fwd)[W], const uint64_t (&rc)[W], uint64_t root) {
+                n_win++;
+                if constexpr (MODE == 1) {
+                    bloom_insert(bf, root, bl);
+                } else {
+                    if (!bloom_gate(bf, root)) return;
+                    uint64_t key[W], tk[W];
+                    canonical<W>(fwd, rc, key);
+                    to_tkey<W>(key, tk);
+                    n_ins++;
+                    if (!table_insert<W>(tv, tk)) n_fail++;
+                }
+            });
+        }
     }
     if constexpr (MODE == 1)
         block_add4(n_win, bl.new_first, bl.new_second, bl.failed, &ctr->bf_windows, &ctr->new_in_first,
@@ -268,13 +278,14 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_count(PackedView sv, int k, T
 // --------------------------------------------------------------------------------
 // partitioned path
 // --------------------------------------------------------------------------------
+// LDS of a scatter pass: tilehist, tilestart, tilecur (u32 x F), gbase (u64 x F), keys
 constexpr size_t hist_smem(uint32_t F) { return ((size_t)F * 3 + 1) * 4 + 4 + (size_t)F * 8; }
 template <int W>
-constexpr size_t part_smem(uint32_t F) {  // tilehist, tilestart, tilecur (u32), gbase (u64), keys
-    return ((size_t)F * 3 + 1) * 4 + 4 + (size_t)F * 8 + (size_t)tile_win<W>() * 8 * W;
+constexpr size_t part_smem(uint32_t F) {
+    return hist_smem(F) + (size_t)tile_win<W>() * 8 * W;
 }
 
-// exclusive scan of an LDS u32 array of n entries (n <= 4096) by one 256-thread block
+// exclusive scan of an LDS u32 array of n entries by one COUNT_THREADS block
 DEV void block_excl_scan_lds(const uint32_t* in, uint32_t* out, uint32_t n) {
     __shared__ uint32_t s_w[COUNT_THREADS / 64];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -295,101 +306,146 @@ DEV void block_excl_scan_lds(const uint32_t* in, uint32_t* out, uint32_t n) {
     __syncthreads();
 }
 
-// Level 1: windows of a contiguous symbol range -> coarse bins mulhi(h, F1).
+struct PartLds {
+    uint32_t* hist;
+    uint32_t* start;
+    uint32_t* cur;
+    uint64_t* gbase;
+    uint64_t* keys;
+};
+DEV PartLds part_lds(uint8_t* smem, uint32_t F) {
+    PartLds l;
+    l.hist = reinterpret_cast<uint32_t*>(smem);
+    l.start = l.hist + F;
+    l.cur = l.start + F;
+    l.gbase = reinterpret_cast<uint64_t*>(l.cur + F + (F & 1));
+    l.keys = l.gbase + F;
+    return l;
+}
+
+// Counting-sort the tile's keys (in registers: tk[j] valid where ok[j]) by bin into
+// LDS and write each bin as one contiguous run at gbase[bin]; bin = bit field of tk[.][0].
+template <int W, int RUNW>
+DEV void scatter_tile(const PartLds& l, uint32_t F, int shift, uint32_t fmask, const uint64_t (&tk)[RUNW][W],
+                      const bool (&ok)[RUNW], uint64_t* __restrict__ out) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < RUNW; j++)
+        if (ok[j]) atomicAdd(&l.hist[(uint32_t)(tk[j][0] >> shift) & fmask], 1u);
+    __syncthreads();
+    block_excl_scan_lds(l.hist, l.start, F);
+    for (uint32_t b = tid; b < F; b += COUNT_THREADS) l.cur[b] = l.start[b];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < RUNW; j++)
+        if (ok[j]) {
+            const uint32_t slot = atomicAdd(&l.cur[(uint32_t)(tk[j][0] >> shift) & fmask], 1u);
+#pragma unroll
+            for (int w = 0; w < W; w++) l.keys[slot * W + w] = tk[j][w];
+        }
+    __syncthreads();
+    const uint32_t n = l.start[F - 1] + l.hist[F - 1];
+    for (uint32_t i = tid; i < n; i += COUNT_THREADS) {
+        uint64_t key[W];
+#pragma unroll
+        for (int w = 0; w < W; w++) key[w] = l.keys[i * W + w];
+        const uint32_t b = (uint32_t)(key[0] >> shift) & fmask;
+        const uint64_t dst = l.gbase[b] + (i - l.start[b]);
+#pragma unroll
+        for (int w = 0; w < W; w++) out[dst * W + w] = key[w];
+    }
+    __syncthreads();
+    for (uint32_t b = tid; b < F; b += COUNT_THREADS) {
+        l.gbase[b] += l.hist[b];
+        l.hist[b] = 0;
+    }
+    __syncthreads();
+}
+
+// Level 1: windows of a contiguous symbol range -> coarse bins (top f1bits of tkey[0]).
 // SCATTER = false: histogram only ([bin][block] into hist1); true: write the keys.
 template <int W, int MODE, bool SCATTER>
 __global__ __launch_bounds__(COUNT_THREADS) void k_p1(PackedView sv, int k, TableView tv, BloomView bf,
                                                       DevCounters* __restrict__ ctr, PartBufs pb, uint64_t pow5_k,
                                                       uint64_t pow5_km1) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    constexpr int TW = tile_win<W>();
+    constexpr int RUNW = run_w<W>(), TW = tile_win<W>();
     const uint32_t F = tv.F1;
-    uint32_t* tilehist = reinterpret_cast<uint32_t*>(smem);
-    uint32_t* tilestart = tilehist + F;
-    uint32_t* tilecur = tilestart + F;
-    uint64_t* gbase = reinterpret_cast<uint64_t*>(tilecur + F + (F & 1));
-    uint64_t* lkeys = gbase + F;
+    const int shift = tv.f1bits ? 64 - tv.f1bits : 63;  // F == 1: every key in bin 0
+    const uint32_t fmask = F - 1;
+    const PartLds l = part_lds(smem, F);
     const int tid = threadIdx.x;
     const uint64_t M = ctr->stream_len;
-    const uint64_t per = (M + pb.nblk1 - 1) / pb.nblk1;
+    const uint64_t per = ((M + pb.nblk1 - 1) / pb.nblk1 + TW - 1) / TW * TW;
     const uint64_t lo = min(M, (uint64_t)blockIdx.x * per), hi = min(M, lo + per);
     for (uint32_t b = tid; b < F; b += COUNT_THREADS) {
-        tilehist[b] = 0;
-        if constexpr (SCATTER) gbase[b] = pb.off1[(uint64_t)b * pb.nblk1 + blockIdx.x];
+        l.hist[b] = 0;
+        if constexpr (SCATTER) l.gbase[b] = pb.off1[(uint64_t)b * pb.nblk1 + blockIdx.x];
     }
     __syncthreads();
     const RollConst rk = make_roll<W>(k, pow5_k, pow5_km1);
     uint32_t n_win = 0, n_ins = 0;
     for (uint64_t t0 = lo; t0 < hi; t0 += TW) {
         const uint64_t t1 = min(t0 + TW, hi);
-        // (a) histogram of this tile
-        tile_windows<W, MODE == 0 ? 0 : 2>(sv, t0, t1, rk,
-                                          [&](const uint64_t (&fwd)[W], const uint64_t (&rc)[W], uint64_t root) {
-            if constexpr (!SCATTER) n_win++;
-            if constexpr (MODE == 2) {
-                if (!bloom_gate(bf, root)) return;
-            }
-            uint64_t key[W];
-            canonical<W>(fwd, rc, key);
-            if constexpr (!SCATTER) n_ins++;
-            atomicAdd(&tilehist[(uint32_t)__umul64hi(key_hash<W>(key), F)], 1u);
-        });
-        if constexpr (SCATTER) {
-            __syncthreads();
-            block_excl_scan_lds(tilehist, tilestart, F);
-            for (uint32_t b = tid; b < F; b += COUNT_THREADS) tilecur[b] = tilestart[b];
-            __syncthreads();
-            // (b) place keys in bin order in LDS
-            tile_windows<W, MODE == 0 ? 0 : 2>(sv, t0, t1, rk,
-                                              [&](const uint64_t (&fwd)[W], const uint64_t (&rc)[W], uint64_t root) {
-                if constexpr (MODE == 2) {
-                    if (!bloom_gate(bf, root)) return;
+        uint64_t tk[RUNW][W];
+        bool ok[RUNW];
+        if constexpr (MODE == 0) {
+#pragma unroll
+            for (int j = 0; j < RUNW; j++) {
+                const uint64_t p = t0 + tid + (uint64_t)j * COUNT_THREADS;
+                ok[j] = p < t1 && window_tkey<W>(sv, p, rk, tk[j]);
+                if constexpr (!SCATTER) {
+                    n_win += ok[j];
+                    n_ins += ok[j];
                 }
-                uint64_t key[W];
+            }
+        } else {
+            // rolled run: slot j <- the j-th symbol of the thread's run (static indices)
+#pragma unroll
+            for (int j = 0; j < RUNW; j++) ok[j] = false;
+            tile_rolled<W>(sv, t0, t1, rk, [&](const uint64_t (&fwd)[W], const uint64_t (&rc)[W], uint64_t root) {
+                (void)fwd;
+                if constexpr (!SCATTER) n_win++;
+                if (!bloom_gate(bf, root)) return;
+                if constexpr (!SCATTER) n_ins++;
+                uint64_t key[W], t[W];
                 canonical<W>(fwd, rc, key);
-                const uint32_t b = (uint32_t)__umul64hi(key_hash<W>(key), F);
-                const uint32_t slot = atomicAdd(&tilecur[b], 1u);
+                to_tkey<W>(key, t);
+                // at most run_w windows per run: append into the first free register slot
 #pragma unroll
-                for (int i = 0; i < W; i++) lkeys[slot * W + i] = key[i];
+                for (int j = 0; j < RUNW; j++)
+                    if (!ok[j]) {
+                        ok[j] = true;
+#pragma unroll
+                        for (int w = 0; w < W; w++) tk[j][w] = t[w];
+                        break;
+                    }
             });
-            __syncthreads();
-            // (c) contiguous runs per bin -> global
-            const uint32_t n = tilestart[F - 1] + tilehist[F - 1];
-            for (uint32_t i = tid; i < n; i += COUNT_THREADS) {
-                uint64_t key[W];
+        }
+        if constexpr (SCATTER) {
+            scatter_tile<W, RUNW>(l, F, shift, fmask, tk, ok, pb.keys1);
+        } else {
 #pragma unroll
-                for (int w = 0; w < W; w++) key[w] = lkeys[i * W + w];
-                const uint32_t b = (uint32_t)__umul64hi(key_hash<W>(key), F);
-                const uint64_t dst = gbase[b] + (i - tilestart[b]);
-#pragma unroll
-                for (int w = 0; w < W; w++) pb.keys1[dst * W + w] = key[w];
-            }
-            __syncthreads();
-            for (uint32_t b = tid; b < F; b += COUNT_THREADS) {
-                gbase[b] += tilehist[b];
-                tilehist[b] = 0;
-            }
-            __syncthreads();
+            for (int j = 0; j < RUNW; j++)
+                if (ok[j]) atomicAdd(&l.hist[(uint32_t)(tk[j][0] >> shift) & fmask], 1u);
         }
     }
     if constexpr (!SCATTER) {
         __syncthreads();
-        for (uint32_t b = tid; b < F; b += COUNT_THREADS) pb.hist1[(uint64_t)b * pb.nblk1 + blockIdx.x] = tilehist[b];
+        for (uint32_t b = tid; b < F; b += COUNT_THREADS) pb.hist1[(uint64_t)b * pb.nblk1 + blockIdx.x] = l.hist[b];
         block_add4(n_win, n_ins, 0, 0, &ctr->windows, &ctr->inserted, nullptr, nullptr);
     }
 }
 
-// Level 2: coarse bin c (block = c * B2 + j) -> its F2 regions.
+// Level 2: coarse bin c (block = c * B2 + j) -> its F2 regions (next bits of tkey[0]).
 template <int W, bool SCATTER>
 __global__ __launch_bounds__(COUNT_THREADS) void k_p2(TableView tv, PartBufs pb) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    constexpr int TW = tile_win<W>();
+    constexpr int RUNW = run_w<W>(), TW = tile_win<W>();
     const uint32_t F = tv.F2;
-    uint32_t* tilehist = reinterpret_cast<uint32_t*>(smem);
-    uint32_t* tilestart = tilehist + F;
-    uint32_t* tilecur = tilestart + F;
-    uint64_t* gbase = reinterpret_cast<uint64_t*>(tilecur + F + (F & 1));
-    uint64_t* lkeys = gbase + F;
+    const int shift = tv.rbits ? 64 - tv.rbits : 63;
+    const uint32_t fmask = F - 1;
+    const PartLds l = part_lds(smem, F);
     const int tid = threadIdx.x;
     const uint32_t c = blockIdx.x / pb.B2, j = blockIdx.x % pb.B2;
     const uint64_t cs = pb.off1[(uint64_t)c * pb.nblk1], ce = pb.off1[(uint64_t)(c + 1) * pb.nblk1];
@@ -397,57 +453,39 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_p2(TableView tv, PartBufs pb)
     const uint64_t lo = min(ce, cs + j * part), hi = min(ce, lo + part);
     const uint64_t rbase = (uint64_t)c * F;
     for (uint32_t b = tid; b < F; b += COUNT_THREADS) {
-        tilehist[b] = 0;
-        if constexpr (SCATTER) gbase[b] = pb.off2[(rbase + b) * pb.B2 + j];
+        l.hist[b] = 0;
+        if constexpr (SCATTER) l.gbase[b] = pb.off2[(rbase + b) * pb.B2 + j];
     }
     __syncthreads();
     for (uint64_t t0 = lo; t0 < hi; t0 += TW) {
-        const uint32_t n = (uint32_t)min((uint64_t)TW, hi - t0);
-        // (a) histogram of this tile
-        for (uint32_t i = tid; i < n; i += COUNT_THREADS) {
-            uint64_t key[W];
+        uint64_t tk[RUNW][W];
+        bool ok[RUNW];
 #pragma unroll
-            for (int w = 0; w < W; w++) key[w] = pb.keys1[(t0 + i) * W + w];
-            atomicAdd(&tilehist[(uint32_t)(region_of(key_hash<W>(key), tv.R) - rbase)], 1u);
+        for (int q = 0; q < RUNW; q++) {
+            const uint64_t i = t0 + tid + (uint64_t)q * COUNT_THREADS;
+            ok[q] = i < hi;
+#pragma unroll
+            for (int w = 0; w < W; w++) tk[q][w] = ok[q] ? pb.keys1[i * W + w] : 0;
         }
         if constexpr (SCATTER) {
-            __syncthreads();
-            block_excl_scan_lds(tilehist, tilestart, F);
-            for (uint32_t b = tid; b < F; b += COUNT_THREADS) tilecur[b] = tilestart[b];
-            __syncthreads();
-            // (b) counting sort into LDS (the tile is re-read from L2)
-            for (uint32_t i = tid; i < n; i += COUNT_THREADS) {
-                uint64_t key[W];
+            scatter_tile<W, RUNW>(l, F, shift, fmask, tk, ok, pb.keys2);
+        } else {
 #pragma unroll
-                for (int w = 0; w < W; w++) key[w] = pb.keys1[(t0 + i) * W + w];
-                const uint32_t f = (uint32_t)(region_of(key_hash<W>(key), tv.R) - rbase);
-                const uint32_t slot = atomicAdd(&tilecur[f], 1u);
-#pragma unroll
-                for (int w = 0; w < W; w++) lkeys[slot * W + w] = key[w];
-            }
-            __syncthreads();
-            // (c) contiguous runs per region -> global
-            for (uint32_t i = tid; i < n; i += COUNT_THREADS) {
-                uint64_t key[W];
-#pragma unroll
-                for (int w = 0; w < W; w++) key[w] = lkeys[i * W + w];
-                const uint32_t f = (uint32_t)(region_of(key_hash<W>(key), tv.R) - rbase);
-                const uint64_t dst = gbase[f] + (i - tilestart[f]);
-#pragma unroll
-                for (int w = 0; w < W; w++) pb.keys2[dst * W + w] = key[w];
-            }
-            __syncthreads();
-            for (uint32_t b = tid; b < F; b += COUNT_THREADS) {
-                gbase[b] += tilehist[b];
-                tilehist[b] = 0;
-            }
-            __syncthreads();
+            for (int q = 0; q < RUNW; q++)
+                if (ok[q]) atomicAdd(&l.hist[(uint32_t)(tk[q][0] >> shift) & fmask], 1u);
         }
     }
     if constexpr (!SCATTER) {
         __syncthreads();
-        for (uint32_t b = tid; b < F; b += COUNT_THREADS) pb.hist2[(rbase + b) * pb.B2 + j] = tilehist[b];
+        for (uint32_t b = tid; b < F; b += COUNT_THREADS) pb.hist2[(rbase + b) * pb.B2 + j] = l.hist[b];
     }
+}
+
+// LDS image of a region: the 16-byte chunks of each 128-byte bucket are XOR-swizzled
+// with the bucket index so that lanes probing random buckets spread over the banks.
+DEV uint32_t lds_chunk(uint32_t b, uint32_t q) { return b * 8 + (q ^ (b & 7)); }
+DEV uint64_t* lds_word(uint64_t* lt, uint32_t b, uint32_t word) {
+    return lt + lds_chunk(b, word >> 1) * 2 + (word & 1);
 }
 
 // Level 3: one workgroup per region: LDS-resident table
@@ -455,6 +493,7 @@ template <int W>
 __global__ __launch_bounds__(COUNT_THREADS) void k_p3(TableView tv, PartBufs pb, DevCounters* __restrict__ ctr) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int S = BUCKET_WORDS / (W + 1);
+    constexpr int KB = 8;  // keys loaded per thread before inserting (memory-level parallelism)
     uint64_t* lt = reinterpret_cast<uint64_t*>(smem);  // BPR * BUCKET_WORDS words
     const uint64_t r = blockIdx.x;
     const uint64_t start = pb.off2[r * pb.B2], end = pb.off2[(r + 1) * pb.B2];
@@ -462,83 +501,90 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_p3(TableView tv, PartBufs pb,
     uint4* g4 = reinterpret_cast<uint4*>(tv.buckets + r * BPR * BUCKET_WORDS);
     uint4* l4 = reinterpret_cast<uint4*>(lt);
     constexpr int N4 = BPR * BUCKET_WORDS / 2;
-    for (int i = threadIdx.x; i < N4; i += COUNT_THREADS) l4[i] = g4[i];
+    for (int i = threadIdx.x; i < N4; i += COUNT_THREADS) l4[lds_chunk(i >> 3, i & 7)] = g4[i];
     __syncthreads();
     uint32_t n_fail = 0;
-    for (uint64_t i = start + threadIdx.x; i < end; i += COUNT_THREADS) {
-        uint64_t key[W];
+    for (uint64_t base = start; base < end; base += (uint64_t)KB * COUNT_THREADS) {
+        uint64_t kk[KB][W];
 #pragma unroll
-        for (int w = 0; w < W; w++) key[w] = pb.keys2[i * W + w];
-        const uint64_t h = key_hash<W>(key);
-        uint32_t b = bucket_in_region(h, tv.R);
-        const uint64_t k0 = key[0] | OCC;
-        bool done = false;
-        for (int probe = 0; probe < BPR && !done; probe++) {
-            uint64_t* bk = lt + b * BUCKET_WORDS;
-            uint64_t w0[S];
-            if constexpr (W == 1) {
-                const uint4* b4 = reinterpret_cast<const uint4*>(bk);
+        for (int q = 0; q < KB; q++) {
+            const uint64_t i = base + threadIdx.x + (uint64_t)q * COUNT_THREADS;
 #pragma unroll
-                for (int q = 0; q < S / 2; q++) {
-                    const uint4 v = b4[q];
-                    w0[2 * q] = ((uint64_t)v.y << 32) | v.x;
-                    w0[2 * q + 1] = ((uint64_t)v.w << 32) | v.z;
-                }
-            } else {
+            for (int w = 0; w < W; w++) kk[q][w] = i < end ? pb.keys2[i * W + w] : 0;
+        }
 #pragma unroll
-                for (int q = 0; q < S; q++) w0[q] = bk[q * W];
-            }
-            int s = 0;
-            while (s < S) {
-                uint64_t* kp = bk + s * W;
-                unsigned long long* cp = reinterpret_cast<unsigned long long*>(bk + S * W + s);
-                uint64_t v0 = w0[s];
-                if (v0 == EMPTY) {
-                    const uint64_t old = atomicCAS((unsigned long long*)kp, 0ULL, (unsigned long long)k0);
-                    if (old == EMPTY) {
-                        if constexpr (W == 1) {
-                            atomicAdd(cp, 1ULL);
-                        } else {
+        for (int q = 0; q < KB; q++) {
+            if (base + threadIdx.x + (uint64_t)q * COUNT_THREADS >= end) continue;
+            const uint64_t k0 = kk[q][0];
+            uint32_t b = bucket_in_region(k0, tv.rbits);
+            bool done = false;
+            for (int probe = 0; probe < BPR && !done; probe++) {
+                uint64_t w0[S];
+                if constexpr (W == 1) {
 #pragma unroll
-                            for (int w = 1; w < W; w++)
-                                __hip_atomic_store(kp + w, key[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                            atomicAdd(cp, (unsigned long long)(READY + 1));
-                        }
-                        done = true;
-                        break;
+                    for (int c = 0; c < S / 2; c++) {
+                        const uint4 v = l4[lds_chunk(b, c)];
+                        w0[2 * c] = ((uint64_t)v.y << 32) | v.x;
+                        w0[2 * c + 1] = ((uint64_t)v.w << 32) | v.z;
                     }
-                    v0 = old;
-                    w0[s] = old;
-                }
-                if (v0 == k0) {
-                    if constexpr (W == 1) {
-                        atomicAdd(cp, 1ULL);
-                        done = true;
-                        break;
-                    } else {
-                        const uint64_t c = __hip_atomic_load(cp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        if (!(c & READY)) continue;  // claimed by another lane, words not published yet
-                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                        bool eq = true;
+                } else {
 #pragma unroll
-                        for (int w = 1; w < W; w++)
-                            eq &= __hip_atomic_load(kp + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == key[w];
-                        if (eq) {
-                            atomicAdd(cp, 1ULL);
+                    for (int c = 0; c < S; c++) w0[c] = *lds_word(lt, b, c * W);
+                }
+                int s = 0;
+                while (s < S) {
+                    uint64_t* kp = lds_word(lt, b, s * W);
+                    unsigned long long* cp = reinterpret_cast<unsigned long long*>(lds_word(lt, b, S * W + s));
+                    uint64_t v0 = w0[s];
+                    if (v0 == EMPTY) {
+                        const uint64_t old = atomicCAS((unsigned long long*)kp, 0ULL, (unsigned long long)k0);
+                        if (old == EMPTY) {
+                            if constexpr (W == 1) {
+                                atomicAdd(cp, 1ULL);
+                            } else {
+#pragma unroll
+                                for (int w = 1; w < W; w++)
+                                    __hip_atomic_store(lds_word(lt, b, s * W + w), kk[q][w], __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+                                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                                atomicAdd(cp, (unsigned long long)(READY + 1));
+                            }
                             done = true;
                             break;
                         }
+                        v0 = old;
+                        w0[s] = old;
                     }
+                    if (v0 == k0) {
+                        if constexpr (W == 1) {
+                            atomicAdd(cp, 1ULL);
+                            done = true;
+                            break;
+                        } else {
+                            const uint64_t cv = __hip_atomic_load(cp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            if (!(cv & READY)) continue;  // claimed by another lane, words not published yet
+                            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                            bool eq = true;
+#pragma unroll
+                            for (int w = 1; w < W; w++)
+                                eq &= __hip_atomic_load(lds_word(lt, b, s * W + w), __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_WORKGROUP) == kk[q][w];
+                            if (eq) {
+                                atomicAdd(cp, 1ULL);
+                                done = true;
+                                break;
+                            }
+                        }
+                    }
+                    s++;
                 }
-                s++;
+                b = (b + 1) & (BPR - 1);
             }
-            b = b + 1 == BPR ? 0 : b + 1;
+            if (!done) n_fail++;
         }
-        if (!done) n_fail++;
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < N4; i += COUNT_THREADS) g4[i] = l4[i];
+    for (int i = threadIdx.x; i < N4; i += COUNT_THREADS) g4[i] = l4[lds_chunk(i >> 3, i & 7)];
     if (n_fail) atomicAdd(&ctr->overflow, (unsigned long long)n_fail);
 }
 
@@ -603,9 +649,13 @@ __global__ __launch_bounds__(256) void k_dump(TableView tv, int count_mode, uint
 #pragma unroll
     for (int s = 0; s < S; s++)
         if (out && emit[s]) {
+            uint64_t t[W], key[W];
+#pragma unroll
+            for (int i = 0; i < W; i++) t[i] = b[s * W + i];
+            from_tkey<W>(t, key);
             uint64_t* o = out + idx * (W + 1);
 #pragma unroll
-            for (int i = 0; i < W; i++) o[i] = b[s * W + i] & (i == 0 ? ~OCC : ~0ULL);
+            for (int i = 0; i < W; i++) o[i] = key[i];
             o[W] = tv_c[s];
             idx++;
         }
@@ -623,7 +673,7 @@ static uint64_t pow5_mod54(int e) {
     return r;
 }
 
-int run_width(int W) { return W == 1 ? 32 : (W == 2 ? 16 : 8); }
+int run_width(int W) { return W == 1 ? 16 : (W == 2 ? 8 : 4); }
 
 template <int W>
 static hipError_t launch_count_w(PackedView sym, uint64_t sym_bound, int k, int mode, TableView t, BloomView bf,

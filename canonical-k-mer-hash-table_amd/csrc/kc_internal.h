@@ -15,9 +15,9 @@ constexpr int TILE_THREADS = 256;          // 16 bytes per thread
 constexpr int COUNT_THREADS = 256;
 constexpr int RUN = 32;                    // consecutive symbols rolled per thread
 constexpr int BUCKET_WORDS = 16;           // 128-byte buckets
-constexpr int BPR = 512;                   // buckets per region: 64 KiB, one LDS-resident table
-constexpr uint64_t EMPTY = 0;              // empty slot: word 0 of a stored key carries OCC
-constexpr uint64_t OCC = 1ULL << 63;       // word 0 always has spare top bits (W = k/32 + 1)
+constexpr int BPR = 512;                   // buckets per region: 64 KiB, one LDS-resident table (2^BPR_BITS)
+constexpr uint64_t EMPTY = 0;              // empty slot (a stored word 0 is never 0, see kc_common.h)
+constexpr int BPR_BITS = 9;
 constexpr uint64_t READY = 1ULL << 62;     // multi-word slot published flag, in the count word
 constexpr uint64_t CNT_MASK = READY - 1;
 constexpr int MAX_NH = 10;                 // -f >= 0.001  =>  ceil(-ln f / ln 2) <= 10
@@ -75,8 +75,9 @@ struct PackedView {
 struct TableView {
     uint64_t* buckets;      // nbuckets * BUCKET_WORDS
     uint64_t nbuckets;      // R * BPR
-    uint64_t R;             // regions = F1 * F2
-    uint32_t F1, F2;        // partition fan-outs of the two scatter levels
+    uint64_t R;             // regions = F1 * F2 = 2^rbits
+    uint32_t F1, F2;        // partition fan-outs of the two scatter levels (powers of two)
+    int rbits, f1bits;      // log2 R, log2 F1
     int W;                  // key words
     int S;                  // slots per bucket
 };
