@@ -271,4 +271,78 @@ DEV void canonical(const uint64_t (&fwd)[W], const uint64_t (&rc)[W], uint64_t (
     for (int i = 0; i < W; i++) key[i] = fwd_le ? fwd[i] : rc[i];
 }
 
+
+// Table keys of the RUNW consecutive windows ending at r0 .. r0+RUNW-1: the state of
+// the window ending at r0-1 is extracted in O(1) (funnel shifts + the position of the
+// last break), then RUNW unrolled rolling steps (kmer_factory.cpp:172-239) produce the
+// rest, so every slot index is static.  ok[j] is false for windows that contain a
+// break or end at or beyond t1.
+template <int W, int RUNW, class G>
+DEV void run_windows(const PackedView& sv, uint64_t r0, uint64_t t1, const RollConst& rk, G&& emit) {
+    static_assert(RUNW <= 32, "run must fit two packed words");
+    const int k = rk.k;
+    uint64_t fwd[W], rc[W];
+    int since;  // consecutive non-break symbols ending at r0-1, capped at k
+    {
+        // symbols [r0-k, r0-1]: words wl-W..wl of the packed stream
+        const int64_t last = (int64_t)r0 - 1;
+        if (last < 0) {
+#pragma unroll
+            for (int i = 0; i < W; i++) fwd[i] = 0;
+            since = 0;
+        } else {
+            const uint64_t wl = (uint64_t)last >> 5;
+            const int s = 2 * ((int)(last & 31) + 1);
+            uint64_t lo = sv.pk[wl];
+#pragma unroll
+            for (int i = 0; i < W; i++) {
+                const uint64_t hi = wl >= (uint64_t)(i + 1) ? sv.pk[wl - i - 1] : 0;
+                fwd[W - 1 - i] = s == 64 ? lo : ((hi << s) | (lo >> (64 - s)));
+                lo = hi;
+            }
+            fwd[0] &= rk.topmask;
+            // last break at or before `last`, looking back at most k symbols
+            const int64_t first = last - k + 1;
+            since = k;
+            const int64_t wfirst = first < 0 ? 0 : (first >> 5);
+            for (int64_t w = (int64_t)wl; w >= wfirst; w--) {
+                uint32_t m = sv.bk[w];
+                if (w == (int64_t)wl) m &= 0xFFFFFFFFu << (31 - (last & 31));
+                if (m) {
+                    const int64_t q = (w << 5) + (31 - __builtin_ctz(m));  // highest-index break in word w
+                    since = (int)min((int64_t)k, last - q);
+                    break;
+                }
+            }
+            if (first < 0 && since > last + 1) since = (int)(last + 1);  // the stream starts at 0
+        }
+        revcomp<W>(fwd, rk, rc);
+    }
+    const uint64_t wa = r0 >> 5;
+    const uint64_t pa = sv.pk[wa], pb = sv.pk[wa + 1];
+    const uint32_t ba = sv.bk[wa], bb = sv.bk[wa + 1];
+    const int o0 = (int)(r0 & 31);
+#pragma unroll
+    for (int j = 0; j < RUNW; j++) {
+        const int o = o0 + j;
+        const uint64_t pw = o < 32 ? pa : pb;
+        const uint32_t bw = o < 32 ? ba : bb;
+        const int oo = o & 31;
+        const uint32_t c = (uint32_t)(pw >> (62 - 2 * oo)) & 3;
+        const bool br = (bw >> (31 - oo)) & 1;
+        since = br ? 0 : min(since + 1, k);
+#pragma unroll
+        for (int i = 0; i < W - 1; i++) fwd[i] = (fwd[i] << 2) | (fwd[i + 1] >> 62);
+        fwd[W - 1] = (fwd[W - 1] << 2) | c;
+        fwd[0] &= rk.topmask;
+#pragma unroll
+        for (int i = W - 1; i >= 1; i--) rc[i] = (rc[i] >> 2) | (rc[i - 1] << 62);
+        rc[0] >>= 2;
+#pragma unroll
+        for (int i = 0; i < W; i++)
+            if (i == rk.rc_word) rc[i] |= (uint64_t)(3 - c) << rk.rc_bit;
+        emit(j, r0 + j < t1 && since >= k, fwd, rc);
+    }
+}
+
 }  // namespace kc

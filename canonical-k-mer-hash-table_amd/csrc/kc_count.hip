@@ -245,13 +245,19 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_count(PackedView sv, int k, T
         const uint64_t t1 = min(t0 + TW, M);
         const RollConst rk = make_roll<W>(k, pow5_k, pow5_km1);
         if constexpr (MODE == 0) {
-            for (uint64_t p = t0 + threadIdx.x; p < t1; p += COUNT_THREADS) {
-                uint64_t tk[W];
-                if (!window_tkey<W>(sv, p, rk, tk)) continue;
-                n_win++;
-                n_ins++;
-                if (!table_insert<W>(tv, tk)) n_fail++;
-            }
+            constexpr int RUNW = run_w<W>();
+            const uint64_t r0 = t0 + (uint64_t)threadIdx.x * RUNW;
+            if (r0 < t1)
+                run_windows<W, RUNW>(sv, r0, t1, rk,
+                                     [&](int, bool valid, const uint64_t (&fwd)[W], const uint64_t (&rc)[W]) {
+                    if (!valid) return;
+                    uint64_t key[W], tk[W];
+                    canonical<W>(fwd, rc, key);
+                    to_tkey<W>(key, tk);
+                    n_win++;
+                    n_ins++;
+                    if (!table_insert<W>(tv, tk)) n_fail++;
+                });
         } else {
             tile_rolled<W>(sv, t0, t1, rk, [&](const uint64_t (&fwd)[W], const uint64_t (&rc)[W], uint64_t root) {
                 n_win++;
@@ -390,11 +396,20 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_p1(PackedView sv, int k, Tabl
         uint64_t tk[RUNW][W];
         bool ok[RUNW];
         if constexpr (MODE == 0) {
+            const uint64_t r0 = t0 + (uint64_t)tid * RUNW;
 #pragma unroll
-            for (int j = 0; j < RUNW; j++) {
-                const uint64_t p = t0 + tid + (uint64_t)j * COUNT_THREADS;
-                ok[j] = p < t1 && window_tkey<W>(sv, p, rk, tk[j]);
-                if constexpr (!SCATTER) {
+            for (int j = 0; j < RUNW; j++) ok[j] = false;
+            if (r0 < t1)
+                run_windows<W, RUNW>(sv, r0, t1, rk,
+                                     [&](int j, bool valid, const uint64_t (&fwd)[W], const uint64_t (&rc)[W]) {
+                    uint64_t key[W];
+                    canonical<W>(fwd, rc, key);
+                    to_tkey<W>(key, tk[j]);
+                    ok[j] = valid;
+                });
+            if constexpr (!SCATTER) {
+#pragma unroll
+                for (int j = 0; j < RUNW; j++) {
                     n_win += ok[j];
                     n_ins += ok[j];
                 }
@@ -518,7 +533,37 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_p3(TableView tv, PartBufs pb,
             const uint64_t k0 = kk[q][0];
             uint32_t b = bucket_in_region(k0, tv.rbits);
             bool done = false;
-            for (int probe = 0; probe < BPR && !done; probe++) {
+            if constexpr (W == 1) {
+                // branch-light probe: match / first-empty masks over the 8 slots of a bucket
+                for (int probe = 0; probe < 2 * BPR && !done;) {
+                    uint32_t eqm = 0, emm = 0;
+#pragma unroll
+                    for (int c = 0; c < 4; c++) {
+                        const uint4 v = l4[lds_chunk(b, c)];
+                        const uint64_t x0 = ((uint64_t)v.y << 32) | v.x, x1 = ((uint64_t)v.w << 32) | v.z;
+                        eqm |= (uint32_t)(x0 == k0) << (2 * c) | (uint32_t)(x1 == k0) << (2 * c + 1);
+                        emm |= (uint32_t)(x0 == 0) << (2 * c) | (uint32_t)(x1 == 0) << (2 * c + 1);
+                    }
+                    int slot = -1;
+                    if (eqm) {
+                        slot = __builtin_ctz(eqm);
+                    } else if (emm) {
+                        const int e = __builtin_ctz(emm);
+                        const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long*>(lds_word(lt, b, e)), 0ULL,
+                                                       (unsigned long long)k0);
+                        if (old == 0 || old == k0) slot = e;
+                        else { probe++; continue; }  // lost the slot to another key: re-read this bucket
+                    }
+                    if (slot >= 0) {
+                        atomicAdd(reinterpret_cast<unsigned long long*>(lds_word(lt, b, S + slot)), 1ULL);
+                        done = true;
+                    } else {
+                        b = (b + 1) & (BPR - 1);
+                        probe++;
+                    }
+                }
+            }
+            for (int probe = 0; W > 1 && probe < BPR && !done; probe++) {
                 uint64_t w0[S];
                 if constexpr (W == 1) {
 #pragma unroll
