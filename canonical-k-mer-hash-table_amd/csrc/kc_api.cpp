@@ -60,6 +60,7 @@ struct kc_ctx {
     uint32_t* d_bk = nullptr;  // break bitmap
     TileInfo* d_tiles = nullptr;
     TileOut* d_touts = nullptr;
+    TileOut* d_tblk = nullptr;  // per-1024-tile block prefixes
     ChunkDesc* d_chunks = nullptr;
     DevCounters* d_ctr = nullptr;
 
@@ -189,8 +190,9 @@ static int ensure_part(kc_ctx* c, uint64_t syms) {
         c->pb_nblk1_cap = cap;
     }
     if (!c->pb.hist2) {
-        if (hipMalloc(&c->pb.hist2, (size_t)c->R * B2 * 4) != hipSuccess ||
-            hipMalloc(&c->pb.off2, ((size_t)c->R * B2 + 1) * 8) != hipSuccess)
+        const size_t n2 = (size_t)c->R * B2, n1 = (size_t)c->F1 * 2048;
+        if (hipMalloc(&c->pb.hist2, n2 * 4) != hipSuccess || hipMalloc(&c->pb.off2, (n2 + 1) * 8) != hipSuccess ||
+            hipMalloc(&c->pb.bsum, ((std::max(n1, n2) + 4095) / 4096 + 2) * 8) != hipSuccess)
             return c->fail(KC_ERR_NOMEM, "partition histogram allocation failed");
     }
     if (syms > c->pb_key_cap) {
@@ -242,8 +244,8 @@ static int run_batch(kc_ctx* c, uint64_t used, uint64_t nchunks, int fmt, int pa
         ev[3] = c->get_event();
     }
     const PackedView sv{c->d_pk, c->d_bk};
-    HIPCHK(c, launch_tokenize(c->d_stage, ntiles, c->d_chunks, (int)nchunks, fmt, c->d_tiles, c->d_touts, sv,
-                              used + nchunks, c->d_ctr, s));
+    HIPCHK(c, launch_tokenize(c->d_stage, ntiles, c->d_chunks, (int)nchunks, fmt, c->d_tiles, c->d_touts, c->d_tblk,
+                              sv, used + nchunks, c->d_ctr, s));
     if (c->profiling) HIPCHK(c, hipEventRecord(ev[2], s));
     TableView tv = table_view(c);
     BloomView bv{c->d_bloom, c->bf_bits ? c->bf_bits - 1 : 0, c->nh, c->nh_gate};
@@ -416,6 +418,7 @@ int kc_create(const kc_config* cfg, kc_ctx** out) {
         hipMalloc(&c->d_bk, ((c->batch_bytes + c->max_chunks) / 32 + 4) * 4) != hipSuccess ||
         hipMalloc(&c->d_tiles, ntiles * sizeof(TileInfo)) != hipSuccess ||
         hipMalloc(&c->d_touts, ntiles * sizeof(TileOut)) != hipSuccess ||
+        hipMalloc(&c->d_tblk, (ntiles / 1024 + 2) * sizeof(TileOut)) != hipSuccess ||
         hipMalloc(&c->d_chunks, c->max_chunks * sizeof(ChunkDesc)) != hipSuccess ||
         hipMalloc(&c->d_ctr, sizeof(DevCounters)) != hipSuccess)
         return bail(KC_ERR_NOMEM, "device staging allocation failed");
@@ -450,6 +453,7 @@ void kc_destroy(kc_ctx* c) {
     hipFree(c->d_bk);
     hipFree(c->d_tiles);
     hipFree(c->d_touts);
+    hipFree(c->d_tblk);
     hipFree(c->d_chunks);
     hipFree(c->d_ctr);
     hipFree(c->d_table);
@@ -458,6 +462,7 @@ void kc_destroy(kc_ctx* c) {
     hipFree(c->pb.off1);
     hipFree(c->pb.hist2);
     hipFree(c->pb.off2);
+    hipFree(c->pb.bsum);
     hipFree(c->pb.keys1);
     hipFree(c->pb.keys2);
     if (c->xev) hipEventDestroy(c->xev);
@@ -562,8 +567,10 @@ int kc_reset(kc_ctx* c) {
             hipFree(c->d_table);
             hipFree(c->pb.hist2);
             hipFree(c->pb.off2);
+            hipFree(c->pb.bsum);
             c->pb.hist2 = nullptr;
             c->pb.off2 = nullptr;
+            c->pb.bsum = nullptr;
             c->d_table = nullptr;
             c->nbuckets = 0;
             c->bloom_final = false;

@@ -633,31 +633,75 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_p3(TableView tv, PartBufs pb,
     if (n_fail) atomicAdd(&ctr->overflow, (unsigned long long)n_fail);
 }
 
-// single-workgroup exclusive scan of n u32 -> u64 (out has n+1 entries)
+// exclusive scan of n u32 -> u64 (out has n+1 entries), three passes:
+// per-block scans of 4096 elements, a scan of the block sums, the add-back
 constexpr int SCAN_T = 1024;
-__global__ __launch_bounds__(SCAN_T) void k_scan_u32(const uint32_t* __restrict__ in, uint64_t n,
-                                                    uint64_t* __restrict__ out) {
+constexpr int SCAN_PER = 4;
+DEV unsigned long long block_incl_sum_1024(unsigned long long v) {
     __shared__ unsigned long long s_w[SCAN_T / 64];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const uint64_t per = (n + SCAN_T - 1) / SCAN_T;
-    const uint64_t lo = min(n, (uint64_t)tid * per), hi = min(n, lo + per);
-    unsigned long long sum = 0;
-    for (uint64_t i = lo; i < hi; i++) sum += in[i];
-    unsigned long long incl = sum;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-        unsigned long long o = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += o;
+        const unsigned long long o = __shfl_up(v, d, 64);
+        if (lane >= d) v += o;
     }
-    if (lane == 63) s_w[wid] = incl;
+    if (lane == 63) s_w[wid] = v;
     __syncthreads();
-    unsigned long long base = incl - sum;
+    unsigned long long base = 0;
     for (int w = 0; w < wid; w++) base += s_w[w];
-    for (uint64_t i = lo; i < hi; i++) {
-        out[i] = base;
-        base += in[i];
+    __syncthreads();
+    return v + base;
+}
+__global__ __launch_bounds__(SCAN_T) void k_scanA(const uint32_t* __restrict__ in, uint64_t n,
+                                                 uint64_t* __restrict__ out, uint64_t* __restrict__ bsum) {
+    const uint64_t i0 = ((uint64_t)blockIdx.x * SCAN_T + threadIdx.x) * SCAN_PER;
+    uint32_t v[SCAN_PER];
+    unsigned long long sum = 0;
+#pragma unroll
+    for (int q = 0; q < SCAN_PER; q++) {
+        v[q] = i0 + q < n ? in[i0 + q] : 0;
+        sum += v[q];
     }
-    if (tid == SCAN_T - 1) out[n] = base;
+    const unsigned long long incl = block_incl_sum_1024(sum);
+    unsigned long long run = incl - sum;
+#pragma unroll
+    for (int q = 0; q < SCAN_PER; q++) {
+        if (i0 + q < n) out[i0 + q] = run;
+        run += v[q];
+    }
+    if (threadIdx.x == SCAN_T - 1) bsum[blockIdx.x] = incl;
+}
+__global__ __launch_bounds__(SCAN_T) void k_scanB(uint64_t* __restrict__ bsum, uint64_t nb, uint64_t* __restrict__ out,
+                                                 uint64_t n) {
+    __shared__ unsigned long long s_carry;
+    if (threadIdx.x == 0) s_carry = 0;
+    __syncthreads();
+    for (uint64_t base = 0; base < nb; base += SCAN_T) {
+        const uint64_t i = base + threadIdx.x;
+        const unsigned long long v = i < nb ? bsum[i] : 0;
+        const unsigned long long incl = block_incl_sum_1024(v);
+        const unsigned long long carry = s_carry;
+        if (i < nb) bsum[i] = carry + incl - v;
+        __syncthreads();
+        if (threadIdx.x == SCAN_T - 1) s_carry = carry + incl;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[n] = s_carry;
+}
+__global__ __launch_bounds__(SCAN_T) void k_scanC(uint64_t* __restrict__ out, uint64_t n,
+                                                 const uint64_t* __restrict__ bsum) {
+    const uint64_t i0 = ((uint64_t)blockIdx.x * SCAN_T + threadIdx.x) * SCAN_PER;
+    const uint64_t add = bsum[blockIdx.x];
+#pragma unroll
+    for (int q = 0; q < SCAN_PER; q++)
+        if (i0 + q < n) out[i0 + q] += add;
+}
+static void launch_scan(const uint32_t* in, uint64_t n, uint64_t* out, uint64_t* bsum, hipStream_t s) {
+    const uint64_t per = (uint64_t)SCAN_T * SCAN_PER;
+    const unsigned nb = (unsigned)((n + per - 1) / per);
+    hipLaunchKernelGGL(k_scanA, dim3(nb), dim3(SCAN_T), 0, s, in, n, out, bsum);
+    hipLaunchKernelGGL(k_scanB, dim3(1), dim3(SCAN_T), 0, s, bsum, (uint64_t)nb, out, n);
+    hipLaunchKernelGGL(k_scanC, dim3(nb), dim3(SCAN_T), 0, s, out, n, bsum);
 }
 
 // --------------------------------------------------------------------------------
@@ -767,11 +811,11 @@ static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf
     if ((e = set_smem(k_p3<W>, sm3)) != hipSuccess) return e;
     hipLaunchKernelGGL((k_p1<W, MODE, false>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1h, s, sym, k, t, bf, ctr, pb,
                        pk, pkm1);
-    hipLaunchKernelGGL(k_scan_u32, dim3(1), dim3(SCAN_T), 0, s, pb.hist1, (uint64_t)t.F1 * pb.nblk1, pb.off1);
+    launch_scan(pb.hist1, (uint64_t)t.F1 * pb.nblk1, pb.off1, pb.bsum, s);
     hipLaunchKernelGGL((k_p1<W, MODE, true>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1, s, sym, k, t, bf, ctr, pb,
                        pk, pkm1);
     hipLaunchKernelGGL((k_p2<W, false>), dim3(t.F1 * pb.B2), dim3(COUNT_THREADS), sm2h, s, t, pb);
-    hipLaunchKernelGGL(k_scan_u32, dim3(1), dim3(SCAN_T), 0, s, pb.hist2, t.R * pb.B2, pb.off2);
+    launch_scan(pb.hist2, t.R * pb.B2, pb.off2, pb.bsum, s);
     hipLaunchKernelGGL((k_p2<W, true>), dim3(t.F1 * pb.B2), dim3(COUNT_THREADS), sm2, s, t, pb);
     hipLaunchKernelGGL((k_p3<W>), dim3((unsigned)t.R), dim3(COUNT_THREADS), sm3, s, t, pb, ctr);
     return hipGetLastError();

@@ -44,9 +44,9 @@ struct TileInfo {           // written by k_tile_summary, consumed by k_tile_sca
     uint32_t pad2;
 };
 
-struct TileOut {            // written by k_tile_scan
+struct TileOut {            // written by the tile scan (per tile: block-local; per 1024-tile block: prefix)
     uint64_t out_off;       // first symbol index of the tile in the stream
-    uint32_t hs_in;         // header state entering the tile
+    uint32_t hs_in;         // header state entering the tile (block-local: transform code)
     uint32_t pad;
 };
 
@@ -90,6 +90,7 @@ struct PartBufs {
     uint64_t* off1;         // F1*nblk1 + 1 exclusive offsets
     uint32_t* hist2;        // [R][B2]
     uint64_t* off2;         // R*B2 + 1
+    uint64_t* bsum;         // scan scratch: one entry per 4096 histogram entries
     uint64_t* keys1;        // coarse-binned keys (W words each)
     uint64_t* keys2;        // region-binned keys
 };
@@ -108,8 +109,8 @@ inline int slots_per_bucket(int W) { return BUCKET_WORDS / (W + 1); }
 hipError_t launch_gather(const uint8_t* src, uint8_t* stage, const ChunkDesc* d_chunks, int n_chunks,
                          const ChunkDesc* h_chunks, hipStream_t s);
 hipError_t launch_tokenize(const uint8_t* stage, uint64_t ntiles, const ChunkDesc* d_chunks, int n_chunks,
-                           int fmt, TileInfo* tiles, TileOut* touts, PackedView sv, uint64_t sym_bound,
-                           DevCounters* ctr, hipStream_t s);
+                           int fmt, TileInfo* tiles, TileOut* touts, TileOut* tblk, PackedView sv,
+                           uint64_t sym_bound, DevCounters* ctr, hipStream_t s);
 // mode: 0 count all windows, 1 Bloom pass 1, 2 count windows passing the Bloom gate
 hipError_t launch_count(PackedView sv, uint64_t sym_bound, int k, int mode, TableView t, BloomView bf,
                         DevCounters* ctr, hipStream_t s);

@@ -2,7 +2,7 @@
 //
 //   k_gather        device-resident source image -> TILE-aligned chunk stage
 //   k_tile_summary  per 4 KiB tile: FASTA newline count + last header marker
-//   k_tile_scan     one workgroup: stream offsets + header state entering each tile
+//   k_tscan_*       two-level scan: stream offsets + header state entering each tile
 //   k_emit          per tile: bytes -> symbol codes (0..3 base, 4 break); FASTA
 //                   newlines are removed (they do not reset the window,
 //                   parallel_parser.hpp:1432-1436), header bytes become breaks, and
@@ -121,154 +121,228 @@ __global__ __launch_bounds__(TILE_THREADS) void k_tile_summary(const uint8_t* __
 }
 
 // --------------------------------------------------------------------------------
-// k_tile_scan: one 1024-thread workgroup over all tiles.
+// tile scan, two levels:
 //   kept(t)  = valid - (FASTA ? nl : 0) + first   (one break symbol per chunk start)
 //   hs_in(t) = first ? bh : hs_out(t-1);  hs_out = marker ? (marker == '>') : hs_in
-// The header-state recurrence is a scan of "last defining tile" (a chunk start or a
-// marker defines the state), composed left to right.
+// The header-state recurrence is a "last defining tile" scan (a chunk start or a
+// marker defines the state): transform code 0 = identity, 1 = state 0, 2 = state 1.
 // --------------------------------------------------------------------------------
-constexpr int SCAN_THREADS = 1024;
-__global__ __launch_bounds__(SCAN_THREADS) void k_tile_scan(const TileInfo* __restrict__ tiles, uint64_t ntiles,
-                                                           int fmt, TileOut* __restrict__ out,
-                                                           DevCounters* __restrict__ ctr) {
-    __shared__ unsigned long long s_sum[SCAN_THREADS];
-    __shared__ uint32_t s_tr[SCAN_THREADS];
-    const int tid = threadIdx.x;
-    const uint64_t per = (ntiles + SCAN_THREADS - 1) / SCAN_THREADS;
-    const uint64_t lo = min(ntiles, (uint64_t)tid * per), hi = min(ntiles, lo + per);
-    unsigned long long sum = 0;
-    uint32_t tr = 0;  // 0 identity, 1 const 0, 2 const 1
-    for (uint64_t t = lo; t < hi; t++) {
-        const TileInfo ti = tiles[t];
-        sum += ti.valid - (fmt == FMT_FASTA ? ti.nl : 0) + ti.first;
-        if (ti.marker) tr = ti.marker == 2 ? 2 : 1;
-        else if (ti.first) tr = ti.bh ? 2 : 1;
+constexpr int TSCAN = 1024;
+DEV uint32_t tile_kept(const TileInfo& ti, int fmt) { return ti.valid - (fmt == FMT_FASTA ? ti.nl : 0) + ti.first; }
+DEV uint32_t tile_tr(const TileInfo& ti) { return ti.marker ? (ti.marker == 2 ? 2u : 1u) : (ti.first ? (ti.bh ? 2u : 1u) : 0u); }
+
+// block-wide inclusive scans over 1024 threads (sum, last non-zero)
+DEV void block_scan_1024(unsigned long long& sum, uint32_t& tr) {
+    __shared__ unsigned long long s_s[TSCAN / 64];
+    __shared__ uint32_t s_t[TSCAN / 64];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned long long os = __shfl_up(sum, d, 64);
+        const uint32_t ot = __shfl_up(tr, d, 64);
+        if (lane >= d) {
+            sum += os;
+            if (!tr) tr = ot;
+        }
     }
-    s_sum[tid] = sum;
-    s_tr[tid] = tr;
+    if (lane == 63) { s_s[wid] = sum; s_t[wid] = tr; }
     __syncthreads();
-    // Hillis-Steele inclusive scans in LDS
-    for (int d = 1; d < SCAN_THREADS; d <<= 1) {
-        unsigned long long vs = tid >= d ? s_sum[tid - d] : 0;
-        uint32_t vt = tid >= d ? s_tr[tid - d] : 0;
-        __syncthreads();
-        s_sum[tid] += vs;
-        if (s_tr[tid] == 0) s_tr[tid] = vt;
-        __syncthreads();
+    unsigned long long base = 0;
+    uint32_t btr = 0;
+    for (int w = 0; w < wid; w++) {
+        base += s_s[w];
+        if (s_t[w]) btr = s_t[w];
     }
-    unsigned long long run = tid ? s_sum[tid - 1] : 0;
-    uint32_t st = tid ? (s_tr[tid - 1] == 2 ? 1u : 0u) : 0u;
-    for (uint64_t t = lo; t < hi; t++) {
-        const TileInfo ti = tiles[t];
+    sum += base;
+    if (!tr) tr = btr;
+}
+
+__global__ __launch_bounds__(TSCAN) void k_tscan_block(const TileInfo* __restrict__ tiles, uint64_t ntiles, int fmt,
+                                                      TileOut* __restrict__ touts, TileOut* __restrict__ agg) {
+    const uint64_t t = (uint64_t)blockIdx.x * TSCAN + threadIdx.x;
+    TileInfo ti{};
+    if (t < ntiles) ti = tiles[t];
+    const unsigned long long kept = t < ntiles ? tile_kept(ti, fmt) : 0;
+    const uint32_t tr0 = t < ntiles ? tile_tr(ti) : 0;
+    unsigned long long sum = kept;
+    uint32_t tr = tr0;
+    block_scan_1024(sum, tr);
+    // exclusive values for this tile
+    const unsigned long long ex_sum = sum - kept;
+    uint32_t ex_tr = __shfl_up(tr, 1, 64);
+    __shared__ uint32_t s_last[TSCAN / 64];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 63) s_last[wid] = tr;
+    __syncthreads();
+    if (lane == 0) ex_tr = wid ? s_last[wid - 1] : 0;
+    if (t < ntiles) {
         TileOut to;
-        to.out_off = run;
-        uint32_t hin = ti.first ? ti.bh : st;
-        to.hs_in = fmt == FMT_FASTA ? hin : 0;
+        to.out_off = ex_sum;
+        to.hs_in = ex_tr;  // transform code, resolved against the block prefix in k_emit
         to.pad = 0;
-        out[t] = to;
-        st = ti.marker ? (ti.marker == 2 ? 1u : 0u) : hin;
-        run += ti.valid - (fmt == FMT_FASTA ? ti.nl : 0) + ti.first;
+        touts[t] = to;
     }
-    if (tid == SCAN_THREADS - 1) ctr->stream_len = s_sum[SCAN_THREADS - 1];
+    if (threadIdx.x == TSCAN - 1) {
+        TileOut a;
+        a.out_off = sum;
+        a.hs_in = tr;
+        a.pad = 0;
+        agg[blockIdx.x] = a;
+    }
+}
+
+// single workgroup: exclusive scan of the block aggregates -> block prefixes
+__global__ __launch_bounds__(TSCAN) void k_tscan_top(TileOut* __restrict__ agg, uint64_t nblk,
+                                                    DevCounters* __restrict__ ctr) {
+    __shared__ unsigned long long s_carry;
+    __shared__ uint32_t s_tr;
+    if (threadIdx.x == 0) { s_carry = 0; s_tr = 0; }
+    __syncthreads();
+    for (uint64_t base = 0; base < nblk; base += TSCAN) {
+        const uint64_t i = base + threadIdx.x;
+        TileOut a{};
+        if (i < nblk) a = agg[i];
+        unsigned long long sum = i < nblk ? a.out_off : 0;
+        uint32_t tr = i < nblk ? a.hs_in : 0;
+        const unsigned long long mine = sum;
+        block_scan_1024(sum, tr);
+        const unsigned long long carry = s_carry;
+        const uint32_t ctr_in = s_tr;
+        // exclusive transform: inclusive of the previous thread
+        __shared__ uint32_t s_inc[TSCAN];
+        s_inc[threadIdx.x] = tr;
+        __syncthreads();
+        uint32_t ex_tr = threadIdx.x ? s_inc[threadIdx.x - 1] : 0;
+        if (!ex_tr) ex_tr = ctr_in;
+        if (i < nblk) {
+            TileOut p;
+            p.out_off = carry + sum - mine;
+            p.hs_in = ex_tr == 2 ? 1u : 0u;  // state entering the block (block 0: tile 0 is a chunk start)
+            p.pad = 0;
+            agg[i] = p;
+        }
+        __syncthreads();
+        if (threadIdx.x == TSCAN - 1) {
+            s_carry = carry + sum;
+            if (tr) s_tr = tr;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) ctr->stream_len = s_carry;
 }
 
 // --------------------------------------------------------------------------------
-// k_emit: bytes -> symbol codes
+// k_emit: bytes -> packed 2-bit symbols + break bits (branch-free per byte)
 // --------------------------------------------------------------------------------
+DEV uint32_t acgt_code(uint32_t ch) { return ((ch >> 1) ^ (ch >> 2)) & 3; }  // A/a 0, C/c 1, G/g 2, T/t 3
+DEV bool is_acgt(uint32_t ch) {
+    const uint32_t l = ch | 0x20;
+    return l == 'a' || l == 'c' || l == 'g' || l == 't';
+}
+
 __global__ __launch_bounds__(TILE_THREADS) void k_emit(const uint8_t* __restrict__ stage,
                                                        const TileInfo* __restrict__ tiles,
-                                                       const TileOut* __restrict__ touts, int fmt,
+                                                       const TileOut* __restrict__ touts,
+                                                       const TileOut* __restrict__ bpre, int fmt,
                                                        uint64_t* __restrict__ pk, uint32_t* __restrict__ bk) {
-    __shared__ uint8_t s_codes[TILE + 16];
+    constexpr int NW = TILE / 32 + 2;  // output words a tile can touch
+    __shared__ unsigned long long s_pk[NW];
+    __shared__ uint32_t s_bk[NW];
     __shared__ uint32_t s_wsum[TILE_THREADS / 64];
     __shared__ uint32_t s_wmk[TILE_THREADS / 64];
     const uint64_t t = blockIdx.x;
     const TileInfo ti = tiles[t];
     const TileOut to = touts[t];
+    const TileOut bp = bpre[t / TSCAN];
+    const uint64_t g0 = bp.out_off + to.out_off;  // global index of the tile's first symbol
+    uint32_t hs_in = to.hs_in ? (to.hs_in == 2 ? 1u : 0u) : bp.hs_in;
+    if (ti.first) hs_in = ti.bh;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    for (int i = tid; i < NW; i += TILE_THREADS) { s_pk[i] = 0; s_bk[i] = 0; }
     const uint32_t my0 = tid * 16;
-    const uint32_t vh = ti.valid > my0 ? ti.valid - my0 : 0;
+    const uint32_t vh = ti.valid > my0 ? min(ti.valid - my0, 16u) : 0;
     uint8_t b[16];
     load_tile_bytes(stage + t * TILE + my0, vh, b);
-
-    uint32_t state = 0;
-    if (fmt == FMT_FASTA) {
-        // header state entering this thread: last marker of the lower threads, else hs_in
-        uint32_t mk = 0;
+    const bool fasta = fmt == FMT_FASTA;
+    // per-byte masks
+    uint32_t nlm = 0, gtm = 0;
 #pragma unroll
-        for (int j = 0; j < 16; j++)
-            if ((uint32_t)j < vh) {
-                if (b[j] == '\n') mk = 1;
-                else if (b[j] == '>') mk = 2;
-            }
-        uint32_t incl = wave_incl_last(mk);
+    for (int j = 0; j < 16; j++) {
+        nlm |= (uint32_t)(b[j] == '\n') << j;
+        gtm |= (uint32_t)(b[j] == '>') << j;
+    }
+    const uint32_t vmask = vh >= 16 ? 0xFFFFu : ((1u << vh) - 1);
+    nlm &= vmask;
+    gtm &= vmask;
+    uint32_t state = 0;
+    if (fasta) {
+        const uint32_t any = nlm | gtm;
+        const uint32_t mk = any ? ((gtm >> (31 - __builtin_clz(any))) & 1 ? 2u : 1u) : 0u;
+        const uint32_t incl = wave_incl_last(mk);
         if (lane == 63) s_wmk[wid] = incl;
         __syncthreads();
         uint32_t excl = __shfl_up(incl, 1, 64);
         if (lane == 0) excl = 0;
-        if (excl == 0) {
+        if (excl == 0)
             for (int w = wid - 1; w >= 0; w--)
                 if (s_wmk[w]) { excl = s_wmk[w]; break; }
-        }
-        state = excl ? (excl == 2 ? 1u : 0u) : to.hs_in;
+        state = excl ? (excl == 2 ? 1u : 0u) : hs_in;
     }
-
-    uint8_t codes[16];
-    uint32_t kept = 0;
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-        codes[j] = 0xff;
-        if ((uint32_t)j < vh) {
-            const uint8_t ch = b[j];
-            if (fmt == FMT_FASTA) {
-                if (ch == '\n') { state = 0; continue; }
-                if (ch == '>') state = 1;
-                codes[j] = state ? SYM_BREAK : char_code(ch);
-            } else {
-                codes[j] = char_code(ch);
-            }
-            kept++;
-        }
-    }
-    uint32_t incl = wave_incl_sum(kept);
+    const uint32_t keptm = fasta ? (vmask & ~nlm) : vmask;
+    const uint32_t kept = __builtin_popcount(keptm);
+    const uint32_t incl = wave_incl_sum(kept);
     if (lane == 63) s_wsum[wid] = incl;
     __syncthreads();
-    // a chunk's first tile starts with the chunk-separating break
     uint32_t pos = incl - kept + ti.first;
     uint32_t total = ti.first;
     for (int w = 0; w < TILE_THREADS / 64; w++) {
         if (w < wid) pos += s_wsum[w];
         total += s_wsum[w];
     }
-    if (ti.first && tid == 0) s_codes[0] = SYM_BREAK;
-#pragma unroll
-    for (int j = 0; j < 16; j++)
-        if (codes[j] != 0xff) s_codes[pos++] = codes[j];
-    __syncthreads();
     if (total == 0) return;
-    // pack: 32 symbols per word, symbol j of word w at bits 62-2j (codes) / 31-j (breaks);
-    // words shared with the neighbouring tiles are OR-ed into the zeroed buffers
-    const uint64_t g0 = to.out_off;
-    const uint64_t w_lo = g0 >> 5, w_hi = (g0 + total - 1) >> 5;
-    for (uint64_t w = w_lo + tid; w <= w_hi; w += TILE_THREADS) {
-        const int64_t l0 = (int64_t)(w << 5) - (int64_t)g0;
-        uint64_t pv = 0;
-        uint32_t bv = 0;
-#pragma unroll 8
-        for (int j = 0; j < 32; j++) {
-            const int64_t l = l0 + j;
-            if (l >= 0 && l < (int64_t)total) {
-                const uint8_t c = s_codes[l];
-                if (c > 3) bv |= 1u << (31 - j);
-                else pv |= (uint64_t)c << (62 - 2 * j);
-            }
+    // pack this thread's kept symbols into (at most) two words of the tile's LDS image
+    const uint64_t wbase = g0 >> 5;
+    const uint32_t o0 = (uint32_t)(g0 & 31) + pos;  // bit-slot of my first symbol, relative to wbase
+    uint64_t pa = 0, pb = 0;
+    uint32_t ba = 0, bb = 0;
+    uint32_t o = o0;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const uint32_t ch = b[j];
+        if (fasta) state = (gtm >> j) & 1 ? 1u : ((nlm >> j) & 1 ? 0u : state);
+        const bool keep = (keptm >> j) & 1;
+        const bool brk = (fasta && state) || !is_acgt(ch);
+        const uint64_t code = brk ? 0 : acgt_code(ch);
+        const uint32_t r = o & 31;
+        const bool first_word = (o >> 5) == (o0 >> 5);
+        const uint64_t cv = code << (62 - 2 * r);
+        const uint32_t bv = (uint32_t)brk << (31 - r);
+        if (keep) {
+            if (first_word) { pa |= cv; ba |= bv; }
+            else { pb |= cv; bb |= bv; }
         }
-        if (l0 >= 0 && l0 + 32 <= (int64_t)total) {
-            pk[w] = pv;
-            bk[w] = bv;
+        o += keep;
+    }
+    const uint32_t wa = o0 >> 5;
+    if (kept) {
+        if (pa) atomicOr(&s_pk[wa], (unsigned long long)pa);
+        if (ba) atomicOr(&s_bk[wa], ba);
+        if (pb) atomicOr(&s_pk[wa + 1], (unsigned long long)pb);
+        if (bb) atomicOr(&s_bk[wa + 1], bb);
+    }
+    if (ti.first && tid == 0) atomicOr(&s_bk[0], 1u << (31 - (uint32_t)(g0 & 31)));  // chunk-start break
+    __syncthreads();
+    // the tile's words: interior ones are ours alone, the two edge words are shared
+    const uint32_t nw = (uint32_t)(((g0 & 31) + total + 31) >> 5);
+    for (uint32_t i = tid; i < nw; i += TILE_THREADS) {
+        const uint64_t w = wbase + i;
+        const bool edge = (i == 0 && (g0 & 31)) || (i == nw - 1 && ((g0 + total) & 31));
+        if (edge) {
+            if (s_pk[i]) atomicOr((unsigned long long*)(pk + w), s_pk[i]);
+            if (s_bk[i]) atomicOr(bk + w, s_bk[i]);
         } else {
-            if (pv) atomicOr((unsigned long long*)(pk + w), (unsigned long long)pv);
-            if (bv) atomicOr(bk + w, bv);
+            pk[w] = s_pk[i];
+            bk[w] = s_bk[i];
         }
     }
 }
@@ -320,16 +394,19 @@ hipError_t launch_gather(const uint8_t* src, uint8_t* stage, const ChunkDesc* d_
 }
 
 hipError_t launch_tokenize(const uint8_t* stage, uint64_t ntiles, const ChunkDesc* d_chunks, int n_chunks, int fmt,
-                           TileInfo* tiles, TileOut* touts, PackedView sv, uint64_t sym_bound, DevCounters* ctr,
-                           hipStream_t s) {
+                           TileInfo* tiles, TileOut* touts, TileOut* tblk, PackedView sv, uint64_t sym_bound,
+                           DevCounters* ctr, hipStream_t s) {
     const uint64_t words = sym_bound / 32 + 2;
     hipError_t e;
     if ((e = hipMemsetAsync(sv.pk, 0, words * 8, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(sv.bk, 0, words * 4, s)) != hipSuccess) return e;
+    const uint64_t nblk = (ntiles + TSCAN - 1) / TSCAN;
     hipLaunchKernelGGL(k_tile_summary, dim3((unsigned)ntiles), dim3(TILE_THREADS), 0, s, stage, d_chunks, n_chunks,
                        fmt, tiles);
-    hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(SCAN_THREADS), 0, s, tiles, ntiles, fmt, touts, ctr);
-    hipLaunchKernelGGL(k_emit, dim3((unsigned)ntiles), dim3(TILE_THREADS), 0, s, stage, tiles, touts, fmt, sv.pk, sv.bk);
+    hipLaunchKernelGGL(k_tscan_block, dim3((unsigned)nblk), dim3(TSCAN), 0, s, tiles, ntiles, fmt, touts, tblk);
+    hipLaunchKernelGGL(k_tscan_top, dim3(1), dim3(TSCAN), 0, s, tblk, nblk, ctr);
+    hipLaunchKernelGGL(k_emit, dim3((unsigned)ntiles), dim3(TILE_THREADS), 0, s, stage, tiles, touts, tblk, fmt,
+                       sv.pk, sv.bk);
     return hipGetLastError();
 }
 
