@@ -15,7 +15,7 @@ N > 1 (torch.distributed over RCCL): weak scaling, every rank owns its own 10M-r
 slice of one dataset; canonical keys are routed to their hash-prefix owner with one
 all-to-all per step (see kaarme_amd/sharded.py) and counted there.
 
-Extra JSON keys: roofline (dominant kernel k_count vs 8 TB/s HBM), cpu_baseline (the
+Extra JSON keys: roofline (the counting pass vs 8 TB/s HBM), cpu_baseline (the
 reference CLI oracle/_ref/kaarme on a bounded sample of the same workload, rank 0,
 N=1 only).
 """
@@ -201,7 +201,9 @@ def main():
     traffic = load_traffic(workload)
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                "kernel": "k_count<1,0>", "kernel_ms": round(count_ms, 4),
+                "kernel": ("count pass: k_p1 hist+scatter, k_p2 hist+scatter, k_p3 (partitioned insert)"
+                           if world == 1 else "route (k_p1 owner bins) + insert of received keys"),
+                "kernel_ms": round(count_ms, 4),
                 "algorithmic_bytes_per_launch": int(bytes_per_launch)}
     step_ms = elapsed / args.steps * 1e3
     out = {

@@ -468,7 +468,8 @@ void kc_destroy(kc_ctx* c) {
     if (c->xev) hipEventDestroy(c->xev);
     for (auto e : c->ev_pool) hipEventDestroy(e);
     for (auto& ev : c->ev_pending)
-        for (auto e : ev) hipEventDestroy(e);
+        for (auto e : ev)
+            if (e) hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
@@ -511,6 +512,99 @@ int kc_count_device(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, size_
     if (!c || (!img && n) || (!chunks && n)) return KC_ERR_ARG;
     if (!c->d_table) return c->fail(KC_ERR_STATE, "kc_bloom_finalize must precede the counting pass");
     return device_pass(c, img, chunks, n, fmt, 0, pick_stream(c, s));
+}
+
+int kc_route_device(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, size_t n, int fmt, uint32_t nshards,
+                    uint64_t* dev_out, uint64_t out_capacity, uint64_t* counts, void* sp) {
+    if (!c || !counts || !dev_out || nshards == 0 || (!img && n) || (!chunks && n)) return KC_ERR_ARG;
+    if (fmt == KC_FMT_FASTQ) return c->fail(KC_ERR_UNSUPPORTED, "Input file format not supported.");
+    if (fmt != KC_FMT_FASTA && fmt != KC_FMT_PLAIN) return c->fail(KC_ERR_ARG, "unknown format");
+    if (c->cfg.bf_enable) return c->fail(KC_ERR_UNSUPPORTED, "sharded counting with the Bloom filter is not supported");
+    hipStream_t s = pick_stream(c, sp);
+    int rc = flush_host(c);
+    if (rc) return rc;
+    std::vector<ChunkDesc> batch;
+    uint64_t used = 0;
+    for (size_t i = 0; i < n; i++) {
+        if (!chunks[i].len) continue;
+        ChunkDesc d{chunks[i].off, used, chunks[i].len, (uint32_t)(chunks[i].broken_header ? 1 : 0), 0};
+        batch.push_back(d);
+        used += round_up(chunks[i].len, TILE);
+        c->n_chunks++;
+        c->n_bytes += chunks[i].len;
+    }
+    if (used > c->batch_bytes || batch.size() > c->max_chunks)
+        return c->fail(KC_ERR_ARG, "kc_route_device: the chunks must fit one staging batch");
+    const uint64_t syms = used + batch.size();
+    if (out_capacity < syms) return c->fail(KC_ERR_ARG, "kc_route_device: output capacity too small");
+    for (uint32_t d = 0; d < nshards; d++) counts[d] = 0;
+    if (batch.empty()) return KC_OK;
+    if (s != c->stream) {
+        HIPCHK(c, hipEventRecord(c->xev, c->stream));
+        HIPCHK(c, hipStreamWaitEvent(s, c->xev, 0));
+    }
+    rc = ensure_part(c, syms);
+    if (rc) return rc;
+    if ((uint64_t)nshards * c->pb.nblk1 > (uint64_t)c->F1 * c->pb_nblk1_cap)
+        return c->fail(KC_ERR_ARG, "too many shards");
+    std::array<hipEvent_t, 4> ev{};
+    if (c->profiling)
+        for (auto& e : ev) e = c->get_event();
+    if (c->profiling) HIPCHK(c, hipEventRecord(ev[0], s));
+    std::memcpy(c->h_desc[c->cur], batch.data(), batch.size() * sizeof(ChunkDesc));
+    HIPCHK(c, hipMemcpyAsync(c->d_chunks, c->h_desc[c->cur], batch.size() * sizeof(ChunkDesc), hipMemcpyHostToDevice, s));
+    HIPCHK(c, launch_gather(img, c->d_stage, c->d_chunks, (int)batch.size(), batch.data(), s));
+    if (c->profiling) HIPCHK(c, hipEventRecord(ev[1], s));
+    const PackedView sv{c->d_pk, c->d_bk};
+    HIPCHK(c, launch_tokenize(c->d_stage, used / TILE, c->d_chunks, (int)batch.size(), fmt, c->d_tiles, c->d_touts,
+                              c->d_tblk, sv, syms, c->d_ctr, s));
+    if (c->profiling) HIPCHK(c, hipEventRecord(ev[2], s));
+    HIPCHK(c, launch_route(sv, c->cfg.k, c->W, c->d_ctr, c->pb, nshards, dev_out, s));
+    if (c->profiling) {
+        HIPCHK(c, hipEventRecord(ev[3], s));
+        c->ev_pending.push_back(ev);
+    }
+    // per-owner totals: off1[d * nblk1], d = 0..nshards (the last one is the total)
+    std::vector<uint64_t> offs(nshards + 1);
+    for (uint32_t d = 0; d <= nshards; d++)
+        HIPCHK(c, hipMemcpyAsync(&offs[d], c->pb.off1 + (uint64_t)d * c->pb.nblk1, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    for (uint32_t d = 0; d < nshards; d++) counts[d] = offs[d + 1] - offs[d];
+    return KC_OK;
+}
+
+int kc_insert_keys_device(kc_ctx* c, const uint64_t* keys, uint64_t n, void* sp) {
+    if (!c || (!keys && n)) return KC_ERR_ARG;
+    if (!c->d_table) return c->fail(KC_ERR_STATE, "no table");
+    hipStream_t s = pick_stream(c, sp);
+    int rc = flush_host(c);
+    if (rc) return rc;
+    if (n == 0) return KC_OK;
+    if (s != c->stream) {
+        HIPCHK(c, hipEventRecord(c->xev, c->stream));
+        HIPCHK(c, hipStreamWaitEvent(s, c->xev, 0));
+    }
+    const bool part = use_partitioned(c, n);
+    if (part) {
+        rc = ensure_part(c, n);
+        if (rc) return rc;
+    }
+    std::array<hipEvent_t, 4> ev{};
+    if (c->profiling) {
+        ev[2] = c->get_event();
+        ev[3] = c->get_event();
+        HIPCHK(c, hipEventRecord(ev[2], s));
+    }
+    HIPCHK(c, launch_insert_keys(keys, n, part, table_view(c), c->d_ctr, c->pb, s));
+    if (c->profiling) {
+        HIPCHK(c, hipEventRecord(ev[3], s));
+        c->ev_pending.push_back(ev);
+    }
+    if (s != c->stream) {
+        HIPCHK(c, hipEventRecord(c->xev, s));
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->xev, 0));
+    }
+    return KC_OK;
 }
 
 int kc_sync(kc_ctx* c) {
@@ -594,14 +688,17 @@ int kc_get_timing(kc_ctx* c, kc_timing* t) {
     if (rc) return rc;
     for (auto& ev : c->ev_pending) {
         float a = 0, b = 0, d = 0;
-        HIPCHK(c, hipEventElapsedTime(&a, ev[0], ev[1]));
-        HIPCHK(c, hipEventElapsedTime(&b, ev[1], ev[2]));
-        HIPCHK(c, hipEventElapsedTime(&d, ev[2], ev[3]));
+        if (ev[0]) {  // a full batch: {start, gather, tokenize, count/route}
+            HIPCHK(c, hipEventElapsedTime(&a, ev[0], ev[1]));
+            HIPCHK(c, hipEventElapsedTime(&b, ev[1], ev[2]));
+            c->timing.launches++;
+        }
+        HIPCHK(c, hipEventElapsedTime(&d, ev[2], ev[3]));  // insert of received keys: {-, -, start, end}
         c->timing.gather_ms += a;
         c->timing.tokenize_ms += b;
         c->timing.count_ms += d;
-        c->timing.launches++;
-        for (auto e : ev) c->ev_pool.push_back(e);
+        for (auto e : ev)
+            if (e) c->ev_pool.push_back(e);
     }
     c->ev_pending.clear();
     unsigned long long sl = 0;

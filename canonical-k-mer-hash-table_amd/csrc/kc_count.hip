@@ -329,15 +329,26 @@ DEV PartLds part_lds(uint8_t* smem, uint32_t F) {
     return l;
 }
 
+// bin of a table key: a bit field of word 0 (table levels) or the shard owner (routing)
+struct BinFn {
+    int owner;       // 1: owner_of(t0, parts)
+    int shift;
+    uint32_t mask;
+    uint32_t parts;
+    DEV uint32_t operator()(uint64_t t0) const {
+        return owner ? owner_of(t0, parts) : (uint32_t)(t0 >> shift) & mask;
+    }
+};
+
 // Counting-sort the tile's keys (in registers: tk[j] valid where ok[j]) by bin into
-// LDS and write each bin as one contiguous run at gbase[bin]; bin = bit field of tk[.][0].
+// LDS and write each bin as one contiguous run at gbase[bin].
 template <int W, int RUNW>
-DEV void scatter_tile(const PartLds& l, uint32_t F, int shift, uint32_t fmask, const uint64_t (&tk)[RUNW][W],
+DEV void scatter_tile(const PartLds& l, uint32_t F, const BinFn& bin, const uint64_t (&tk)[RUNW][W],
                       const bool (&ok)[RUNW], uint64_t* __restrict__ out) {
     const int tid = threadIdx.x;
 #pragma unroll
     for (int j = 0; j < RUNW; j++)
-        if (ok[j]) atomicAdd(&l.hist[(uint32_t)(tk[j][0] >> shift) & fmask], 1u);
+        if (ok[j]) atomicAdd(&l.hist[bin(tk[j][0])], 1u);
     __syncthreads();
     block_excl_scan_lds(l.hist, l.start, F);
     for (uint32_t b = tid; b < F; b += COUNT_THREADS) l.cur[b] = l.start[b];
@@ -345,7 +356,7 @@ DEV void scatter_tile(const PartLds& l, uint32_t F, int shift, uint32_t fmask, c
 #pragma unroll
     for (int j = 0; j < RUNW; j++)
         if (ok[j]) {
-            const uint32_t slot = atomicAdd(&l.cur[(uint32_t)(tk[j][0] >> shift) & fmask], 1u);
+            const uint32_t slot = atomicAdd(&l.cur[bin(tk[j][0])], 1u);
 #pragma unroll
             for (int w = 0; w < W; w++) l.keys[slot * W + w] = tk[j][w];
         }
@@ -355,7 +366,7 @@ DEV void scatter_tile(const PartLds& l, uint32_t F, int shift, uint32_t fmask, c
         uint64_t key[W];
 #pragma unroll
         for (int w = 0; w < W; w++) key[w] = l.keys[i * W + w];
-        const uint32_t b = (uint32_t)(key[0] >> shift) & fmask;
+        const uint32_t b = bin(key[0]);
         const uint64_t dst = l.gbase[b] + (i - l.start[b]);
 #pragma unroll
         for (int w = 0; w < W; w++) out[dst * W + w] = key[w];
@@ -371,14 +382,11 @@ DEV void scatter_tile(const PartLds& l, uint32_t F, int shift, uint32_t fmask, c
 // Level 1: windows of a contiguous symbol range -> coarse bins (top f1bits of tkey[0]).
 // SCATTER = false: histogram only ([bin][block] into hist1); true: write the keys.
 template <int W, int MODE, bool SCATTER>
-__global__ __launch_bounds__(COUNT_THREADS) void k_p1(PackedView sv, int k, TableView tv, BloomView bf,
-                                                      DevCounters* __restrict__ ctr, PartBufs pb, uint64_t pow5_k,
-                                                      uint64_t pow5_km1) {
+__global__ __launch_bounds__(COUNT_THREADS) void k_p1(PackedView sv, int k, BloomView bf,
+                                                      DevCounters* __restrict__ ctr, PartBufs pb, uint32_t F, BinFn bin,
+                                                      uint64_t* __restrict__ out, uint64_t pow5_k, uint64_t pow5_km1) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int RUNW = run_w<W>(), TW = tile_win<W>();
-    const uint32_t F = tv.F1;
-    const int shift = tv.f1bits ? 64 - tv.f1bits : 63;  // F == 1: every key in bin 0
-    const uint32_t fmask = F - 1;
     const PartLds l = part_lds(smem, F);
     const int tid = threadIdx.x;
     const uint64_t M = ctr->stream_len;
@@ -438,18 +446,76 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_p1(PackedView sv, int k, Tabl
             });
         }
         if constexpr (SCATTER) {
-            scatter_tile<W, RUNW>(l, F, shift, fmask, tk, ok, pb.keys1);
+            scatter_tile<W, RUNW>(l, F, bin, tk, ok, out);
         } else {
 #pragma unroll
             for (int j = 0; j < RUNW; j++)
-                if (ok[j]) atomicAdd(&l.hist[(uint32_t)(tk[j][0] >> shift) & fmask], 1u);
+                if (ok[j]) atomicAdd(&l.hist[bin(tk[j][0])], 1u);
         }
     }
     if constexpr (!SCATTER) {
         __syncthreads();
         for (uint32_t b = tid; b < F; b += COUNT_THREADS) pb.hist1[(uint64_t)b * pb.nblk1 + blockIdx.x] = l.hist[b];
-        block_add4(n_win, n_ins, 0, 0, &ctr->windows, &ctr->inserted, nullptr, nullptr);
+        // routing (owner bins) counts windows here and insertions at the owner
+        block_add4(n_win, bin.owner ? 0 : n_ins, 0, 0, &ctr->windows, &ctr->inserted, nullptr, nullptr);
     }
+}
+
+// Level 1 over a key array (keys received from other shards): [0, n) split over nblk1
+// blocks, bins = top f1bits of the table key.
+template <int W, bool SCATTER>
+__global__ __launch_bounds__(COUNT_THREADS) void k_p1k(const uint64_t* __restrict__ in, uint64_t n, PartBufs pb,
+                                                       uint32_t F, BinFn bin, DevCounters* __restrict__ ctr) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int RUNW = run_w<W>(), TW = tile_win<W>();
+    const PartLds l = part_lds(smem, F);
+    const int tid = threadIdx.x;
+    const uint64_t per = ((n + pb.nblk1 - 1) / pb.nblk1 + TW - 1) / TW * TW;
+    const uint64_t lo = min(n, (uint64_t)blockIdx.x * per), hi = min(n, lo + per);
+    for (uint32_t b = tid; b < F; b += COUNT_THREADS) {
+        l.hist[b] = 0;
+        if constexpr (SCATTER) l.gbase[b] = pb.off1[(uint64_t)b * pb.nblk1 + blockIdx.x];
+    }
+    __syncthreads();
+    for (uint64_t t0 = lo; t0 < hi; t0 += TW) {
+        uint64_t tk[RUNW][W];
+        bool ok[RUNW];
+#pragma unroll
+        for (int q = 0; q < RUNW; q++) {
+            const uint64_t i = t0 + tid + (uint64_t)q * COUNT_THREADS;
+            ok[q] = i < hi;
+#pragma unroll
+            for (int w = 0; w < W; w++) tk[q][w] = ok[q] ? in[i * W + w] : 0;
+        }
+        if constexpr (SCATTER) {
+            scatter_tile<W, RUNW>(l, F, bin, tk, ok, pb.keys1);
+        } else {
+#pragma unroll
+            for (int q = 0; q < RUNW; q++)
+                if (ok[q]) atomicAdd(&l.hist[bin(tk[q][0])], 1u);
+        }
+    }
+    if constexpr (!SCATTER) {
+        __syncthreads();
+        for (uint32_t b = tid; b < F; b += COUNT_THREADS) pb.hist1[(uint64_t)b * pb.nblk1 + blockIdx.x] = l.hist[b];
+        if (blockIdx.x == 0 && tid == 0) atomicAdd(&ctr->inserted, (unsigned long long)n);
+    }
+}
+
+// direct insert of a key array (small batches)
+template <int W>
+__global__ __launch_bounds__(COUNT_THREADS) void k_insert_keys(const uint64_t* __restrict__ in, uint64_t n,
+                                                               TableView tv, DevCounters* __restrict__ ctr) {
+    uint32_t n_fail = 0;
+    const uint64_t i = (uint64_t)blockIdx.x * COUNT_THREADS + threadIdx.x;
+    if (i < n) {
+        uint64_t tk[W];
+#pragma unroll
+        for (int w = 0; w < W; w++) tk[w] = in[i * W + w];
+        if (!table_insert<W>(tv, tk)) n_fail++;
+    }
+    block_add4(blockIdx.x == 0 && threadIdx.x == 0 ? n : 0, n_fail, 0, 0, &ctr->inserted, &ctr->overflow, nullptr,
+               nullptr);
 }
 
 // Level 2: coarse bin c (block = c * B2 + j) -> its F2 regions (next bits of tkey[0]).
@@ -458,8 +524,7 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_p2(TableView tv, PartBufs pb)
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int RUNW = run_w<W>(), TW = tile_win<W>();
     const uint32_t F = tv.F2;
-    const int shift = tv.rbits ? 64 - tv.rbits : 63;
-    const uint32_t fmask = F - 1;
+    const BinFn bin{0, tv.rbits ? 64 - tv.rbits : 63, F - 1, 0};
     const PartLds l = part_lds(smem, F);
     const int tid = threadIdx.x;
     const uint32_t c = blockIdx.x / pb.B2, j = blockIdx.x % pb.B2;
@@ -483,11 +548,11 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_p2(TableView tv, PartBufs pb)
             for (int w = 0; w < W; w++) tk[q][w] = ok[q] ? pb.keys1[i * W + w] : 0;
         }
         if constexpr (SCATTER) {
-            scatter_tile<W, RUNW>(l, F, shift, fmask, tk, ok, pb.keys2);
+            scatter_tile<W, RUNW>(l, F, bin, tk, ok, pb.keys2);
         } else {
 #pragma unroll
             for (int q = 0; q < RUNW; q++)
-                if (ok[q]) atomicAdd(&l.hist[(uint32_t)(tk[q][0] >> shift) & fmask], 1u);
+                if (ok[q]) atomicAdd(&l.hist[bin(tk[q][0])], 1u);
         }
     }
     if constexpr (!SCATTER) {
@@ -796,29 +861,46 @@ static hipError_t set_smem(K kernel, size_t bytes) {
                                (int)bytes);
 }
 
-template <int W, int MODE>
-static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf, DevCounters* ctr, PartBufs pb,
-                                hipStream_t s) {
-    const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
-    const size_t sm1 = part_smem<W>(t.F1), sm2 = part_smem<W>(t.F2);
-    const size_t sm1h = hist_smem(t.F1), sm2h = hist_smem(t.F2);  // histogram passes: no key buffer
+static BinFn coarse_bins(const TableView& t) { return BinFn{0, t.f1bits ? 64 - t.f1bits : 63, t.F1 - 1, 0}; }
+
+template <int W>
+static hipError_t part_levels23(TableView t, DevCounters* ctr, PartBufs pb, hipStream_t s) {
+    const size_t sm2 = part_smem<W>(t.F2), sm2h = hist_smem(t.F2);
     const size_t sm3 = (size_t)BPR * BUCKET_WORDS * 8;
     hipError_t e;
-    if ((e = set_smem(k_p1<W, MODE, false>, sm1h)) != hipSuccess) return e;
-    if ((e = set_smem(k_p1<W, MODE, true>, sm1)) != hipSuccess) return e;
     if ((e = set_smem(k_p2<W, false>, sm2h)) != hipSuccess) return e;
     if ((e = set_smem(k_p2<W, true>, sm2)) != hipSuccess) return e;
     if ((e = set_smem(k_p3<W>, sm3)) != hipSuccess) return e;
-    hipLaunchKernelGGL((k_p1<W, MODE, false>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1h, s, sym, k, t, bf, ctr, pb,
-                       pk, pkm1);
-    launch_scan(pb.hist1, (uint64_t)t.F1 * pb.nblk1, pb.off1, pb.bsum, s);
-    hipLaunchKernelGGL((k_p1<W, MODE, true>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1, s, sym, k, t, bf, ctr, pb,
-                       pk, pkm1);
     hipLaunchKernelGGL((k_p2<W, false>), dim3(t.F1 * pb.B2), dim3(COUNT_THREADS), sm2h, s, t, pb);
     launch_scan(pb.hist2, t.R * pb.B2, pb.off2, pb.bsum, s);
     hipLaunchKernelGGL((k_p2<W, true>), dim3(t.F1 * pb.B2), dim3(COUNT_THREADS), sm2, s, t, pb);
     hipLaunchKernelGGL((k_p3<W>), dim3((unsigned)t.R), dim3(COUNT_THREADS), sm3, s, t, pb, ctr);
     return hipGetLastError();
+}
+
+// level 1 from the symbol stream: windows -> F bins by `bin`, keys into `out`
+template <int W, int MODE>
+static hipError_t part_level1(PackedView sym, int k, BloomView bf, DevCounters* ctr, PartBufs pb, uint32_t F,
+                              BinFn bin, uint64_t* out, hipStream_t s) {
+    const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
+    const size_t sm1 = part_smem<W>(F), sm1h = hist_smem(F);
+    hipError_t e;
+    if ((e = set_smem(k_p1<W, MODE, false>, sm1h)) != hipSuccess) return e;
+    if ((e = set_smem(k_p1<W, MODE, true>, sm1)) != hipSuccess) return e;
+    hipLaunchKernelGGL((k_p1<W, MODE, false>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1h, s, sym, k, bf, ctr, pb, F,
+                       bin, out, pk, pkm1);
+    launch_scan(pb.hist1, (uint64_t)F * pb.nblk1, pb.off1, pb.bsum, s);
+    hipLaunchKernelGGL((k_p1<W, MODE, true>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1, s, sym, k, bf, ctr, pb, F,
+                       bin, out, pk, pkm1);
+    return hipGetLastError();
+}
+
+template <int W, int MODE>
+static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf, DevCounters* ctr, PartBufs pb,
+                                hipStream_t s) {
+    hipError_t e = part_level1<W, MODE>(sym, k, bf, ctr, pb, t.F1, coarse_bins(t), pb.keys1, s);
+    if (e != hipSuccess) return e;
+    return part_levels23<W>(t, ctr, pb, s);
 }
 
 hipError_t launch_count_partitioned(PackedView sym, uint64_t sym_bound, int k, int mode, TableView t,
@@ -830,6 +912,55 @@ hipError_t launch_count_partitioned(PackedView sym, uint64_t sym_bound, int k, i
     case 2: return gate ? launch_part_w<2, 2>(sym, k, t, bf, ctr, pb, s) : launch_part_w<2, 0>(sym, k, t, bf, ctr, pb, s);
     case 3: return gate ? launch_part_w<3, 2>(sym, k, t, bf, ctr, pb, s) : launch_part_w<3, 0>(sym, k, t, bf, ctr, pb, s);
     case 4: return gate ? launch_part_w<4, 2>(sym, k, t, bf, ctr, pb, s) : launch_part_w<4, 0>(sym, k, t, bf, ctr, pb, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+// Routing for hash-prefix sharding: windows -> table keys grouped by owner shard into
+// `out`; per-owner offsets in pb.off1 ([owner][block], exclusive, last entry = total).
+template <int W>
+static hipError_t route_w(PackedView sym, int k, DevCounters* ctr, PartBufs pb, uint32_t parts, uint64_t* out,
+                          hipStream_t s) {
+    return part_level1<W, 0>(sym, k, BloomView{}, ctr, pb, parts, BinFn{1, 0, 0, parts}, out, s);
+}
+hipError_t launch_route(PackedView sym, int k, int W, DevCounters* ctr, PartBufs pb, uint32_t parts, uint64_t* out,
+                        hipStream_t s) {
+    switch (W) {
+    case 1: return route_w<1>(sym, k, ctr, pb, parts, out, s);
+    case 2: return route_w<2>(sym, k, ctr, pb, parts, out, s);
+    case 3: return route_w<3>(sym, k, ctr, pb, parts, out, s);
+    case 4: return route_w<4>(sym, k, ctr, pb, parts, out, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+// Insert an array of table keys (e.g. received from other shards).
+template <int W>
+static hipError_t insert_keys_w(const uint64_t* keys, uint64_t n, bool partitioned, TableView t, DevCounters* ctr,
+                                PartBufs pb, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    if (!partitioned) {
+        hipLaunchKernelGGL((k_insert_keys<W>), dim3((unsigned)((n + COUNT_THREADS - 1) / COUNT_THREADS)),
+                           dim3(COUNT_THREADS), 0, s, keys, n, t, ctr);
+        return hipGetLastError();
+    }
+    const BinFn bin = coarse_bins(t);
+    const size_t sm1 = part_smem<W>(t.F1), sm1h = hist_smem(t.F1);
+    hipError_t e;
+    if ((e = set_smem(k_p1k<W, false>, sm1h)) != hipSuccess) return e;
+    if ((e = set_smem(k_p1k<W, true>, sm1)) != hipSuccess) return e;
+    hipLaunchKernelGGL((k_p1k<W, false>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1h, s, keys, n, pb, t.F1, bin, ctr);
+    launch_scan(pb.hist1, (uint64_t)t.F1 * pb.nblk1, pb.off1, pb.bsum, s);
+    hipLaunchKernelGGL((k_p1k<W, true>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1, s, keys, n, pb, t.F1, bin, ctr);
+    return part_levels23<W>(t, ctr, pb, s);
+}
+hipError_t launch_insert_keys(const uint64_t* keys, uint64_t n, bool partitioned, TableView t, DevCounters* ctr,
+                              PartBufs pb, hipStream_t s) {
+    switch (t.W) {
+    case 1: return insert_keys_w<1>(keys, n, partitioned, t, ctr, pb, s);
+    case 2: return insert_keys_w<2>(keys, n, partitioned, t, ctr, pb, s);
+    case 3: return insert_keys_w<3>(keys, n, partitioned, t, ctr, pb, s);
+    case 4: return insert_keys_w<4>(keys, n, partitioned, t, ctr, pb, s);
     default: return hipErrorInvalidValue;
     }
 }

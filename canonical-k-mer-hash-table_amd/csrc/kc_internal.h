@@ -118,6 +118,12 @@ hipError_t launch_count(PackedView sv, uint64_t sym_bound, int k, int mode, Tabl
 hipError_t launch_count_partitioned(PackedView sv, uint64_t sym_bound, int k, int mode, TableView t,
                                     BloomView bf, DevCounters* ctr, PartBufs pb, hipStream_t s);
 int run_width(int W);  // windows rolled per thread in the partitioned kernels
+// hash-prefix sharding: windows -> table keys grouped by owner (offsets in pb.off1)
+hipError_t launch_route(PackedView sym, int k, int W, DevCounters* ctr, PartBufs pb, uint32_t parts, uint64_t* out,
+                        hipStream_t s);
+// insert an array of table keys into this shard's table
+hipError_t launch_insert_keys(const uint64_t* keys, uint64_t n, bool partitioned, TableView t, DevCounters* ctr,
+                              PartBufs pb, hipStream_t s);
 hipError_t launch_dump(TableView t, int count_mode, uint64_t min_abundance, uint64_t* out, DevCounters* ctr,
                        hipStream_t s);
 hipError_t launch_synth(uint8_t* dst, uint64_t first_read, uint64_t n_reads, uint64_t seed, uint64_t genome_len,

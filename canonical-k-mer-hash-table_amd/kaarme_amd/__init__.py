@@ -43,7 +43,7 @@ EXPORTS = (
     "kc_create", "kc_destroy", "kc_last_error", "kc_bloom_chunk", "kc_bloom_finalize",
     "kc_count_chunk", "kc_bloom_device", "kc_count_device", "kc_sync", "kc_finish", "kc_dump",
     "kc_write", "kc_key_words", "kc_free", "kc_plan_chunks", "kc_synth_bytes", "kc_synth_device",
-    "kc_reset", "kc_profile", "kc_get_timing",
+    "kc_reset", "kc_profile", "kc_get_timing", "kc_route_device", "kc_insert_keys_device",
 )
 
 
@@ -122,6 +122,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                                  ctypes.POINTER(U64)]),
         "kc_synth_bytes": (U64, [U64, U64, ctypes.c_uint32, ctypes.c_uint32]),
         "kc_reset": (I32, [P]),
+        "kc_route_device": (I32, [P, P, ctypes.POINTER(kc_chunk), ctypes.c_size_t, I32, ctypes.c_uint32, P, U64,
+                                  ctypes.POINTER(U64), P]),
+        "kc_insert_keys_device": (I32, [P, P, U64, P]),
         "kc_profile": (I32, [P, I32]),
         "kc_get_timing": (I32, [P, ctypes.POINTER(kc_timing)]),
         "kc_synth_device": (I32, [P, U64, U64, U64, U64, ctypes.c_uint32, ctypes.c_uint32,
@@ -262,6 +265,23 @@ class KmerCounter:
         arr = self._chunk_array(chunks)
         self._chk(self.lib.kc_count_device(self._ctx, ctypes.c_void_p(dev_ptr), arr, len(chunks), fmt,
                                            ctypes.c_void_p(stream or None)), "kc_count_device")
+
+    def route_device(self, dev_ptr: int, chunks, fmt: int, nshards: int, out_ptr: int, out_capacity: int,
+                     stream: int = 0) -> List[int]:
+        """Table keys of the image's windows grouped by owner shard into out_ptr; returns counts."""
+        arr = self._chunk_array(chunks)
+        counts = (ctypes.c_uint64 * nshards)()
+        self._chk(self.lib.kc_route_device(self._ctx, ctypes.c_void_p(dev_ptr), arr, len(chunks), fmt, nshards,
+                                           ctypes.c_void_p(out_ptr), out_capacity, counts,
+                                           ctypes.c_void_p(stream or None)), "kc_route_device")
+        return [int(x) for x in counts]
+
+    def insert_keys_device(self, keys_ptr: int, n_keys: int, stream: int = 0):
+        self._chk(self.lib.kc_insert_keys_device(self._ctx, ctypes.c_void_p(keys_ptr), n_keys,
+                                                 ctypes.c_void_p(stream or None)), "kc_insert_keys_device")
+
+    def key_words(self) -> int:
+        return self.lib.kc_key_words(self._ctx)
 
     def sync(self):
         self._chk(self.lib.kc_sync(self._ctx), "kc_sync")

@@ -110,6 +110,17 @@ int kc_count_device(kc_ctx* ctx, const uint8_t* dev_image, const kc_chunk* chunk
 /* Wait for all work enqueued on the context. */
 int kc_sync(kc_ctx* ctx);
 
+/* Multi-GPU hash-prefix sharding (the reference is single-process):
+ * kc_route_device tokenizes a device image (its chunks must fit one staging batch) and
+ * writes the table keys of its windows to dev_out grouped by owner shard (kc_key_words()
+ * u64 per key, the engine's internal bijective key encoding); counts[d] = keys for
+ * shard d.  out_capacity (keys) must be >= the image bytes + chunks.  The caller
+ * exchanges the groups (all-to-all) and every owner inserts what it received with
+ * kc_insert_keys_device.  Not available with the Bloom filter. */
+int kc_route_device(kc_ctx* ctx, const uint8_t* dev_image, const kc_chunk* chunks, size_t n_chunks, int fmt,
+                    uint32_t nshards, uint64_t* dev_out, uint64_t out_capacity, uint64_t* counts, void* hip_stream);
+int kc_insert_keys_device(kc_ctx* ctx, const uint64_t* dev_keys, uint64_t n_keys, void* hip_stream);
+
 /* Re-initialise the table, the Bloom filter and all counters (the table/filter
  * constructors again, without reallocating). */
 int kc_reset(kc_ctx* ctx);

@@ -1,0 +1,75 @@
+"""GPU: the sharded counting path (kc_route_device -> exchange -> kc_insert_keys_device).
+
+One GPU, G emulated ranks: each rank is its own engine (own table) and counts its own
+slice of the reads; the all-to-all is emulated in-process by slicing the owner groups.
+The per-rank outputs must be disjoint and their union must equal the oracle's count of
+the whole input (bit-exact sorted output).  The same ranks over RCCL are what bench.py
+runs at N > 1; tests/test_sharded.py covers the collective itself over gloo.
+"""
+import subprocess
+
+import pytest
+import torch
+
+from conftest import GEN, oracle_count, sorted_digest_file, sorted_digest_lines
+import kaarme_amd as ka
+from kaarme_amd.sharded import DeviceEngine
+
+pytestmark = pytest.mark.gpu
+
+
+def _image(path):
+    data = open(path, "rb").read()
+    return data, torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+
+
+@pytest.mark.parametrize("k,mode,G,path", [(31, 2, 2, "direct"), (31, 2, 3, "partitioned"),
+                                            (21, 0, 4, "partitioned"), (51, 2, 2, "direct"),
+                                            (51, 0, 3, "partitioned"), (95, 1, 2, "partitioned")])
+def test_emulated_ranks_union(tmp_path, monkeypatch, k, mode, G, path):
+    monkeypatch.setenv("KC_INSERT_PATH", path)
+    n_reads = 30000
+    per = n_reads // G
+    images = []
+    for r in range(G):
+        fa = tmp_path / f"r{r}.fasta"
+        cnt = per if r < G - 1 else n_reads - per * (G - 1)
+        subprocess.run([GEN, str(fa), str(n_reads), "150", "200000", "--first", str(r * per), "--count", str(cnt)],
+                       check=True)
+        images.append(_image(str(fa)))
+    whole = tmp_path / "all.fasta"
+    with open(whole, "wb") as f:
+        for data, _ in images:
+            f.write(data)
+    engines = [DeviceEngine(ka.Config(k=k, mode=mode, table_slots=400000, min_abundance=1,
+                                      batch_bytes=max(len(d) for d, _ in images) * 2 + (1 << 20)))
+               for _ in range(G)]
+    W = engines[0].W
+    stream = torch.cuda.current_stream().cuda_stream
+    routed = []
+    for r, (data, img) in enumerate(images):
+        chunks = ka.plan_chunks(data, k, ka.FMT_FASTA, chunk_size=256 * 1024)
+        buf, counts = engines[r].route(img.data_ptr(), chunks, ka.FMT_FASTA, G, stream)
+        torch.cuda.synchronize()
+        assert sum(counts) == engines[r].kc.finish()["windows"]
+        routed.append((buf.clone(), counts))
+    for d in range(G):  # emulated all-to-all: rank d receives group d of every source, in rank order
+        parts = []
+        for buf, counts in routed:
+            lo = sum(counts[:d]) * W
+            parts.append(buf[lo:lo + counts[d] * W])
+        recv = torch.cat(parts)
+        n = recv.numel() // W
+        engines[d].insert(recv, n, stream)
+        torch.cuda.synchronize()
+        assert engines[d].kc.finish()["inserted"] == n
+    shard_lines = [set(e.kc.lines()) for e in engines]
+    kmers = [set(l.rsplit(" ", 1)[0] for l in s) for s in shard_lines]
+    for a in range(G):
+        for b in range(a + 1, G):
+            assert not (kmers[a] & kmers[b]), "a k-mer has two owners"
+        assert kmers[a], "empty shard"
+    union = set().union(*shard_lines)
+    out = tmp_path / "oracle.txt"
+    oracle_count(str(whole), k, ["-m", str(mode), "-a", "1"], out)
+    assert sorted_digest_lines(union) == sorted_digest_file(out)
