@@ -217,6 +217,7 @@ def main():
         "hbm_gbs_step": round(bytes_per_launch * (launches / args.steps) / (step_ms * 1e-3) / 1e9, 2),
         "kernel_ms": {"gather": round(tm["gather_ms"] / launches, 4), "tokenize": round(tm["tokenize_ms"] / launches, 4),
                       "count": round(count_ms, 4)},
+        "image_bytes": nbytes, "stage_bytes": sum(c[1] for c in chunks),
         "windows_per_step_per_gpu": windows_step, "distinct_per_gpu": st["distinct"],
         "cpu_baseline": None,
     }

@@ -223,7 +223,13 @@ static bool use_partitioned(const kc_ctx* c, uint64_t syms) {
     return (double)syms * 275.0 > (double)syms * (4.0 * c->W + 1) * 8.0 + 2.0 * table_bytes;
 }
 
-static hipStream_t pick_stream(kc_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
+// The device entry points run on the caller's stream, ordered after the work already
+// enqueued there (NULL = the HIP null stream, PyTorch's default current stream), and
+// hand over to/from the context's own stream with events.
+static hipStream_t pick_stream(kc_ctx* c, void* s) {
+    (void)c;
+    return (hipStream_t)s;
+}
 
 // ------------------------------------------------------------------------------
 // batch execution
@@ -644,6 +650,9 @@ int kc_finish(kc_ctx* c, kc_stats* st) {
             st->distinct = occ;
         }
     }
+    if (h.invalid)
+        return c->fail(KC_ERR_ARG, std::to_string(h.invalid) + " keys passed to kc_insert_keys_device were not table keys "
+                                   "(word 0 == 0) and were skipped");
     if (h.overflow) return c->fail(KC_ERR_TABLE_FULL, "Hash table is full (" + std::to_string(h.overflow) +
                                                            " k-mers could not be inserted)");
     return KC_OK;

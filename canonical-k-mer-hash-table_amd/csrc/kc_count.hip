@@ -329,21 +329,24 @@ DEV PartLds part_lds(uint8_t* smem, uint32_t F) {
     return l;
 }
 
-// bin of a table key: a bit field of word 0 (table levels) or the shard owner (routing)
-struct BinFn {
-    int owner;       // 1: owner_of(t0, parts)
+// bin of a table key: a bit field of word 0 (table levels) or the shard owner (routing);
+// the kind is a template parameter so the table levels carry no routing branch.
+struct BinBits {
+    static constexpr bool kOwner = false;
     int shift;
     uint32_t mask;
+    DEV uint32_t operator()(uint64_t t0) const { return (uint32_t)(t0 >> shift) & mask; }
+};
+struct BinOwner {
+    static constexpr bool kOwner = true;
     uint32_t parts;
-    DEV uint32_t operator()(uint64_t t0) const {
-        return owner ? owner_of(t0, parts) : (uint32_t)(t0 >> shift) & mask;
-    }
+    DEV uint32_t operator()(uint64_t t0) const { return owner_of(t0, parts); }
 };
 
 // Counting-sort the tile's keys (in registers: tk[j] valid where ok[j]) by bin into
 // LDS and write each bin as one contiguous run at gbase[bin].
-template <int W, int RUNW>
-DEV void scatter_tile(const PartLds& l, uint32_t F, const BinFn& bin, const uint64_t (&tk)[RUNW][W],
+template <int W, int RUNW, class Bin>
+DEV void scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const uint64_t (&tk)[RUNW][W],
                       const bool (&ok)[RUNW], uint64_t* __restrict__ out) {
     const int tid = threadIdx.x;
 #pragma unroll
@@ -381,9 +384,9 @@ DEV void scatter_tile(const PartLds& l, uint32_t F, const BinFn& bin, const uint
 
 // Level 1: windows of a contiguous symbol range -> coarse bins (top f1bits of tkey[0]).
 // SCATTER = false: histogram only ([bin][block] into hist1); true: write the keys.
-template <int W, int MODE, bool SCATTER>
+template <int W, int MODE, bool SCATTER, class Bin>
 __global__ __launch_bounds__(COUNT_THREADS) void k_p1(PackedView sv, int k, BloomView bf,
-                                                      DevCounters* __restrict__ ctr, PartBufs pb, uint32_t F, BinFn bin,
+                                                      DevCounters* __restrict__ ctr, PartBufs pb, uint32_t F, Bin bin,
                                                       uint64_t* __restrict__ out, uint64_t pow5_k, uint64_t pow5_km1) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int RUNW = run_w<W>(), TW = tile_win<W>();
@@ -457,7 +460,7 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_p1(PackedView sv, int k, Bloo
         __syncthreads();
         for (uint32_t b = tid; b < F; b += COUNT_THREADS) pb.hist1[(uint64_t)b * pb.nblk1 + blockIdx.x] = l.hist[b];
         // routing (owner bins) counts windows here and insertions at the owner
-        block_add4(n_win, bin.owner ? 0 : n_ins, 0, 0, &ctr->windows, &ctr->inserted, nullptr, nullptr);
+        block_add4(n_win, Bin::kOwner ? 0 : n_ins, 0, 0, &ctr->windows, &ctr->inserted, nullptr, nullptr);
     }
 }
 
@@ -465,7 +468,7 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_p1(PackedView sv, int k, Bloo
 // blocks, bins = top f1bits of the table key.
 template <int W, bool SCATTER>
 __global__ __launch_bounds__(COUNT_THREADS) void k_p1k(const uint64_t* __restrict__ in, uint64_t n, PartBufs pb,
-                                                       uint32_t F, BinFn bin, DevCounters* __restrict__ ctr) {
+                                                       uint32_t F, BinBits bin, DevCounters* __restrict__ ctr) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int RUNW = run_w<W>(), TW = tile_win<W>();
     const PartLds l = part_lds(smem, F);
@@ -477,15 +480,17 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_p1k(const uint64_t* __restric
         if constexpr (SCATTER) l.gbase[b] = pb.off1[(uint64_t)b * pb.nblk1 + blockIdx.x];
     }
     __syncthreads();
+    uint32_t n_inv = 0;
     for (uint64_t t0 = lo; t0 < hi; t0 += TW) {
         uint64_t tk[RUNW][W];
         bool ok[RUNW];
 #pragma unroll
         for (int q = 0; q < RUNW; q++) {
             const uint64_t i = t0 + tid + (uint64_t)q * COUNT_THREADS;
-            ok[q] = i < hi;
 #pragma unroll
-            for (int w = 0; w < W; w++) tk[q][w] = ok[q] ? in[i * W + w] : 0;
+            for (int w = 0; w < W; w++) tk[q][w] = i < hi ? in[i * W + w] : 0;
+            ok[q] = tk[q][0] != EMPTY;  // 0 is never a table key: skip (counted as invalid)
+            if constexpr (!SCATTER) n_inv += (i < hi) & !ok[q];
         }
         if constexpr (SCATTER) {
             scatter_tile<W, RUNW>(l, F, bin, tk, ok, pb.keys1);
@@ -498,7 +503,7 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_p1k(const uint64_t* __restric
     if constexpr (!SCATTER) {
         __syncthreads();
         for (uint32_t b = tid; b < F; b += COUNT_THREADS) pb.hist1[(uint64_t)b * pb.nblk1 + blockIdx.x] = l.hist[b];
-        if (blockIdx.x == 0 && tid == 0) atomicAdd(&ctr->inserted, (unsigned long long)n);
+        block_add4(blockIdx.x == 0 && tid == 0 ? n : 0, n_inv, 0, 0, &ctr->inserted, &ctr->invalid, nullptr, nullptr);
     }
 }
 
@@ -506,16 +511,17 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_p1k(const uint64_t* __restric
 template <int W>
 __global__ __launch_bounds__(COUNT_THREADS) void k_insert_keys(const uint64_t* __restrict__ in, uint64_t n,
                                                                TableView tv, DevCounters* __restrict__ ctr) {
-    uint32_t n_fail = 0;
+    uint32_t n_fail = 0, n_inv = 0;
     const uint64_t i = (uint64_t)blockIdx.x * COUNT_THREADS + threadIdx.x;
     if (i < n) {
         uint64_t tk[W];
 #pragma unroll
         for (int w = 0; w < W; w++) tk[w] = in[i * W + w];
-        if (!table_insert<W>(tv, tk)) n_fail++;
+        if (tk[0] == EMPTY) n_inv++;  // 0 is never a table key: skip (counted as invalid)
+        else if (!table_insert<W>(tv, tk)) n_fail++;
     }
-    block_add4(blockIdx.x == 0 && threadIdx.x == 0 ? n : 0, n_fail, 0, 0, &ctr->inserted, &ctr->overflow, nullptr,
-               nullptr);
+    block_add4(blockIdx.x == 0 && threadIdx.x == 0 ? n : 0, n_fail, n_inv, 0, &ctr->inserted, &ctr->overflow,
+               &ctr->invalid, nullptr);
 }
 
 // Level 2: coarse bin c (block = c * B2 + j) -> its F2 regions (next bits of tkey[0]).
@@ -524,7 +530,7 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_p2(TableView tv, PartBufs pb)
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int RUNW = run_w<W>(), TW = tile_win<W>();
     const uint32_t F = tv.F2;
-    const BinFn bin{0, tv.rbits ? 64 - tv.rbits : 63, F - 1, 0};
+    const BinBits bin{tv.rbits ? 64 - tv.rbits : 63, F - 1};
     const PartLds l = part_lds(smem, F);
     const int tid = threadIdx.x;
     const uint32_t c = blockIdx.x / pb.B2, j = blockIdx.x % pb.B2;
@@ -861,7 +867,7 @@ static hipError_t set_smem(K kernel, size_t bytes) {
                                (int)bytes);
 }
 
-static BinFn coarse_bins(const TableView& t) { return BinFn{0, t.f1bits ? 64 - t.f1bits : 63, t.F1 - 1, 0}; }
+static BinBits coarse_bins(const TableView& t) { return BinBits{t.f1bits ? 64 - t.f1bits : 63, t.F1 - 1}; }
 
 template <int W>
 static hipError_t part_levels23(TableView t, DevCounters* ctr, PartBufs pb, hipStream_t s) {
@@ -879,18 +885,18 @@ static hipError_t part_levels23(TableView t, DevCounters* ctr, PartBufs pb, hipS
 }
 
 // level 1 from the symbol stream: windows -> F bins by `bin`, keys into `out`
-template <int W, int MODE>
+template <int W, int MODE, class Bin>
 static hipError_t part_level1(PackedView sym, int k, BloomView bf, DevCounters* ctr, PartBufs pb, uint32_t F,
-                              BinFn bin, uint64_t* out, hipStream_t s) {
+                              Bin bin, uint64_t* out, hipStream_t s) {
     const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
     const size_t sm1 = part_smem<W>(F), sm1h = hist_smem(F);
     hipError_t e;
-    if ((e = set_smem(k_p1<W, MODE, false>, sm1h)) != hipSuccess) return e;
-    if ((e = set_smem(k_p1<W, MODE, true>, sm1)) != hipSuccess) return e;
-    hipLaunchKernelGGL((k_p1<W, MODE, false>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1h, s, sym, k, bf, ctr, pb, F,
+    if ((e = set_smem(k_p1<W, MODE, false, Bin>, sm1h)) != hipSuccess) return e;
+    if ((e = set_smem(k_p1<W, MODE, true, Bin>, sm1)) != hipSuccess) return e;
+    hipLaunchKernelGGL((k_p1<W, MODE, false, Bin>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1h, s, sym, k, bf, ctr, pb, F,
                        bin, out, pk, pkm1);
     launch_scan(pb.hist1, (uint64_t)F * pb.nblk1, pb.off1, pb.bsum, s);
-    hipLaunchKernelGGL((k_p1<W, MODE, true>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1, s, sym, k, bf, ctr, pb, F,
+    hipLaunchKernelGGL((k_p1<W, MODE, true, Bin>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1, s, sym, k, bf, ctr, pb, F,
                        bin, out, pk, pkm1);
     return hipGetLastError();
 }
@@ -921,7 +927,7 @@ hipError_t launch_count_partitioned(PackedView sym, uint64_t sym_bound, int k, i
 template <int W>
 static hipError_t route_w(PackedView sym, int k, DevCounters* ctr, PartBufs pb, uint32_t parts, uint64_t* out,
                           hipStream_t s) {
-    return part_level1<W, 0>(sym, k, BloomView{}, ctr, pb, parts, BinFn{1, 0, 0, parts}, out, s);
+    return part_level1<W, 0>(sym, k, BloomView{}, ctr, pb, parts, BinOwner{parts}, out, s);
 }
 hipError_t launch_route(PackedView sym, int k, int W, DevCounters* ctr, PartBufs pb, uint32_t parts, uint64_t* out,
                         hipStream_t s) {
@@ -944,7 +950,7 @@ static hipError_t insert_keys_w(const uint64_t* keys, uint64_t n, bool partition
                            dim3(COUNT_THREADS), 0, s, keys, n, t, ctr);
         return hipGetLastError();
     }
-    const BinFn bin = coarse_bins(t);
+    const BinBits bin = coarse_bins(t);
     const size_t sm1 = part_smem<W>(t.F1), sm1h = hist_smem(t.F1);
     hipError_t e;
     if ((e = set_smem(k_p1k<W, false>, sm1h)) != hipSuccess) return e;

@@ -1,4 +1,4 @@
-// kc_internal.h -- declarations shared by the HIP kernels (kc_device.hip) and the
+// kc_internal.h -- declarations shared by the HIP kernels (kc_tokenize.hip, kc_count.hip) and the
 // host side of the C ABI (kc_api.cpp).  Not part of the public boundary
 // (that is include/kc_api.h).
 #pragma once
@@ -62,6 +62,7 @@ struct DevCounters {
     unsigned long long occupied;        uint64_t _p7[15];
     unsigned long long stream_len;      uint64_t _p8[15];
     unsigned long long bf_windows;      uint64_t _p9[15];
+    unsigned long long invalid;         uint64_t _p10[15];  // received keys with word 0 == 0 (skipped)
 };
 
 // The symbol stream: 32 symbols per word, symbol j of word w at bits 62-2j of pk[w]
@@ -105,7 +106,7 @@ struct BloomView {
 inline int words_for_k(int k) { return k / 32 + 1; }          // spare top bit for EMPTY
 inline int slots_per_bucket(int W) { return BUCKET_WORDS / (W + 1); }
 
-// ---- launchers (kc_device.hip) -------------------------------------------------
+// ---- launchers (kc_tokenize.hip, kc_count.hip) -------------------------------------------------
 hipError_t launch_gather(const uint8_t* src, uint8_t* stage, const ChunkDesc* d_chunks, int n_chunks,
                          const ChunkDesc* h_chunks, hipStream_t s);
 hipError_t launch_tokenize(const uint8_t* stage, uint64_t ntiles, const ChunkDesc* d_chunks, int n_chunks,

@@ -101,8 +101,10 @@ int kc_bloom_finalize(kc_ctx* ctx, uint64_t* new_in_second);
 int kc_count_chunk(kc_ctx* ctx, const uint8_t* buf, size_t len, int fmt, int broken_header);
 
 /* The same two passes over a DEVICE-resident file image and a chunk table
- * (kc_plan_chunks), enqueued on hip_stream (a hipStream_t, NULL = the context's
- * stream).  The image must stay valid until the work completes (kc_sync). */
+ * (kc_plan_chunks), enqueued on hip_stream (a hipStream_t; NULL = the HIP null
+ * stream) after the work already queued there, so a buffer produced on that stream
+ * (e.g. by PyTorch on its current stream) is safe to pass.  The image must stay valid
+ * until the work completes (kc_sync).  Every *_device entry point follows this rule. */
 int kc_bloom_device(kc_ctx* ctx, const uint8_t* dev_image, const kc_chunk* chunks, size_t n_chunks, int fmt,
                     void* hip_stream);
 int kc_count_device(kc_ctx* ctx, const uint8_t* dev_image, const kc_chunk* chunks, size_t n_chunks, int fmt,

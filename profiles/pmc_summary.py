@@ -1,0 +1,85 @@
+#!/usr/bin/env python3
+"""Summarise profiles/collect_pmc.sh output: per-kernel mean counters per dispatch and
+the HBM traffic of one counting pass (bench.py's roofline.traffic).
+
+HBM bytes follow MI355X_MICROARCH.md (HBM / rocprofv3): FETCH_SIZE and WRITE_SIZE are
+the L2 memory-side request counters; on gfx950 FETCH_SIZE reports half the bytes of
+wide coalesced reads, so reads are doubled.  The unit of both (KiB in rocprofv3) is
+calibrated on k_gather's stores, 16-byte streaming writes of exactly `stage_bytes`
+bytes per step (a known byte count), and applied to every kernel.
+
+usage: pmc_summary.py OUTDIR [--write profiles/pmc_traffic.json]
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+COUNT_PASS = ("k_p1<", "k_p2<", "k_p3<", "k_scanA", "k_scanB", "k_scanC", "k_count<")
+
+
+def short(name):
+    n = name.split("(")[0].replace("void ", "").replace("kc::", "")
+    return n
+
+
+def load(outdir):
+    vals = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> [per dispatch]
+    for f in glob.glob(os.path.join(outdir, "pmc*", "**", "*counter_collection.csv"), recursive=True):
+        per = defaultdict(float)
+        names = {}
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                key = (r["Dispatch_Id"], r["Counter_Name"])
+                per[key] += float(r["Counter_Value"])
+                names[r["Dispatch_Id"]] = r["Kernel_Name"]
+        for (d, c), v in per.items():
+            vals[short(names[d])][c].append(v)
+    return vals
+
+
+def main():
+    outdir = sys.argv[1]
+    dest = sys.argv[sys.argv.index("--write") + 1] if "--write" in sys.argv else None
+    vals = load(outdir)
+    bench = None
+    for j in sorted(glob.glob(os.path.join(outdir, "pmc*.json"))):
+        try:
+            bench = json.loads(open(j).read().strip().splitlines()[-1])
+            break
+        except (ValueError, IndexError):
+            continue
+    steps = bench["steps"] + bench["warmup"]
+    mean = {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in vals.items()}
+    gather = [k for k in mean if k.startswith("k_gather")]
+    unit = None
+    if gather and "WRITE_SIZE" in mean[gather[0]] and bench.get("stage_bytes"):
+        unit = bench["stage_bytes"] / mean[gather[0]]["WRITE_SIZE"]
+    print(f"unit (bytes per counter unit, from k_gather writes): {unit}")
+    print(f"{'kernel':60s} {'calls':>5s} {'read GB':>9s} {'write GB':>9s}")
+    total = 0.0
+    per_kernel = {}
+    for k in sorted(mean, key=lambda x: -mean[x].get("FETCH_SIZE", 0)):
+        m = mean[k]
+        calls = max(len(v) for v in vals[k].values())
+        rd = 2 * m.get("FETCH_SIZE", 0) * (unit or 1)
+        wr = m.get("WRITE_SIZE", 0) * (unit or 1)
+        per_kernel[k] = {"calls": calls, "read_bytes": rd, "write_bytes": wr,
+                         **{c: m[c] for c in m if c not in ("FETCH_SIZE", "WRITE_SIZE")}}
+        print(f"{k[:60]:60s} {calls:5d} {rd / 1e9:9.3f} {wr / 1e9:9.3f}")
+        if k.startswith(COUNT_PASS):
+            total += (rd + wr) * calls / steps
+    print(f"count pass HBM bytes per launch: {total / 1e9:.3f} GB")
+    if dest:
+        with open(dest, "w") as f:
+            json.dump({"workload": bench["config"]["workload"], "bytes_per_launch": int(total),
+                       "unit_bytes": unit, "method": "2*FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md HBM), "
+                       "unit calibrated on k_gather 16-B stores; count-pass kernels summed per step",
+                       "per_kernel": per_kernel}, f, indent=1)
+        print("wrote", dest)
+
+
+if __name__ == "__main__":
+    main()

@@ -52,6 +52,8 @@ def test_emulated_ranks_union(tmp_path, monkeypatch, k, mode, G, path):
         buf, counts = engines[r].route(img.data_ptr(), chunks, ka.FMT_FASTA, G, stream)
         torch.cuda.synchronize()
         assert sum(counts) == engines[r].kc.finish()["windows"]
+        keys = buf[: sum(counts) * W].view(-1, W)
+        assert int((keys[:, 0] == 0).sum()) == 0, "table key word 0 is never 0"
         routed.append((buf.clone(), counts))
     for d in range(G):  # emulated all-to-all: rank d receives group d of every source, in rank order
         parts = []
@@ -73,3 +75,16 @@ def test_emulated_ranks_union(tmp_path, monkeypatch, k, mode, G, path):
     out = tmp_path / "oracle.txt"
     oracle_count(str(whole), k, ["-m", str(mode), "-a", "1"], out)
     assert sorted_digest_lines(union) == sorted_digest_file(out)
+
+
+@pytest.mark.parametrize("path", ["direct", "partitioned"])
+def test_insert_rejects_non_table_keys(monkeypatch, path):
+    """Word 0 == 0 marks an empty slot and is never a table key: such keys are skipped
+    (no hang, no corrupted slot) and kc_finish reports them."""
+    monkeypatch.setenv("KC_INSERT_PATH", path)
+    e = DeviceEngine(ka.Config(k=51, mode=0, table_slots=100000, min_abundance=1))
+    keys = torch.zeros(2 * 5000, dtype=torch.int64, device="cuda")
+    keys[::4] = 12345  # every other key (word 0 of even keys) is a valid table key
+    e.insert(keys, 5000, torch.cuda.current_stream().cuda_stream)
+    with pytest.raises(ka.KcError, match="not table keys"):
+        e.kc.finish()
