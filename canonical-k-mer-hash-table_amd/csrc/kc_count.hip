@@ -23,6 +23,8 @@
 // its probe sequence starts at the bucket given by the next 9 bits and wraps inside
 // the region.  W > 1 keys: word 0 claimed by CAS, other words
 // stored, then READY|1 added to the count word; readers matching word 0 wait for READY.
+#include <cstdlib>
+
 #include "kc_common.h"
 
 namespace kc {
@@ -575,8 +577,8 @@ DEV uint64_t* lds_word(uint64_t* lt, uint32_t b, uint32_t word) {
 }
 
 // Level 3: one workgroup per region: LDS-resident table
-template <int W>
-__global__ __launch_bounds__(COUNT_THREADS) void k_p3(TableView tv, PartBufs pb, DevCounters* __restrict__ ctr) {
+template <int W, int NT>
+__global__ __launch_bounds__(NT) void k_p3(TableView tv, PartBufs pb, DevCounters* __restrict__ ctr) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int S = BUCKET_WORDS / (W + 1);
     constexpr int KB = 8;  // keys loaded per thread before inserting (memory-level parallelism)
@@ -587,20 +589,20 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_p3(TableView tv, PartBufs pb,
     uint4* g4 = reinterpret_cast<uint4*>(tv.buckets + r * BPR * BUCKET_WORDS);
     uint4* l4 = reinterpret_cast<uint4*>(lt);
     constexpr int N4 = BPR * BUCKET_WORDS / 2;
-    for (int i = threadIdx.x; i < N4; i += COUNT_THREADS) l4[lds_chunk(i >> 3, i & 7)] = g4[i];
+    for (int i = threadIdx.x; i < N4; i += NT) l4[lds_chunk(i >> 3, i & 7)] = g4[i];
     __syncthreads();
     uint32_t n_fail = 0;
-    for (uint64_t base = start; base < end; base += (uint64_t)KB * COUNT_THREADS) {
+    for (uint64_t base = start; base < end; base += (uint64_t)KB * NT) {
         uint64_t kk[KB][W];
 #pragma unroll
         for (int q = 0; q < KB; q++) {
-            const uint64_t i = base + threadIdx.x + (uint64_t)q * COUNT_THREADS;
+            const uint64_t i = base + threadIdx.x + (uint64_t)q * NT;
 #pragma unroll
             for (int w = 0; w < W; w++) kk[q][w] = i < end ? pb.keys2[i * W + w] : 0;
         }
 #pragma unroll
         for (int q = 0; q < KB; q++) {
-            if (base + threadIdx.x + (uint64_t)q * COUNT_THREADS >= end) continue;
+            if (base + threadIdx.x + (uint64_t)q * NT >= end) continue;
             const uint64_t k0 = kk[q][0];
             uint32_t b = bucket_in_region(k0, tv.rbits);
             bool done = false;
@@ -700,7 +702,7 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_p3(TableView tv, PartBufs pb,
         }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < N4; i += COUNT_THREADS) g4[i] = l4[lds_chunk(i >> 3, i & 7)];
+    for (int i = threadIdx.x; i < N4; i += NT) g4[i] = l4[lds_chunk(i >> 3, i & 7)];
     if (n_fail) atomicAdd(&ctr->overflow, (unsigned long long)n_fail);
 }
 
@@ -876,11 +878,16 @@ static hipError_t part_levels23(TableView t, DevCounters* ctr, PartBufs pb, hipS
     hipError_t e;
     if ((e = set_smem(k_p2<W, false>, sm2h)) != hipSuccess) return e;
     if ((e = set_smem(k_p2<W, true>, sm2)) != hipSuccess) return e;
-    if ((e = set_smem(k_p3<W>, sm3)) != hipSuccess) return e;
+    static const int p3nt = [] {
+        const char* v = std::getenv("KC_P3_THREADS");  // tuning knob: 256 / 512 / 1024
+        return v ? std::atoi(v) : 1024;
+    }();
+    auto p3 = p3nt == 256 ? k_p3<W, 256> : (p3nt == 512 ? k_p3<W, 512> : k_p3<W, 1024>);
+    if ((e = set_smem(p3, sm3)) != hipSuccess) return e;
     hipLaunchKernelGGL((k_p2<W, false>), dim3(t.F1 * pb.B2), dim3(COUNT_THREADS), sm2h, s, t, pb);
     launch_scan(pb.hist2, t.R * pb.B2, pb.off2, pb.bsum, s);
     hipLaunchKernelGGL((k_p2<W, true>), dim3(t.F1 * pb.B2), dim3(COUNT_THREADS), sm2, s, t, pb);
-    hipLaunchKernelGGL((k_p3<W>), dim3((unsigned)t.R), dim3(COUNT_THREADS), sm3, s, t, pb, ctr);
+    hipLaunchKernelGGL(p3, dim3((unsigned)t.R), dim3((unsigned)p3nt), sm3, s, t, pb, ctr);
     return hipGetLastError();
 }
 
