@@ -27,31 +27,26 @@ DEV uint64_t fmix64(uint64_t k) {
     return k;
 }
 
-// 64-bit hash of a canonical key (word 0 most significant)
-template <int W>
-DEV uint64_t key_hash(const uint64_t (&key)[W]) {
-    uint64_t h = fmix64(key[W - 1] ^ 0x243f6a8885a308d3ULL);
-#pragma unroll
-    for (int i = W - 2; i >= 0; i--) h = fmix64(h ^ key[i]);
-    return h;
-}
 // ---- table keys -------------------------------------------------------------------
 // The table stores the canonical key through a bijection ("tkey"): word 0 becomes
-// fmix64(key0 ^ MIX_C ^ (g & M62)), g = a hash of the other words; words 1.. are kept.
-// The hash is computed once per window, every later level (bins, regions, buckets,
-// shard owner) is a bit field of tkey word 0, and k_dump inverts the mix.  key0 < 2^62
-// and MIX_C has bit 63 set, so the fmix64 argument is never 0 and neither is tkey word 0
-// (fmix64 is a bijection with fmix64(0) = 0): 0 marks an empty slot.
+// tmix(key0 ^ MIX_C ^ (g & M62)), g = a hash of the other words; words 1.. are kept.
+// tmix(x) = y ^ (y >> 32) with y = x * TMUL (odd, so both steps are bijections): one
+// 64-bit multiply per window.  The top bits of y (regions, buckets, coarse bins) depend
+// on every bit of x; the low half (shard owner) is folded with the high half.  The hash
+// is computed once per window, every later level is a bit field of tkey word 0, and
+// k_dump inverts the mix.  key0 < 2^62 and MIX_C has bit 63 set, so the tmix argument
+// is never 0 and neither is tkey word 0 (tmix(x) = 0 only for x = 0): 0 marks an empty slot.
 constexpr uint64_t MIX_C = 0x9E3779B97F4A7C15ULL;  // bit 63 set
 constexpr uint64_t M62 = (1ULL << 62) - 1;
+constexpr uint64_t TMUL = 0x9E3779B97F4A7C15ULL;      // odd
+constexpr uint64_t TMUL_INV = 0xF1DE83E19937733DULL;  // TMUL * TMUL_INV = 1 (mod 2^64)
 
-DEV uint64_t fmix64_inv(uint64_t k) {
-    k ^= k >> 33;
-    k *= 0x9cb4b2f8129337dbULL;  // inverse of 0xc4ceb9fe1a85ec53
-    k ^= k >> 33;
-    k *= 0x4f74430c22a54005ULL;  // inverse of 0xff51afd7ed558ccd
-    k ^= k >> 33;
-    return k;
+DEV uint64_t tmix(uint64_t x) {
+    const uint64_t y = x * TMUL;
+    return y ^ (y >> 32);
+}
+DEV uint64_t tmix_inv(uint64_t t) {
+    return (t ^ (t >> 32)) * TMUL_INV;  // y ^ (y >> 32) is an involution
 }
 template <int W>
 DEV uint64_t side_hash(const uint64_t (&w)[W]) {
@@ -62,7 +57,7 @@ DEV uint64_t side_hash(const uint64_t (&w)[W]) {
 }
 template <int W>
 DEV void to_tkey(const uint64_t (&key)[W], uint64_t (&t)[W]) {
-    t[0] = fmix64(key[0] ^ MIX_C ^ side_hash<W>(key));
+    t[0] = tmix(key[0] ^ MIX_C ^ side_hash<W>(key));
 #pragma unroll
     for (int i = 1; i < W; i++) t[i] = key[i];
 }
@@ -70,7 +65,7 @@ template <int W>
 DEV void from_tkey(const uint64_t (&t)[W], uint64_t (&key)[W]) {
 #pragma unroll
     for (int i = 1; i < W; i++) key[i] = t[i];
-    key[0] = fmix64_inv(t[0]) ^ MIX_C ^ side_hash<W>(t);
+    key[0] = tmix_inv(t[0]) ^ MIX_C ^ side_hash<W>(t);
 }
 
 // ---- table geometry -------------------------------------------------------------
