@@ -74,7 +74,7 @@ struct kc_ctx {
     // partitioned insert buffers
     PartBufs pb{};
     uint32_t pb_nblk1_cap = 0;
-    uint64_t pb_key_cap = 0;
+    uint64_t pb_k1_cap = 0, pb_k2_cap = 0;  // keys the level-1 / level-2 buffers hold
 
     // bloom
     uint32_t* d_bloom = nullptr;
@@ -173,8 +173,13 @@ static TableView table_view(const kc_ctx* c) {
     return tv;
 }
 
-// Partition buffers for a batch of up to `syms` symbols (lazily grown).
-static int ensure_part(kc_ctx* c, uint64_t syms) {
+// Partition buffers for a batch of up to `syms` symbols (lazily grown).  seg: use the
+// segmented single-pass layout (fixed-capacity segments, kc_count.hip OutSeg); its
+// capacities are the expected fill of a segment (keys are hash-uniform over bins) plus
+// 8 standard deviations plus 32, from the batch's symbol bound (>= its windows).  A
+// batch whose keys still overflow a segment (e.g. one k-mer repeated millions of times
+// inside one workgroup's range) is redone on the exact layout by the device itself.
+static int ensure_part(kc_ctx* c, uint64_t syms, bool seg) {
     const uint64_t tile = (uint64_t)COUNT_THREADS * run_width(c->W);
     const uint32_t nblk1 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(2048, (syms + tile - 1) / tile));
     const uint32_t B2 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(64, 2048 / c->F1));
@@ -195,20 +200,38 @@ static int ensure_part(kc_ctx* c, uint64_t syms) {
             hipMalloc(&c->pb.bsum, ((std::max(n1, n2) + 4095) / 4096 + 2) * 8) != hipSuccess)
             return c->fail(KC_ERR_NOMEM, "partition histogram allocation failed");
     }
-    if (syms > c->pb_key_cap) {
-        hipFree(c->pb.keys1);
-        hipFree(c->pb.keys2);
-        c->pb.keys1 = c->pb.keys2 = nullptr;
-        const size_t bytes = (size_t)syms * c->W * 8;
-        if (hipMalloc(&c->pb.keys1, bytes) != hipSuccess || hipMalloc(&c->pb.keys2, bytes) != hipSuccess) {
-            c->pb_key_cap = 0;
-            return c->fail(KC_ERR_NOMEM, "partition key buffers allocation failed (" + std::to_string(2 * bytes) +
-                                             " bytes)");
-        }
-        c->pb_key_cap = syms;
+    uint64_t cap1 = 0, cap2 = 0;
+    if (seg) {
+        auto capacity = [](double e) { return ((uint64_t)std::ceil(e + 8.0 * std::sqrt(e) + 32.0) + 7) / 8 * 8; };
+        const uint64_t per1 = ((syms + nblk1 - 1) / nblk1 + tile - 1) / tile * tile;  // windows per level-1 block
+        const uint64_t nseg = (nblk1 + B2 - 1) / B2;                               // level-1 segments per p2 block
+        cap1 = capacity((double)per1 / c->F1);
+        cap2 = capacity((double)nseg * per1 / c->F1 / c->F2);
+        if (const char* v = std::getenv("KC_SEG_CAP")) cap1 = cap2 = std::max<uint64_t>(1, std::strtoull(v, 0, 10));
+        // the segment walks index a virtual run with 32-bit offsets
+        if (nseg * cap1 >= (1ULL << 31) || (uint64_t)B2 * cap2 >= (1ULL << 31)) cap1 = cap2 = 0;
     }
+    const uint64_t need1 = std::max<uint64_t>(syms, (uint64_t)c->F1 * nblk1 * cap1);
+    const uint64_t need2 = std::max<uint64_t>(syms, c->R * B2 * cap2);
+    auto grow = [&](uint64_t** buf, uint64_t* have, uint64_t need) -> int {
+        if (need <= *have) return KC_OK;
+        hipFree(*buf);
+        *buf = nullptr;
+        *have = 0;
+        const size_t bytes = (size_t)need * c->W * 8;
+        if (hipMalloc(buf, bytes) != hipSuccess)
+            return c->fail(KC_ERR_NOMEM, "partition key buffer allocation failed (" + std::to_string(bytes) + " bytes)");
+        *have = need;
+        return KC_OK;
+    };
+    int rc = grow(&c->pb.keys1, &c->pb_k1_cap, need1);
+    if (rc) return rc;
+    rc = grow(&c->pb.keys2, &c->pb_k2_cap, need2);
+    if (rc) return rc;
     c->pb.nblk1 = nblk1;
     c->pb.B2 = B2;
+    c->pb.cap1 = cap1;
+    c->pb.cap2 = cap2;
     return KC_OK;
 }
 
@@ -218,7 +241,7 @@ static int ensure_part(kc_ctx* c, uint64_t syms) {
 static bool use_partitioned(const kc_ctx* c, uint64_t syms) {
     const char* env = std::getenv("KC_INSERT_PATH");
     if (env && !std::strcmp(env, "direct")) return false;
-    if (env && !std::strcmp(env, "partitioned")) return true;
+    if (env && (!std::strcmp(env, "partitioned") || !std::strcmp(env, "exact"))) return true;
     const double table_bytes = (double)c->nbuckets * 128.0;
     return (double)syms * 275.0 > (double)syms * (4.0 * c->W + 1) * 8.0 + 2.0 * table_bytes;
 }
@@ -260,7 +283,8 @@ static int run_batch(kc_ctx* c, uint64_t used, uint64_t nchunks, int fmt, int pa
     else mode = (c->cfg.bf_enable && c->cfg.mode != 1) ? 2 : 0;  // -m 1 -b ignores the filter (main.cpp:482-489)
     const uint64_t syms = used + nchunks;
     if (mode != 1 && use_partitioned(c, syms)) {
-        int rc = ensure_part(c, syms);
+        const char* env = std::getenv("KC_INSERT_PATH");
+        int rc = ensure_part(c, syms, !(env && !std::strcmp(env, "exact")));
         if (rc) return rc;
         HIPCHK(c, launch_count_partitioned(sv, syms, c->cfg.k, mode, tv, bv, c->d_ctr, c->pb, s));
     } else {
@@ -549,7 +573,7 @@ int kc_route_device(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, size_
         HIPCHK(c, hipEventRecord(c->xev, c->stream));
         HIPCHK(c, hipStreamWaitEvent(s, c->xev, 0));
     }
-    rc = ensure_part(c, syms);
+    rc = ensure_part(c, syms, false);
     if (rc) return rc;
     if ((uint64_t)nshards * c->pb.nblk1 > (uint64_t)c->F1 * c->pb_nblk1_cap)
         return c->fail(KC_ERR_ARG, "too many shards");
@@ -592,7 +616,7 @@ int kc_insert_keys_device(kc_ctx* c, const uint64_t* keys, uint64_t n, void* sp)
     }
     const bool part = use_partitioned(c, n);
     if (part) {
-        rc = ensure_part(c, n);
+        rc = ensure_part(c, n, false);
         if (rc) return rc;
     }
     std::array<hipEvent_t, 4> ev{};
@@ -637,6 +661,7 @@ int kc_finish(kc_ctx* c, kc_stats* st) {
         st->new_in_second = h.new_in_second;
         st->failed_in_first = h.failed_in_first;
         st->chunks = c->n_chunks;
+        st->part_fallbacks = h.part_fallbacks;
         st->bytes = c->n_bytes;
         // occupied slots
         if (c->d_table) {

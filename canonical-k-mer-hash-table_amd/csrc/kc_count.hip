@@ -345,36 +345,59 @@ struct BinOwner {
     DEV uint32_t operator()(uint64_t t0) const { return owner_of(t0, parts); }
 };
 
+// Where a scatter pass writes bin b.  Exact layout: one contiguous run per bin at offsets
+// from a histogram pass + scan.  Segmented layout (single pass, no histogram): a
+// fixed-capacity segment per (bin, producing workgroup); keys that would pass a
+// segment's end are dropped and raise DevCounters::part_overflow, and the exact
+// pipeline then redoes the batch (launched behind a device-side gate).
+struct OutExact {
+    static constexpr bool kSeg = false;
+    DEV bool fits(uint32_t, uint64_t) const { return true; }
+};
+struct OutSeg {
+    static constexpr bool kSeg = true;
+    uint64_t stride;  // keys between the segments of bins b and b+1
+    uint64_t base;    // first key of bin 0's segment for this workgroup
+    uint64_t cap;     // keys per segment
+    DEV uint64_t start(uint32_t b) const { return (uint64_t)b * stride + base; }
+    DEV bool fits(uint32_t b, uint64_t dst) const { return dst < start(b) + cap; }
+};
+
 // Counting-sort the tile's keys (in registers: tk[j] valid where ok[j]) by bin into
-// LDS and write each bin as one contiguous run at gbase[bin].
-template <int W, int RUNW, class Bin>
-DEV void scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const uint64_t (&tk)[RUNW][W],
+// LDS and write each bin as one contiguous run at gbase[bin].  The rank of a key inside
+// its bin comes back from the histogram atomic, so one LDS atomic per key suffices.
+// Returns true if a segmented run did not fit.
+template <int W, int RUNW, class Bin, class Out>
+DEV bool scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const Out& o, const uint64_t (&tk)[RUNW][W],
                       const bool (&ok)[RUNW], uint64_t* __restrict__ out) {
     const int tid = threadIdx.x;
+    uint32_t rank[RUNW];
 #pragma unroll
-    for (int j = 0; j < RUNW; j++)
-        if (ok[j]) atomicAdd(&l.hist[bin(tk[j][0])], 1u);
+    for (int j = 0; j < RUNW; j++) rank[j] = ok[j] ? atomicAdd(&l.hist[bin(tk[j][0])], 1u) : 0;
     __syncthreads();
     block_excl_scan_lds(l.hist, l.start, F);
-    for (uint32_t b = tid; b < F; b += COUNT_THREADS) l.cur[b] = l.start[b];
-    __syncthreads();
 #pragma unroll
     for (int j = 0; j < RUNW; j++)
         if (ok[j]) {
-            const uint32_t slot = atomicAdd(&l.cur[bin(tk[j][0])], 1u);
+            const uint32_t slot = l.start[bin(tk[j][0])] + rank[j];
 #pragma unroll
             for (int w = 0; w < W; w++) l.keys[slot * W + w] = tk[j][w];
         }
     __syncthreads();
     const uint32_t n = l.start[F - 1] + l.hist[F - 1];
+    bool over = false;
     for (uint32_t i = tid; i < n; i += COUNT_THREADS) {
         uint64_t key[W];
 #pragma unroll
         for (int w = 0; w < W; w++) key[w] = l.keys[i * W + w];
         const uint32_t b = bin(key[0]);
         const uint64_t dst = l.gbase[b] + (i - l.start[b]);
+        if (o.fits(b, dst)) {
 #pragma unroll
-        for (int w = 0; w < W; w++) out[dst * W + w] = key[w];
+            for (int w = 0; w < W; w++) out[dst * W + w] = key[w];
+        } else {
+            over = true;
+        }
     }
     __syncthreads();
     for (uint32_t b = tid; b < F; b += COUNT_THREADS) {
@@ -382,26 +405,43 @@ DEV void scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const uint64
         l.hist[b] = 0;
     }
     __syncthreads();
+    return over;
 }
 
+// gated kernels (the exact fallback of a segmented batch) run only if *gate != 0
+DEV bool gated_off(const unsigned long long* gate) { return gate && *gate == 0; }
+
 // Level 1: windows of a contiguous symbol range -> coarse bins (top f1bits of tkey[0]).
-// SCATTER = false: histogram only ([bin][block] into hist1); true: write the keys.
-template <int W, int MODE, bool SCATTER, class Bin>
-__global__ __launch_bounds__(COUNT_THREADS) void k_p1(PackedView sv, int k, BloomView bf,
+// SCATTER = false: histogram only ([bin][block] into hist1); true: write the keys,
+// exact layout (offsets off1) or segmented (Out = OutSeg: single pass, the segment
+// fill counts go to hist1).  `count`: add windows / inserted to the counters (off for
+// the histogram pass of a fallback, whose windows the segmented pass counted already).
+template <int W, int MODE, bool SCATTER, class Bin, class Out>
+__global__ __launch_bounds__(COUNT_THREADS, 4) void k_p1(PackedView sv, int k, BloomView bf,
                                                       DevCounters* __restrict__ ctr, PartBufs pb, uint32_t F, Bin bin,
-                                                      uint64_t* __restrict__ out, uint64_t pow5_k, uint64_t pow5_km1) {
+                                                      uint64_t* __restrict__ out, uint64_t pow5_k, uint64_t pow5_km1,
+                                                      Out o, const unsigned long long* gate, int count) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int RUNW = run_w<W>(), TW = tile_win<W>();
+    constexpr bool COUNTS = !SCATTER || Out::kSeg;
+    if (gated_off(gate)) return;
+    if (gate && !SCATTER && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&ctr->part_fallbacks, 1ULL);
     const PartLds l = part_lds(smem, F);
     const int tid = threadIdx.x;
     const uint64_t M = ctr->stream_len;
     const uint64_t per = ((M + pb.nblk1 - 1) / pb.nblk1 + TW - 1) / TW * TW;
     const uint64_t lo = min(M, (uint64_t)blockIdx.x * per), hi = min(M, lo + per);
+    Out ob = o;
+    if constexpr (Out::kSeg) ob.base = (uint64_t)blockIdx.x * o.cap;  // segment (b, block) = b * nblk1 + block
     for (uint32_t b = tid; b < F; b += COUNT_THREADS) {
         l.hist[b] = 0;
-        if constexpr (SCATTER) l.gbase[b] = pb.off1[(uint64_t)b * pb.nblk1 + blockIdx.x];
+        if constexpr (SCATTER) {
+            if constexpr (Out::kSeg) l.gbase[b] = ob.start(b);
+            else l.gbase[b] = pb.off1[(uint64_t)b * pb.nblk1 + blockIdx.x];
+        }
     }
     __syncthreads();
+    bool over = false;
     const RollConst rk = make_roll<W>(k, pow5_k, pow5_km1);
     uint32_t n_win = 0, n_ins = 0;
     for (uint64_t t0 = lo; t0 < hi; t0 += TW) {
@@ -420,7 +460,7 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_p1(PackedView sv, int k, Bloo
                     to_tkey<W>(key, tk[j]);
                     ok[j] = valid;
                 });
-            if constexpr (!SCATTER) {
+            if constexpr (COUNTS) {
 #pragma unroll
                 for (int j = 0; j < RUNW; j++) {
                     n_win += ok[j];
@@ -433,9 +473,9 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_p1(PackedView sv, int k, Bloo
             for (int j = 0; j < RUNW; j++) ok[j] = false;
             tile_rolled<W>(sv, t0, t1, rk, [&](const uint64_t (&fwd)[W], const uint64_t (&rc)[W], uint64_t root) {
                 (void)fwd;
-                if constexpr (!SCATTER) n_win++;
+                if constexpr (COUNTS) n_win++;
                 if (!bloom_gate(bf, root)) return;
-                if constexpr (!SCATTER) n_ins++;
+                if constexpr (COUNTS) n_ins++;
                 uint64_t key[W], t[W];
                 canonical<W>(fwd, rc, key);
                 to_tkey<W>(key, t);
@@ -451,7 +491,7 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_p1(PackedView sv, int k, Bloo
             });
         }
         if constexpr (SCATTER) {
-            scatter_tile<W, RUNW>(l, F, bin, tk, ok, out);
+            over |= scatter_tile<W, RUNW>(l, F, bin, ob, tk, ok, out);
         } else {
 #pragma unroll
             for (int j = 0; j < RUNW; j++)
@@ -461,15 +501,21 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_p1(PackedView sv, int k, Bloo
     if constexpr (!SCATTER) {
         __syncthreads();
         for (uint32_t b = tid; b < F; b += COUNT_THREADS) pb.hist1[(uint64_t)b * pb.nblk1 + blockIdx.x] = l.hist[b];
-        // routing (owner bins) counts windows here and insertions at the owner
-        block_add4(n_win, Bin::kOwner ? 0 : n_ins, 0, 0, &ctr->windows, &ctr->inserted, nullptr, nullptr);
     }
+    if constexpr (Out::kSeg) {  // segment fills (the scatter's last barrier ordered gbase)
+        for (uint32_t b = tid; b < F; b += COUNT_THREADS)
+            pb.hist1[(uint64_t)b * pb.nblk1 + blockIdx.x] = (uint32_t)(l.gbase[b] - ob.start(b));
+        if (over) atomicOr(&ctr->part_overflow, 1ULL);
+    }
+    // routing (owner bins) counts windows here and insertions at the owner
+    if constexpr (COUNTS)
+        if (count) block_add4(n_win, Bin::kOwner ? 0 : n_ins, 0, 0, &ctr->windows, &ctr->inserted, nullptr, nullptr);
 }
 
 // Level 1 over a key array (keys received from other shards): [0, n) split over nblk1
 // blocks, bins = top f1bits of the table key.
 template <int W, bool SCATTER>
-__global__ __launch_bounds__(COUNT_THREADS) void k_p1k(const uint64_t* __restrict__ in, uint64_t n, PartBufs pb,
+__global__ __launch_bounds__(COUNT_THREADS, 4) void k_p1k(const uint64_t* __restrict__ in, uint64_t n, PartBufs pb,
                                                        uint32_t F, BinBits bin, DevCounters* __restrict__ ctr) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int RUNW = run_w<W>(), TW = tile_win<W>();
@@ -495,7 +541,7 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_p1k(const uint64_t* __restric
             if constexpr (!SCATTER) n_inv += (i < hi) & !ok[q];
         }
         if constexpr (SCATTER) {
-            scatter_tile<W, RUNW>(l, F, bin, tk, ok, pb.keys1);
+            scatter_tile<W, RUNW>(l, F, bin, OutExact{}, tk, ok, pb.keys1);
         } else {
 #pragma unroll
             for (int q = 0; q < RUNW; q++)
@@ -528,9 +574,10 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_insert_keys(const uint64_t* _
 
 // Level 2: coarse bin c (block = c * B2 + j) -> its F2 regions (next bits of tkey[0]).
 template <int W, bool SCATTER>
-__global__ __launch_bounds__(COUNT_THREADS) void k_p2(TableView tv, PartBufs pb) {
+__global__ __launch_bounds__(COUNT_THREADS, 4) void k_p2(TableView tv, PartBufs pb, const unsigned long long* gate) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int RUNW = run_w<W>(), TW = tile_win<W>();
+    if (gated_off(gate)) return;
     const uint32_t F = tv.F2;
     const BinBits bin{tv.rbits ? 64 - tv.rbits : 63, F - 1};
     const PartLds l = part_lds(smem, F);
@@ -556,7 +603,7 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_p2(TableView tv, PartBufs pb)
             for (int w = 0; w < W; w++) tk[q][w] = ok[q] ? pb.keys1[i * W + w] : 0;
         }
         if constexpr (SCATTER) {
-            scatter_tile<W, RUNW>(l, F, bin, tk, ok, pb.keys2);
+            scatter_tile<W, RUNW>(l, F, bin, OutExact{}, tk, ok, pb.keys2);
         } else {
 #pragma unroll
             for (int q = 0; q < RUNW; q++)
@@ -569,6 +616,63 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_p2(TableView tv, PartBufs pb)
     }
 }
 
+// Level 2, segmented: coarse bin c's level-1 segments of workgroups [s_lo, s_hi)
+// (block = c * B2 + j) -> segments (c * F2 + region, j) of capacity cap2, one pass.
+// The input segments are read as one virtual run (exclusive prefix of their fills in
+// LDS; each thread walks a monotone segment cursor).
+constexpr uint32_t P2F_MAX_SEG = 2048;  // nblk1 <= 2048
+template <int W>
+constexpr size_t p2f_smem(uint32_t F) { return part_smem<W>(F) + (P2F_MAX_SEG + 1) * 4; }
+
+template <int W>
+__global__ __launch_bounds__(COUNT_THREADS, 4) void k_p2f(TableView tv, PartBufs pb, DevCounters* __restrict__ ctr) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int RUNW = run_w<W>(), TW = tile_win<W>();
+    if (ctr->part_overflow) return;  // level 1 overflowed: the exact pipeline redoes the batch
+    const uint32_t F = tv.F2;
+    const BinBits bin{tv.rbits ? 64 - tv.rbits : 63, F - 1};
+    const PartLds l = part_lds(smem, F);
+    uint32_t* pre = reinterpret_cast<uint32_t*>(smem + part_smem<W>(F));
+    const int tid = threadIdx.x;
+    const uint32_t c = blockIdx.x / pb.B2, j = blockIdx.x % pb.B2;
+    const uint32_t s_lo = (uint32_t)((uint64_t)j * pb.nblk1 / pb.B2);
+    const uint32_t nseg = (uint32_t)((uint64_t)(j + 1) * pb.nblk1 / pb.B2) - s_lo;
+    const uint64_t seg0 = (uint64_t)c * pb.nblk1 + s_lo;  // level-1 segment index of cursor 0
+    const OutSeg o{(uint64_t)pb.B2 * pb.cap2, ((uint64_t)c * F * pb.B2 + j) * pb.cap2, pb.cap2};
+    for (uint32_t i = tid; i <= nseg; i += COUNT_THREADS) pre[i] = i < nseg ? pb.hist1[seg0 + i] : 0;
+    for (uint32_t b = tid; b < F; b += COUNT_THREADS) {
+        l.hist[b] = 0;
+        l.gbase[b] = o.start(b);
+    }
+    __syncthreads();
+    block_excl_scan_lds(pre, pre, nseg + 1);  // in place; pre[nseg] = total
+    const uint32_t total = pre[nseg];
+    bool over = false;
+    uint32_t cs = 0;  // segment cursor of this thread
+    for (uint32_t t0 = 0; t0 < total; t0 += TW) {
+        uint64_t tk[RUNW][W];
+        bool ok[RUNW];
+#pragma unroll
+        for (int q = 0; q < RUNW; q++) {
+            const uint32_t i = t0 + tid + q * COUNT_THREADS;
+            ok[q] = i < total;
+            if (ok[q]) {
+                while (pre[cs + 1] <= i) cs++;
+                const uint64_t* src = pb.keys1 + ((seg0 + cs) * pb.cap1 + (i - pre[cs])) * W;
+#pragma unroll
+                for (int w = 0; w < W; w++) tk[q][w] = src[w];
+            } else {
+#pragma unroll
+                for (int w = 0; w < W; w++) tk[q][w] = 0;
+            }
+        }
+        over |= scatter_tile<W, RUNW>(l, F, bin, o, tk, ok, pb.keys2);
+    }
+    for (uint32_t b = tid; b < F; b += COUNT_THREADS)
+        pb.hist2[((uint64_t)c * F + b) * pb.B2 + j] = (uint32_t)(l.gbase[b] - o.start(b));
+    if (over) atomicOr(&ctr->part_overflow, 1ULL);
+}
+
 // LDS image of a region: the 16-byte chunks of each 128-byte bucket are XOR-swizzled
 // with the bucket index so that lanes probing random buckets spread over the banks.
 DEV uint32_t lds_chunk(uint32_t b, uint32_t q) { return b * 8 + (q ^ (b & 7)); }
@@ -577,14 +681,43 @@ DEV uint64_t* lds_word(uint64_t* lt, uint32_t b, uint32_t word) {
 }
 
 // Level 3: one workgroup per region: LDS-resident table
-template <int W, int NT>
-__global__ __launch_bounds__(NT) void k_p3(TableView tv, PartBufs pb, DevCounters* __restrict__ ctr) {
+// SEG: the region's keys are the B2 level-2 segments (region, j) (fills in hist2);
+// otherwise the contiguous run [off2[r * B2], off2[(r + 1) * B2]).  A segmented launch
+// leaves the table alone when the batch overflowed; an exact one can be gated.
+template <int W, int NT, bool SEG>
+// two 64 KiB regions per CU: NT / 128 waves per SIMD must fit the register file
+__global__ __launch_bounds__(NT, NT / 128) void k_p3(TableView tv, PartBufs pb, DevCounters* __restrict__ ctr,
+                                           const unsigned long long* gate) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ uint32_t s_pre[65];  // SEG: exclusive prefix of the B2 (<= 64) segment fills
     constexpr int S = BUCKET_WORDS / (W + 1);
-    constexpr int KB = 8;  // keys loaded per thread before inserting (memory-level parallelism)
+    // keys loaded per thread before inserting (memory-level parallelism); 1024-thread
+    // groups already keep 8 waves per SIMD in flight
+    constexpr int KB = NT >= 1024 ? 4 : 8;
+    if constexpr (SEG) {
+        if (ctr->part_overflow) return;
+    } else {
+        if (gated_off(gate)) return;
+    }
     uint64_t* lt = reinterpret_cast<uint64_t*>(smem);  // BPR * BUCKET_WORDS words
     const uint64_t r = blockIdx.x;
-    const uint64_t start = pb.off2[r * pb.B2], end = pb.off2[(r + 1) * pb.B2];
+    uint64_t start, end;
+    if constexpr (SEG) {
+        if (threadIdx.x == 0) {
+            uint32_t acc = 0;
+            for (uint32_t j = 0; j < pb.B2; j++) {
+                s_pre[j] = acc;
+                acc += pb.hist2[r * pb.B2 + j];
+            }
+            s_pre[pb.B2] = acc;
+        }
+        __syncthreads();
+        start = 0;
+        end = s_pre[pb.B2];
+    } else {
+        start = pb.off2[r * pb.B2];
+        end = pb.off2[(r + 1) * pb.B2];
+    }
     if (start == end) return;  // nothing to insert: leave the region untouched
     uint4* g4 = reinterpret_cast<uint4*>(tv.buckets + r * BPR * BUCKET_WORDS);
     uint4* l4 = reinterpret_cast<uint4*>(lt);
@@ -592,13 +725,23 @@ __global__ __launch_bounds__(NT) void k_p3(TableView tv, PartBufs pb, DevCounter
     for (int i = threadIdx.x; i < N4; i += NT) l4[lds_chunk(i >> 3, i & 7)] = g4[i];
     __syncthreads();
     uint32_t n_fail = 0;
+    uint32_t cs = 0;  // SEG: segment cursor of this thread (indices grow monotonically)
     for (uint64_t base = start; base < end; base += (uint64_t)KB * NT) {
         uint64_t kk[KB][W];
 #pragma unroll
         for (int q = 0; q < KB; q++) {
             const uint64_t i = base + threadIdx.x + (uint64_t)q * NT;
+            const uint64_t* src = nullptr;
+            if (i < end) {
+                if constexpr (SEG) {
+                    while (s_pre[cs + 1] <= i) cs++;
+                    src = pb.keys2 + ((r * pb.B2 + cs) * pb.cap2 + (i - s_pre[cs])) * W;
+                } else {
+                    src = pb.keys2 + i * W;
+                }
+            }
 #pragma unroll
-            for (int w = 0; w < W; w++) kk[q][w] = i < end ? pb.keys2[i * W + w] : 0;
+            for (int w = 0; w < W; w++) kk[q][w] = src ? src[w] : 0;
         }
 #pragma unroll
         for (int q = 0; q < KB; q++) {
@@ -726,7 +869,9 @@ DEV unsigned long long block_incl_sum_1024(unsigned long long v) {
     return v + base;
 }
 __global__ __launch_bounds__(SCAN_T) void k_scanA(const uint32_t* __restrict__ in, uint64_t n,
-                                                 uint64_t* __restrict__ out, uint64_t* __restrict__ bsum) {
+                                                 uint64_t* __restrict__ out, uint64_t* __restrict__ bsum,
+                                                 const unsigned long long* gate) {
+    if (gated_off(gate)) return;
     const uint64_t i0 = ((uint64_t)blockIdx.x * SCAN_T + threadIdx.x) * SCAN_PER;
     uint32_t v[SCAN_PER];
     unsigned long long sum = 0;
@@ -745,7 +890,8 @@ __global__ __launch_bounds__(SCAN_T) void k_scanA(const uint32_t* __restrict__ i
     if (threadIdx.x == SCAN_T - 1) bsum[blockIdx.x] = incl;
 }
 __global__ __launch_bounds__(SCAN_T) void k_scanB(uint64_t* __restrict__ bsum, uint64_t nb, uint64_t* __restrict__ out,
-                                                 uint64_t n) {
+                                                 uint64_t n, const unsigned long long* gate) {
+    if (gated_off(gate)) return;
     __shared__ unsigned long long s_carry;
     if (threadIdx.x == 0) s_carry = 0;
     __syncthreads();
@@ -762,19 +908,21 @@ __global__ __launch_bounds__(SCAN_T) void k_scanB(uint64_t* __restrict__ bsum, u
     if (threadIdx.x == 0) out[n] = s_carry;
 }
 __global__ __launch_bounds__(SCAN_T) void k_scanC(uint64_t* __restrict__ out, uint64_t n,
-                                                 const uint64_t* __restrict__ bsum) {
+                                                 const uint64_t* __restrict__ bsum, const unsigned long long* gate) {
+    if (gated_off(gate)) return;
     const uint64_t i0 = ((uint64_t)blockIdx.x * SCAN_T + threadIdx.x) * SCAN_PER;
     const uint64_t add = bsum[blockIdx.x];
 #pragma unroll
     for (int q = 0; q < SCAN_PER; q++)
         if (i0 + q < n) out[i0 + q] += add;
 }
-static void launch_scan(const uint32_t* in, uint64_t n, uint64_t* out, uint64_t* bsum, hipStream_t s) {
+static void launch_scan(const uint32_t* in, uint64_t n, uint64_t* out, uint64_t* bsum, hipStream_t s,
+                        const unsigned long long* gate = nullptr) {
     const uint64_t per = (uint64_t)SCAN_T * SCAN_PER;
     const unsigned nb = (unsigned)((n + per - 1) / per);
-    hipLaunchKernelGGL(k_scanA, dim3(nb), dim3(SCAN_T), 0, s, in, n, out, bsum);
-    hipLaunchKernelGGL(k_scanB, dim3(1), dim3(SCAN_T), 0, s, bsum, (uint64_t)nb, out, n);
-    hipLaunchKernelGGL(k_scanC, dim3(nb), dim3(SCAN_T), 0, s, out, n, bsum);
+    hipLaunchKernelGGL(k_scanA, dim3(nb), dim3(SCAN_T), 0, s, in, n, out, bsum, gate);
+    hipLaunchKernelGGL(k_scanB, dim3(1), dim3(SCAN_T), 0, s, bsum, (uint64_t)nb, out, n, gate);
+    hipLaunchKernelGGL(k_scanC, dim3(nb), dim3(SCAN_T), 0, s, out, n, bsum, gate);
 }
 
 // --------------------------------------------------------------------------------
@@ -871,49 +1019,87 @@ static hipError_t set_smem(K kernel, size_t bytes) {
 
 static BinBits coarse_bins(const TableView& t) { return BinBits{t.f1bits ? 64 - t.f1bits : 63, t.F1 - 1}; }
 
-template <int W>
-static hipError_t part_levels23(TableView t, DevCounters* ctr, PartBufs pb, hipStream_t s) {
-    const size_t sm2 = part_smem<W>(t.F2), sm2h = hist_smem(t.F2);
-    const size_t sm3 = (size_t)BPR * BUCKET_WORDS * 8;
-    hipError_t e;
-    if ((e = set_smem(k_p2<W, false>, sm2h)) != hipSuccess) return e;
-    if ((e = set_smem(k_p2<W, true>, sm2)) != hipSuccess) return e;
-    static const int p3nt = [] {
+static int p3_threads() {
+    static const int nt = [] {
         const char* v = std::getenv("KC_P3_THREADS");  // tuning knob: 256 / 512 / 1024
         return v ? std::atoi(v) : 1024;
     }();
-    auto p3 = p3nt == 256 ? k_p3<W, 256> : (p3nt == 512 ? k_p3<W, 512> : k_p3<W, 1024>);
-    if ((e = set_smem(p3, sm3)) != hipSuccess) return e;
-    hipLaunchKernelGGL((k_p2<W, false>), dim3(t.F1 * pb.B2), dim3(COUNT_THREADS), sm2h, s, t, pb);
-    launch_scan(pb.hist2, t.R * pb.B2, pb.off2, pb.bsum, s);
-    hipLaunchKernelGGL((k_p2<W, true>), dim3(t.F1 * pb.B2), dim3(COUNT_THREADS), sm2, s, t, pb);
-    hipLaunchKernelGGL(p3, dim3((unsigned)t.R), dim3((unsigned)p3nt), sm3, s, t, pb, ctr);
+    return nt;
+}
+template <int W, bool SEG>
+static hipError_t launch_p3(TableView t, DevCounters* ctr, PartBufs pb, const unsigned long long* gate,
+                            hipStream_t s) {
+    const size_t sm3 = (size_t)BPR * BUCKET_WORDS * 8;
+    const int nt = p3_threads();
+    auto p3 = nt == 256 ? k_p3<W, 256, SEG> : (nt == 512 ? k_p3<W, 512, SEG> : k_p3<W, 1024, SEG>);
+    hipError_t e = set_smem(p3, sm3);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(p3, dim3((unsigned)t.R), dim3((unsigned)nt), sm3, s, t, pb, ctr, gate);
     return hipGetLastError();
 }
 
-// level 1 from the symbol stream: windows -> F bins by `bin`, keys into `out`
+// levels 2 and 3 on the exact layout (after an exact level 1); `gate` as in k_p1
+template <int W>
+static hipError_t part_levels23(TableView t, DevCounters* ctr, PartBufs pb, hipStream_t s,
+                                const unsigned long long* gate = nullptr) {
+    const size_t sm2 = part_smem<W>(t.F2), sm2h = hist_smem(t.F2);
+    hipError_t e;
+    if ((e = set_smem(k_p2<W, false>, sm2h)) != hipSuccess) return e;
+    if ((e = set_smem(k_p2<W, true>, sm2)) != hipSuccess) return e;
+    hipLaunchKernelGGL((k_p2<W, false>), dim3(t.F1 * pb.B2), dim3(COUNT_THREADS), sm2h, s, t, pb, gate);
+    launch_scan(pb.hist2, t.R * pb.B2, pb.off2, pb.bsum, s, gate);
+    hipLaunchKernelGGL((k_p2<W, true>), dim3(t.F1 * pb.B2), dim3(COUNT_THREADS), sm2, s, t, pb, gate);
+    return launch_p3<W, false>(t, ctr, pb, gate, s);
+}
+
+// level 1 from the symbol stream, exact layout: windows -> F bins by `bin`, keys into `out`
 template <int W, int MODE, class Bin>
 static hipError_t part_level1(PackedView sym, int k, BloomView bf, DevCounters* ctr, PartBufs pb, uint32_t F,
-                              Bin bin, uint64_t* out, hipStream_t s) {
+                              Bin bin, uint64_t* out, hipStream_t s, const unsigned long long* gate = nullptr) {
     const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
     const size_t sm1 = part_smem<W>(F), sm1h = hist_smem(F);
     hipError_t e;
-    if ((e = set_smem(k_p1<W, MODE, false, Bin>, sm1h)) != hipSuccess) return e;
-    if ((e = set_smem(k_p1<W, MODE, true, Bin>, sm1)) != hipSuccess) return e;
-    hipLaunchKernelGGL((k_p1<W, MODE, false, Bin>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1h, s, sym, k, bf, ctr, pb, F,
-                       bin, out, pk, pkm1);
-    launch_scan(pb.hist1, (uint64_t)F * pb.nblk1, pb.off1, pb.bsum, s);
-    hipLaunchKernelGGL((k_p1<W, MODE, true, Bin>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1, s, sym, k, bf, ctr, pb, F,
-                       bin, out, pk, pkm1);
+    auto kh = k_p1<W, MODE, false, Bin, OutExact>;
+    auto ks = k_p1<W, MODE, true, Bin, OutExact>;
+    if ((e = set_smem(kh, sm1h)) != hipSuccess) return e;
+    if ((e = set_smem(ks, sm1)) != hipSuccess) return e;
+    // a gated launch is the fallback of a segmented batch, whose windows are counted
+    const int count = gate ? 0 : 1;
+    hipLaunchKernelGGL(kh, dim3(pb.nblk1), dim3(COUNT_THREADS), sm1h, s, sym, k, bf, ctr, pb, F, bin, out, pk, pkm1,
+                       OutExact{}, gate, count);
+    launch_scan(pb.hist1, (uint64_t)F * pb.nblk1, pb.off1, pb.bsum, s, gate);
+    hipLaunchKernelGGL(ks, dim3(pb.nblk1), dim3(COUNT_THREADS), sm1, s, sym, k, bf, ctr, pb, F, bin, out, pk, pkm1,
+                       OutExact{}, gate, 0);
     return hipGetLastError();
 }
 
+// Segmented pipeline (pb.cap1 != 0): p1 -> p2f -> p3<SEG>, each a single pass; then
+// the exact pipeline behind the overflow gate (its kernels return at once unless a
+// segment overflowed, in which case the segmented p3 left the table untouched).
 template <int W, int MODE>
 static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf, DevCounters* ctr, PartBufs pb,
                                 hipStream_t s) {
-    hipError_t e = part_level1<W, MODE>(sym, k, bf, ctr, pb, t.F1, coarse_bins(t), pb.keys1, s);
-    if (e != hipSuccess) return e;
-    return part_levels23<W>(t, ctr, pb, s);
+    if (pb.cap1 == 0) {
+        hipError_t e = part_level1<W, MODE>(sym, k, bf, ctr, pb, t.F1, coarse_bins(t), pb.keys1, s);
+        if (e != hipSuccess) return e;
+        return part_levels23<W>(t, ctr, pb, s);
+    }
+    hipError_t e;
+    const unsigned long long* gate = &ctr->part_overflow;
+    if ((e = hipMemsetAsync(&ctr->part_overflow, 0, sizeof(ctr->part_overflow), s)) != hipSuccess) return e;
+    const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
+    auto k1 = k_p1<W, MODE, true, BinBits, OutSeg>;
+    const size_t sm1 = part_smem<W>(t.F1), sm2 = p2f_smem<W>(t.F2);
+    if ((e = set_smem(k1, sm1)) != hipSuccess) return e;
+    if ((e = set_smem(k_p2f<W>, sm2)) != hipSuccess) return e;
+    const OutSeg o1{(uint64_t)pb.nblk1 * pb.cap1, 0, pb.cap1};
+    hipLaunchKernelGGL(k1, dim3(pb.nblk1), dim3(COUNT_THREADS), sm1, s, sym, k, bf, ctr, pb, t.F1, coarse_bins(t),
+                       pb.keys1, pk, pkm1, o1, (const unsigned long long*)nullptr, 1);
+    hipLaunchKernelGGL(k_p2f<W>, dim3(t.F1 * pb.B2), dim3(COUNT_THREADS), sm2, s, t, pb, ctr);
+    if ((e = launch_p3<W, true>(t, ctr, pb, nullptr, s)) != hipSuccess) return e;
+    if ((e = part_level1<W, MODE>(sym, k, bf, ctr, pb, t.F1, coarse_bins(t), pb.keys1, s, gate)) != hipSuccess)
+        return e;
+    return part_levels23<W>(t, ctr, pb, s, gate);
 }
 
 hipError_t launch_count_partitioned(PackedView sym, uint64_t sym_bound, int k, int mode, TableView t,

@@ -63,6 +63,8 @@ struct DevCounters {
     unsigned long long stream_len;      uint64_t _p8[15];
     unsigned long long bf_windows;      uint64_t _p9[15];
     unsigned long long invalid;         uint64_t _p10[15];  // received keys with word 0 == 0 (skipped)
+    unsigned long long part_overflow;   uint64_t _p11[15];  // a fixed-capacity segment overflowed (this batch)
+    unsigned long long part_fallbacks;  uint64_t _p12[15];  // batches redone on the exact layout
 };
 
 // The symbol stream: 32 symbols per word, symbol j of word w at bits 62-2j of pk[w]
@@ -94,6 +96,7 @@ struct PartBufs {
     uint64_t* bsum;         // scan scratch: one entry per 4096 histogram entries
     uint64_t* keys1;        // coarse-binned keys (W words each)
     uint64_t* keys2;        // region-binned keys
+    uint64_t cap1, cap2;    // segmented layout: keys per segment of levels 1 / 2 (0 = exact layout)
 };
 
 struct BloomView {

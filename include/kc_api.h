@@ -78,6 +78,7 @@ typedef struct {
     uint64_t failed_in_first;
     uint64_t chunks;          /* chunks processed by the counting pass */
     uint64_t bytes;           /* input bytes processed by the counting pass */
+    uint64_t part_fallbacks;  /* partitioned batches redone on the exact layout (segment overflow) */
 } kc_stats;
 
 /* Creates the device table (PointerHashTableCanonicalAV ctor,

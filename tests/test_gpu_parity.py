@@ -58,9 +58,11 @@ def bf_singleton_check(lines, path, k, mode, tmp_path):
             assert truth.get(s) == "1", s
 
 
-@pytest.fixture(params=["direct", "partitioned"])
+@pytest.fixture(params=["direct", "partitioned", "exact"])
 def insert_path(request, monkeypatch):
-    """Both insert paths must give the reference's result (KC_INSERT_PATH forces one)."""
+    """Every insert path must give the reference's result (KC_INSERT_PATH forces one):
+    direct = device-scope atomics, partitioned = single-pass segmented scatters,
+    exact = the histogram-offset scatters (the segmented path's fallback)."""
     monkeypatch.setenv("KC_INSERT_PATH", request.param)
     return request.param
 
@@ -190,3 +192,26 @@ def test_counts_sum_to_windows_at_scale(insert_path):
         b = rec2[np.lexsort(rec2[:, :-1].T[::-1])]
         assert np.array_equal(a[:, :-1], b[:, :-1])
         assert np.array_equal(2 * a[:, -1], b[:, -1])
+
+
+@pytest.mark.parametrize("name,k,args", [("reads_w60.fasta", 31, ["-a", "1", "-s", "1000000"]),
+                                         ("reads_w60.fasta", 51, ["-m", "0", "-a", "2", "-s", "1000000"]),
+                                         ("long.fasta", 127, ["-a", "1", "-s", "1000000"])])
+def test_segment_overflow_falls_back_to_exact(name, k, args, golden_input, tmp_path, monkeypatch):
+    """Tiny forced segment capacities overflow: the device redoes the batch on the exact
+    layout (behind the overflow gate) and the result is still the reference's."""
+    monkeypatch.setenv("KC_INSERT_PATH", "partitioned")
+    monkeypatch.setenv("KC_SEG_CAP", "8")
+    path = golden_input(name)
+    o = parse_ref_args(args)
+    cfg = ka.Config(k=k, mode=o["mode"], min_abundance=o["min_abundance"], table_slots=o["table_slots"])
+    data = open(path, "rb").read()
+    with ka.KmerCounter(cfg) as kc:
+        for off, ln, bh in ka.plan_chunks(data, k, ka.FMT_FASTA):
+            kc.count_chunk(data[off:off + ln], ka.FMT_FASTA, bool(bh))
+        st = kc.finish()
+        assert st["part_fallbacks"] >= 1
+        lines = kc.lines()
+    out = tmp_path / "oracle.txt"
+    oracle_count(path, k, args, out)
+    assert sorted_digest_lines(lines) == sorted_digest_file(out)
