@@ -2,22 +2,25 @@
 """bench.py -- canonical k-mer counting throughput on MI355X.
 
 Metric (BASELINE.json): canonical k-mers/s inserted (+ achieved HBM GB/s).
-Workload at N=1: BASELINE.json configs[1] = "C2": synthetic 10M x 150 bp reads
-(seeded generator, SURVEY.md 8d: uniform 50 Mbp genome, 50 % reverse complement,
-0.1 % substitutions, single-line FASTA), k = 31, Kaarme table (-m 2 -s 200000000).
+Workload (--config, BASELINE.md CPU-baseline plan; SURVEY.md 8d generator: uniform
+genome, 50 % reverse complement, 0.1 % substitutions, single-line FASTA):
+  C2 (default, BASELINE.json configs[1]): 10M x 150 bp reads per GPU, k=31, -m 2 -s 200000000
+  C3: 10M x 150 bp per GPU, k=51, -m 2 -b -u 400000000 (Bloom pass + gated counting pass)
+  C4: 100M x 150 bp over the GPUs, k=51, -m 2 -s 2600000000 (split over the shards)
+  C5: 1M x 10 kbp over the GPUs, k=127 (4-word keys), -m 2 -s 3600000000 (split)
 
 One step = one full counting job over the resident input: table re-initialised
-(kc_reset, the table constructor), reference chunking of the FASTA image, gather
-into the chunk stage, tokenize, canonicalise + insert every window.  The FASTA image
-is generated directly in HBM before timing (inputs resident, as the contract asks).
+(kc_reset, the table constructor), [Bloom pass,] reference chunking of the FASTA image,
+gather into the chunk stage, tokenize, canonicalise + insert every window.  The FASTA
+image is generated directly in HBM before timing (inputs resident, as the contract asks).
 
-N > 1 (torch.distributed over RCCL): weak scaling, every rank owns its own 10M-read
-slice of one dataset; canonical keys are routed to their hash-prefix owner with one
-all-to-all per step (see kaarme_amd/sharded.py) and counted there.
+N > 1 (torch.distributed over RCCL): every rank counts its own slice; canonical keys are
+routed to their hash-prefix owner with one all-to-all per staged batch
+(kaarme_amd/sharded.py) and counted there.
 
-Extra JSON keys: roofline (the counting pass vs 8 TB/s HBM), cpu_baseline (the
-reference CLI oracle/_ref/kaarme on a bounded sample of the same workload, rank 0,
-N=1 only).
+Extra JSON keys: roofline (the counting pass vs 8 TB/s HBM; traffic from the committed
+PMC summary profiles/pmc_traffic.json when it matches the workload), cpu_baseline (the
+reference CLI oracle/_ref/kaarme on a bounded sample of the same workload, rank 0, N=1).
 """
 import argparse
 import json
@@ -41,6 +44,22 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+PRESETS = {
+    # BASELINE.md CPU-baseline plan (SURVEY.md 8d generator).  "weak": every rank counts
+    # its own `reads`; "strong": the `reads` and the -s capacity are split over the ranks.
+    "C2": dict(reads=10_000_000, read_len=150, genome=50_000_000, k=31, slots=200_000_000, unique=0, scale="weak"),
+    "C3": dict(reads=10_000_000, read_len=150, genome=50_000_000, k=51, slots=0, unique=400_000_000, scale="weak"),
+    "C4": dict(reads=100_000_000, read_len=150, genome=500_000_000, k=51, slots=2_600_000_000, unique=0,
+               scale="strong"),
+    "C5": dict(reads=1_000_000, read_len=10_000, genome=500_000_000, k=127, slots=3_600_000_000, unique=0,
+               scale="strong"),
+}
+
+
+def table_args(slots, unique):
+    return ["-b", "-u", str(unique)] if unique else ["-s", str(slots)]
+
+
 def cpu_baseline(args):
     """Time the reference CLI (or, if it was not built, the C oracle) on a bounded sample."""
     ref = os.path.join(REPO, "oracle", "_ref", "kaarme")
@@ -51,7 +70,10 @@ def cpu_baseline(args):
     kind = "reference" if os.path.exists(ref) else ("port" if os.path.exists(orc) else None)
     if kind is None:
         return None
-    n = args.cpu_sample_reads if kind == "reference" else max(1, args.cpu_sample_reads // 20)
+    # about 150 M bases (10-30 s of reference work on a 16-core share)
+    n = max(1, args.cpu_sample_bases // args.read_len)
+    if kind == "port":
+        n = max(1, n // 20)
     # The box gives one GPU's job a 16-core share of a larger host (OMP_NUM_THREADS is set to
     # it; the affinity mask still lists every CPU).  -t = share + 2: share hashing workers plus
     # the IO thread (main.cpp:383).
@@ -59,30 +81,34 @@ def cpu_baseline(args):
     threads = max(3, min(args.cpu_threads or share + 2, 64))
     with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
         fa = os.path.join(td, "sample.fasta")
-        subprocess.run([gen, fa, str(n), str(args.read_len), str(args.genome), "-s", str(args.seed),
-                        "-e", str(args.err)], check=True)
+        subprocess.run([gen, fa, str(args.reads), str(args.read_len), str(args.genome), "-s", str(args.seed),
+                        "-e", str(args.err), "--first", "0", "--count", str(n)], check=True)
         with open(fa, "rb") as f:  # pre-warm the page cache
             while f.read(1 << 24):
                 pass
         windows = n * (args.read_len - args.k + 1)
-        slots = args.slots  # the sample's distinct k-mers approach the genome size: keep C2's -s
+        # distinct <= windows: never ask the reference for more slots than the sample can fill
+        slots = min(args.slots, int(windows * 1.3) + 1000) if args.slots else 0
+        targs = table_args(slots, args.unique)
         if kind == "reference":
-            cmd = [ref, fa, str(args.k), "-m", "2", "-s", str(slots), "-t", str(threads), "-a", "0"]
+            cmd = [ref, fa, str(args.k), "-m", "2", "-t", str(threads), "-a", "0"] + targs
             p = subprocess.run(cmd, capture_output=True, text=True, timeout=1800)
             m = re.search(r"Time used to build hash table: (\d+) microseconds", p.stdout)
+            mb = re.search(r"Time used to bloom filter k-mers: (\d+) microseconds", p.stdout)
             if p.returncode != 0 or not m:
                 log("cpu baseline failed:", p.stdout[-500:], p.stderr[-500:])
                 return None
-            secs = int(m.group(1)) / 1e6
+            secs = (int(m.group(1)) + (int(mb.group(1)) if mb else 0)) / 1e6
             cores = threads - 2  # t-2 hashing workers (+ 1 mostly idle IO thread, main.cpp:383)
         else:
             t0 = time.perf_counter()
-            subprocess.run([orc, "count", fa, str(args.k), "-a", "0"], check=True, capture_output=True)
+            subprocess.run([orc, "count", fa, str(args.k), "-a", "0"] + targs, check=True, capture_output=True)
             secs = time.perf_counter() - t0
             cores = 1
     return {"value": windows / secs, "unit": "k-mers/s", "cores": cores, "kind": kind,
             "sample": f"first {n} reads of the same generator ({windows} windows, k={args.k}, "
-                      f"-m 2 -s {slots} -t {threads}, {secs:.2f} s counting time)"}
+                      f"-m 2 {' '.join(targs)} -t {threads}, {secs:.2f} s counting time"
+                      f"{' incl. the Bloom pass' if args.unique else ''})"}
 
 
 def load_traffic(workload):
@@ -103,17 +129,33 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--reads", type=int, default=10_000_000, help="reads per GPU")
-    ap.add_argument("--read-len", type=int, default=150)
-    ap.add_argument("--genome", type=int, default=50_000_000)
-    ap.add_argument("--k", type=int, default=31)
-    ap.add_argument("--slots", type=int, default=200_000_000, help="-s per GPU (C2: 200000000)")
+    ap.add_argument("--config", default="C2", choices=sorted(PRESETS), help="BASELINE.md workload (default C2)")
+    ap.add_argument("--reads", type=int, default=None, help="reads (per GPU for weak, total for strong presets)")
+    ap.add_argument("--read-len", type=int, default=None)
+    ap.add_argument("--genome", type=int, default=None)
+    ap.add_argument("--k", type=int, default=None)
+    ap.add_argument("--slots", type=int, default=None, help="-s (total for strong presets)")
+    ap.add_argument("--unique", type=int, default=None, help="-b -u U (Bloom filter) instead of -s")
+    ap.add_argument("--batch-mib", type=int, default=0, help="staging batch (0 = whole image up to 2 GiB/W)")
     ap.add_argument("--err", type=float, default=0.001)
     ap.add_argument("--seed", type=int, default=42)
-    ap.add_argument("--cpu-sample-reads", type=int, default=1_000_000)
+    ap.add_argument("--cpu-sample-bases", type=int, default=150_000_000)
     ap.add_argument("--cpu-threads", type=int, default=0, help="-t of the reference (0 = core share + 2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--force-sharded", action="store_true",
+                    help="use the sharded (RCCL) path even at one rank (testing)")
     args = ap.parse_args()
+    # stdout carries exactly one JSON line: libraries (RCCL prints a version banner at
+    # communicator init) write to fd 1 too, so fd 1 becomes stderr and the JSON goes to a
+    # private copy of the original stdout
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+    preset = PRESETS[args.config]
+    for key in ("reads", "read_len", "genome", "k", "slots", "unique"):
+        if getattr(args, key) is None:
+            setattr(args, key, preset[key])
+    if args.unique:
+        args.slots = 0
 
     import torch
 
@@ -124,15 +166,24 @@ def main():
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     torch.cuda.set_device(local)
     dist = None
-    if world > 1:
+    if world > 1 or args.force_sharded:
         import torch.distributed as dist
+        for key, val in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29531"), ("RANK", "0"), ("WORLD_SIZE", "1")):
+            os.environ.setdefault(key, val)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import kaarme_amd as ka
 
     lib = ka.load_library()
-    L, k, N = args.read_len, args.k, args.reads
-    first = rank * N
+    L, k = args.read_len, args.k
+    W = ka.words_for_k(k)
+    strong = preset["scale"] == "strong"
+    if strong:  # this rank's share of the reads and of the table capacity
+        first = args.reads * rank // world
+        N = args.reads * (rank + 1) // world - first
+        slots = -(-args.slots // world) if args.slots else 0
+    else:
+        first, N, slots = rank * args.reads, args.reads, args.slots
     stream = torch.cuda.current_stream()
     nbytes = lib.kc_synth_bytes(first, N, L, 0)
     image = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
@@ -143,20 +194,25 @@ def main():
     host = image.cpu().numpy().tobytes()  # setup only: the host chunker reads boundary bytes
     chunks = ka.plan_chunks(host, k, ka.FMT_FASTA)
     del host
-    batch = (nbytes + len(chunks) * 4096 + (1 << 20)) // 4096 * 4096
+    cap = (args.batch_mib << 20) if args.batch_mib else (2 << 30) // W
+    batch = min((nbytes + len(chunks) * 4096 + (1 << 20)) // 4096 * 4096, cap // 4096 * 4096)
     windows_expected = N * (L - k + 1)
-    workload = f"C2: synthetic {N} x {L} bp reads/GPU, k={k}, -m 2 -s {args.slots}"
-
-    if world > 1:
+    tbl = " ".join(["-m", "2"] + table_args(slots, args.unique))
+    workload = (f"{args.config}: synthetic {N} x {L} bp reads/GPU, k={k}, {tbl}" if not strong else
+                f"{args.config}: synthetic {args.reads} x {L} bp reads over {world} GPU(s), k={k}, {tbl} per GPU")
+    cfg = ka.Config(k=k, mode=2, table_slots=slots, min_abundance=2, batch_bytes=batch, device=local,
+                    bf_enable=bool(args.unique), est_unique=args.unique)
+    if dist:
         from kaarme_amd.sharded import ShardedCounter
-        counter = ShardedCounter(ka.Config(k=k, mode=2, table_slots=args.slots, min_abundance=2,
-                                           batch_bytes=batch, device=local), dist)
+        counter = ShardedCounter(cfg, dist)
     else:
-        counter = ka.KmerCounter(ka.Config(k=k, mode=2, table_slots=args.slots, min_abundance=2,
-                                           batch_bytes=batch, device=local))
+        counter = ka.KmerCounter(cfg)
 
     def step():
         counter.reset()
+        if args.unique:  # Bloom pass, table sized 2 * new_in_second, counting pass behind the gate
+            counter.bloom_device(image.data_ptr(), chunks, ka.FMT_FASTA, stream.cuda_stream)
+            counter.bloom_finalize()
         counter.count_device(image.data_ptr(), chunks, ka.FMT_FASTA, stream.cuda_stream)
         counter.sync()
 
@@ -184,37 +240,46 @@ def main():
         elapsed = float(t.item())
     windows_step = st["windows"]
     assert windows_step == windows_expected, (windows_step, windows_expected)
-    total_windows = windows_step * world * args.steps
+    total_windows = windows_step * args.steps
+    if dist:
+        t = torch.tensor([total_windows], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t)
+        total_windows = float(t.item())
     value = total_windows / elapsed
 
-    # --- roofline of the dominant kernel (k_count), SURVEY.md 8d:
-    # A = sym_B + (1+u)*K + 8 bytes per window (K = 8*ceil(2k/64) key bytes, u = distinct/W,
-    # 8 = 4-byte count read + write), times the windows of one launch.
+    # --- roofline of the counting pass: A = sym_B + (1+u)*K + 8 bytes per
+    # window (K = 8*ceil(2k/64) key bytes, u = distinct/windows, 8 = count read + write),
+    # times the windows of one launch (one staged batch), over the pass's event time.
     K = 8 * math.ceil(2 * k / 64)
     u = st["distinct"] / max(1, windows_step)
     launches = max(1, tm["launches"])
-    sym_per_launch = tm["symbols"] if tm["symbols"] else nbytes
-    win_per_launch = windows_step / (launches / args.steps)
+    per_step = launches / args.steps
+    sym_per_launch = nbytes / per_step
+    win_per_launch = windows_step / per_step
     bytes_per_launch = sym_per_launch + win_per_launch * ((1 + u) * K + 8)
     count_ms = tm["count_ms"] / launches
     achieved = bytes_per_launch / (count_ms * 1e-3) / 1e9
     traffic = load_traffic(workload)
+    if dist:
+        kname = "local count pass + merge insert of the received {key, count} records"
+    elif args.unique:
+        kname = "Bloom pass (k_count<W,1>) + gated counting pass (k_p1, k_p2f, k_p3)"
+    else:
+        kname = "count pass: k_p1 (segmented scatter), k_p2f, k_p3 (partitioned insert)"
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                "kernel": ("count pass: k_p1 hist+scatter, k_p2 hist+scatter, k_p3 (partitioned insert)"
-                           if world == 1 else "route (k_p1 owner bins) + insert of received keys"),
-                "kernel_ms": round(count_ms, 4),
-                "algorithmic_bytes_per_launch": int(bytes_per_launch)}
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": kname,
+                "kernel_ms": round(count_ms, 4), "algorithmic_bytes_per_launch": int(bytes_per_launch)}
     step_ms = elapsed / args.steps * 1e3
     out = {
         "metric": METRIC, "value": value, "unit": "k-mers/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": step_ms, "higher_is_better": True, "scaling": "weak",
+        "warmup": args.warmup, "ms_per_step": step_ms, "higher_is_better": True,
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None, "dtype": "u64", "data": "synthetic (seeded generator, SURVEY.md 8d)",
         "config": {"workload": workload, "reads_per_gpu": N, "read_len": L, "k": k, "genome": args.genome,
-                   "table": f"-m 2 -s {args.slots}",
-                   "parallelism": f"hash-prefix shard x{world}" if world > 1 else "single"},
+                   "table": tbl, "batches_per_step": per_step,
+                   "parallelism": f"hash-prefix shard x{world}" if dist else "single"},
         "roofline": roofline,
-        "hbm_gbs_step": round(bytes_per_launch * (launches / args.steps) / (step_ms * 1e-3) / 1e9, 2),
+        "hbm_gbs_step": round(bytes_per_launch * per_step / (step_ms * 1e-3) / 1e9, 2),
         "kernel_ms": {"gather": round(tm["gather_ms"] / launches, 4), "tokenize": round(tm["tokenize_ms"] / launches, 4),
                       "count": round(count_ms, 4)},
         "image_bytes": nbytes, "stage_bytes": sum(c[1] for c in chunks),
@@ -224,7 +289,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     if dist:
         dist.barrier()
         dist.destroy_process_group()

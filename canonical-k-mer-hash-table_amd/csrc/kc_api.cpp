@@ -75,6 +75,11 @@ struct kc_ctx {
     PartBufs pb{};
     uint32_t pb_nblk1_cap = 0;
     uint64_t pb_k1_cap = 0, pb_k2_cap = 0;  // keys the level-1 / level-2 buffers hold
+    // kc_route_table_device: per-(owner, block) record counts, their scan, scan scratch
+    uint32_t* d_rhist = nullptr;
+    uint64_t* d_roff = nullptr;
+    uint64_t* d_rbsum = nullptr;
+    uint64_t r_cap = 0;
 
     // bloom
     uint32_t* d_bloom = nullptr;
@@ -495,6 +500,9 @@ void kc_destroy(kc_ctx* c) {
     hipFree(c->pb.bsum);
     hipFree(c->pb.keys1);
     hipFree(c->pb.keys2);
+    hipFree(c->d_rhist);
+    hipFree(c->d_roff);
+    hipFree(c->d_rbsum);
     if (c->xev) hipEventDestroy(c->xev);
     for (auto e : c->ev_pool) hipEventDestroy(e);
     for (auto& ev : c->ev_pending)
@@ -600,6 +608,89 @@ int kc_route_device(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, size_
         HIPCHK(c, hipMemcpyAsync(&offs[d], c->pb.off1 + (uint64_t)d * c->pb.nblk1, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
     for (uint32_t d = 0; d < nshards; d++) counts[d] = offs[d + 1] - offs[d];
+    return KC_OK;
+}
+
+int kc_route_table_device(kc_ctx* c, uint32_t nshards, uint64_t* dev_out, uint64_t out_capacity, uint64_t* counts,
+                          void* sp) {
+    if (!c || !counts || nshards == 0 || nshards > 64) return KC_ERR_ARG;
+    if (!c->d_table) return c->fail(KC_ERR_STATE, "no table");
+    hipStream_t s = pick_stream(c, sp);
+    int rc = flush_host(c);
+    if (rc) return rc;
+    if (s != c->stream) {
+        HIPCHK(c, hipEventRecord(c->xev, c->stream));
+        HIPCHK(c, hipStreamWaitEvent(s, c->xev, 0));
+    }
+    const uint64_t nblk = (c->nbuckets + 255) / 256, n = nshards * nblk;
+    if (n > c->r_cap) {
+        hipFree(c->d_rhist);
+        hipFree(c->d_roff);
+        hipFree(c->d_rbsum);
+        c->d_rhist = nullptr;
+        c->d_roff = c->d_rbsum = nullptr;
+        c->r_cap = 0;
+        if (hipMalloc(&c->d_rhist, n * 4) != hipSuccess || hipMalloc(&c->d_roff, (n + 1) * 8) != hipSuccess ||
+            hipMalloc(&c->d_rbsum, ((n + 4095) / 4096 + 2) * 8) != hipSuccess)
+            return c->fail(KC_ERR_NOMEM, "route buffers allocation failed");
+        c->r_cap = n;
+    }
+    const TableView tv = table_view(c);
+    std::array<hipEvent_t, 4> ev{};
+    if (c->profiling) {
+        ev[2] = c->get_event();
+        ev[3] = c->get_event();
+        HIPCHK(c, hipEventRecord(ev[2], s));
+    }
+    HIPCHK(c, launch_route_table(tv, nshards, c->d_rhist, c->d_roff, c->d_rbsum, nullptr, s));
+    std::vector<uint64_t> offs(nshards + 1);
+    for (uint32_t d = 0; d <= nshards; d++)
+        HIPCHK(c, hipMemcpyAsync(&offs[d], c->d_roff + d * nblk, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    for (uint32_t d = 0; d < nshards; d++) counts[d] = offs[d + 1] - offs[d];
+    if (!dev_out) {  // count only
+        for (auto e : ev)
+            if (e) c->ev_pool.push_back(e);
+        return KC_OK;
+    }
+    if (out_capacity < offs[nshards])
+        return c->fail(KC_ERR_ARG, "kc_route_table_device: output capacity too small (" +
+                                       std::to_string(offs[nshards]) + " records)");
+    HIPCHK(c, launch_route_table(tv, nshards, c->d_rhist, c->d_roff, c->d_rbsum, dev_out, s));
+    if (c->profiling) {
+        HIPCHK(c, hipEventRecord(ev[3], s));
+        c->ev_pending.push_back(ev);
+    }
+    HIPCHK(c, hipStreamSynchronize(s));
+    return KC_OK;
+}
+
+int kc_insert_counts_device(kc_ctx* c, const uint64_t* recs, uint64_t n, void* sp) {
+    if (!c || (!recs && n)) return KC_ERR_ARG;
+    if (!c->d_table) return c->fail(KC_ERR_STATE, "no table");
+    hipStream_t s = pick_stream(c, sp);
+    int rc = flush_host(c);
+    if (rc) return rc;
+    if (n == 0) return KC_OK;
+    if (s != c->stream) {
+        HIPCHK(c, hipEventRecord(c->xev, c->stream));
+        HIPCHK(c, hipStreamWaitEvent(s, c->xev, 0));
+    }
+    std::array<hipEvent_t, 4> ev{};
+    if (c->profiling) {
+        ev[2] = c->get_event();
+        ev[3] = c->get_event();
+        HIPCHK(c, hipEventRecord(ev[2], s));
+    }
+    HIPCHK(c, launch_insert_counts(recs, n, table_view(c), c->d_ctr, s));
+    if (c->profiling) {
+        HIPCHK(c, hipEventRecord(ev[3], s));
+        c->ev_pending.push_back(ev);
+    }
+    if (s != c->stream) {
+        HIPCHK(c, hipEventRecord(c->xev, s));
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->xev, 0));
+    }
     return KC_OK;
 }
 

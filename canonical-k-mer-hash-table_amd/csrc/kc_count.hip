@@ -35,7 +35,7 @@ __constant__ uint64_t c_bf_seeds[MAX_NH] = {2411, 3253, 1061, 1129, 2269, 7309, 
 // direct insert of one table key into the HBM table
 // --------------------------------------------------------------------------------
 template <int W>
-DEV bool table_insert(const TableView& tv, const uint64_t (&tk)[W]) {
+DEV bool table_insert(const TableView& tv, const uint64_t (&tk)[W], uint64_t add = 1) {
     constexpr int S = BUCKET_WORDS / (W + 1);
     const uint64_t region = region_of(tk[0], tv.rbits);
     uint32_t b = bucket_in_region(tk[0], tv.rbits);
@@ -64,12 +64,12 @@ DEV bool table_insert(const TableView& tv, const uint64_t (&tk)[W]) {
                                                (unsigned long long)tk[0]);
                 if (old == EMPTY) {
                     if constexpr (W == 1) {
-                        atomicAdd((unsigned long long*)cp, 1ULL);
+                        atomicAdd((unsigned long long*)cp, (unsigned long long)add);
                     } else {
 #pragma unroll
                         for (int i = 1; i < W; i++) atomic_store_agent(kp + i, tk[i]);
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // words land before READY
-                        atomicAdd((unsigned long long*)cp, (unsigned long long)(READY + 1));
+                        atomicAdd((unsigned long long*)cp, (unsigned long long)(READY + add));
                     }
                     return true;
                 }
@@ -78,7 +78,7 @@ DEV bool table_insert(const TableView& tv, const uint64_t (&tk)[W]) {
             }
             if (v0 == tk[0]) {
                 if constexpr (W == 1) {
-                    atomicAdd((unsigned long long*)cp, 1ULL);
+                    atomicAdd((unsigned long long*)cp, (unsigned long long)add);
                     return true;
                 } else {
                     const uint64_t c = atomic_load_agent(cp);
@@ -88,7 +88,7 @@ DEV bool table_insert(const TableView& tv, const uint64_t (&tk)[W]) {
 #pragma unroll
                     for (int i = 1; i < W; i++) eq &= atomic_load_agent(kp + i) == tk[i];
                     if (eq) {
-                        atomicAdd((unsigned long long*)cp, 1ULL);
+                        atomicAdd((unsigned long long*)cp, (unsigned long long)add);
                         return true;
                     }
                 }
@@ -572,6 +572,69 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_insert_keys(const uint64_t* _
                &ctr->invalid, nullptr);
 }
 
+// --------------------------------------------------------------------------------
+// shard merge (pre-aggregated sharding): a rank's table -> {table key, count} records
+// grouped by owner shard; the owner adds the counts into its own table.
+// --------------------------------------------------------------------------------
+constexpr int RT_MAX_PARTS = 64;
+// SCATTER = false: per-block record counts per owner ([owner][block] into hist);
+// true: records {W table-key words, raw count} at off[owner][block] + rank.
+template <int W, bool SCATTER>
+__global__ __launch_bounds__(256) void k_route_table(TableView tv, uint32_t parts, uint32_t* __restrict__ hist,
+                                                     const uint64_t* __restrict__ off, uint64_t* __restrict__ out) {
+    constexpr int S = BUCKET_WORDS / (W + 1);
+    __shared__ uint32_t s_cnt[RT_MAX_PARTS];
+    __shared__ uint64_t s_base[RT_MAX_PARTS];
+    const uint32_t nblk = gridDim.x;
+    for (uint32_t d = threadIdx.x; d < parts; d += 256) {
+        s_cnt[d] = 0;
+        if constexpr (SCATTER) s_base[d] = off[(uint64_t)d * nblk + blockIdx.x];
+    }
+    __syncthreads();
+    const uint64_t bkt = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (bkt < tv.nbuckets) {
+        const uint64_t* b = tv.buckets + bkt * BUCKET_WORDS;
+#pragma unroll
+        for (int sl = 0; sl < S; sl++) {
+            const uint64_t t0 = b[sl * W];
+            if (t0 == EMPTY) continue;
+            const uint32_t d = owner_of(t0, parts);
+            const uint32_t r = atomicAdd(&s_cnt[d], 1u);
+            if constexpr (SCATTER) {
+                uint64_t* o = out + (s_base[d] + r) * (W + 1);
+                o[0] = t0;
+#pragma unroll
+                for (int w = 1; w < W; w++) o[w] = b[sl * W + w];
+                o[W] = b[S * W + sl] & CNT_MASK;
+            }
+        }
+    }
+    if constexpr (!SCATTER) {
+        __syncthreads();
+        for (uint32_t d = threadIdx.x; d < parts; d += 256) hist[(uint64_t)d * nblk + blockIdx.x] = s_cnt[d];
+    }
+}
+
+// add the counts of {W table-key words, count} records into the table (direct inserts:
+// one record per distinct key of a sending shard, far fewer than windows)
+template <int W>
+__global__ __launch_bounds__(COUNT_THREADS) void k_insert_counts(const uint64_t* __restrict__ rec, uint64_t n,
+                                                                 TableView tv, DevCounters* __restrict__ ctr) {
+    uint32_t n_fail = 0, n_inv = 0;
+    unsigned long long added = 0;
+    const uint64_t i = (uint64_t)blockIdx.x * COUNT_THREADS + threadIdx.x;
+    if (i < n) {
+        uint64_t tk[W];
+#pragma unroll
+        for (int w = 0; w < W; w++) tk[w] = rec[i * (W + 1) + w];
+        const uint64_t c = rec[i * (W + 1) + W] & CNT_MASK;
+        if (tk[0] == EMPTY) n_inv++;
+        else if (c && !table_insert<W>(tv, tk, c)) n_fail++;
+        else added = c;
+    }
+    block_add4(added, n_fail, n_inv, 0, &ctr->inserted, &ctr->overflow, &ctr->invalid, nullptr);
+}
+
 // Level 2: coarse bin c (block = c * B2 + j) -> its F2 regions (next bits of tkey[0]).
 template <int W, bool SCATTER>
 __global__ __launch_bounds__(COUNT_THREADS, 4) void k_p2(TableView tv, PartBufs pb, const unsigned long long* gate) {
@@ -693,7 +756,7 @@ __global__ __launch_bounds__(NT, NT / 128) void k_p3(TableView tv, PartBufs pb, 
     constexpr int S = BUCKET_WORDS / (W + 1);
     // keys loaded per thread before inserting (memory-level parallelism); 1024-thread
     // groups already keep 8 waves per SIMD in flight
-    constexpr int KB = NT >= 1024 ? 4 : 8;
+    constexpr int KB = NT >= 1024 ? (W >= 3 ? 2 : 4) : 8;
     if constexpr (SEG) {
         if (ctr->part_overflow) return;
     } else {
@@ -779,67 +842,66 @@ __global__ __launch_bounds__(NT, NT / 128) void k_p3(TableView tv, PartBufs pb, 
                     }
                 }
             }
-            for (int probe = 0; W > 1 && probe < BPR && !done; probe++) {
-                uint64_t w0[S];
-                if constexpr (W == 1) {
+            if constexpr (W > 1) {
+                // branch-light probe over a whole bucket: the count words are read first and
+                // the key words after a wait, so a READY count guarantees that the key words
+                // read after it are published (the claimer stores them before setting READY)
+                constexpr int C0 = S * W / 2;  // first 16-byte chunk holding counts
+                static_assert((S * W) % 2 == 0, "keys end on a chunk boundary");
+                for (int probe = 0; probe < 4 * BPR && !done;) {
+                    uint64_t bw[BUCKET_WORDS];
 #pragma unroll
-                    for (int c = 0; c < S / 2; c++) {
+                    for (int c = C0; c < BUCKET_WORDS / 2; c++) {
                         const uint4 v = l4[lds_chunk(b, c)];
-                        w0[2 * c] = ((uint64_t)v.y << 32) | v.x;
-                        w0[2 * c + 1] = ((uint64_t)v.w << 32) | v.z;
+                        bw[2 * c] = ((uint64_t)v.y << 32) | v.x;
+                        bw[2 * c + 1] = ((uint64_t)v.w << 32) | v.z;
                     }
-                } else {
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-                    for (int c = 0; c < S; c++) w0[c] = *lds_word(lt, b, c * W);
-                }
-                int s = 0;
-                while (s < S) {
-                    uint64_t* kp = lds_word(lt, b, s * W);
-                    unsigned long long* cp = reinterpret_cast<unsigned long long*>(lds_word(lt, b, S * W + s));
-                    uint64_t v0 = w0[s];
-                    if (v0 == EMPTY) {
-                        const uint64_t old = atomicCAS((unsigned long long*)kp, 0ULL, (unsigned long long)k0);
+                    for (int c = 0; c < C0; c++) {
+                        const uint4 v = l4[lds_chunk(b, c)];
+                        bw[2 * c] = ((uint64_t)v.y << 32) | v.x;
+                        bw[2 * c + 1] = ((uint64_t)v.w << 32) | v.z;
+                    }
+                    uint32_t eqm = 0, pend = 0, emm = 0;
+#pragma unroll
+                    for (int sl = 0; sl < S; sl++) {
+                        const bool w0eq = bw[sl * W] == k0;
+                        bool rest = true;
+#pragma unroll
+                        for (int w = 1; w < W; w++) rest &= bw[sl * W + w] == kk[q][w];
+                        const bool ready = (bw[S * W + sl] & READY) != 0;
+                        eqm |= (uint32_t)(w0eq && rest && ready) << sl;
+                        pend |= (uint32_t)(w0eq && !ready) << sl;
+                        emm |= (uint32_t)(bw[sl * W] == EMPTY) << sl;
+                    }
+                    if (eqm) {
+                        atomicAdd(reinterpret_cast<unsigned long long*>(lds_word(lt, b, S * W + __builtin_ctz(eqm))),
+                                  1ULL);
+                        done = true;
+                    } else if (pend) {
+                        probe++;  // another wave is publishing a key with this word 0: read again
+                    } else if (emm) {
+                        const int e = __builtin_ctz(emm);
+                        const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long*>(lds_word(lt, b, e * W)),
+                                                       0ULL, (unsigned long long)k0);
                         if (old == EMPTY) {
-                            if constexpr (W == 1) {
-                                atomicAdd(cp, 1ULL);
-                            } else {
-#pragma unroll
-                                for (int w = 1; w < W; w++)
-                                    __hip_atomic_store(lds_word(lt, b, s * W + w), kk[q][w], __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_WORKGROUP);
-                                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                                atomicAdd(cp, (unsigned long long)(READY + 1));
-                            }
-                            done = true;
-                            break;
-                        }
-                        v0 = old;
-                        w0[s] = old;
-                    }
-                    if (v0 == k0) {
-                        if constexpr (W == 1) {
-                            atomicAdd(cp, 1ULL);
-                            done = true;
-                            break;
-                        } else {
-                            const uint64_t cv = __hip_atomic_load(cp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            if (!(cv & READY)) continue;  // claimed by another lane, words not published yet
-                            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                            bool eq = true;
 #pragma unroll
                             for (int w = 1; w < W; w++)
-                                eq &= __hip_atomic_load(lds_word(lt, b, s * W + w), __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_WORKGROUP) == kk[q][w];
-                            if (eq) {
-                                atomicAdd(cp, 1ULL);
-                                done = true;
-                                break;
-                            }
+                                __hip_atomic_store(lds_word(lt, b, e * W + w), kk[q][w], __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+                            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                            atomicAdd(reinterpret_cast<unsigned long long*>(lds_word(lt, b, S * W + e)),
+                                      (unsigned long long)(READY + 1));
+                            done = true;
+                        } else {
+                            probe++;  // lost the slot: read the bucket again
                         }
+                    } else {
+                        b = (b + 1) & (BPR - 1);  // bucket full, key absent: next bucket
+                        probe++;
                     }
-                    s++;
                 }
-                b = (b + 1) & (BPR - 1);
             }
             if (!done) n_fail++;
         }
@@ -1162,6 +1224,41 @@ hipError_t launch_insert_keys(const uint64_t* keys, uint64_t n, bool partitioned
     case 4: return insert_keys_w<4>(keys, n, partitioned, t, ctr, pb, s);
     default: return hipErrorInvalidValue;
     }
+}
+
+hipError_t launch_route_table(TableView t, uint32_t parts, uint32_t* hist, uint64_t* off, uint64_t* bsum,
+                              uint64_t* out, hipStream_t s) {
+    if (parts == 0 || parts > RT_MAX_PARTS) return hipErrorInvalidValue;
+    const unsigned nblk = (unsigned)((t.nbuckets + 255) / 256);
+    auto go = [&](auto kh, auto ks) {
+        if (!out) {
+            hipLaunchKernelGGL(kh, dim3(nblk), dim3(256), 0, s, t, parts, hist, off, out);
+            launch_scan(hist, (uint64_t)parts * nblk, off, bsum, s);
+        } else {
+            hipLaunchKernelGGL(ks, dim3(nblk), dim3(256), 0, s, t, parts, hist, off, out);
+        }
+        return hipGetLastError();
+    };
+    switch (t.W) {
+    case 1: return go(k_route_table<1, false>, k_route_table<1, true>);
+    case 2: return go(k_route_table<2, false>, k_route_table<2, true>);
+    case 3: return go(k_route_table<3, false>, k_route_table<3, true>);
+    case 4: return go(k_route_table<4, false>, k_route_table<4, true>);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_insert_counts(const uint64_t* rec, uint64_t n, TableView t, DevCounters* ctr, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const dim3 grid((unsigned)((n + COUNT_THREADS - 1) / COUNT_THREADS));
+    switch (t.W) {
+    case 1: hipLaunchKernelGGL(k_insert_counts<1>, grid, dim3(COUNT_THREADS), 0, s, rec, n, t, ctr); break;
+    case 2: hipLaunchKernelGGL(k_insert_counts<2>, grid, dim3(COUNT_THREADS), 0, s, rec, n, t, ctr); break;
+    case 3: hipLaunchKernelGGL(k_insert_counts<3>, grid, dim3(COUNT_THREADS), 0, s, rec, n, t, ctr); break;
+    case 4: hipLaunchKernelGGL(k_insert_counts<4>, grid, dim3(COUNT_THREADS), 0, s, rec, n, t, ctr); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 hipError_t launch_dump(TableView t, int count_mode, uint64_t min_abundance, uint64_t* out, DevCounters* ctr,

@@ -128,6 +128,11 @@ hipError_t launch_route(PackedView sym, int k, int W, DevCounters* ctr, PartBufs
 // insert an array of table keys into this shard's table
 hipError_t launch_insert_keys(const uint64_t* keys, uint64_t n, bool partitioned, TableView t, DevCounters* ctr,
                               PartBufs pb, hipStream_t s);
+// pre-aggregated sharding: out == nullptr -> per-(owner, block) record counts into hist and
+// their exclusive scan into off (off[parts * nblk] = total); else scatter the records
+hipError_t launch_route_table(TableView t, uint32_t parts, uint32_t* hist, uint64_t* off, uint64_t* bsum,
+                              uint64_t* out, hipStream_t s);
+hipError_t launch_insert_counts(const uint64_t* rec, uint64_t n, TableView t, DevCounters* ctr, hipStream_t s);
 hipError_t launch_dump(TableView t, int count_mode, uint64_t min_abundance, uint64_t* out, DevCounters* ctr,
                        hipStream_t s);
 hipError_t launch_synth(uint8_t* dst, uint64_t first_read, uint64_t n_reads, uint64_t seed, uint64_t genome_len,

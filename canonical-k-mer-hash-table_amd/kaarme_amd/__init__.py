@@ -44,6 +44,7 @@ EXPORTS = (
     "kc_count_chunk", "kc_bloom_device", "kc_count_device", "kc_sync", "kc_finish", "kc_dump",
     "kc_write", "kc_key_words", "kc_free", "kc_plan_chunks", "kc_synth_bytes", "kc_synth_device",
     "kc_reset", "kc_profile", "kc_get_timing", "kc_route_device", "kc_insert_keys_device",
+    "kc_route_table_device", "kc_insert_counts_device",
 )
 
 
@@ -125,6 +126,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "kc_route_device": (I32, [P, P, ctypes.POINTER(kc_chunk), ctypes.c_size_t, I32, ctypes.c_uint32, P, U64,
                                   ctypes.POINTER(U64), P]),
         "kc_insert_keys_device": (I32, [P, P, U64, P]),
+        "kc_route_table_device": (I32, [P, ctypes.c_uint32, P, U64, P, P]),
+        "kc_insert_counts_device": (I32, [P, P, U64, P]),
         "kc_profile": (I32, [P, I32]),
         "kc_get_timing": (I32, [P, ctypes.POINTER(kc_timing)]),
         "kc_synth_device": (I32, [P, U64, U64, U64, U64, ctypes.c_uint32, ctypes.c_uint32,
@@ -279,6 +282,18 @@ class KmerCounter:
     def insert_keys_device(self, keys_ptr: int, n_keys: int, stream: int = 0):
         self._chk(self.lib.kc_insert_keys_device(self._ctx, ctypes.c_void_p(keys_ptr), n_keys,
                                                  ctypes.c_void_p(stream or None)), "kc_insert_keys_device")
+
+    def route_table_device(self, nshards: int, out_ptr: int, out_capacity: int, stream: int = 0) -> List[int]:
+        """The table's occupied slots as {W table-key words, raw count} records grouped by
+        owner shard into out_ptr (0 = count only); returns the per-owner record counts."""
+        counts = (ctypes.c_uint64 * nshards)()
+        self._chk(self.lib.kc_route_table_device(self._ctx, nshards, ctypes.c_void_p(out_ptr or None), out_capacity,
+                                                 counts, ctypes.c_void_p(stream or None)), "kc_route_table_device")
+        return [int(x) for x in counts]
+
+    def insert_counts_device(self, rec_ptr: int, n_records: int, stream: int = 0):
+        self._chk(self.lib.kc_insert_counts_device(self._ctx, ctypes.c_void_p(rec_ptr), n_records,
+                                                   ctypes.c_void_p(stream or None)), "kc_insert_counts_device")
 
     def key_words(self) -> int:
         return self.lib.kc_key_words(self._ctx)

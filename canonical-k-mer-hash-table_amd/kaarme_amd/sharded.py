@@ -1,14 +1,24 @@
 """Hash-prefix owner sharding of the counting table across GPUs.
 
 One process per GPU (torch.distributed; backend "nccl" is RCCL on ROCm, over xGMI).
-Per batch every rank
-  1. tokenizes its own input and routes the table keys of its windows to their owner
-     shard (``kc_route_device``: keys grouped by owner, owner = a bit field of the
-     engine's bijective table key, independent of the table's region/bucket bits);
-  2. exchanges the groups with ONE all-to-all (counts first, then the keys);
-  3. inserts what it received into its private table (``kc_insert_keys_device``).
-Every canonical k-mer has exactly one owner, so the union of the per-shard tables is
-the exact global count and the output is the concatenation of the per-shard dumps.
+
+Pre-aggregated exchange (`ShardedCounter`):
+  1. every rank counts its own input into a private *local* table with the full
+     single-GPU pipeline (kc_count_device);
+  2. at the end of the job (`sync`/`merge`), `kc_route_table_device` writes the local
+     table's occupied slots as records {table key, raw count}, grouped by owner shard
+     (owner = a bit field of the table key, independent of the table's region/bucket
+     bits), and ONE all-to-all exchanges them (counts first, then the records);
+  3. every rank adds what it received into its *owner* table (kc_insert_counts_device).
+Every canonical k-mer has exactly one owner, so the union of the owner tables is the
+exact global count, and the output is the concatenation of the per-rank outputs.  The
+exchange moves one record per distinct k-mer of each rank instead of one key per window
+(86 M records instead of 1.2 G keys for C2), which keeps xGMI off the critical path.
+The count transforms (mod 65536 / min(c, 16383)) apply to the merged counts.
+
+The per-window alternative (kc_route_device + kc_insert_keys_device: route every
+window's key to its owner, no local table) stays in the C ABI and is exercised by
+tests/test_gpu_sharded.py.
 
 The exchange logic (:func:`exchange`) is backend-agnostic torch code: the CPU tests run
 it over ``gloo`` with a NumPy engine, the GPU path over RCCL with the HIP engine.
@@ -20,33 +30,91 @@ from typing import List, Sequence, Tuple
 from . import Config, KmerCounter, words_for_k
 
 
-def exchange(dist, keys, counts: Sequence[int], W: int, group=None):
-    """All-to-all of owner-grouped keys.  keys: int64 tensor holding sum(counts)*W words
-    (group d = the keys for rank d, in rank order).  Returns (received keys, n received)."""
+# Largest message per (peer, all-to-all) in int64 words.  RCCL 2.26 (the ROCm torch
+# wheel's) returned only part of a 1.4 GB single-peer all_to_all_single on MI355X, so big
+# exchanges go in rounds of at most this many words per peer.
+EXCHANGE_CHUNK_WORDS = 1 << 24
+
+
+def exchange(dist, keys, counts: Sequence[int], W: int, group=None, chunk_words: int = EXCHANGE_CHUNK_WORDS):
+    """All-to-all of owner-grouped items of W int64 words each.  keys: int64 tensor
+    holding sum(counts)*W words (group d = the items for rank d, in rank order).
+    Returns (received items, n received); the items from rank s follow those of s-1."""
     import torch
 
     dev = keys.device
+    world = len(counts)
     send_counts = torch.tensor(list(counts), dtype=torch.int64, device=dev)
     recv_counts = torch.empty_like(send_counts)
     dist.all_to_all_single(recv_counts, send_counts, group=group)
     recv = [int(x) for x in recv_counts.cpu().tolist()]
     total = sum(recv)
     out = torch.empty(max(1, total * W), dtype=torch.int64, device=dev)
-    dist.all_to_all_single(out[: total * W], keys[: sum(counts) * W],
-                           output_split_sizes=[r * W for r in recv],
-                           input_split_sizes=[c * W for c in counts], group=group)
+    sw = [c * W for c in counts]
+    rw = [r * W for r in recv]
+    big = torch.tensor([max(sw + rw + [0])], dtype=torch.int64, device=dev)
+    dist.all_reduce(big, op=dist.ReduceOp.MAX, group=group)
+    rounds = max(1, -(-int(big.item()) // chunk_words))
+    if rounds == 1:
+        dist.all_to_all_single(out[: total * W], keys[: sum(sw)], output_split_sizes=rw, input_split_sizes=sw,
+                               group=group)
+        return out, total
+    so = [sum(sw[:d]) for d in range(world)]
+    ro = [sum(rw[:d]) for d in range(world)]
+    for r in range(rounds):
+        lo = r * chunk_words
+        sin = [min(max(sw[d] - lo, 0), chunk_words) for d in range(world)]
+        rin = [min(max(rw[d] - lo, 0), chunk_words) for d in range(world)]
+        send = torch.cat([keys[so[d] + lo: so[d] + lo + sin[d]] for d in range(world)])
+        got = torch.empty(max(1, sum(rin)), dtype=torch.int64, device=dev)
+        dist.all_to_all_single(got[: sum(rin)], send, output_split_sizes=rin, input_split_sizes=sin, group=group)
+        pos = 0
+        for d in range(world):
+            if rin[d]:
+                out[ro[d] + lo: ro[d] + lo + rin[d]].copy_(got[pos: pos + rin[d]])
+            pos += rin[d]
     return out, total
 
 
+TILE = 4096
+DEFAULT_BATCH = 256 << 20  # kc_api.cpp kDefaultBatch
+
+
+def batch_groups(chunks, batch_bytes: int):
+    """Split a chunk table into groups that each fit one staging batch (kc_api.cpp:
+    chunks are placed at 4 KiB-aligned offsets of a batch_bytes stage)."""
+    cap = (batch_bytes or DEFAULT_BATCH) // TILE * TILE
+    groups, cur, used = [], [], 0
+    for c in chunks:
+        need = (c[1] + TILE - 1) // TILE * TILE
+        if c[1] == 0:
+            continue
+        if need > cap:
+            raise ValueError("chunk larger than the staging batch")
+        if cur and used + need > cap:
+            groups.append(cur)
+            cur, used = [], 0
+        cur.append(c)
+        used += need
+    if cur:
+        groups.append(cur)
+    return groups
+
+
 class DeviceEngine:
-    """The HIP engine of one rank: routes device images, inserts received keys."""
+    """The HIP engine of one rank: a local table counting the rank's input and an owner
+    table holding the merged counts of the k-mers this rank owns."""
 
     def __init__(self, cfg: Config):
         self.cfg = cfg
-        self.kc = KmerCounter(cfg)
+        self.kc = KmerCounter(cfg)      # local table (also used by the per-window route path)
+        self.owner = None               # created on first use
         self.W = words_for_k(cfg.k)
+        self.device = "cuda"
         self._buf = None
+        self._rec = None
 
+    # -- per-window routing (no local table)
     def route(self, dev_ptr: int, chunks, fmt: int, parts: int, stream: int = 0):
         import torch
 
@@ -58,6 +126,32 @@ class DeviceEngine:
 
     def insert(self, keys, n: int, stream: int = 0):
         self.kc.insert_keys_device(keys.data_ptr(), n, stream)
+
+    # -- pre-aggregated path
+    def count(self, dev_ptr: int, chunks, fmt: int, stream: int = 0):
+        self.kc.count_device(dev_ptr, chunks, fmt, stream)
+
+    def route_table(self, parts: int, stream: int = 0):
+        import torch
+
+        counts = self.kc.route_table_device(parts, 0, 0, stream)  # record counts per owner
+        need = max(1, sum(counts)) * (self.W + 1)
+        if self._rec is None or self._rec.numel() < need:
+            self._rec = torch.empty(need + need // 8, dtype=torch.int64, device="cuda")
+        counts = self.kc.route_table_device(parts, self._rec.data_ptr(), self._rec.numel() // (self.W + 1), stream)
+        return self._rec, counts
+
+    def owner_table(self) -> KmerCounter:
+        if self.owner is None:
+            self.owner = KmerCounter(self.cfg)
+        return self.owner
+
+    def insert_counts(self, recs, n: int, stream: int = 0):
+        self.owner_table().insert_counts_device(recs.data_ptr(), n, stream)
+
+    def reset(self):
+        self.kc.reset()
+        self.owner_table().reset()
 
 
 class ShardedCounter:
@@ -71,38 +165,74 @@ class ShardedCounter:
         self.rank = dist.get_rank(group)
         self.W = words_for_k(cfg.k)
         self.engine = engine if engine is not None else DeviceEngine(cfg)
+        self.device = getattr(self.engine, "device", "cpu")
+        self._pending = False
+        self._stream = 0
         self._inflight = []
 
-    # the counting pass over a device image (chunks from kaarme_amd.plan_chunks)
+    # the counting pass over a device image (chunks from kaarme_amd.plan_chunks): local
     def count_device(self, dev_ptr: int, chunks: List[Tuple[int, int, int]], fmt: int, stream: int = 0):
-        keys, counts = self.engine.route(dev_ptr, chunks, fmt, self.world, stream)
-        recv, n = exchange(self.dist, keys, counts, self.W, self.group)
-        self.engine.insert(recv, n, stream)
-        self._inflight = [recv]  # keep the receive buffer alive until the insert completed
+        self.engine.count(dev_ptr, chunks, fmt, stream)
+        self._pending = True
+        self._stream = stream
 
-    # delegation to the local shard
+    def merge(self, stream: int = 0):
+        """Route the local table's records to their owners (one all-to-all) and add them
+        into the owner tables.  Collective: every rank calls it the same number of times."""
+        recs, counts = self.engine.route_table(self.world, stream)
+        recv, n = exchange(self.dist, recs, counts, self.W + 1, self.group)
+        self.engine.insert_counts(recv, n, stream)
+        self._inflight = [recv]  # the receive buffer must outlive the insert
+        self._pending = False
+
+    def bloom_device(self, *a, **kw):
+        raise NotImplementedError("the Bloom-filter prefilter is not sharded (run it on one GPU)")
+
+    bloom_finalize = bloom_device
+
     @property
     def kc(self) -> KmerCounter:
-        return self.engine.kc
+        """The owner table (this rank's share of the merged counts)."""
+        return self.engine.owner_table()
 
     def reset(self):
-        self.kc.reset()
+        self.engine.reset()
+        self._pending = False
 
     def sync(self):
+        """Completes the job: the (collective) merge if counts are pending, then waits."""
+        if self._pending:
+            self.merge(self._stream)
+        self.engine.kc.sync()
         self.kc.sync()
         self._inflight = []
 
     def profile(self, enable: bool = True):
+        self.engine.kc.profile(enable)
         self.kc.profile(enable)
 
     def timing(self) -> dict:
-        return self.kc.timing()
+        """Local counting batches (+ the table routing) plus the merge insert (count_ms)."""
+        a, b = self.engine.kc.timing(), self.kc.timing()
+        out = dict(a)
+        out["count_ms"] = a["count_ms"] + b["count_ms"]
+        return out
 
     def finish(self) -> dict:
-        return self.kc.finish()
+        """Stats of the owner table; windows / chunks / bytes are this rank's input."""
+        self.sync()
+        local, own = self.engine.kc.finish(), self.kc.finish()
+        st = dict(own)
+        for key in ("windows", "chunks", "bytes", "bf_windows"):
+            st[key] = local[key]
+        st["local_distinct"] = local["distinct"]
+        return st
 
     def dump(self):
         return self.kc.dump()
 
     def lines(self):
         return self.kc.lines()
+
+    def write(self, path: str):
+        self.kc.write(path)

@@ -124,6 +124,18 @@ int kc_route_device(kc_ctx* ctx, const uint8_t* dev_image, const kc_chunk* chunk
                     uint32_t nshards, uint64_t* dev_out, uint64_t out_capacity, uint64_t* counts, void* hip_stream);
 int kc_insert_keys_device(kc_ctx* ctx, const uint64_t* dev_keys, uint64_t n_keys, void* hip_stream);
 
+/* Pre-aggregated sharding (the multi-GPU path of kaarme_amd.sharded): every rank counts
+ * its own input into its own table, then kc_route_table_device writes the table's
+ * occupied slots as records {W table-key words, raw count} grouped by owner shard
+ * (the owner_of bit field of word 0) into dev_out (capacity in records; NULL = counts
+ * only) and the per-owner record counts into counts[nshards] (nshards <= 64); after
+ * the exchange kc_insert_counts_device adds received records into the owner's table.
+ * Replaces the reference's single shared table (kmer_hash_table.cpp:2207-2567): the union
+ * of the owners' tables is the count of the whole input. */
+int kc_route_table_device(kc_ctx* ctx, uint32_t nshards, uint64_t* dev_out, uint64_t out_capacity,
+                          uint64_t* counts, void* hip_stream);
+int kc_insert_counts_device(kc_ctx* ctx, const uint64_t* dev_records, uint64_t n_records, void* hip_stream);
+
 /* Re-initialise the table, the Bloom filter and all counters (the table/filter
  * constructors again, without reallocating). */
 int kc_reset(kc_ctx* ctx);

@@ -88,3 +88,54 @@ def test_insert_rejects_non_table_keys(monkeypatch, path):
     e.insert(keys, 5000, torch.cuda.current_stream().cuda_stream)
     with pytest.raises(ka.KcError, match="not table keys"):
         e.kc.finish()
+
+
+@pytest.mark.parametrize("k,mode,G", [(31, 2, 2), (31, 0, 3), (51, 2, 4), (63, 1, 2), (127, 0, 2)])
+def test_preaggregated_merge_union(tmp_path, k, mode, G):
+    """Pre-aggregated sharding (ShardedCounter's path): each emulated rank counts its own
+    reads locally, routes its table as {key, count} records by owner, and every owner adds
+    the records it receives; the owners' outputs are disjoint and their union is the
+    oracle's count of the whole input (transforms applied to the merged counts)."""
+    n_reads = 20000
+    per = n_reads // G
+    images = []
+    for r in range(G):
+        fa = tmp_path / f"r{r}.fasta"
+        cnt = per if r < G - 1 else n_reads - per * (G - 1)
+        # a small genome: every k-mer occurs on several ranks, so the merge adds counts
+        subprocess.run([GEN, str(fa), str(n_reads), "150", "20000", "--first", str(r * per), "--count", str(cnt)],
+                       check=True)
+        images.append(_image(str(fa)))
+    whole = tmp_path / "all.fasta"
+    with open(whole, "wb") as f:
+        for data, _ in images:
+            f.write(data)
+    engines = [DeviceEngine(ka.Config(k=k, mode=mode, table_slots=400000, min_abundance=1)) for _ in range(G)]
+    W = engines[0].W
+    stream = torch.cuda.current_stream().cuda_stream
+    routed = []
+    for r, (data, img) in enumerate(images):
+        engines[r].reset()
+        engines[r].count(img.data_ptr(), ka.plan_chunks(data, k, ka.FMT_FASTA, chunk_size=128 * 1024), ka.FMT_FASTA,
+                         stream)
+        recs, counts = engines[r].route_table(G, stream)
+        torch.cuda.synchronize()
+        assert sum(counts) == engines[r].kc.finish()["distinct"]
+        routed.append((recs[: sum(counts) * (W + 1)].clone(), counts))
+    for d in range(G):
+        parts = []
+        for recs, counts in routed:
+            lo = sum(counts[:d]) * (W + 1)
+            parts.append(recs[lo:lo + counts[d] * (W + 1)])
+        recv = torch.cat(parts)
+        engines[d].insert_counts(recv, recv.numel() // (W + 1), stream)
+        torch.cuda.synchronize()
+    shard_lines = [set(e.owner_table().lines()) for e in engines]
+    kmers = [set(l.rsplit(" ", 1)[0] for l in s) for s in shard_lines]
+    for a in range(G):
+        for b in range(a + 1, G):
+            assert not (kmers[a] & kmers[b]), "a k-mer has two owners"
+    union = set().union(*shard_lines)
+    out = tmp_path / "oracle.txt"
+    oracle_count(str(whole), k, ["-m", str(mode), "-a", "1"], out)
+    assert sorted_digest_lines(union) == sorted_digest_file(out)

@@ -1,10 +1,11 @@
 """Multi-rank sharding on CPU: world_size 2 over gloo.
 
-The exchange of kaarme_amd.sharded (owner-grouped keys, one all-to-all of counts and
-one of keys, insert at the owner) runs unchanged; the HIP engine is replaced by a NumPy
-engine that tokenizes PLAIN lines, canonicalises, splits keys into W words and owns
-keys by a hash of the key.  The union of the shard tables must equal a single-process
-count and the shards must be disjoint.
+The pre-aggregated exchange of kaarme_amd.sharded (local counts -> owner-grouped
+{key, count} records -> one all-to-all of counts and one of records -> merge at the
+owner) runs unchanged; the HIP engine is replaced by a NumPy engine that tokenizes
+PLAIN lines, canonicalises, splits keys into W words and owns keys by a hash of the key.
+The union of the owner tables must equal a single-process count and the owners must be
+disjoint.
 """
 import collections
 import json
@@ -65,41 +66,50 @@ def owner(words, parts):
     return ((h & 0xFFFFFFFF) * parts) >> 32
 
 
+class _Table:
+    def __init__(self):
+        self.table = collections.Counter()
+
+    def sync(self):
+        pass
+
+
 class NumpyEngine:
-    """Stand-in for sharded.DeviceEngine: same route/insert contract on CPU tensors."""
+    """Stand-in for sharded.DeviceEngine: same count / route_table / insert_counts contract
+    on CPU tensors (records: W key words + 1 count word)."""
 
     def __init__(self, k, lines):
         self.k = k
         self.W = 2 * k // 64 + 1
         self.lines = lines
-        self.table = collections.Counter()
-        self.kc = self
+        self.kc = _Table()      # local
+        self.owner = _Table()
 
-    def route(self, dev_ptr, chunks, fmt, parts, stream=0):
-        groups = [[] for _ in range(parts)]
+    def count(self, dev_ptr, chunks, fmt, stream=0):
         for off, ln, _ in chunks:
             for line in self.lines[off:off + ln]:
-                for km in canonical_windows(line, self.k):
-                    ws = to_words(km, self.W)
-                    groups[owner(ws, parts)].extend(ws)
+                self.kc.table.update(canonical_windows(line, self.k))
+
+    def route_table(self, parts, stream=0):
+        groups = [[] for _ in range(parts)]
+        for km, c in self.kc.table.items():
+            ws = to_words(km, self.W)
+            groups[owner(ws, parts)].extend(ws + [c])
         flat = [w for g in groups for w in g]
         arr = np.array(flat, dtype=np.uint64).view(np.int64)
-        return torch.from_numpy(arr.copy()), [len(g) // self.W for g in groups]
+        return torch.from_numpy(arr.copy()), [len(g) // (self.W + 1) for g in groups]
 
-    def insert(self, keys, n, stream=0):
-        ws = keys[: n * self.W].numpy().view(np.uint64).reshape(n, self.W)
-        for row in ws:
-            self.table[from_words(row, self.k)] += 1
+    def insert_counts(self, recs, n, stream=0):
+        rows = recs[: n * (self.W + 1)].numpy().view(np.uint64).reshape(n, self.W + 1)
+        for row in rows:
+            self.owner.table[from_words(row[:self.W], self.k)] += int(row[self.W])
 
-    # delegated KmerCounter surface
+    def owner_table(self):
+        return self.owner
+
     def reset(self):
-        self.table.clear()
-
-    def sync(self):
-        pass
-
-    def lines_out(self):
-        return self.table
+        self.kc.table.clear()
+        self.owner.table.clear()
 
 
 def _free_port():
@@ -140,11 +150,11 @@ def _worker(rank, world, port, k, reads, outdir, rounds):
         step = max(1, (hi - lo + rounds - 1) // rounds)
         for b in range(lo, hi, step):
             sc.count_device(0, [(b, min(step, hi - b), 0)], 2)
-        # an empty batch on every rank must not deadlock or change anything
-        sc.count_device(0, [], 2)
-        sc.sync()
+        sc.count_device(0, [], 2)  # an empty batch changes nothing
+        sc.sync()                  # the collective merge
+        sc.sync()                  # nothing pending: no second exchange
         with open(os.path.join(outdir, f"shard{rank}.json"), "w") as f:
-            json.dump(dict(eng.table), f)
+            json.dump(dict(eng.owner.table), f)
     finally:
         dist.destroy_process_group()
 
@@ -164,7 +174,7 @@ def test_sharded_union_equals_single(tmp_path, k):
     assert all(len(s) > 0 for s in shards)
 
 
-def _exchange_worker(rank, world, port, outdir):
+def _exchange_worker(rank, world, port, outdir, chunk):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -175,7 +185,7 @@ def _exchange_worker(rank, world, port, outdir):
         rows = [[rank * 1000000 + d * 10000 + i * 10 + j for j in range(W)] for d in range(world)
                 for i in range(counts[d])]
         keys = torch.tensor(sum(rows, []) + [-1] * 7, dtype=torch.int64)  # slack past the groups
-        out, n = exchange(dist, keys, counts, W)
+        out, n = exchange(dist, keys, counts, W, chunk_words=chunk)
         got = out[: n * W].view(n, W).tolist()
         with open(os.path.join(outdir, f"x{rank}.json"), "w") as f:
             json.dump({"n": n, "rows": got}, f)
@@ -183,12 +193,26 @@ def _exchange_worker(rank, world, port, outdir):
         dist.destroy_process_group()
 
 
-def test_exchange_splits(tmp_path):
+@pytest.mark.parametrize("chunk", [1 << 24, 5, 3])
+def test_exchange_splits(tmp_path, chunk):
+    """One all-to-all, or rounds of at most `chunk` words per peer: same result."""
     world = 3
-    mp.spawn(_exchange_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_exchange_worker, args=(world, _free_port(), str(tmp_path), chunk), nprocs=world, join=True)
     for d in range(world):
         r = json.load(open(tmp_path / f"x{d}.json"))
         want = [[s * 1000000 + d * 10000 + i * 10 + j for j in range(3)] for s in range(world)
                 for i in range((s + 1) * (d + 1))]
         assert r["n"] == len(want)
         assert r["rows"] == want
+
+
+def test_batch_groups():
+    from kaarme_amd.sharded import batch_groups
+    chunks = [(0, 4096, 0), (4096, 1, 0), (5000, 0, 0), (6000, 8192, 0), (20000, 100, 1)]
+    assert batch_groups(chunks, 3 * 4096) == [[(0, 4096, 0), (4096, 1, 0)], [(6000, 8192, 0), (20000, 100, 1)]]
+    g = batch_groups(chunks, 3 * 4096)
+    assert [c for grp in g for c in grp] == [c for c in chunks if c[1]]
+    for grp in g:
+        assert sum((c[1] + 4095) // 4096 * 4096 for c in grp) <= 3 * 4096
+    with pytest.raises(ValueError):
+        batch_groups([(0, 5 * 4096, 0)], 4 * 4096)
