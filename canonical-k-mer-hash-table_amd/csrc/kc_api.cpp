@@ -75,6 +75,7 @@ struct kc_ctx {
     PartBufs pb{};
     uint32_t pb_nblk1_cap = 0;
     uint64_t pb_k1_cap = 0, pb_k2_cap = 0;  // keys the level-1 / level-2 buffers hold
+    bool table_fresh = false;  // the table is all zero (allocated / reset, nothing inserted since)
     // kc_route_table_device: per-(owner, block) record counts, their scan, scan scratch
     uint32_t* d_rhist = nullptr;
     uint64_t* d_roff = nullptr;
@@ -161,6 +162,7 @@ static int alloc_table(kc_ctx* c, uint64_t min_slots) {
     hipError_t e = hipMalloc(&c->d_table, bytes);
     if (e != hipSuccess) return c->fail(KC_ERR_NOMEM, "table allocation failed (" + std::to_string(bytes) + " bytes)");
     HIPCHK(c, hipMemsetAsync(c->d_table, 0, bytes, c->stream));
+    c->table_fresh = true;
     return KC_OK;
 }
 
@@ -291,10 +293,11 @@ static int run_batch(kc_ctx* c, uint64_t used, uint64_t nchunks, int fmt, int pa
         const char* env = std::getenv("KC_INSERT_PATH");
         int rc = ensure_part(c, syms, !(env && !std::strcmp(env, "exact")));
         if (rc) return rc;
-        HIPCHK(c, launch_count_partitioned(sv, syms, c->cfg.k, mode, tv, bv, c->d_ctr, c->pb, s));
+        HIPCHK(c, launch_count_partitioned(sv, syms, c->cfg.k, mode, tv, bv, c->d_ctr, c->pb, c->table_fresh, s));
     } else {
         HIPCHK(c, launch_count(sv, syms, c->cfg.k, mode, tv, bv, c->d_ctr, s));
     }
+    if (mode != 1) c->table_fresh = false;
     if (c->profiling) {
         HIPCHK(c, hipEventRecord(ev[3], s));
         c->ev_pending.push_back(ev);
@@ -682,7 +685,13 @@ int kc_insert_counts_device(kc_ctx* c, const uint64_t* recs, uint64_t n, void* s
         ev[3] = c->get_event();
         HIPCHK(c, hipEventRecord(ev[2], s));
     }
-    HIPCHK(c, launch_insert_counts(recs, n, table_view(c), c->d_ctr, s));
+    const bool part = use_partitioned(c, n);
+    if (part) {
+        rc = ensure_part(c, (n * (c->W + 1) + c->W - 1) / c->W, false);  // records are W + 1 words
+        if (rc) return rc;
+    }
+    HIPCHK(c, launch_insert_counts(recs, n, part, table_view(c), c->d_ctr, c->pb, c->table_fresh, s));
+    c->table_fresh = false;
     if (c->profiling) {
         HIPCHK(c, hipEventRecord(ev[3], s));
         c->ev_pending.push_back(ev);
@@ -716,7 +725,8 @@ int kc_insert_keys_device(kc_ctx* c, const uint64_t* keys, uint64_t n, void* sp)
         ev[3] = c->get_event();
         HIPCHK(c, hipEventRecord(ev[2], s));
     }
-    HIPCHK(c, launch_insert_keys(keys, n, part, table_view(c), c->d_ctr, c->pb, s));
+    HIPCHK(c, launch_insert_keys(keys, n, part, table_view(c), c->d_ctr, c->pb, c->table_fresh, s));
+    c->table_fresh = false;
     if (c->profiling) {
         HIPCHK(c, hipEventRecord(ev[3], s));
         c->ev_pending.push_back(ev);
@@ -778,7 +788,10 @@ int kc_reset(kc_ctx* c) {
     if (!c) return KC_ERR_ARG;
     int rc = kc_sync(c);
     if (rc) return rc;
-    if (c->d_table) HIPCHK(c, hipMemsetAsync(c->d_table, 0, c->nbuckets * BUCKET_WORDS * sizeof(uint64_t), c->stream));
+    if (c->d_table) {
+        HIPCHK(c, hipMemsetAsync(c->d_table, 0, c->nbuckets * BUCKET_WORDS * sizeof(uint64_t), c->stream));
+        c->table_fresh = true;
+    }
     if (c->d_bloom) {
         const uint64_t words = std::max<uint64_t>(1, (2 * c->bf_bits + 31) / 32);
         HIPCHK(c, hipMemsetAsync(c->d_bloom, 0, words * 4, c->stream));

@@ -516,7 +516,8 @@ __global__ __launch_bounds__(COUNT_THREADS, 4) void k_p1(PackedView sv, int k, B
 // blocks, bins = top f1bits of the table key.
 template <int W, bool SCATTER>
 __global__ __launch_bounds__(COUNT_THREADS, 4) void k_p1k(const uint64_t* __restrict__ in, uint64_t n, PartBufs pb,
-                                                       uint32_t F, BinBits bin, DevCounters* __restrict__ ctr) {
+                                                       uint32_t F, BinBits bin, DevCounters* __restrict__ ctr,
+                                                       int cnt_word) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int RUNW = run_w<W>(), TW = tile_win<W>();
     const PartLds l = part_lds(smem, F);
@@ -529,6 +530,7 @@ __global__ __launch_bounds__(COUNT_THREADS, 4) void k_p1k(const uint64_t* __rest
     }
     __syncthreads();
     uint32_t n_inv = 0;
+    unsigned long long added = 0;  // records (cnt_word >= 0): sum of their counts
     for (uint64_t t0 = lo; t0 < hi; t0 += TW) {
         uint64_t tk[RUNW][W];
         bool ok[RUNW];
@@ -538,7 +540,12 @@ __global__ __launch_bounds__(COUNT_THREADS, 4) void k_p1k(const uint64_t* __rest
 #pragma unroll
             for (int w = 0; w < W; w++) tk[q][w] = i < hi ? in[i * W + w] : 0;
             ok[q] = tk[q][0] != EMPTY;  // 0 is never a table key: skip (counted as invalid)
-            if constexpr (!SCATTER) n_inv += (i < hi) & !ok[q];
+            if constexpr (!SCATTER) {
+                n_inv += (i < hi) & !ok[q];
+#pragma unroll
+                for (int w = 0; w < W; w++)
+                    if (w == cnt_word && ok[q]) added += tk[q][w] & CNT_MASK;
+            }
         }
         if constexpr (SCATTER) {
             scatter_tile<W, RUNW>(l, F, bin, OutExact{}, tk, ok, pb.keys1);
@@ -551,7 +558,8 @@ __global__ __launch_bounds__(COUNT_THREADS, 4) void k_p1k(const uint64_t* __rest
     if constexpr (!SCATTER) {
         __syncthreads();
         for (uint32_t b = tid; b < F; b += COUNT_THREADS) pb.hist1[(uint64_t)b * pb.nblk1 + blockIdx.x] = l.hist[b];
-        block_add4(blockIdx.x == 0 && tid == 0 ? n : 0, n_inv, 0, 0, &ctr->inserted, &ctr->invalid, nullptr, nullptr);
+        if (cnt_word < 0) added = blockIdx.x == 0 && tid == 0 ? n : 0;
+        block_add4(added, n_inv, 0, 0, &ctr->inserted, &ctr->invalid, nullptr, nullptr);
     }
 }
 
@@ -576,6 +584,19 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_insert_keys(const uint64_t* _
 // shard merge (pre-aggregated sharding): a rank's table -> {table key, count} records
 // grouped by owner shard; the owner adds the counts into its own table.
 // --------------------------------------------------------------------------------
+// one 128-byte bucket into registers: eight 16-byte loads issued together
+DEV void load_bucket(const uint64_t* __restrict__ b, uint64_t (&bw)[BUCKET_WORDS]) {
+    const uint4* b4 = reinterpret_cast<const uint4*>(b);
+    uint4 v[BUCKET_WORDS / 2];
+#pragma unroll
+    for (int c = 0; c < BUCKET_WORDS / 2; c++) v[c] = b4[c];
+#pragma unroll
+    for (int c = 0; c < BUCKET_WORDS / 2; c++) {
+        bw[2 * c] = ((uint64_t)v[c].y << 32) | v[c].x;
+        bw[2 * c + 1] = ((uint64_t)v[c].w << 32) | v[c].z;
+    }
+}
+
 constexpr int RT_MAX_PARTS = 64;
 // SCATTER = false: per-block record counts per owner ([owner][block] into hist);
 // true: records {W table-key words, raw count} at off[owner][block] + rank.
@@ -593,19 +614,19 @@ __global__ __launch_bounds__(256) void k_route_table(TableView tv, uint32_t part
     __syncthreads();
     const uint64_t bkt = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (bkt < tv.nbuckets) {
-        const uint64_t* b = tv.buckets + bkt * BUCKET_WORDS;
+        uint64_t bw[BUCKET_WORDS];
+        load_bucket(tv.buckets + bkt * BUCKET_WORDS, bw);
 #pragma unroll
         for (int sl = 0; sl < S; sl++) {
-            const uint64_t t0 = b[sl * W];
+            const uint64_t t0 = bw[sl * W];
             if (t0 == EMPTY) continue;
             const uint32_t d = owner_of(t0, parts);
             const uint32_t r = atomicAdd(&s_cnt[d], 1u);
             if constexpr (SCATTER) {
                 uint64_t* o = out + (s_base[d] + r) * (W + 1);
-                o[0] = t0;
 #pragma unroll
-                for (int w = 1; w < W; w++) o[w] = b[sl * W + w];
-                o[W] = b[S * W + sl] & CNT_MASK;
+                for (int w = 0; w < W; w++) o[w] = bw[sl * W + w];
+                o[W] = bw[S * W + sl] & CNT_MASK;
             }
         }
     }
@@ -747,10 +768,15 @@ DEV uint64_t* lds_word(uint64_t* lt, uint32_t b, uint32_t word) {
 // SEG: the region's keys are the B2 level-2 segments (region, j) (fills in hist2);
 // otherwise the contiguous run [off2[r * B2], off2[(r + 1) * B2]).  A segmented launch
 // leaves the table alone when the batch overflowed; an exact one can be gated.
-template <int W, int NT, bool SEG>
-// two 64 KiB regions per CU: NT / 128 waves per SIMD must fit the register file
-__global__ __launch_bounds__(NT, NT / 128) void k_p3(TableView tv, PartBufs pb, DevCounters* __restrict__ ctr,
-                                           const unsigned long long* gate) {
+// CNT: items are {W key words, count} records (shard merge) and add their count.
+// fresh: the table is known to be all zero (just reset), so the region is not read.
+constexpr int P3_THREADS = 1024;  // two 64 KiB regions per CU: 8 waves per SIMD
+template <int W, bool SEG, bool CNT>
+__global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView tv, PartBufs pb,
+                                                                  DevCounters* __restrict__ ctr,
+                                                                  const unsigned long long* gate, int fresh) {
+    constexpr int NT = P3_THREADS;
+    constexpr int IW = CNT ? W + 1 : W;  // words per item
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ uint32_t s_pre[65];  // SEG: exclusive prefix of the B2 (<= 64) segment fills
     constexpr int S = BUCKET_WORDS / (W + 1);
@@ -785,12 +811,17 @@ __global__ __launch_bounds__(NT, NT / 128) void k_p3(TableView tv, PartBufs pb, 
     uint4* g4 = reinterpret_cast<uint4*>(tv.buckets + r * BPR * BUCKET_WORDS);
     uint4* l4 = reinterpret_cast<uint4*>(lt);
     constexpr int N4 = BPR * BUCKET_WORDS / 2;
-    for (int i = threadIdx.x; i < N4; i += NT) l4[lds_chunk(i >> 3, i & 7)] = g4[i];
+    if (fresh) {
+        for (int i = threadIdx.x; i < N4; i += NT) l4[i] = make_uint4(0, 0, 0, 0);
+    } else {
+        for (int i = threadIdx.x; i < N4; i += NT) l4[lds_chunk(i >> 3, i & 7)] = g4[i];
+    }
     __syncthreads();
     uint32_t n_fail = 0;
     uint32_t cs = 0;  // SEG: segment cursor of this thread (indices grow monotonically)
     for (uint64_t base = start; base < end; base += (uint64_t)KB * NT) {
         uint64_t kk[KB][W];
+        uint64_t add[KB];
 #pragma unroll
         for (int q = 0; q < KB; q++) {
             const uint64_t i = base + threadIdx.x + (uint64_t)q * NT;
@@ -798,13 +829,15 @@ __global__ __launch_bounds__(NT, NT / 128) void k_p3(TableView tv, PartBufs pb, 
             if (i < end) {
                 if constexpr (SEG) {
                     while (s_pre[cs + 1] <= i) cs++;
-                    src = pb.keys2 + ((r * pb.B2 + cs) * pb.cap2 + (i - s_pre[cs])) * W;
+                    src = pb.keys2 + ((r * pb.B2 + cs) * pb.cap2 + (i - s_pre[cs])) * IW;
                 } else {
-                    src = pb.keys2 + i * W;
+                    src = pb.keys2 + i * IW;
                 }
             }
 #pragma unroll
             for (int w = 0; w < W; w++) kk[q][w] = src ? src[w] : 0;
+            if constexpr (CNT) add[q] = src ? src[W] & CNT_MASK : 0;
+            else add[q] = 1;
         }
 #pragma unroll
         for (int q = 0; q < KB; q++) {
@@ -834,7 +867,8 @@ __global__ __launch_bounds__(NT, NT / 128) void k_p3(TableView tv, PartBufs pb, 
                         else { probe++; continue; }  // lost the slot to another key: re-read this bucket
                     }
                     if (slot >= 0) {
-                        atomicAdd(reinterpret_cast<unsigned long long*>(lds_word(lt, b, S + slot)), 1ULL);
+                        atomicAdd(reinterpret_cast<unsigned long long*>(lds_word(lt, b, S + slot)),
+                                  (unsigned long long)add[q]);
                         done = true;
                     } else {
                         b = (b + 1) & (BPR - 1);
@@ -877,7 +911,7 @@ __global__ __launch_bounds__(NT, NT / 128) void k_p3(TableView tv, PartBufs pb, 
                     }
                     if (eqm) {
                         atomicAdd(reinterpret_cast<unsigned long long*>(lds_word(lt, b, S * W + __builtin_ctz(eqm))),
-                                  1ULL);
+                                  (unsigned long long)add[q]);
                         done = true;
                     } else if (pend) {
                         probe++;  // another wave is publishing a key with this word 0: read again
@@ -892,7 +926,7 @@ __global__ __launch_bounds__(NT, NT / 128) void k_p3(TableView tv, PartBufs pb, 
                                                    __HIP_MEMORY_SCOPE_WORKGROUP);
                             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                             atomicAdd(reinterpret_cast<unsigned long long*>(lds_word(lt, b, S * W + e)),
-                                      (unsigned long long)(READY + 1));
+                                      (unsigned long long)(READY + add[q]));
                             done = true;
                         } else {
                             probe++;  // lost the slot: read the bucket again
@@ -999,14 +1033,15 @@ __global__ __launch_bounds__(256) void k_dump(TableView tv, int count_mode, uint
     uint32_t occ = 0, nout = 0;
     uint64_t tv_c[S];
     bool emit[S];
-    const uint64_t* b = tv.buckets + bkt * BUCKET_WORDS;
+    uint64_t bw[BUCKET_WORDS];
+    if (bkt < tv.nbuckets) load_bucket(tv.buckets + bkt * BUCKET_WORDS, bw);
 #pragma unroll
     for (int s = 0; s < S; s++) {
         emit[s] = false;
         tv_c[s] = 0;
-        if (bkt < tv.nbuckets && b[s * W] != EMPTY) {
+        if (bkt < tv.nbuckets && bw[s * W] != EMPTY) {
             occ++;
-            const uint64_t c = b[S * W + s] & CNT_MASK;
+            const uint64_t c = bw[S * W + s] & CNT_MASK;
             const uint64_t t = count_mode == 0 ? (c & 0xFFFF) : (c < 16383 ? c : 16383);
             if (t >= min_abundance) { emit[s] = true; tv_c[s] = t; nout++; }
         }
@@ -1023,7 +1058,7 @@ __global__ __launch_bounds__(256) void k_dump(TableView tv, int count_mode, uint
         if (out && emit[s]) {
             uint64_t t[W], key[W];
 #pragma unroll
-            for (int i = 0; i < W; i++) t[i] = b[s * W + i];
+            for (int i = 0; i < W; i++) t[i] = bw[s * W + i];
             from_tkey<W>(t, key);
             uint64_t* o = out + idx * (W + 1);
 #pragma unroll
@@ -1081,37 +1116,31 @@ static hipError_t set_smem(K kernel, size_t bytes) {
 
 static BinBits coarse_bins(const TableView& t) { return BinBits{t.f1bits ? 64 - t.f1bits : 63, t.F1 - 1}; }
 
-static int p3_threads() {
-    static const int nt = [] {
-        const char* v = std::getenv("KC_P3_THREADS");  // tuning knob: 256 / 512 / 1024
-        return v ? std::atoi(v) : 1024;
-    }();
-    return nt;
-}
-template <int W, bool SEG>
-static hipError_t launch_p3(TableView t, DevCounters* ctr, PartBufs pb, const unsigned long long* gate,
+template <int W, bool SEG, bool CNT = false>
+static hipError_t launch_p3(TableView t, DevCounters* ctr, PartBufs pb, const unsigned long long* gate, int fresh,
                             hipStream_t s) {
     const size_t sm3 = (size_t)BPR * BUCKET_WORDS * 8;
-    const int nt = p3_threads();
-    auto p3 = nt == 256 ? k_p3<W, 256, SEG> : (nt == 512 ? k_p3<W, 512, SEG> : k_p3<W, 1024, SEG>);
+    auto p3 = k_p3<W, SEG, CNT>;
     hipError_t e = set_smem(p3, sm3);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(p3, dim3((unsigned)t.R), dim3((unsigned)nt), sm3, s, t, pb, ctr, gate);
+    hipLaunchKernelGGL(p3, dim3((unsigned)t.R), dim3(P3_THREADS), sm3, s, t, pb, ctr, gate, fresh);
     return hipGetLastError();
 }
 
-// levels 2 and 3 on the exact layout (after an exact level 1); `gate` as in k_p1
-template <int W>
+// levels 2 and 3 on the exact layout (after an exact level 1); `gate` as in k_p1.
+// CNT: the items are {W key words, count} records (W + 1 words each).
+template <int W, bool CNT = false>
 static hipError_t part_levels23(TableView t, DevCounters* ctr, PartBufs pb, hipStream_t s,
-                                const unsigned long long* gate = nullptr) {
-    const size_t sm2 = part_smem<W>(t.F2), sm2h = hist_smem(t.F2);
+                                const unsigned long long* gate = nullptr, int fresh = 0) {
+    constexpr int IW = CNT ? W + 1 : W;
+    const size_t sm2 = part_smem<IW>(t.F2), sm2h = hist_smem(t.F2);
     hipError_t e;
-    if ((e = set_smem(k_p2<W, false>, sm2h)) != hipSuccess) return e;
-    if ((e = set_smem(k_p2<W, true>, sm2)) != hipSuccess) return e;
-    hipLaunchKernelGGL((k_p2<W, false>), dim3(t.F1 * pb.B2), dim3(COUNT_THREADS), sm2h, s, t, pb, gate);
+    if ((e = set_smem(k_p2<IW, false>, sm2h)) != hipSuccess) return e;
+    if ((e = set_smem(k_p2<IW, true>, sm2)) != hipSuccess) return e;
+    hipLaunchKernelGGL((k_p2<IW, false>), dim3(t.F1 * pb.B2), dim3(COUNT_THREADS), sm2h, s, t, pb, gate);
     launch_scan(pb.hist2, t.R * pb.B2, pb.off2, pb.bsum, s, gate);
-    hipLaunchKernelGGL((k_p2<W, true>), dim3(t.F1 * pb.B2), dim3(COUNT_THREADS), sm2, s, t, pb, gate);
-    return launch_p3<W, false>(t, ctr, pb, gate, s);
+    hipLaunchKernelGGL((k_p2<IW, true>), dim3(t.F1 * pb.B2), dim3(COUNT_THREADS), sm2, s, t, pb, gate);
+    return launch_p3<W, false, CNT>(t, ctr, pb, gate, fresh, s);
 }
 
 // level 1 from the symbol stream, exact layout: windows -> F bins by `bin`, keys into `out`
@@ -1140,11 +1169,11 @@ static hipError_t part_level1(PackedView sym, int k, BloomView bf, DevCounters* 
 // segment overflowed, in which case the segmented p3 left the table untouched).
 template <int W, int MODE>
 static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf, DevCounters* ctr, PartBufs pb,
-                                hipStream_t s) {
+                                int fresh, hipStream_t s) {
     if (pb.cap1 == 0) {
         hipError_t e = part_level1<W, MODE>(sym, k, bf, ctr, pb, t.F1, coarse_bins(t), pb.keys1, s);
         if (e != hipSuccess) return e;
-        return part_levels23<W>(t, ctr, pb, s);
+        return part_levels23<W>(t, ctr, pb, s, nullptr, fresh);
     }
     hipError_t e;
     const unsigned long long* gate = &ctr->part_overflow;
@@ -1158,21 +1187,21 @@ static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf
     hipLaunchKernelGGL(k1, dim3(pb.nblk1), dim3(COUNT_THREADS), sm1, s, sym, k, bf, ctr, pb, t.F1, coarse_bins(t),
                        pb.keys1, pk, pkm1, o1, (const unsigned long long*)nullptr, 1);
     hipLaunchKernelGGL(k_p2f<W>, dim3(t.F1 * pb.B2), dim3(COUNT_THREADS), sm2, s, t, pb, ctr);
-    if ((e = launch_p3<W, true>(t, ctr, pb, nullptr, s)) != hipSuccess) return e;
+    if ((e = launch_p3<W, true>(t, ctr, pb, nullptr, fresh, s)) != hipSuccess) return e;
     if ((e = part_level1<W, MODE>(sym, k, bf, ctr, pb, t.F1, coarse_bins(t), pb.keys1, s, gate)) != hipSuccess)
         return e;
-    return part_levels23<W>(t, ctr, pb, s, gate);
+    return part_levels23<W>(t, ctr, pb, s, gate, fresh);
 }
 
 hipError_t launch_count_partitioned(PackedView sym, uint64_t sym_bound, int k, int mode, TableView t,
-                                    BloomView bf, DevCounters* ctr, PartBufs pb, hipStream_t s) {
+                                    BloomView bf, DevCounters* ctr, PartBufs pb, int fresh, hipStream_t s) {
     (void)sym_bound;
     const bool gate = mode == 2;
     switch (t.W) {
-    case 1: return gate ? launch_part_w<1, 2>(sym, k, t, bf, ctr, pb, s) : launch_part_w<1, 0>(sym, k, t, bf, ctr, pb, s);
-    case 2: return gate ? launch_part_w<2, 2>(sym, k, t, bf, ctr, pb, s) : launch_part_w<2, 0>(sym, k, t, bf, ctr, pb, s);
-    case 3: return gate ? launch_part_w<3, 2>(sym, k, t, bf, ctr, pb, s) : launch_part_w<3, 0>(sym, k, t, bf, ctr, pb, s);
-    case 4: return gate ? launch_part_w<4, 2>(sym, k, t, bf, ctr, pb, s) : launch_part_w<4, 0>(sym, k, t, bf, ctr, pb, s);
+    case 1: return gate ? launch_part_w<1, 2>(sym, k, t, bf, ctr, pb, fresh, s) : launch_part_w<1, 0>(sym, k, t, bf, ctr, pb, fresh, s);
+    case 2: return gate ? launch_part_w<2, 2>(sym, k, t, bf, ctr, pb, fresh, s) : launch_part_w<2, 0>(sym, k, t, bf, ctr, pb, fresh, s);
+    case 3: return gate ? launch_part_w<3, 2>(sym, k, t, bf, ctr, pb, fresh, s) : launch_part_w<3, 0>(sym, k, t, bf, ctr, pb, fresh, s);
+    case 4: return gate ? launch_part_w<4, 2>(sym, k, t, bf, ctr, pb, fresh, s) : launch_part_w<4, 0>(sym, k, t, bf, ctr, pb, fresh, s);
     default: return hipErrorInvalidValue;
     }
 }
@@ -1195,33 +1224,44 @@ hipError_t launch_route(PackedView sym, int k, int W, DevCounters* ctr, PartBufs
     }
 }
 
-// Insert an array of table keys (e.g. received from other shards).
+// Insert an array of table keys (e.g. received from other shards), or, CNT, of
+// {W key words, count} records (shard merge), partitioned through the exact pipeline.
+template <int W, bool CNT>
+static hipError_t insert_items_part(const uint64_t* items, uint64_t n, TableView t, DevCounters* ctr, PartBufs pb,
+                                    int fresh, hipStream_t s) {
+    constexpr int IW = CNT ? W + 1 : W;
+    const BinBits bin = coarse_bins(t);
+    const size_t sm1 = part_smem<IW>(t.F1), sm1h = hist_smem(t.F1);
+    hipError_t e;
+    if ((e = set_smem(k_p1k<IW, false>, sm1h)) != hipSuccess) return e;
+    if ((e = set_smem(k_p1k<IW, true>, sm1)) != hipSuccess) return e;
+    const int cw = CNT ? W : -1;
+    hipLaunchKernelGGL((k_p1k<IW, false>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1h, s, items, n, pb, t.F1, bin, ctr,
+                       cw);
+    launch_scan(pb.hist1, (uint64_t)t.F1 * pb.nblk1, pb.off1, pb.bsum, s);
+    hipLaunchKernelGGL((k_p1k<IW, true>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1, s, items, n, pb, t.F1, bin, ctr,
+                       cw);
+    return part_levels23<W, CNT>(t, ctr, pb, s, nullptr, fresh);
+}
+
 template <int W>
 static hipError_t insert_keys_w(const uint64_t* keys, uint64_t n, bool partitioned, TableView t, DevCounters* ctr,
-                                PartBufs pb, hipStream_t s) {
+                                PartBufs pb, int fresh, hipStream_t s) {
     if (n == 0) return hipSuccess;
     if (!partitioned) {
         hipLaunchKernelGGL((k_insert_keys<W>), dim3((unsigned)((n + COUNT_THREADS - 1) / COUNT_THREADS)),
                            dim3(COUNT_THREADS), 0, s, keys, n, t, ctr);
         return hipGetLastError();
     }
-    const BinBits bin = coarse_bins(t);
-    const size_t sm1 = part_smem<W>(t.F1), sm1h = hist_smem(t.F1);
-    hipError_t e;
-    if ((e = set_smem(k_p1k<W, false>, sm1h)) != hipSuccess) return e;
-    if ((e = set_smem(k_p1k<W, true>, sm1)) != hipSuccess) return e;
-    hipLaunchKernelGGL((k_p1k<W, false>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1h, s, keys, n, pb, t.F1, bin, ctr);
-    launch_scan(pb.hist1, (uint64_t)t.F1 * pb.nblk1, pb.off1, pb.bsum, s);
-    hipLaunchKernelGGL((k_p1k<W, true>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1, s, keys, n, pb, t.F1, bin, ctr);
-    return part_levels23<W>(t, ctr, pb, s);
+    return insert_items_part<W, false>(keys, n, t, ctr, pb, fresh, s);
 }
 hipError_t launch_insert_keys(const uint64_t* keys, uint64_t n, bool partitioned, TableView t, DevCounters* ctr,
-                              PartBufs pb, hipStream_t s) {
+                              PartBufs pb, int fresh, hipStream_t s) {
     switch (t.W) {
-    case 1: return insert_keys_w<1>(keys, n, partitioned, t, ctr, pb, s);
-    case 2: return insert_keys_w<2>(keys, n, partitioned, t, ctr, pb, s);
-    case 3: return insert_keys_w<3>(keys, n, partitioned, t, ctr, pb, s);
-    case 4: return insert_keys_w<4>(keys, n, partitioned, t, ctr, pb, s);
+    case 1: return insert_keys_w<1>(keys, n, partitioned, t, ctr, pb, fresh, s);
+    case 2: return insert_keys_w<2>(keys, n, partitioned, t, ctr, pb, fresh, s);
+    case 3: return insert_keys_w<3>(keys, n, partitioned, t, ctr, pb, fresh, s);
+    case 4: return insert_keys_w<4>(keys, n, partitioned, t, ctr, pb, fresh, s);
     default: return hipErrorInvalidValue;
     }
 }
@@ -1248,8 +1288,18 @@ hipError_t launch_route_table(TableView t, uint32_t parts, uint32_t* hist, uint6
     }
 }
 
-hipError_t launch_insert_counts(const uint64_t* rec, uint64_t n, TableView t, DevCounters* ctr, hipStream_t s) {
+hipError_t launch_insert_counts(const uint64_t* rec, uint64_t n, bool partitioned, TableView t, DevCounters* ctr,
+                                PartBufs pb, int fresh, hipStream_t s) {
     if (n == 0) return hipSuccess;
+    if (partitioned) {
+        switch (t.W) {
+        case 1: return insert_items_part<1, true>(rec, n, t, ctr, pb, fresh, s);
+        case 2: return insert_items_part<2, true>(rec, n, t, ctr, pb, fresh, s);
+        case 3: return insert_items_part<3, true>(rec, n, t, ctr, pb, fresh, s);
+        case 4: return insert_items_part<4, true>(rec, n, t, ctr, pb, fresh, s);
+        default: return hipErrorInvalidValue;
+        }
+    }
     const dim3 grid((unsigned)((n + COUNT_THREADS - 1) / COUNT_THREADS));
     switch (t.W) {
     case 1: hipLaunchKernelGGL(k_insert_counts<1>, grid, dim3(COUNT_THREADS), 0, s, rec, n, t, ctr); break;

@@ -119,20 +119,22 @@ hipError_t launch_tokenize(const uint8_t* stage, uint64_t ntiles, const ChunkDes
 hipError_t launch_count(PackedView sv, uint64_t sym_bound, int k, int mode, TableView t, BloomView bf,
                         DevCounters* ctr, hipStream_t s);
 // partitioned insert for modes 0 and 2 (same table, same result as launch_count)
+// fresh: the table is all zero (just allocated or reset): level 3 does not read it
 hipError_t launch_count_partitioned(PackedView sv, uint64_t sym_bound, int k, int mode, TableView t,
-                                    BloomView bf, DevCounters* ctr, PartBufs pb, hipStream_t s);
+                                    BloomView bf, DevCounters* ctr, PartBufs pb, int fresh, hipStream_t s);
 int run_width(int W);  // windows rolled per thread in the partitioned kernels
 // hash-prefix sharding: windows -> table keys grouped by owner (offsets in pb.off1)
 hipError_t launch_route(PackedView sym, int k, int W, DevCounters* ctr, PartBufs pb, uint32_t parts, uint64_t* out,
                         hipStream_t s);
 // insert an array of table keys into this shard's table
 hipError_t launch_insert_keys(const uint64_t* keys, uint64_t n, bool partitioned, TableView t, DevCounters* ctr,
-                              PartBufs pb, hipStream_t s);
+                              PartBufs pb, int fresh, hipStream_t s);
 // pre-aggregated sharding: out == nullptr -> per-(owner, block) record counts into hist and
 // their exclusive scan into off (off[parts * nblk] = total); else scatter the records
 hipError_t launch_route_table(TableView t, uint32_t parts, uint32_t* hist, uint64_t* off, uint64_t* bsum,
                               uint64_t* out, hipStream_t s);
-hipError_t launch_insert_counts(const uint64_t* rec, uint64_t n, TableView t, DevCounters* ctr, hipStream_t s);
+hipError_t launch_insert_counts(const uint64_t* rec, uint64_t n, bool partitioned, TableView t, DevCounters* ctr,
+                                PartBufs pb, int fresh, hipStream_t s);
 hipError_t launch_dump(TableView t, int count_mode, uint64_t min_abundance, uint64_t* out, DevCounters* ctr,
                        hipStream_t s);
 hipError_t launch_synth(uint8_t* dst, uint64_t first_read, uint64_t n_reads, uint64_t seed, uint64_t genome_len,

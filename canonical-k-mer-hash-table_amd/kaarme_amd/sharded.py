@@ -44,6 +44,8 @@ def exchange(dist, keys, counts: Sequence[int], W: int, group=None, chunk_words:
 
     dev = keys.device
     world = len(counts)
+    if world == 1:  # nothing leaves the rank
+        return keys, int(counts[0])
     send_counts = torch.tensor(list(counts), dtype=torch.int64, device=dev)
     recv_counts = torch.empty_like(send_counts)
     dist.all_to_all_single(recv_counts, send_counts, group=group)
@@ -134,12 +136,19 @@ class DeviceEngine:
     def route_table(self, parts: int, stream: int = 0):
         import torch
 
+        from . import KcError
+
+        R = self.W + 1
+        if self._rec is not None:
+            try:  # the usual case: the buffer of the previous merge is large enough
+                return self._rec, self.kc.route_table_device(parts, self._rec.data_ptr(), self._rec.numel() // R,
+                                                             stream)
+            except KcError:
+                pass
         counts = self.kc.route_table_device(parts, 0, 0, stream)  # record counts per owner
-        need = max(1, sum(counts)) * (self.W + 1)
-        if self._rec is None or self._rec.numel() < need:
-            self._rec = torch.empty(need + need // 8, dtype=torch.int64, device="cuda")
-        counts = self.kc.route_table_device(parts, self._rec.data_ptr(), self._rec.numel() // (self.W + 1), stream)
-        return self._rec, counts
+        need = max(1, sum(counts)) * R
+        self._rec = torch.empty(need + need // 4, dtype=torch.int64, device="cuda")
+        return self._rec, self.kc.route_table_device(parts, self._rec.data_ptr(), self._rec.numel() // R, stream)
 
     def owner_table(self) -> KmerCounter:
         if self.owner is None:

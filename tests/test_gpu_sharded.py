@@ -90,12 +90,14 @@ def test_insert_rejects_non_table_keys(monkeypatch, path):
         e.kc.finish()
 
 
+@pytest.mark.parametrize("path", ["direct", "partitioned"])
 @pytest.mark.parametrize("k,mode,G", [(31, 2, 2), (31, 0, 3), (51, 2, 4), (63, 1, 2), (127, 0, 2)])
-def test_preaggregated_merge_union(tmp_path, k, mode, G):
+def test_preaggregated_merge_union(tmp_path, monkeypatch, k, mode, G, path):
     """Pre-aggregated sharding (ShardedCounter's path): each emulated rank counts its own
     reads locally, routes its table as {key, count} records by owner, and every owner adds
     the records it receives; the owners' outputs are disjoint and their union is the
     oracle's count of the whole input (transforms applied to the merged counts)."""
+    monkeypatch.setenv("KC_INSERT_PATH", path)  # local counting and the merge insert
     n_reads = 20000
     per = n_reads // G
     images = []
