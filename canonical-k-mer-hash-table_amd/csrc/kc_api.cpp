@@ -264,7 +264,9 @@ static hipStream_t pick_stream(kc_ctx* c, void* s) {
 // ------------------------------------------------------------------------------
 // batch execution
 // ------------------------------------------------------------------------------
-static int run_batch(kc_ctx* c, uint64_t used, uint64_t nchunks, int fmt, int pass, hipStream_t s,
+// src: the bytes the chunk descriptors' src_off point into (the host stage, or a
+// device-resident image read in place)
+static int run_batch(kc_ctx* c, const uint8_t* src, uint64_t used, uint64_t nchunks, int fmt, int pass, hipStream_t s,
                      hipEvent_t ev_start = nullptr, hipEvent_t ev_gather = nullptr) {
     const uint64_t ntiles = used / TILE;
     if (ntiles == 0) return KC_OK;
@@ -280,8 +282,8 @@ static int run_batch(kc_ctx* c, uint64_t used, uint64_t nchunks, int fmt, int pa
         ev[3] = c->get_event();
     }
     const PackedView sv{c->d_pk, c->d_bk};
-    HIPCHK(c, launch_tokenize(c->d_stage, ntiles, c->d_chunks, (int)nchunks, fmt, c->d_tiles, c->d_touts, c->d_tblk,
-                              sv, used + nchunks, c->d_ctr, s));
+    HIPCHK(c, launch_tokenize(src, ntiles, c->d_chunks, (int)nchunks, fmt, c->d_tiles, c->d_touts, c->d_tblk, sv,
+                              used + nchunks, c->d_ctr, s));
     if (c->profiling) HIPCHK(c, hipEventRecord(ev[2], s));
     TableView tv = table_view(c);
     BloomView bv{c->d_bloom, c->bf_bits ? c->bf_bits - 1 : 0, c->nh, c->nh_gate};
@@ -313,7 +315,7 @@ static int flush_host(kc_ctx* c) {
     HIPCHK(c, hipMemcpyAsync(c->d_chunks, c->h_desc[b], c->cur_n * sizeof(ChunkDesc), hipMemcpyHostToDevice,
                              c->stream));
     HIPCHK(c, hipEventRecord(c->h_free[b], c->stream));
-    int rc = run_batch(c, c->cur_used, c->cur_n, c->cur_fmt, c->cur_pass, c->stream);
+    int rc = run_batch(c, c->d_stage, c->cur_used, c->cur_n, c->cur_fmt, c->cur_pass, c->stream);
     if (rc) return rc;
     c->cur ^= 1;
     c->cur_used = 0;
@@ -335,7 +337,7 @@ static int add_host_chunk(kc_ctx* c, const uint8_t* buf, size_t len, int fmt, in
         if (rc) return rc;
     }
     ChunkDesc d;
-    d.src_off = 0;
+    d.src_off = c->cur_used;  // host chunks are tokenized from the stage itself
     d.stage_off = c->cur_used;
     d.len = len;
     d.bh = bh ? 1 : 0;
@@ -374,9 +376,9 @@ static int device_pass(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, si
             e1 = c->get_event();
             HIPCHK(c, hipEventRecord(e0, s));
         }
-        HIPCHK(c, launch_gather(img, c->d_stage, c->d_chunks, (int)batch.size(), batch.data(), s));
+        // the image is tokenized in place (no gather into the stage): "gather" is ~0
         if (c->profiling) HIPCHK(c, hipEventRecord(e1, s));
-        int r = run_batch(c, used, batch.size(), fmt, pass, s, e0, e1);
+        int r = run_batch(c, img, used, batch.size(), fmt, pass, s, e0, e1);
         if (r) return r;
         HIPCHK(c, hipEventSynchronize(c->h_free[c->cur]));
         batch.clear();
@@ -594,10 +596,9 @@ int kc_route_device(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, size_
     if (c->profiling) HIPCHK(c, hipEventRecord(ev[0], s));
     std::memcpy(c->h_desc[c->cur], batch.data(), batch.size() * sizeof(ChunkDesc));
     HIPCHK(c, hipMemcpyAsync(c->d_chunks, c->h_desc[c->cur], batch.size() * sizeof(ChunkDesc), hipMemcpyHostToDevice, s));
-    HIPCHK(c, launch_gather(img, c->d_stage, c->d_chunks, (int)batch.size(), batch.data(), s));
     if (c->profiling) HIPCHK(c, hipEventRecord(ev[1], s));
     const PackedView sv{c->d_pk, c->d_bk};
-    HIPCHK(c, launch_tokenize(c->d_stage, used / TILE, c->d_chunks, (int)batch.size(), fmt, c->d_tiles, c->d_touts,
+    HIPCHK(c, launch_tokenize(img, used / TILE, c->d_chunks, (int)batch.size(), fmt, c->d_tiles, c->d_touts,
                               c->d_tblk, sv, syms, c->d_ctr, s));
     if (c->profiling) HIPCHK(c, hipEventRecord(ev[2], s));
     HIPCHK(c, launch_route(sv, c->cfg.k, c->W, c->d_ctr, c->pb, nshards, dev_out, s));

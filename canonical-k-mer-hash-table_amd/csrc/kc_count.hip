@@ -704,9 +704,10 @@ __global__ __launch_bounds__(COUNT_THREADS, 4) void k_p2(TableView tv, PartBufs 
 // (block = c * B2 + j) -> segments (c * F2 + region, j) of capacity cap2, one pass.
 // The input segments are read as one virtual run (exclusive prefix of their fills in
 // LDS; each thread walks a monotone segment cursor).
-constexpr uint32_t P2F_MAX_SEG = 2048;  // nblk1 <= 2048
+// LDS: the scatter's arrays plus the segment-fill prefix (a level-2 workgroup reads
+// ceil(nblk1 / B2) level-1 segments)
 template <int W>
-constexpr size_t p2f_smem(uint32_t F) { return part_smem<W>(F) + (P2F_MAX_SEG + 1) * 4; }
+constexpr size_t p2f_smem(uint32_t F, uint32_t nseg_max) { return part_smem<W>(F) + (size_t)(nseg_max + 1) * 4; }
 
 template <int W>
 __global__ __launch_bounds__(COUNT_THREADS, 4) void k_p2f(TableView tv, PartBufs pb, DevCounters* __restrict__ ctr) {
@@ -1180,7 +1181,12 @@ static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf
     if ((e = hipMemsetAsync(&ctr->part_overflow, 0, sizeof(ctr->part_overflow), s)) != hipSuccess) return e;
     const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
     auto k1 = k_p1<W, MODE, true, BinBits, OutSeg>;
-    const size_t sm1 = part_smem<W>(t.F1), sm2 = p2f_smem<W>(t.F2);
+    static const uint32_t p2f_pad = [] {  // A/B knob: reserve LDS as if for this many segments
+        const char* v = std::getenv("KC_P2F_SEGS");
+        return v ? (uint32_t)std::atoi(v) : 0u;
+    }();
+    const size_t sm1 = part_smem<W>(t.F1),
+                 sm2 = p2f_smem<W>(t.F2, std::max<uint32_t>(p2f_pad, (pb.nblk1 + pb.B2 - 1) / pb.B2));
     if ((e = set_smem(k1, sm1)) != hipSuccess) return e;
     if ((e = set_smem(k_p2f<W>, sm2)) != hipSuccess) return e;
     const OutSeg o1{(uint64_t)pb.nblk1 * pb.cap1, 0, pb.cap1};

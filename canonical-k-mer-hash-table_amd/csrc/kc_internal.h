@@ -41,7 +41,8 @@ struct TileInfo {           // written by k_tile_summary, consumed by k_tile_sca
     uint8_t first;          // tile starts a chunk
     uint8_t bh;             // chunk's broken_header (only meaningful when first)
     uint8_t pad;
-    uint32_t pad2;
+    uint32_t avail;         // readable chunk bytes from the tile start (capped at TILE + 64)
+    uint64_t src;           // source offset of the tile's first byte
 };
 
 struct TileOut {            // written by the tile scan (per tile: block-local; per 1024-tile block: prefix)
@@ -110,9 +111,8 @@ inline int words_for_k(int k) { return k / 32 + 1; }          // spare top bit f
 inline int slots_per_bucket(int W) { return BUCKET_WORDS / (W + 1); }
 
 // ---- launchers (kc_tokenize.hip, kc_count.hip) -------------------------------------------------
-hipError_t launch_gather(const uint8_t* src, uint8_t* stage, const ChunkDesc* d_chunks, int n_chunks,
-                         const ChunkDesc* h_chunks, hipStream_t s);
-hipError_t launch_tokenize(const uint8_t* stage, uint64_t ntiles, const ChunkDesc* d_chunks, int n_chunks,
+// src: bytes the chunk descriptors' src_off point into (host stage or device image)
+hipError_t launch_tokenize(const uint8_t* src, uint64_t ntiles, const ChunkDesc* d_chunks, int n_chunks,
                            int fmt, TileInfo* tiles, TileOut* touts, TileOut* tblk, PackedView sv,
                            uint64_t sym_bound, DevCounters* ctr, hipStream_t s);
 // mode: 0 count all windows, 1 Bloom pass 1, 2 count windows passing the Bloom gate

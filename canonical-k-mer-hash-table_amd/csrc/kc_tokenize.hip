@@ -1,6 +1,5 @@
 // kc_tokenize.hip -- bytes -> symbol stream, and the device read generator.
 //
-//   k_gather        device-resident source image -> TILE-aligned chunk stage
 //   k_tile_summary  per 4 KiB tile: FASTA newline count + last header marker
 //   k_tscan_*       two-level scan: stream offsets + header state entering each tile
 //   k_emit          per tile: bytes -> symbol codes (0..3 base, 4 break); FASTA
@@ -17,38 +16,47 @@
 #include "kc_synth.h"
 
 namespace kc {
-// --------------------------------------------------------------------------------
-// k_gather: copy chunks of a device-resident source image into the TILE-aligned stage
-// (the device twin of the host's memcpy into pinned staging).
-// --------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_gather(const uint8_t* __restrict__ src, uint8_t* __restrict__ stage,
-                                                const ChunkDesc* __restrict__ chunks) {
-    const ChunkDesc c = chunks[blockIdx.y];
-    const uint64_t per_block = 16 * 256 * 4;
-    uint64_t base = (uint64_t)blockIdx.x * per_block;
-    if (base >= c.len) return;
-    const uint8_t* s = src + c.src_off;
-    uint8_t* d = stage + c.stage_off;
-    const bool aligned = ((c.src_off & 15) == 0);
-    for (int r = 0; r < 4; r++) {
-        uint64_t off = base + (uint64_t)r * 4096 + threadIdx.x * 16;
-        if (off + 16 <= c.len) {
-            if (aligned) {
-                *reinterpret_cast<uint4*>(d + off) = *reinterpret_cast<const uint4*>(s + off);
-            } else {
-                uint4 v;
-                uint8_t* pv = reinterpret_cast<uint8_t*>(&v);
+// ---- 16 source bytes per thread, as four little-endian words ----------------------
+// The tile's bytes are read straight from the source (device image or host stage) at
+// the chunk's offset, which has any alignment: five aligned dwords are funnel-shifted.
+// The fast path needs 3 readable bytes past the 16 (still inside the chunk), so the
+// last few bytes of a chunk take the byte path and nothing is read past a chunk.
+DEV void load16(const uint8_t* __restrict__ p, uint32_t vh, uint32_t (&w)[4]) {
+    if (vh >= 19) {
+        const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+        const uint32_t sh = (uint32_t)(a & 3);
+        uint32_t x[5];
 #pragma unroll
-                for (int j = 0; j < 16; j++) pv[j] = s[off + j];
-                *reinterpret_cast<uint4*>(d + off) = v;
-            }
-        } else {
-            for (uint64_t j = off; j < c.len && j < off + 16; j++) d[j] = s[j];
+        for (int i = 0; i < 5; i++) x[i] = q[i];
+#pragma unroll
+        for (int i = 0; i < 4; i++) w[i] = __builtin_amdgcn_alignbyte(x[i + 1], x[i], sh);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                if ((uint32_t)(4 * i + j) < vh) v |= (uint32_t)p[4 * i + j] << (8 * j);
+            w[i] = v;
         }
     }
 }
 
-// chunk owning tile t (chunks sorted by stage_off, tiles contiguous)
+// ---- SWAR byte classification ------------------------------------------------------
+DEV uint32_t zero_bytes(uint32_t v) {  // 0x80 in exactly the bytes of v that are 0
+    const uint32_t t = (v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+    return ~(t | v | 0x7F7F7F7Fu);
+}
+DEV uint32_t flags4(uint32_t z) { return ((z >> 7) * 0x10204080u) >> 28; }  // bit i = byte i's 0x80
+DEV uint32_t eq_mask16(const uint32_t (&w)[4], uint32_t pat) {  // bit j: byte j == pattern byte
+    uint32_t m = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) m |= flags4(zero_bytes(w[i] ^ pat)) << (4 * i);
+    return m;
+}
+
+// chunk owning stage position pos (chunks sorted by stage_off, tiles contiguous)
 DEV int find_chunk(const ChunkDesc* __restrict__ chunks, int n, uint64_t pos) {
     int lo = 0, hi = n - 1;
     while (lo < hi) {
@@ -58,46 +66,35 @@ DEV int find_chunk(const ChunkDesc* __restrict__ chunks, int n, uint64_t pos) {
     return lo;
 }
 
-DEV void load_tile_bytes(const uint8_t* __restrict__ p, uint32_t valid_here, uint8_t (&b)[16]) {
-    if (valid_here >= 16) {
-        uint4 v = *reinterpret_cast<const uint4*>(p);
-        const uint8_t* pv = reinterpret_cast<const uint8_t*>(&v);
-#pragma unroll
-        for (int j = 0; j < 16; j++) b[j] = pv[j];
-    } else {
-#pragma unroll
-        for (int j = 0; j < 16; j++) b[j] = (uint32_t)j < valid_here ? p[j] : 0;
-    }
-}
-
 // --------------------------------------------------------------------------------
 // k_tile_summary
 // --------------------------------------------------------------------------------
-__global__ __launch_bounds__(TILE_THREADS) void k_tile_summary(const uint8_t* __restrict__ stage,
+__global__ __launch_bounds__(TILE_THREADS) void k_tile_summary(const uint8_t* __restrict__ src,
                                                                const ChunkDesc* __restrict__ chunks, int n_chunks,
                                                                int fmt, TileInfo* __restrict__ tiles) {
     __shared__ uint32_t s_nl[TILE_THREADS / 64];
     __shared__ uint32_t s_mk[TILE_THREADS / 64];
+    __shared__ int s_c;
     const uint64_t t = blockIdx.x;
     const uint64_t base = t * TILE;
-    const int c = find_chunk(chunks, n_chunks, base);
-    const ChunkDesc cd = chunks[c];
+    if (threadIdx.x == 0) s_c = find_chunk(chunks, n_chunks, base);
+    __syncthreads();
+    const ChunkDesc cd = chunks[s_c];
     const uint64_t rel = base - cd.stage_off;
     const uint32_t valid = (uint32_t)min((uint64_t)TILE, cd.len - rel);
+    const uint32_t avail = (uint32_t)min((uint64_t)TILE + 64, cd.len - rel);
     const int tid = threadIdx.x;
     const uint32_t my0 = tid * 16;
     const uint32_t vh = valid > my0 ? valid - my0 : 0;
-    uint8_t b[16];
-    load_tile_bytes(stage + base + my0, vh, b);
     uint32_t nl = 0, mk = 0;
-    if (fmt == FMT_FASTA) {
-#pragma unroll
-        for (int j = 0; j < 16; j++) {
-            if ((uint32_t)j < vh) {
-                if (b[j] == '\n') { nl++; mk = 1; }
-                else if (b[j] == '>') mk = 2;
-            }
-        }
+    if (fmt == FMT_FASTA && vh) {
+        uint32_t w[4];
+        load16(src + cd.src_off + rel + my0, avail - my0, w);
+        const uint32_t vmask = vh >= 16 ? 0xFFFFu : ((1u << vh) - 1);
+        const uint32_t nlm = eq_mask16(w, 0x0A0A0A0Au) & vmask, gtm = eq_mask16(w, 0x3E3E3E3Eu) & vmask;
+        nl = __builtin_popcount(nlm);
+        const uint32_t any = nlm | gtm;
+        if (any) mk = (gtm >> (31 - __builtin_clz(any))) & 1 ? 2u : 1u;
     }
     // block reductions: sum of nl, last marker
     for (int d = 32; d >= 1; d >>= 1) nl += __shfl_xor(nl, d, 64);
@@ -115,7 +112,8 @@ __global__ __launch_bounds__(TILE_THREADS) void k_tile_summary(const uint8_t* __
         ti.first = rel == 0;
         ti.bh = (uint8_t)cd.bh;
         ti.pad = 0;
-        ti.pad2 = 0;
+        ti.avail = avail;
+        ti.src = cd.src_off + rel;
         tiles[t] = ti;
     }
 }
@@ -232,15 +230,14 @@ __global__ __launch_bounds__(TSCAN) void k_tscan_top(TileOut* __restrict__ agg, 
 }
 
 // --------------------------------------------------------------------------------
-// k_emit: bytes -> packed 2-bit symbols + break bits (branch-free per byte)
+// k_emit: bytes -> packed 2-bit symbols + break bits, 16 bytes per thread in SWAR:
+// byte classes as 16-bit masks, the FASTA header state as a doubling scan over the
+// thread's markers, FASTA newlines squeezed out of the 2-bit code word, then the
+// thread's (at most 16) symbols land in one or two words of the tile's LDS image.
 // --------------------------------------------------------------------------------
-DEV uint32_t acgt_code(uint32_t ch) { return ((ch >> 1) ^ (ch >> 2)) & 3; }  // A/a 0, C/c 1, G/g 2, T/t 3
-DEV bool is_acgt(uint32_t ch) {
-    const uint32_t l = ch | 0x20;
-    return l == 'a' || l == 'c' || l == 'g' || l == 't';
-}
+DEV uint32_t swap_pairs(uint32_t x) { return ((x >> 1) & 0x55555555u) | ((x & 0x55555555u) << 1); }
 
-__global__ __launch_bounds__(TILE_THREADS) void k_emit(const uint8_t* __restrict__ stage,
+__global__ __launch_bounds__(TILE_THREADS) void k_emit(const uint8_t* __restrict__ src,
                                                        const TileInfo* __restrict__ tiles,
                                                        const TileOut* __restrict__ touts,
                                                        const TileOut* __restrict__ bpre, int fmt,
@@ -261,20 +258,25 @@ __global__ __launch_bounds__(TILE_THREADS) void k_emit(const uint8_t* __restrict
     for (int i = tid; i < NW; i += TILE_THREADS) { s_pk[i] = 0; s_bk[i] = 0; }
     const uint32_t my0 = tid * 16;
     const uint32_t vh = ti.valid > my0 ? min(ti.valid - my0, 16u) : 0;
-    uint8_t b[16];
-    load_tile_bytes(stage + t * TILE + my0, vh, b);
+    uint32_t w[4] = {0, 0, 0, 0};
+    if (vh) load16(src + ti.src + my0, ti.avail - my0, w);
     const bool fasta = fmt == FMT_FASTA;
-    // per-byte masks
-    uint32_t nlm = 0, gtm = 0;
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-        nlm |= (uint32_t)(b[j] == '\n') << j;
-        gtm |= (uint32_t)(b[j] == '>') << j;
-    }
     const uint32_t vmask = vh >= 16 ? 0xFFFFu : ((1u << vh) - 1);
-    nlm &= vmask;
-    gtm &= vmask;
+    const uint32_t nlm = eq_mask16(w, 0x0A0A0A0Au) & vmask, gtm = eq_mask16(w, 0x3E3E3E3Eu) & vmask;
+    // A/C/G/T in either case: the 2-bit code ((b >> 1) ^ (b >> 2)) & 3 names the only
+    // letter the byte can be; v_perm looks that letter up and the byte must equal it
+    uint32_t acgt = 0, L = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t code = ((w[i] >> 1) ^ (w[i] >> 2)) & 0x03030303u;
+        const uint32_t expect = __builtin_amdgcn_perm(0u, 0x74676361u, code);  // "acgt"[code]
+        acgt |= flags4(zero_bytes((w[i] | 0x20202020u) ^ expect)) << (4 * i);
+        uint32_t x = (code | (code >> 6)) & 0x000F000Fu;
+        x = (x | (x >> 12)) & 0xFFu;
+        L |= x << (8 * i);  // symbol j at bits 2j, 2j+1
+    }
     uint32_t state = 0;
+    uint32_t hdr = 0;
     if (fasta) {
         const uint32_t any = nlm | gtm;
         const uint32_t mk = any ? ((gtm >> (31 - __builtin_clz(any))) & 1 ? 2u : 1u) : 0u;
@@ -284,47 +286,57 @@ __global__ __launch_bounds__(TILE_THREADS) void k_emit(const uint8_t* __restrict
         uint32_t excl = __shfl_up(incl, 1, 64);
         if (lane == 0) excl = 0;
         if (excl == 0)
-            for (int w = wid - 1; w >= 0; w--)
-                if (s_wmk[w]) { excl = s_wmk[w]; break; }
+            for (int ww = wid - 1; ww >= 0; ww--)
+                if (s_wmk[ww]) { excl = s_wmk[ww]; break; }
         state = excl ? (excl == 2 ? 1u : 0u) : hs_in;
+        // header state per byte: value of the last marker at or before it ('>' 1, '\n' 0)
+        uint32_t D = any, V = gtm;
+#pragma unroll
+        for (int s2 = 1; s2 < 16; s2 <<= 1) {
+            V = ((D & V) | (~D & (V << s2))) & 0xFFFFu;
+            D = (D | (D << s2)) & 0xFFFFu;
+        }
+        hdr = (D & V) | (~D & (state ? 0xFFFFu : 0u));
     }
     const uint32_t keptm = fasta ? (vmask & ~nlm) : vmask;
+    uint32_t brk = (hdr | ~acgt) & 0xFFFFu;
+    // squeeze the removed FASTA newlines out of the code and break words
+    uint32_t rm = fasta ? nlm : 0u;
+    uint64_t L64 = L;
+    while (rm) {
+        const uint32_t p = 31 - __builtin_clz(rm);
+        L64 = (L64 & ((1ull << (2 * p)) - 1)) | ((L64 >> (2 * p + 2)) << (2 * p));
+        brk = (brk & ((1u << p) - 1)) | ((brk >> (p + 1)) << p);
+        rm ^= 1u << p;
+    }
     const uint32_t kept = __builtin_popcount(keptm);
     const uint32_t incl = wave_incl_sum(kept);
     if (lane == 63) s_wsum[wid] = incl;
     __syncthreads();
     uint32_t pos = incl - kept + ti.first;
     uint32_t total = ti.first;
-    for (int w = 0; w < TILE_THREADS / 64; w++) {
-        if (w < wid) pos += s_wsum[w];
-        total += s_wsum[w];
+    for (int ww = 0; ww < TILE_THREADS / 64; ww++) {
+        if (ww < wid) pos += s_wsum[ww];
+        total += s_wsum[ww];
     }
     if (total == 0) return;
-    // pack this thread's kept symbols into (at most) two words of the tile's LDS image
     const uint64_t wbase = g0 >> 5;
-    const uint32_t o0 = (uint32_t)(g0 & 31) + pos;  // bit-slot of my first symbol, relative to wbase
-    uint64_t pa = 0, pb = 0;
-    uint32_t ba = 0, bb = 0;
-    uint32_t o = o0;
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-        const uint32_t ch = b[j];
-        if (fasta) state = (gtm >> j) & 1 ? 1u : ((nlm >> j) & 1 ? 0u : state);
-        const bool keep = (keptm >> j) & 1;
-        const bool brk = (fasta && state) || !is_acgt(ch);
-        const uint64_t code = brk ? 0 : acgt_code(ch);
-        const uint32_t r = o & 31;
-        const bool first_word = (o >> 5) == (o0 >> 5);
-        const uint64_t cv = code << (62 - 2 * r);
-        const uint32_t bv = (uint32_t)brk << (31 - r);
-        if (keep) {
-            if (first_word) { pa |= cv; ba |= bv; }
-            else { pb |= cv; bb |= bv; }
-        }
-        o += keep;
-    }
-    const uint32_t wa = o0 >> 5;
+    const uint32_t o0 = (uint32_t)(g0 & 31) + pos;  // slot of my first symbol, relative to wbase
+    const uint32_t wa = o0 >> 5, r = o0 & 31;
     if (kept) {
+        const uint32_t lm = kept >= 16 ? 0xFFFFFFFFu : ((1u << (2 * kept)) - 1);
+        const uint32_t Bs = swap_pairs(__builtin_bitreverse32((uint32_t)L64 & lm));  // symbol 0 at bits 31:30
+        const uint32_t Bk = __builtin_bitreverse32(brk & ((1u << kept) - 1));       // symbol 0 at bit 31
+        uint64_t pa, pb;
+        if (r <= 16) {
+            pa = (uint64_t)Bs << (32 - 2 * r);
+            pb = 0;
+        } else {
+            pa = (uint64_t)Bs >> (2 * r - 32);
+            pb = (uint64_t)Bs << (96 - 2 * r);
+        }
+        const uint64_t kx = ((uint64_t)Bk << 32) >> r;
+        const uint32_t ba = (uint32_t)(kx >> 32), bb = (uint32_t)kx;
         if (pa) atomicOr(&s_pk[wa], (unsigned long long)pa);
         if (ba) atomicOr(&s_bk[wa], ba);
         if (pb) atomicOr(&s_pk[wa + 1], (unsigned long long)pb);
@@ -335,14 +347,14 @@ __global__ __launch_bounds__(TILE_THREADS) void k_emit(const uint8_t* __restrict
     // the tile's words: interior ones are ours alone, the two edge words are shared
     const uint32_t nw = (uint32_t)(((g0 & 31) + total + 31) >> 5);
     for (uint32_t i = tid; i < nw; i += TILE_THREADS) {
-        const uint64_t w = wbase + i;
+        const uint64_t gw = wbase + i;
         const bool edge = (i == 0 && (g0 & 31)) || (i == nw - 1 && ((g0 + total) & 31));
         if (edge) {
-            if (s_pk[i]) atomicOr((unsigned long long*)(pk + w), s_pk[i]);
-            if (s_bk[i]) atomicOr(bk + w, s_bk[i]);
+            if (s_pk[i]) atomicOr((unsigned long long*)(pk + gw), s_pk[i]);
+            if (s_bk[i]) atomicOr(bk + gw, s_bk[i]);
         } else {
-            pk[w] = s_pk[i];
-            bk[w] = s_bk[i];
+            pk[gw] = s_pk[i];
+            bk[gw] = s_bk[i];
         }
     }
 }
@@ -383,17 +395,7 @@ __global__ __launch_bounds__(256) void k_synth(uint8_t* __restrict__ dst, uint64
 // ================================================================================
 // launchers
 // ================================================================================
-hipError_t launch_gather(const uint8_t* src, uint8_t* stage, const ChunkDesc* d_chunks, int n_chunks,
-                         const ChunkDesc* h_chunks, hipStream_t s) {
-    uint64_t maxlen = 0;
-    for (int i = 0; i < n_chunks; i++) maxlen = h_chunks[i].len > maxlen ? h_chunks[i].len : maxlen;
-    const uint64_t per_block = 16 * 256 * 4;
-    dim3 grid((unsigned)((maxlen + per_block - 1) / per_block), (unsigned)n_chunks);
-    hipLaunchKernelGGL(k_gather, grid, dim3(256), 0, s, src, stage, d_chunks);
-    return hipGetLastError();
-}
-
-hipError_t launch_tokenize(const uint8_t* stage, uint64_t ntiles, const ChunkDesc* d_chunks, int n_chunks, int fmt,
+hipError_t launch_tokenize(const uint8_t* src, uint64_t ntiles, const ChunkDesc* d_chunks, int n_chunks, int fmt,
                            TileInfo* tiles, TileOut* touts, TileOut* tblk, PackedView sv, uint64_t sym_bound,
                            DevCounters* ctr, hipStream_t s) {
     const uint64_t words = sym_bound / 32 + 2;
@@ -401,11 +403,11 @@ hipError_t launch_tokenize(const uint8_t* stage, uint64_t ntiles, const ChunkDes
     if ((e = hipMemsetAsync(sv.pk, 0, words * 8, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(sv.bk, 0, words * 4, s)) != hipSuccess) return e;
     const uint64_t nblk = (ntiles + TSCAN - 1) / TSCAN;
-    hipLaunchKernelGGL(k_tile_summary, dim3((unsigned)ntiles), dim3(TILE_THREADS), 0, s, stage, d_chunks, n_chunks,
+    hipLaunchKernelGGL(k_tile_summary, dim3((unsigned)ntiles), dim3(TILE_THREADS), 0, s, src, d_chunks, n_chunks,
                        fmt, tiles);
     hipLaunchKernelGGL(k_tscan_block, dim3((unsigned)nblk), dim3(TSCAN), 0, s, tiles, ntiles, fmt, touts, tblk);
     hipLaunchKernelGGL(k_tscan_top, dim3(1), dim3(TSCAN), 0, s, tblk, nblk, ctr);
-    hipLaunchKernelGGL(k_emit, dim3((unsigned)ntiles), dim3(TILE_THREADS), 0, s, stage, tiles, touts, tblk, fmt,
+    hipLaunchKernelGGL(k_emit, dim3((unsigned)ntiles), dim3(TILE_THREADS), 0, s, src, tiles, touts, tblk, fmt,
                        sv.pk, sv.bk);
     return hipGetLastError();
 }

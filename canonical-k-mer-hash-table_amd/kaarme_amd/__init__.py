@@ -22,7 +22,8 @@ from typing import Iterable, List, Optional, Sequence, Tuple
 import numpy as np
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libkc.so")
+# KC_LIB overrides the library (A/B runs of two builds); default: the in-tree build
+LIB_PATH = os.environ.get("KC_LIB") or os.path.join(PKG_ROOT, "lib", "libkc.so")
 CLI_PATH = os.path.join(PKG_ROOT, "bin", "kaarme")
 GEN_PATH = os.path.join(PKG_ROOT, "bin", "kc_gen")
 
