@@ -76,6 +76,9 @@ struct kc_ctx {
     uint32_t pb_nblk1_cap = 0;
     uint64_t pb_k1_cap = 0, pb_k2_cap = 0;  // keys the level-1 / level-2 buffers hold
     bool table_fresh = false;  // the table is all zero (allocated / reset, nothing inserted since)
+    // kc_reset defers the table memset: a fresh level-3 pass writes every region anyway;
+    // any other use of the table zeroes it first (materialize_zero)
+    bool table_zero_pending = false;
     // kc_route_table_device: per-(owner, block) record counts, their scan, scan scratch
     uint32_t* d_rhist = nullptr;
     uint64_t* d_roff = nullptr;
@@ -178,6 +181,15 @@ static TableView table_view(const kc_ctx* c) {
     tv.W = c->W;
     tv.S = c->S;
     return tv;
+}
+
+// Perform a deferred table reset before the table is read or updated by anything but a
+// fresh level-3 pass.
+static int materialize_zero(kc_ctx* c, hipStream_t s) {
+    if (!c->table_zero_pending || !c->d_table) return KC_OK;
+    HIPCHK(c, hipMemsetAsync(c->d_table, 0, c->nbuckets * BUCKET_WORDS * sizeof(uint64_t), s));
+    c->table_zero_pending = false;
+    return KC_OK;
 }
 
 // Partition buffers for a batch of up to `syms` symbols (lazily grown).  seg: use the
@@ -296,7 +308,12 @@ static int run_batch(kc_ctx* c, const uint8_t* src, uint64_t used, uint64_t nchu
         int rc = ensure_part(c, syms, !(env && !std::strcmp(env, "exact")));
         if (rc) return rc;
         HIPCHK(c, launch_count_partitioned(sv, syms, c->cfg.k, mode, tv, bv, c->d_ctr, c->pb, c->table_fresh, s));
+        c->table_zero_pending = false;  // the fresh pass wrote every region
     } else {
+        if (mode != 1) {
+            const int rc = materialize_zero(c, s);
+            if (rc) return rc;
+        }
         HIPCHK(c, launch_count(sv, syms, c->cfg.k, mode, tv, bv, c->d_ctr, s));
     }
     if (mode != 1) c->table_fresh = false;
@@ -626,6 +643,8 @@ int kc_route_table_device(kc_ctx* c, uint32_t nshards, uint64_t* dev_out, uint64
         HIPCHK(c, hipEventRecord(c->xev, c->stream));
         HIPCHK(c, hipStreamWaitEvent(s, c->xev, 0));
     }
+    rc = materialize_zero(c, s);
+    if (rc) return rc;
     const uint64_t nblk = (c->nbuckets + 255) / 256, n = nshards * nblk;
     if (n > c->r_cap) {
         hipFree(c->d_rhist);
@@ -691,8 +710,12 @@ int kc_insert_counts_device(kc_ctx* c, const uint64_t* recs, uint64_t n, void* s
         rc = ensure_part(c, (n * (c->W + 1) + c->W - 1) / c->W, false);  // records are W + 1 words
         if (rc) return rc;
     }
+    if (!part) {
+        rc = materialize_zero(c, s);
+        if (rc) return rc;
+    }
     HIPCHK(c, launch_insert_counts(recs, n, part, table_view(c), c->d_ctr, c->pb, c->table_fresh, s));
-    c->table_fresh = false;
+    c->table_fresh = c->table_zero_pending = false;
     if (c->profiling) {
         HIPCHK(c, hipEventRecord(ev[3], s));
         c->ev_pending.push_back(ev);
@@ -726,8 +749,12 @@ int kc_insert_keys_device(kc_ctx* c, const uint64_t* keys, uint64_t n, void* sp)
         ev[3] = c->get_event();
         HIPCHK(c, hipEventRecord(ev[2], s));
     }
+    if (!part) {
+        rc = materialize_zero(c, s);
+        if (rc) return rc;
+    }
     HIPCHK(c, launch_insert_keys(keys, n, part, table_view(c), c->d_ctr, c->pb, c->table_fresh, s));
-    c->table_fresh = false;
+    c->table_fresh = c->table_zero_pending = false;
     if (c->profiling) {
         HIPCHK(c, hipEventRecord(ev[3], s));
         c->ev_pending.push_back(ev);
@@ -742,6 +769,8 @@ int kc_insert_keys_device(kc_ctx* c, const uint64_t* keys, uint64_t n, void* sp)
 int kc_sync(kc_ctx* c) {
     if (!c) return KC_ERR_ARG;
     int rc = flush_host(c);
+    if (rc) return rc;
+    rc = materialize_zero(c, c->stream);  // a deferred reset is due before anyone reads the table
     if (rc) return rc;
     HIPCHK(c, hipDeviceSynchronize());
     return KC_OK;
@@ -790,7 +819,7 @@ int kc_reset(kc_ctx* c) {
     int rc = kc_sync(c);
     if (rc) return rc;
     if (c->d_table) {
-        HIPCHK(c, hipMemsetAsync(c->d_table, 0, c->nbuckets * BUCKET_WORDS * sizeof(uint64_t), c->stream));
+        c->table_zero_pending = true;  // deferred: see materialize_zero
         c->table_fresh = true;
     }
     if (c->d_bloom) {

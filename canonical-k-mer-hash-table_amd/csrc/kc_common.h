@@ -317,6 +317,26 @@ DEV void run_windows(const PackedView& sv, uint64_t r0, uint64_t t1, const RollC
     const uint64_t pa = sv.pk[wa], pb = sv.pk[wa + 1];
     const uint32_t ba = sv.bk[wa], bb = sv.bk[wa + 1];
     const int o0 = (int)(r0 & 31);
+    if constexpr (W == 1) {
+        // one-word keys: the run's RUNW incoming symbols and break bits are funnel-shifted
+        // into one register each, so every step reads them at a constant position
+        const uint64_t ins = o0 ? (pa << (2 * o0)) | (pb >> (64 - 2 * o0)) : pa;  // symbol j at bits 63-2j:62-2j
+        const uint32_t inb = o0 ? (ba << o0) | (bb >> (32 - o0)) : ba;            // break j at bit 31-j
+        const uint64_t top = rk.topmask;
+        const int rcb = rk.rc_bit;
+        uint64_t f = fwd[0], r = rc[0];
+#pragma unroll
+        for (int j = 0; j < RUNW; j++) {
+            const uint32_t c = (uint32_t)(ins >> (62 - 2 * j)) & 3;
+            const bool br = (inb >> (31 - j)) & 1;
+            since = br ? 0 : min(since + 1, k);
+            f = ((f << 2) | c) & top;
+            r = (r >> 2) | ((uint64_t)(3 - c) << rcb);
+            const uint64_t fo[1] = {f}, ro[1] = {r};
+            emit(j, r0 + j < t1 && since >= k, fo, ro);
+        }
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < RUNW; j++) {
         const int o = o0 + j;

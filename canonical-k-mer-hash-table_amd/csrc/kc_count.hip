@@ -808,7 +808,9 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
         start = pb.off2[r * pb.B2];
         end = pb.off2[(r + 1) * pb.B2];
     }
-    if (start == end) return;  // nothing to insert: leave the region untouched
+    // nothing to insert: leave the region untouched, unless the table is fresh (its reset may
+    // have been deferred to this pass, which then writes every region)
+    if (start == end && !fresh) return;
     uint4* g4 = reinterpret_cast<uint4*>(tv.buckets + r * BPR * BUCKET_WORDS);
     uint4* l4 = reinterpret_cast<uint4*>(lt);
     constexpr int N4 = BPR * BUCKET_WORDS / 2;
