@@ -92,11 +92,17 @@ def cpu_baseline(args):
         targs = table_args(slots, args.unique)
         if kind == "reference":
             cmd = [ref, fa, str(args.k), "-m", "2", "-t", str(threads), "-a", "0"] + targs
-            p = subprocess.run(cmd, capture_output=True, text=True, timeout=1800)
-            m = re.search(r"Time used to build hash table: (\d+) microseconds", p.stdout)
-            mb = re.search(r"Time used to bloom filter k-mers: (\d+) microseconds", p.stdout)
-            if p.returncode != 0 or not m:
-                log("cpu baseline failed:", p.stdout[-500:], p.stderr[-500:])
+            # the reference's worker threads occasionally crash it (seen once in ~10 runs
+            # on the box: killed before its timers); one more attempt, a CPU-only rerun
+            for attempt in range(2):
+                p = subprocess.run(cmd, capture_output=True, text=True, timeout=1800)
+                m = re.search(r"Time used to build hash table: (\d+) microseconds", p.stdout)
+                mb = re.search(r"Time used to bloom filter k-mers: (\d+) microseconds", p.stdout)
+                if p.returncode == 0 and m:
+                    break
+                log(f"cpu baseline attempt {attempt + 1} failed (exit {p.returncode}):", p.stdout[-300:],
+                    p.stderr[-300:])
+            else:
                 return None
             secs = (int(m.group(1)) + (int(mb.group(1)) if mb else 0)) / 1e6
             cores = threads - 2  # t-2 hashing workers (+ 1 mostly idle IO thread, main.cpp:383)

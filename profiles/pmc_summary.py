@@ -4,9 +4,9 @@ the HBM traffic of one counting pass (bench.py's roofline.traffic).
 
 HBM bytes follow MI355X_MICROARCH.md (HBM / rocprofv3): FETCH_SIZE and WRITE_SIZE are
 the L2 memory-side request counters; on gfx950 FETCH_SIZE reports half the bytes of
-wide coalesced reads, so reads are doubled.  The unit of both (KiB in rocprofv3) is
+wide coalesced reads, so reads are doubled.  The unit of both (KiB in rocprofv3) was
 calibrated on k_gather's stores, 16-byte streaming writes of exactly `stage_bytes`
-bytes per step (a known byte count), and applied to every kernel.
+bytes per step (a known byte count), and is applied to every kernel.
 
 usage: pmc_summary.py OUTDIR [--write profiles/pmc_traffic.json]
 """
@@ -17,7 +17,11 @@ import os
 import sys
 from collections import defaultdict
 
-COUNT_PASS = ("k_p1<", "k_p2<", "k_p3<", "k_scanA", "k_scanB", "k_scanC", "k_count<")
+COUNT_PASS = ("k_p1<", "k_p2<", "k_p2f<", "k_p3<", "k_scanA", "k_scanB", "k_scanC", "k_count<")
+# FETCH_SIZE / WRITE_SIZE unit: 1023.99998 bytes per unit measured in r01_v5 against
+# k_gather's WRITE_SIZE for a known byte count (k_gather no longer exists: the tokenizer
+# reads device images in place), i.e. the counters are in KiB.
+KIB_CALIBRATED = 1024.0
 
 
 def short(name):
@@ -54,10 +58,12 @@ def main():
     steps = bench["steps"] + bench["warmup"]
     mean = {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in vals.items()}
     gather = [k for k in mean if k.startswith("k_gather")]
-    unit = None
+    unit = KIB_CALIBRATED
     if gather and "WRITE_SIZE" in mean[gather[0]] and bench.get("stage_bytes"):
         unit = bench["stage_bytes"] / mean[gather[0]]["WRITE_SIZE"]
-    print(f"unit (bytes per counter unit, from k_gather writes): {unit}")
+        print(f"unit (bytes per counter unit, from k_gather writes): {unit}")
+    else:
+        print(f"unit (bytes per counter unit): {unit} (calibrated in r01_v5 on k_gather's 16-B stores)")
     print(f"{'kernel':60s} {'calls':>5s} {'read GB':>9s} {'write GB':>9s}")
     total = 0.0
     per_kernel = {}
