@@ -142,7 +142,7 @@ def main():
     ap.add_argument("--k", type=int, default=None)
     ap.add_argument("--slots", type=int, default=None, help="-s (total for strong presets)")
     ap.add_argument("--unique", type=int, default=None, help="-b -u U (Bloom filter) instead of -s")
-    ap.add_argument("--batch-mib", type=int, default=0, help="staging batch (0 = whole image up to 2 GiB/W)")
+    ap.add_argument("--batch-mib", type=int, default=0, help="staging batch (0 = the whole image if HBM allows)")
     ap.add_argument("--err", type=float, default=0.001)
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--cpu-sample-bases", type=int, default=150_000_000)
@@ -200,7 +200,11 @@ def main():
     host = image.cpu().numpy().tobytes()  # setup only: the host chunker reads boundary bytes
     chunks = ka.plan_chunks(host, k, ka.FMT_FASTA)
     del host
-    cap = (args.batch_mib << 20) if args.batch_mib else (2 << 30) // W
+    if args.batch_mib:
+        cap = args.batch_mib << 20
+    else:  # as large as HBM allows (kc_api.cpp: ~26 W + 2 bytes of partition buffers per staged byte)
+        free, _ = torch.cuda.mem_get_info()
+        cap = int(0.45 * (free - nbytes)) // (26 * W + 2)
     batch = min((nbytes + len(chunks) * 4096 + (1 << 20)) // 4096 * 4096, cap // 4096 * 4096)
     windows_expected = N * (L - k + 1)
     tbl = " ".join(["-m", "2"] + table_args(slots, args.unique))

@@ -69,7 +69,7 @@ struct kc_ctx {
     uint64_t nbuckets = 0;
     uint64_t R = 0;
     uint32_t F1 = 1, F2 = 1;
-    int rbits = 0, f1bits = 0;
+    int f2bits = 0;
 
     // partitioned insert buffers
     PartBufs pb{};
@@ -152,14 +152,15 @@ static int alloc_table(kc_ctx* c, uint64_t min_slots) {
     want = want + want / 4;
     const uint64_t buckets = (want + c->S - 1) / c->S;
     const uint64_t regions = std::max<uint64_t>(1, (buckets + BPR - 1) / BPR);
+    // R = F1 * F2 regions: F2 = 2^f2bits regions per level-1 bin, F1 ~ sqrt(R) <= 1024 bins
+    // (multiply-shift region index, so R is not rounded up to a power of two)
     int rbits = 0;
-    while ((1ULL << rbits) < regions) rbits++;          // R = 2^rbits regions
-    const int f1bits = std::min(10, (rbits + 1) / 2);   // level-1 fan-out ~ sqrt(R), <= 1024
-    c->rbits = rbits;
-    c->f1bits = f1bits;
-    c->F1 = 1u << f1bits;
-    c->F2 = (uint32_t)(1ULL << (rbits - f1bits));
-    c->R = 1ULL << rbits;
+    while ((1ULL << rbits) < regions) rbits++;
+    const int f1bits = std::min(10, (rbits + 1) / 2);
+    c->f2bits = rbits - f1bits;
+    c->F2 = 1u << c->f2bits;
+    c->F1 = (uint32_t)((regions + c->F2 - 1) / c->F2);
+    c->R = (uint64_t)c->F1 * c->F2;
     c->nbuckets = c->R * BPR;
     const size_t bytes = c->nbuckets * BUCKET_WORDS * sizeof(uint64_t);
     hipError_t e = hipMalloc(&c->d_table, bytes);
@@ -176,8 +177,7 @@ static TableView table_view(const kc_ctx* c) {
     tv.R = c->R;
     tv.F1 = c->F1;
     tv.F2 = c->F2;
-    tv.rbits = c->rbits;
-    tv.f1bits = c->f1bits;
+    tv.f2bits = c->f2bits;
     tv.W = c->W;
     tv.S = c->S;
     return tv;
@@ -359,6 +359,13 @@ static int add_host_chunk(kc_ctx* c, const uint8_t* buf, size_t len, int fmt, in
     d.len = len;
     d.bh = bh ? 1 : 0;
     d.pad = 0;
+    if (!c->h_stage[c->cur]) {  // host chunks: two pinned stages + the device stage, on first use
+        for (int i = 0; i < 2; i++)
+            if (!c->h_stage[i] && hipHostMalloc(&c->h_stage[i], c->batch_bytes, hipHostMallocDefault) != hipSuccess)
+                return c->fail(KC_ERR_NOMEM, "pinned staging allocation failed");
+        if (!c->d_stage && hipMalloc(&c->d_stage, c->batch_bytes) != hipSuccess)
+            return c->fail(KC_ERR_NOMEM, "device stage allocation failed");
+    }
     std::memcpy(c->h_stage[c->cur] + c->cur_used, buf, len);
     c->h_desc[c->cur][c->cur_n++] = d;
     c->cur_used += need;
@@ -449,8 +456,6 @@ int kc_create(const kc_config* cfg, kc_ctx** out) {
     c->cfg = *cfg;
     c->W = words_for_k(cfg->k);
     c->S = slots_per_bucket(c->W);
-    c->batch_bytes = round_up(cfg->batch_bytes ? cfg->batch_bytes : kDefaultBatch, TILE);
-    c->max_chunks = c->batch_bytes / TILE;
     auto bail = [&](int code, const std::string& m) {
         g_create_error = m.empty() ? c->err : m;
         kc_destroy(c);
@@ -458,11 +463,24 @@ int kc_create(const kc_config* cfg, kc_ctx** out) {
     };
     hipError_t e = hipSetDevice(cfg->device);
     if (e != hipSuccess) return bail(KC_ERR_HIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
+    uint64_t batch = cfg->batch_bytes;
+    if (!batch) {
+        // Every staged batch of the partitioned insert sweeps the table once, so batches are
+        // as large as the device allows: the partition buffers take ~26 W + 2 bytes per
+        // staged byte (two segmented key buffers + the packed stream); use ~40 % of free
+        // HBM, within [256 MiB, 2 GiB] (the pinned host stage is two batches).
+        size_t fr = 0, tot = 0;
+        batch = kDefaultBatch;
+        if (hipMemGetInfo(&fr, &tot) == hipSuccess)
+            batch = std::min<uint64_t>(2ull << 30, std::max<uint64_t>(kDefaultBatch,
+                                                                       (uint64_t)(0.4 * fr) / (26 * c->W + 2)));
+    }
+    c->batch_bytes = round_up(batch, TILE);
+    c->max_chunks = c->batch_bytes / TILE;
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
         return bail(KC_ERR_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
-    for (int i = 0; i < 2; i++) {
-        if (hipHostMalloc(&c->h_stage[i], c->batch_bytes, hipHostMallocDefault) != hipSuccess ||
-            hipHostMalloc(&c->h_desc[i], c->max_chunks * sizeof(ChunkDesc), hipHostMallocDefault) != hipSuccess)
+    for (int i = 0; i < 2; i++) {  // (the pinned byte stages are allocated on first host chunk)
+        if (hipHostMalloc(&c->h_desc[i], c->max_chunks * sizeof(ChunkDesc), hipHostMallocDefault) != hipSuccess)
             return bail(KC_ERR_NOMEM, "pinned staging allocation failed");
         if (hipEventCreateWithFlags(&c->h_free[i], hipEventDisableTiming) != hipSuccess)
             return bail(KC_ERR_HIP, "event creation failed");
@@ -470,8 +488,7 @@ int kc_create(const kc_config* cfg, kc_ctx** out) {
     if (hipEventCreateWithFlags(&c->xev, hipEventDisableTiming) != hipSuccess)
         return bail(KC_ERR_HIP, "event creation failed");
     const uint64_t ntiles = c->batch_bytes / TILE;
-    if (hipMalloc(&c->d_stage, c->batch_bytes) != hipSuccess ||
-        hipMalloc(&c->d_pk, ((c->batch_bytes + c->max_chunks) / 32 + 4) * 8) != hipSuccess ||
+    if (hipMalloc(&c->d_pk, ((c->batch_bytes + c->max_chunks) / 32 + 4) * 8) != hipSuccess ||
         hipMalloc(&c->d_bk, ((c->batch_bytes + c->max_chunks) / 32 + 4) * 4) != hipSuccess ||
         hipMalloc(&c->d_tiles, ntiles * sizeof(TileInfo)) != hipSuccess ||
         hipMalloc(&c->d_touts, ntiles * sizeof(TileOut)) != hipSuccess ||

@@ -287,6 +287,12 @@ int main(int argc, char** argv) {
     cfg.est_unique = a.unique;
     cfg.fpr = a.fpr;
     cfg.min_abundance = a.min_abundance;
+    {   // a small input gets a stage of its own size (one batch, little pinned memory);
+        // larger ones the library's default (sized from free HBM)
+        uint64_t staged = 4096;
+        for (uint64_t i = 0; i < nch; i++) staged += (chunks[i].len + 4095) / 4096 * 4096;
+        if (staged <= (256ull << 20)) cfg.batch_bytes = staged;
+    }
     kc_ctx* ctx = nullptr;
     if (kc_create(&cfg, &ctx) != KC_OK) {
         std::cerr << "kc_create: " << kc_last_error(nullptr) << std::endl;

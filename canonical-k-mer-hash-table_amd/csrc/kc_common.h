@@ -69,12 +69,15 @@ DEV void from_tkey(const uint64_t (&t)[W], uint64_t (&key)[W]) {
 }
 
 // ---- table geometry -------------------------------------------------------------
-// region = top rbits of tkey word 0, bucket = the next BPR_BITS bits; linear probing
-// wraps inside the region, so a region is an independent table that fits in LDS.
-// The shard owner (multi-GPU) uses the low bits, independent of both.
-DEV uint64_t region_of(uint64_t t0, int rbits) { return rbits ? t0 >> (64 - rbits) : 0; }
-DEV uint32_t bucket_in_region(uint64_t t0, int rbits) {
-    return (uint32_t)(t0 >> (64 - rbits - BPR_BITS)) & (BPR - 1);
+// Region r = floor(x * R / 2^32) with x = the top 32 bits of tkey word 0 (multiply-shift,
+// so R need not be a power of two); the start bucket is the top BPR_BITS of the
+// fraction (x * R mod 2^32), uniform and independent of r.  Linear probing wraps inside
+// the region, so a region is an independent table that fits in LDS.  For R = F1 * F2
+// (F2 a power of two) the level-1 bin of a key is r >> log2 F2 and its level-2 bin
+// r & (F2 - 1).  The shard owner (multi-GPU) uses the low 32 bits, independent of both.
+DEV uint64_t region_of(uint64_t t0, uint64_t R) { return ((t0 >> 32) * R) >> 32; }
+DEV uint32_t bucket_in_region(uint64_t t0, uint64_t R) {
+    return (uint32_t)((t0 >> 32) * R) >> (32 - BPR_BITS);
 }
 DEV uint32_t owner_of(uint64_t t0, uint32_t parts) { return (uint32_t)(((t0 & 0xFFFFFFFFULL) * parts) >> 32); }
 

@@ -37,8 +37,8 @@ __constant__ uint64_t c_bf_seeds[MAX_NH] = {2411, 3253, 1061, 1129, 2269, 7309, 
 template <int W>
 DEV bool table_insert(const TableView& tv, const uint64_t (&tk)[W], uint64_t add = 1) {
     constexpr int S = BUCKET_WORDS / (W + 1);
-    const uint64_t region = region_of(tk[0], tv.rbits);
-    uint32_t b = bucket_in_region(tk[0], tv.rbits);
+    const uint64_t region = region_of(tk[0], tv.R);
+    uint32_t b = bucket_in_region(tk[0], tv.R);
     for (int probe = 0; probe < BPR; probe++) {
         uint64_t* bk = tv.buckets + (region * BPR + b) * BUCKET_WORDS;
         uint64_t w0[S];
@@ -204,7 +204,7 @@ DEV void block_add4(unsigned long long v0, unsigned long long v1, unsigned long 
 // --------------------------------------------------------------------------------
 // per-thread windows of one tile (the tile is COUNT_THREADS * run_w windows)
 template <int W>
-constexpr int run_w() { return W == 1 ? 16 : (W == 2 ? 8 : 4); }
+constexpr int run_w() { return W == 1 ? 16 : 8; }
 template <int W>
 constexpr int tile_win() { return COUNT_THREADS * run_w<W>(); }
 
@@ -331,13 +331,18 @@ DEV PartLds part_lds(uint8_t* smem, uint32_t F) {
     return l;
 }
 
-// bin of a table key: a bit field of word 0 (table levels) or the shard owner (routing);
+// bin of a table key: its region bin (table levels) or its shard owner (routing);
 // the kind is a template parameter so the table levels carry no routing branch.
-struct BinBits {
+struct BinRegion {  // level-1 bin (coarse: region >> f2bits) or level-2 bin (region & mask)
     static constexpr bool kOwner = false;
-    int shift;
+    uint64_t R;
+    int f2bits;
     uint32_t mask;
-    DEV uint32_t operator()(uint64_t t0) const { return (uint32_t)(t0 >> shift) & mask; }
+    int coarse;
+    DEV uint32_t operator()(uint64_t t0) const {
+        const uint32_t r = (uint32_t)region_of(t0, R);
+        return coarse ? r >> f2bits : r & mask;
+    }
 };
 struct BinOwner {
     static constexpr bool kOwner = true;
@@ -411,7 +416,7 @@ DEV bool scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const Out& o
 // gated kernels (the exact fallback of a segmented batch) run only if *gate != 0
 DEV bool gated_off(const unsigned long long* gate) { return gate && *gate == 0; }
 
-// Level 1: windows of a contiguous symbol range -> coarse bins (top f1bits of tkey[0]).
+// Level 1: windows of a contiguous symbol range -> coarse bins (region >> f2bits).
 // SCATTER = false: histogram only ([bin][block] into hist1); true: write the keys,
 // exact layout (offsets off1) or segmented (Out = OutSeg: single pass, the segment
 // fill counts go to hist1).  `count`: add windows / inserted to the counters (off for
@@ -513,10 +518,10 @@ __global__ __launch_bounds__(COUNT_THREADS, 4) void k_p1(PackedView sv, int k, B
 }
 
 // Level 1 over a key array (keys received from other shards): [0, n) split over nblk1
-// blocks, bins = top f1bits of the table key.
+// blocks, bins = the coarse bins of the table key.
 template <int W, bool SCATTER>
 __global__ __launch_bounds__(COUNT_THREADS, 4) void k_p1k(const uint64_t* __restrict__ in, uint64_t n, PartBufs pb,
-                                                       uint32_t F, BinBits bin, DevCounters* __restrict__ ctr,
+                                                       uint32_t F, BinRegion bin, DevCounters* __restrict__ ctr,
                                                        int cnt_word) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int RUNW = run_w<W>(), TW = tile_win<W>();
@@ -663,7 +668,7 @@ __global__ __launch_bounds__(COUNT_THREADS, 4) void k_p2(TableView tv, PartBufs 
     constexpr int RUNW = run_w<W>(), TW = tile_win<W>();
     if (gated_off(gate)) return;
     const uint32_t F = tv.F2;
-    const BinBits bin{tv.rbits ? 64 - tv.rbits : 63, F - 1};
+    const BinRegion bin{tv.R, tv.f2bits, F - 1, 0};
     const PartLds l = part_lds(smem, F);
     const int tid = threadIdx.x;
     const uint32_t c = blockIdx.x / pb.B2, j = blockIdx.x % pb.B2;
@@ -715,7 +720,7 @@ __global__ __launch_bounds__(COUNT_THREADS, 4) void k_p2f(TableView tv, PartBufs
     constexpr int RUNW = run_w<W>(), TW = tile_win<W>();
     if (ctr->part_overflow) return;  // level 1 overflowed: the exact pipeline redoes the batch
     const uint32_t F = tv.F2;
-    const BinBits bin{tv.rbits ? 64 - tv.rbits : 63, F - 1};
+    const BinRegion bin{tv.R, tv.f2bits, F - 1, 0};
     const PartLds l = part_lds(smem, F);
     uint32_t* pre = reinterpret_cast<uint32_t*>(smem + part_smem<W>(F));
     const int tid = threadIdx.x;
@@ -846,7 +851,7 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
         for (int q = 0; q < KB; q++) {
             if (base + threadIdx.x + (uint64_t)q * NT >= end) continue;
             const uint64_t k0 = kk[q][0];
-            uint32_t b = bucket_in_region(k0, tv.rbits);
+            uint32_t b = bucket_in_region(k0, tv.R);
             bool done = false;
             if constexpr (W == 1) {
                 // branch-light probe: match / first-empty masks over the 8 slots of a bucket
@@ -1083,7 +1088,7 @@ static uint64_t pow5_mod54(int e) {
     return r;
 }
 
-int run_width(int W) { return W == 1 ? 16 : (W == 2 ? 8 : 4); }
+int run_width(int W) { return W == 1 ? 16 : 8; }
 
 template <int W>
 static hipError_t launch_count_w(PackedView sym, uint64_t sym_bound, int k, int mode, TableView t, BloomView bf,
@@ -1117,7 +1122,7 @@ static hipError_t set_smem(K kernel, size_t bytes) {
                                (int)bytes);
 }
 
-static BinBits coarse_bins(const TableView& t) { return BinBits{t.f1bits ? 64 - t.f1bits : 63, t.F1 - 1}; }
+static BinRegion coarse_bins(const TableView& t) { return BinRegion{t.R, t.f2bits, 0, 1}; }
 
 template <int W, bool SEG, bool CNT = false>
 static hipError_t launch_p3(TableView t, DevCounters* ctr, PartBufs pb, const unsigned long long* gate, int fresh,
@@ -1182,7 +1187,7 @@ static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf
     const unsigned long long* gate = &ctr->part_overflow;
     if ((e = hipMemsetAsync(&ctr->part_overflow, 0, sizeof(ctr->part_overflow), s)) != hipSuccess) return e;
     const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
-    auto k1 = k_p1<W, MODE, true, BinBits, OutSeg>;
+    auto k1 = k_p1<W, MODE, true, BinRegion, OutSeg>;
     static const uint32_t p2f_pad = [] {  // A/B knob: reserve LDS as if for this many segments
         const char* v = std::getenv("KC_P2F_SEGS");
         return v ? (uint32_t)std::atoi(v) : 0u;
@@ -1238,7 +1243,7 @@ template <int W, bool CNT>
 static hipError_t insert_items_part(const uint64_t* items, uint64_t n, TableView t, DevCounters* ctr, PartBufs pb,
                                     int fresh, hipStream_t s) {
     constexpr int IW = CNT ? W + 1 : W;
-    const BinBits bin = coarse_bins(t);
+    const BinRegion bin = coarse_bins(t);
     const size_t sm1 = part_smem<IW>(t.F1), sm1h = hist_smem(t.F1);
     hipError_t e;
     if ((e = set_smem(k_p1k<IW, false>, sm1h)) != hipSuccess) return e;

@@ -79,9 +79,9 @@ struct PackedView {
 struct TableView {
     uint64_t* buckets;      // nbuckets * BUCKET_WORDS
     uint64_t nbuckets;      // R * BPR
-    uint64_t R;             // regions = F1 * F2 = 2^rbits
-    uint32_t F1, F2;        // partition fan-outs of the two scatter levels (powers of two)
-    int rbits, f1bits;      // log2 R, log2 F1
+    uint64_t R;             // regions = F1 * F2 (kc_common.h region_of)
+    uint32_t F1, F2;        // partition fan-outs of the two scatter levels (F2 a power of two)
+    int f2bits;             // log2 F2
     int W;                  // key words
     int S;                  // slots per bucket
 };

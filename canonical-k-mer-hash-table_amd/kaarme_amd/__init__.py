@@ -351,6 +351,9 @@ def count_file(path: str, k: int, mode: int = 2, min_abundance: int = 2, table_s
     if fmt == FMT_FASTQ:
         raise KcError(-7, "Input file format not supported.")
     chunks = plan_chunks(image, k, fmt, chunk_size)
+    if not batch_bytes:  # a small input gets a stage of its own size (one batch, little pinned memory)
+        staged = 4096 + sum((ln + 4095) // 4096 * 4096 for _, ln, _ in chunks)
+        batch_bytes = staged if staged <= (256 << 20) else 0
     kc = KmerCounter(Config(k=k, mode=mode, table_slots=table_slots, bf_enable=bf_enable,
                             est_unique=est_unique, fpr=fpr, min_abundance=min_abundance,
                             batch_bytes=batch_bytes, device=device))

@@ -204,7 +204,8 @@ def test_segment_overflow_falls_back_to_exact(name, k, args, golden_input, tmp_p
     monkeypatch.setenv("KC_SEG_CAP", "8")
     path = golden_input(name)
     o = parse_ref_args(args)
-    cfg = ka.Config(k=k, mode=o["mode"], min_abundance=o["min_abundance"], table_slots=o["table_slots"])
+    cfg = ka.Config(k=k, mode=o["mode"], min_abundance=o["min_abundance"], table_slots=o["table_slots"],
+                    batch_bytes=64 << 20)
     data = open(path, "rb").read()
     with ka.KmerCounter(cfg) as kc:
         for off, ln, bh in ka.plan_chunks(data, k, ka.FMT_FASTA):
