@@ -222,7 +222,8 @@ static int ensure_part(kc_ctx* c, uint64_t syms, bool seg) {
     uint64_t cap1 = 0, cap2 = 0;
     if (seg) {
         auto capacity = [](double e) { return ((uint64_t)std::ceil(e + 8.0 * std::sqrt(e) + 32.0) + 7) / 8 * 8; };
-        const uint64_t per1 = ((syms + nblk1 - 1) / nblk1 + tile - 1) / tile * tile;  // windows per level-1 block
+        const uint64_t t1 = (uint64_t)p1_tile(c->W);  // k_p1<..., OutSeg> rounds block ranges to its tile
+        const uint64_t per1 = ((syms + nblk1 - 1) / nblk1 + t1 - 1) / t1 * t1;  // windows per level-1 block
         const uint64_t nseg = (nblk1 + B2 - 1) / B2;                               // level-1 segments per p2 block
         cap1 = capacity((double)per1 / c->F1);
         cap2 = capacity((double)nseg * per1 / c->F1 / c->F2);

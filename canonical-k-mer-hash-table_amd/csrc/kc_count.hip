@@ -181,7 +181,7 @@ DEV bool bloom_gate(const BloomView& bf, uint64_t root) {
 DEV void block_add4(unsigned long long v0, unsigned long long v1, unsigned long long v2, unsigned long long v3,
                     unsigned long long* d0, unsigned long long* d1, unsigned long long* d2,
                     unsigned long long* d3) {
-    __shared__ unsigned long long s_red[4][4];
+    __shared__ unsigned long long s_red[4][16];  // up to 1024-thread blocks
     unsigned long long v[4] = {v0, v1, v2, v3};
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
@@ -207,6 +207,9 @@ template <int W>
 constexpr int run_w() { return W == 1 ? 16 : 8; }
 template <int W>
 constexpr int tile_win() { return COUNT_THREADS * run_w<W>(); }
+// the segmented (single-pass) level 1 runs 512-thread workgroups: 8192-window tiles, twice
+// the run per bin of the 256-thread histogram kernels
+constexpr int P1_THREADS = 512;
 
 // table key of the window ending at p (MODE 0 path: direct extraction)
 template <int W>
@@ -288,16 +291,17 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_count(PackedView sv, int k, T
 // --------------------------------------------------------------------------------
 // LDS of a scatter pass: tilehist, tilestart, tilecur (u32 x F), gbase (u64 x F), keys
 constexpr size_t hist_smem(uint32_t F) { return ((size_t)F * 3 + 1) * 4 + 4 + (size_t)F * 8; }
-template <int W>
+template <int W, int NT = COUNT_THREADS>
 constexpr size_t part_smem(uint32_t F) {
-    return hist_smem(F) + (size_t)tile_win<W>() * 8 * W;
+    return hist_smem(F) + (size_t)NT * run_w<W>() * 8 * W;
 }
 
-// exclusive scan of an LDS u32 array of n entries by one COUNT_THREADS block
+// exclusive scan of an LDS u32 array of n entries by one NT-thread block
+template <int NT = COUNT_THREADS>
 DEV void block_excl_scan_lds(const uint32_t* in, uint32_t* out, uint32_t n) {
-    __shared__ uint32_t s_w[COUNT_THREADS / 64];
+    __shared__ uint32_t s_w[NT / 64];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const uint32_t per = (n + COUNT_THREADS - 1) / COUNT_THREADS;
+    const uint32_t per = (n + NT - 1) / NT;
     const uint32_t lo = min(n, tid * per), hi = min(n, lo + per);
     uint32_t sum = 0;
     for (uint32_t i = lo; i < hi; i++) sum += in[i];
@@ -372,7 +376,7 @@ struct OutSeg {
 // LDS and write each bin as one contiguous run at gbase[bin].  The rank of a key inside
 // its bin comes back from the histogram atomic, so one LDS atomic per key suffices.
 // Returns true if a segmented run did not fit.
-template <int W, int RUNW, class Bin, class Out>
+template <int W, int RUNW, class Bin, class Out, int NT = COUNT_THREADS>
 DEV bool scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const Out& o, const uint64_t (&tk)[RUNW][W],
                       const bool (&ok)[RUNW], uint64_t* __restrict__ out) {
     const int tid = threadIdx.x;
@@ -380,7 +384,7 @@ DEV bool scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const Out& o
 #pragma unroll
     for (int j = 0; j < RUNW; j++) rank[j] = ok[j] ? atomicAdd(&l.hist[bin(tk[j][0])], 1u) : 0;
     __syncthreads();
-    block_excl_scan_lds(l.hist, l.start, F);
+    block_excl_scan_lds<NT>(l.hist, l.start, F);
 #pragma unroll
     for (int j = 0; j < RUNW; j++)
         if (ok[j]) {
@@ -391,7 +395,7 @@ DEV bool scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const Out& o
     __syncthreads();
     const uint32_t n = l.start[F - 1] + l.hist[F - 1];
     bool over = false;
-    for (uint32_t i = tid; i < n; i += COUNT_THREADS) {
+    for (uint32_t i = tid; i < n; i += NT) {
         uint64_t key[W];
 #pragma unroll
         for (int w = 0; w < W; w++) key[w] = l.keys[i * W + w];
@@ -405,7 +409,7 @@ DEV bool scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const Out& o
         }
     }
     __syncthreads();
-    for (uint32_t b = tid; b < F; b += COUNT_THREADS) {
+    for (uint32_t b = tid; b < F; b += NT) {
         l.gbase[b] += l.hist[b];
         l.hist[b] = 0;
     }
@@ -421,13 +425,13 @@ DEV bool gated_off(const unsigned long long* gate) { return gate && *gate == 0; 
 // exact layout (offsets off1) or segmented (Out = OutSeg: single pass, the segment
 // fill counts go to hist1).  `count`: add windows / inserted to the counters (off for
 // the histogram pass of a fallback, whose windows the segmented pass counted already).
-template <int W, int MODE, bool SCATTER, class Bin, class Out>
-__global__ __launch_bounds__(COUNT_THREADS, 4) void k_p1(PackedView sv, int k, BloomView bf,
+template <int W, int MODE, bool SCATTER, class Bin, class Out, int NT = COUNT_THREADS>
+__global__ __launch_bounds__(NT, 4) void k_p1(PackedView sv, int k, BloomView bf,
                                                       DevCounters* __restrict__ ctr, PartBufs pb, uint32_t F, Bin bin,
                                                       uint64_t* __restrict__ out, uint64_t pow5_k, uint64_t pow5_km1,
                                                       Out o, const unsigned long long* gate, int count) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    constexpr int RUNW = run_w<W>(), TW = tile_win<W>();
+    constexpr int RUNW = run_w<W>(), TW = NT * RUNW;
     constexpr bool COUNTS = !SCATTER || Out::kSeg;
     if (gated_off(gate)) return;
     if (gate && !SCATTER && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&ctr->part_fallbacks, 1ULL);
@@ -438,7 +442,7 @@ __global__ __launch_bounds__(COUNT_THREADS, 4) void k_p1(PackedView sv, int k, B
     const uint64_t lo = min(M, (uint64_t)blockIdx.x * per), hi = min(M, lo + per);
     Out ob = o;
     if constexpr (Out::kSeg) ob.base = (uint64_t)blockIdx.x * o.cap;  // segment (b, block) = b * nblk1 + block
-    for (uint32_t b = tid; b < F; b += COUNT_THREADS) {
+    for (uint32_t b = tid; b < F; b += NT) {
         l.hist[b] = 0;
         if constexpr (SCATTER) {
             if constexpr (Out::kSeg) l.gbase[b] = ob.start(b);
@@ -496,7 +500,7 @@ __global__ __launch_bounds__(COUNT_THREADS, 4) void k_p1(PackedView sv, int k, B
             });
         }
         if constexpr (SCATTER) {
-            over |= scatter_tile<W, RUNW>(l, F, bin, ob, tk, ok, out);
+            over |= scatter_tile<W, RUNW, Bin, Out, NT>(l, F, bin, ob, tk, ok, out);
         } else {
 #pragma unroll
             for (int j = 0; j < RUNW; j++)
@@ -505,10 +509,10 @@ __global__ __launch_bounds__(COUNT_THREADS, 4) void k_p1(PackedView sv, int k, B
     }
     if constexpr (!SCATTER) {
         __syncthreads();
-        for (uint32_t b = tid; b < F; b += COUNT_THREADS) pb.hist1[(uint64_t)b * pb.nblk1 + blockIdx.x] = l.hist[b];
+        for (uint32_t b = tid; b < F; b += NT) pb.hist1[(uint64_t)b * pb.nblk1 + blockIdx.x] = l.hist[b];
     }
     if constexpr (Out::kSeg) {  // segment fills (the scatter's last barrier ordered gbase)
-        for (uint32_t b = tid; b < F; b += COUNT_THREADS)
+        for (uint32_t b = tid; b < F; b += NT)
             pb.hist1[(uint64_t)b * pb.nblk1 + blockIdx.x] = (uint32_t)(l.gbase[b] - ob.start(b));
         if (over) atomicOr(&ctr->part_overflow, 1ULL);
     }
@@ -709,33 +713,34 @@ __global__ __launch_bounds__(COUNT_THREADS, 4) void k_p2(TableView tv, PartBufs 
 // (block = c * B2 + j) -> segments (c * F2 + region, j) of capacity cap2, one pass.
 // The input segments are read as one virtual run (exclusive prefix of their fills in
 // LDS; each thread walks a monotone segment cursor).
+constexpr int P2F_THREADS = 512;  // 8192-key tiles: 64-key runs per region
 // LDS: the scatter's arrays plus the segment-fill prefix (a level-2 workgroup reads
 // ceil(nblk1 / B2) level-1 segments)
-template <int W>
-constexpr size_t p2f_smem(uint32_t F, uint32_t nseg_max) { return part_smem<W>(F) + (size_t)(nseg_max + 1) * 4; }
+template <int W, int NT>
+constexpr size_t p2f_smem(uint32_t F, uint32_t nseg_max) { return part_smem<W, NT>(F) + (size_t)(nseg_max + 1) * 4; }
 
-template <int W>
-__global__ __launch_bounds__(COUNT_THREADS, 4) void k_p2f(TableView tv, PartBufs pb, DevCounters* __restrict__ ctr) {
+template <int W, int NT>
+__global__ __launch_bounds__(NT, 1024 / NT) void k_p2f(TableView tv, PartBufs pb, DevCounters* __restrict__ ctr) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    constexpr int RUNW = run_w<W>(), TW = tile_win<W>();
+    constexpr int RUNW = run_w<W>(), TW = NT * RUNW;
     if (ctr->part_overflow) return;  // level 1 overflowed: the exact pipeline redoes the batch
     const uint32_t F = tv.F2;
     const BinRegion bin{tv.R, tv.f2bits, F - 1, 0};
     const PartLds l = part_lds(smem, F);
-    uint32_t* pre = reinterpret_cast<uint32_t*>(smem + part_smem<W>(F));
+    uint32_t* pre = reinterpret_cast<uint32_t*>(smem + part_smem<W, NT>(F));
     const int tid = threadIdx.x;
     const uint32_t c = blockIdx.x / pb.B2, j = blockIdx.x % pb.B2;
     const uint32_t s_lo = (uint32_t)((uint64_t)j * pb.nblk1 / pb.B2);
     const uint32_t nseg = (uint32_t)((uint64_t)(j + 1) * pb.nblk1 / pb.B2) - s_lo;
     const uint64_t seg0 = (uint64_t)c * pb.nblk1 + s_lo;  // level-1 segment index of cursor 0
     const OutSeg o{(uint64_t)pb.B2 * pb.cap2, ((uint64_t)c * F * pb.B2 + j) * pb.cap2, pb.cap2};
-    for (uint32_t i = tid; i <= nseg; i += COUNT_THREADS) pre[i] = i < nseg ? pb.hist1[seg0 + i] : 0;
-    for (uint32_t b = tid; b < F; b += COUNT_THREADS) {
+    for (uint32_t i = tid; i <= nseg; i += NT) pre[i] = i < nseg ? pb.hist1[seg0 + i] : 0;
+    for (uint32_t b = tid; b < F; b += NT) {
         l.hist[b] = 0;
         l.gbase[b] = o.start(b);
     }
     __syncthreads();
-    block_excl_scan_lds(pre, pre, nseg + 1);  // in place; pre[nseg] = total
+    block_excl_scan_lds<NT>(pre, pre, nseg + 1);  // in place; pre[nseg] = total
     const uint32_t total = pre[nseg];
     bool over = false;
     uint32_t cs = 0;  // segment cursor of this thread
@@ -744,7 +749,7 @@ __global__ __launch_bounds__(COUNT_THREADS, 4) void k_p2f(TableView tv, PartBufs
         bool ok[RUNW];
 #pragma unroll
         for (int q = 0; q < RUNW; q++) {
-            const uint32_t i = t0 + tid + q * COUNT_THREADS;
+            const uint32_t i = t0 + tid + q * NT;
             ok[q] = i < total;
             if (ok[q]) {
                 while (pre[cs + 1] <= i) cs++;
@@ -756,9 +761,9 @@ __global__ __launch_bounds__(COUNT_THREADS, 4) void k_p2f(TableView tv, PartBufs
                 for (int w = 0; w < W; w++) tk[q][w] = 0;
             }
         }
-        over |= scatter_tile<W, RUNW>(l, F, bin, o, tk, ok, pb.keys2);
+        over |= scatter_tile<W, RUNW, BinRegion, OutSeg, NT>(l, F, bin, o, tk, ok, pb.keys2);
     }
-    for (uint32_t b = tid; b < F; b += COUNT_THREADS)
+    for (uint32_t b = tid; b < F; b += NT)
         pb.hist2[((uint64_t)c * F + b) * pb.B2 + j] = (uint32_t)(l.gbase[b] - o.start(b));
     if (over) atomicOr(&ctr->part_overflow, 1ULL);
 }
@@ -1089,6 +1094,7 @@ static uint64_t pow5_mod54(int e) {
 }
 
 int run_width(int W) { return W == 1 ? 16 : 8; }
+int p1_tile(int W) { return P1_THREADS * run_width(W); }
 
 template <int W>
 static hipError_t launch_count_w(PackedView sym, uint64_t sym_bound, int k, int mode, TableView t, BloomView bf,
@@ -1187,19 +1193,19 @@ static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf
     const unsigned long long* gate = &ctr->part_overflow;
     if ((e = hipMemsetAsync(&ctr->part_overflow, 0, sizeof(ctr->part_overflow), s)) != hipSuccess) return e;
     const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
-    auto k1 = k_p1<W, MODE, true, BinRegion, OutSeg>;
+    auto k1 = k_p1<W, MODE, true, BinRegion, OutSeg, P1_THREADS>;
     static const uint32_t p2f_pad = [] {  // A/B knob: reserve LDS as if for this many segments
         const char* v = std::getenv("KC_P2F_SEGS");
         return v ? (uint32_t)std::atoi(v) : 0u;
     }();
-    const size_t sm1 = part_smem<W>(t.F1),
-                 sm2 = p2f_smem<W>(t.F2, std::max<uint32_t>(p2f_pad, (pb.nblk1 + pb.B2 - 1) / pb.B2));
+    const size_t sm1 = part_smem<W, P1_THREADS>(t.F1),
+                 sm2 = p2f_smem<W, P2F_THREADS>(t.F2, std::max<uint32_t>(p2f_pad, (pb.nblk1 + pb.B2 - 1) / pb.B2));
     if ((e = set_smem(k1, sm1)) != hipSuccess) return e;
-    if ((e = set_smem(k_p2f<W>, sm2)) != hipSuccess) return e;
+    if ((e = set_smem(k_p2f<W, P2F_THREADS>, sm2)) != hipSuccess) return e;
     const OutSeg o1{(uint64_t)pb.nblk1 * pb.cap1, 0, pb.cap1};
-    hipLaunchKernelGGL(k1, dim3(pb.nblk1), dim3(COUNT_THREADS), sm1, s, sym, k, bf, ctr, pb, t.F1, coarse_bins(t),
+    hipLaunchKernelGGL(k1, dim3(pb.nblk1), dim3(P1_THREADS), sm1, s, sym, k, bf, ctr, pb, t.F1, coarse_bins(t),
                        pb.keys1, pk, pkm1, o1, (const unsigned long long*)nullptr, 1);
-    hipLaunchKernelGGL(k_p2f<W>, dim3(t.F1 * pb.B2), dim3(COUNT_THREADS), sm2, s, t, pb, ctr);
+    hipLaunchKernelGGL((k_p2f<W, P2F_THREADS>), dim3(t.F1 * pb.B2), dim3(P2F_THREADS), sm2, s, t, pb, ctr);
     if ((e = launch_p3<W, true>(t, ctr, pb, nullptr, fresh, s)) != hipSuccess) return e;
     if ((e = part_level1<W, MODE>(sym, k, bf, ctr, pb, t.F1, coarse_bins(t), pb.keys1, s, gate)) != hipSuccess)
         return e;

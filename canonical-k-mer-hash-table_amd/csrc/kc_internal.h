@@ -123,6 +123,7 @@ hipError_t launch_count(PackedView sv, uint64_t sym_bound, int k, int mode, Tabl
 hipError_t launch_count_partitioned(PackedView sv, uint64_t sym_bound, int k, int mode, TableView t,
                                     BloomView bf, DevCounters* ctr, PartBufs pb, int fresh, hipStream_t s);
 int run_width(int W);  // windows rolled per thread in the partitioned kernels
+int p1_tile(int W);    // windows per tile of the segmented level-1 kernel
 // hash-prefix sharding: windows -> table keys grouped by owner (offsets in pb.off1)
 hipError_t launch_route(PackedView sym, int k, int W, DevCounters* ctr, PartBufs pb, uint32_t parts, uint64_t* out,
                         hipStream_t s);
