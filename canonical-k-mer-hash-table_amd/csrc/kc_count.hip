@@ -209,7 +209,11 @@ template <int W>
 constexpr int tile_win() { return COUNT_THREADS * run_w<W>(); }
 // the segmented (single-pass) level 1 runs 512-thread workgroups: 8192-window tiles, twice
 // the run per bin of the 256-thread histogram kernels
-constexpr int P1_THREADS = 512;
+#ifndef KC_SCATTER_NT12
+#define KC_SCATTER_NT12 512
+#endif
+template <int W>
+constexpr int scatter_threads() { return W <= 2 ? KC_SCATTER_NT12 : 512; }
 
 // table key of the window ending at p (MODE 0 path: direct extraction)
 template <int W>
@@ -713,7 +717,6 @@ __global__ __launch_bounds__(COUNT_THREADS, 4) void k_p2(TableView tv, PartBufs 
 // (block = c * B2 + j) -> segments (c * F2 + region, j) of capacity cap2, one pass.
 // The input segments are read as one virtual run (exclusive prefix of their fills in
 // LDS; each thread walks a monotone segment cursor).
-constexpr int P2F_THREADS = 512;  // 8192-key tiles: 64-key runs per region
 // LDS: the scatter's arrays plus the segment-fill prefix (a level-2 workgroup reads
 // ceil(nblk1 / B2) level-1 segments)
 template <int W, int NT>
@@ -770,9 +773,27 @@ __global__ __launch_bounds__(NT, 1024 / NT) void k_p2f(TableView tv, PartBufs pb
 
 // LDS image of a region: the 16-byte chunks of each 128-byte bucket are XOR-swizzled
 // with the bucket index so that lanes probing random buckets spread over the banks.
-DEV uint32_t lds_chunk(uint32_t b, uint32_t q) { return b * 8 + (q ^ (b & 7)); }
+// (bits 1..3 of the bucket: with bit 0 selecting the 128-byte half of a 256-byte bank row,
+// the chunk of a random bucket lands on any of the 16 bank quads)
+DEV uint32_t lds_chunk(uint32_t b, uint32_t q) { return b * 8 + (q ^ ((b >> 1) & 7)); }
 DEV uint64_t* lds_word(uint64_t* lt, uint32_t b, uint32_t word) {
     return lt + lds_chunk(b, word >> 1) * 2 + (word & 1);
+}
+
+// 8-bit slot tags (LDS only, beside the region image): one u64 per bucket, byte s = the tag
+// of slot s, 0 = empty.  A probe reads the bucket's tags (one ds_read_b64) and the key words
+// of the slots whose tag matches, instead of every key word of the bucket.
+#ifndef KC_P3_TAGS
+#define KC_P3_TAGS 1
+#endif
+DEV uint32_t slot_tag(uint64_t t0) { return 1u + (((uint32_t)t0 & 0xFFu) * 255u >> 8); }
+// bit i set iff byte i of x is zero (exact: no borrow between bytes)
+DEV uint32_t zero_byte_mask4(uint32_t x) {
+    const uint32_t z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);  // bit 7 of each zero byte
+    return ((z >> 7) * 0x01020408u) >> 24;                                       // bits 7/15/23/31 -> 0..3
+}
+DEV uint32_t zero_byte_mask8(uint64_t x) {
+    return zero_byte_mask4((uint32_t)x) | zero_byte_mask4((uint32_t)(x >> 32)) << 4;
 }
 
 // Level 3: one workgroup per region: LDS-resident table
@@ -800,6 +821,7 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
         if (gated_off(gate)) return;
     }
     uint64_t* lt = reinterpret_cast<uint64_t*>(smem);  // BPR * BUCKET_WORDS words
+    uint64_t* tg = lt + BPR * BUCKET_WORDS;             // KC_P3_TAGS: BPR tag words
     const uint64_t r = blockIdx.x;
     uint64_t start, end;
     if constexpr (SEG) {
@@ -824,12 +846,26 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
     uint4* g4 = reinterpret_cast<uint4*>(tv.buckets + r * BPR * BUCKET_WORDS);
     uint4* l4 = reinterpret_cast<uint4*>(lt);
     constexpr int N4 = BPR * BUCKET_WORDS / 2;
+    constexpr int NT4 = KC_P3_TAGS ? BPR / 2 : 0;  // tag words, as uint4
     if (fresh) {
-        for (int i = threadIdx.x; i < N4; i += NT) l4[i] = make_uint4(0, 0, 0, 0);
+        for (int i = threadIdx.x; i < N4 + NT4; i += NT) l4[i] = make_uint4(0, 0, 0, 0);
+        __syncthreads();
     } else {
         for (int i = threadIdx.x; i < N4; i += NT) l4[lds_chunk(i >> 3, i & 7)] = g4[i];
+        __syncthreads();
+        if constexpr (KC_P3_TAGS) {
+            for (int bb = threadIdx.x; bb < BPR; bb += NT) {
+                uint64_t t = 0;
+#pragma unroll
+                for (int sl = 0; sl < S; sl++) {
+                    const uint64_t w0 = *lds_word(lt, bb, sl * W);
+                    if (w0 != EMPTY) t |= (uint64_t)slot_tag(w0) << (8 * sl);
+                }
+                tg[bb] = t;
+            }
+            __syncthreads();
+        }
     }
-    __syncthreads();
     uint32_t n_fail = 0;
     uint32_t cs = 0;  // SEG: segment cursor of this thread (indices grow monotonically)
     for (uint64_t base = start; base < end; base += (uint64_t)KB * NT) {
@@ -858,7 +894,60 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
             const uint64_t k0 = kk[q][0];
             uint32_t b = bucket_in_region(k0, tv.R);
             bool done = false;
-            if constexpr (W == 1) {
+            if constexpr (KC_P3_TAGS) {
+                constexpr uint32_t SMASK = (1u << S) - 1;
+                const uint32_t tag = slot_tag(k0);
+                const uint64_t bc = 0x0101010101010101ULL * tag;
+                for (int probe = 0; probe < 4 * BPR && !done;) {
+                    const uint64_t tw = tg[b];
+                    uint32_t m = zero_byte_mask8(tw ^ bc) & SMASK;
+                    int slot = -1;
+                    while (m) {  // candidates: usually none (new key) or exactly the key's slot
+                        const int sl = __builtin_ctz(m);
+                        m &= m - 1;
+                        bool eq = *lds_word(lt, b, sl * W) == k0;
+#pragma unroll
+                        for (int w = 1; w < W; w++) eq &= *lds_word(lt, b, sl * W + w) == kk[q][w];
+                        if (eq) {
+                            slot = sl;
+                            break;
+                        }
+                    }
+                    uint64_t a = add[q];
+                    if (slot < 0) {
+                        const uint32_t em = zero_byte_mask8(tw) & SMASK;
+                        if (!em) {  // bucket full, key absent: next bucket
+                            b = (b + 1) & (BPR - 1);
+                            probe++;
+                            continue;
+                        }
+                        // claim the first untagged slot by its word 0; the tag is stored last, so
+                        // a tag match always finds the key's words published
+                        const int e = __builtin_ctz(em);
+                        const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long*>(lds_word(lt, b, e * W)),
+                                                       0ULL, (unsigned long long)k0);
+                        if (old == EMPTY) {
+#pragma unroll
+                            for (int w = 1; w < W; w++)
+                                __hip_atomic_store(lds_word(lt, b, e * W + w), kk[q][w], __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+                            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                            __hip_atomic_store(reinterpret_cast<uint8_t*>(tg + b) + e, (uint8_t)tag, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+                            if constexpr (W > 1) a += READY;  // the table format's published flag
+                            slot = e;
+                        } else if (W == 1 && old == k0) {
+                            slot = e;  // the same key, claimed an instant ago
+                        } else {
+                            probe++;  // claimed by another key (tag not yet stored): read again
+                            continue;
+                        }
+                    }
+                    atomicAdd(reinterpret_cast<unsigned long long*>(lds_word(lt, b, S * W + slot)),
+                              (unsigned long long)a);
+                    done = true;
+                }
+            } else if constexpr (W == 1) {
                 // branch-light probe: match / first-empty masks over the 8 slots of a bucket
                 for (int probe = 0; probe < 2 * BPR && !done;) {
                     uint32_t eqm = 0, emm = 0;
@@ -889,7 +978,7 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
                     }
                 }
             }
-            if constexpr (W > 1) {
+            if constexpr (!KC_P3_TAGS && W > 1) {
                 // branch-light probe over a whole bucket: the count words are read first and
                 // the key words after a wait, so a READY count guarantees that the key words
                 // read after it are published (the claimer stores them before setting READY)
@@ -1094,7 +1183,7 @@ static uint64_t pow5_mod54(int e) {
 }
 
 int run_width(int W) { return W == 1 ? 16 : 8; }
-int p1_tile(int W) { return P1_THREADS * run_width(W); }
+int p1_tile(int W) { return (W <= 2 ? KC_SCATTER_NT12 : 512) * run_width(W); }
 
 template <int W>
 static hipError_t launch_count_w(PackedView sym, uint64_t sym_bound, int k, int mode, TableView t, BloomView bf,
@@ -1133,7 +1222,7 @@ static BinRegion coarse_bins(const TableView& t) { return BinRegion{t.R, t.f2bit
 template <int W, bool SEG, bool CNT = false>
 static hipError_t launch_p3(TableView t, DevCounters* ctr, PartBufs pb, const unsigned long long* gate, int fresh,
                             hipStream_t s) {
-    const size_t sm3 = (size_t)BPR * BUCKET_WORDS * 8;
+    const size_t sm3 = (size_t)BPR * BUCKET_WORDS * 8 + (KC_P3_TAGS ? (size_t)BPR * 8 : 0);
     auto p3 = k_p3<W, SEG, CNT>;
     hipError_t e = set_smem(p3, sm3);
     if (e != hipSuccess) return e;
@@ -1193,19 +1282,19 @@ static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf
     const unsigned long long* gate = &ctr->part_overflow;
     if ((e = hipMemsetAsync(&ctr->part_overflow, 0, sizeof(ctr->part_overflow), s)) != hipSuccess) return e;
     const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
-    auto k1 = k_p1<W, MODE, true, BinRegion, OutSeg, P1_THREADS>;
+    auto k1 = k_p1<W, MODE, true, BinRegion, OutSeg, scatter_threads<W>()>;
     static const uint32_t p2f_pad = [] {  // A/B knob: reserve LDS as if for this many segments
         const char* v = std::getenv("KC_P2F_SEGS");
         return v ? (uint32_t)std::atoi(v) : 0u;
     }();
-    const size_t sm1 = part_smem<W, P1_THREADS>(t.F1),
-                 sm2 = p2f_smem<W, P2F_THREADS>(t.F2, std::max<uint32_t>(p2f_pad, (pb.nblk1 + pb.B2 - 1) / pb.B2));
+    const size_t sm1 = part_smem<W, scatter_threads<W>()>(t.F1),
+                 sm2 = p2f_smem<W, scatter_threads<W>()>(t.F2, std::max<uint32_t>(p2f_pad, (pb.nblk1 + pb.B2 - 1) / pb.B2));
     if ((e = set_smem(k1, sm1)) != hipSuccess) return e;
-    if ((e = set_smem(k_p2f<W, P2F_THREADS>, sm2)) != hipSuccess) return e;
+    if ((e = set_smem(k_p2f<W, scatter_threads<W>()>, sm2)) != hipSuccess) return e;
     const OutSeg o1{(uint64_t)pb.nblk1 * pb.cap1, 0, pb.cap1};
-    hipLaunchKernelGGL(k1, dim3(pb.nblk1), dim3(P1_THREADS), sm1, s, sym, k, bf, ctr, pb, t.F1, coarse_bins(t),
+    hipLaunchKernelGGL(k1, dim3(pb.nblk1), dim3(scatter_threads<W>()), sm1, s, sym, k, bf, ctr, pb, t.F1, coarse_bins(t),
                        pb.keys1, pk, pkm1, o1, (const unsigned long long*)nullptr, 1);
-    hipLaunchKernelGGL((k_p2f<W, P2F_THREADS>), dim3(t.F1 * pb.B2), dim3(P2F_THREADS), sm2, s, t, pb, ctr);
+    hipLaunchKernelGGL((k_p2f<W, scatter_threads<W>()>), dim3(t.F1 * pb.B2), dim3(scatter_threads<W>()), sm2, s, t, pb, ctr);
     if ((e = launch_p3<W, true>(t, ctr, pb, nullptr, fresh, s)) != hipSuccess) return e;
     if ((e = part_level1<W, MODE>(sym, k, bf, ctr, pb, t.F1, coarse_bins(t), pb.keys1, s, gate)) != hipSuccess)
         return e;
