@@ -931,51 +931,108 @@ int kc_dump(kc_ctx* c, uint64_t** records, uint64_t* n_records) {
     return KC_OK;
 }
 
+// Text output formatted on the device (the reference formats on one host
+// thread, kmer_hash_table.cpp:4318-4524): k_text_bytes + scan give every TEXT_T-bucket
+// block its offset in the text, then pieces of <= KC_TEXT_PIECE bytes are formatted by
+// k_text, copied to pinned memory and written while the next piece is formatted
+// (64 MiB pieces; KC_TEXT_PIECE overrides, >= 128 KiB so a block always fits).
+// Lines come out in table order (the reference's order is unspecified too).
+static uint64_t text_piece_bytes() {
+    const char* e = std::getenv("KC_TEXT_PIECE");  // tests: force many pieces
+    const uint64_t v = e ? std::strtoull(e, nullptr, 10) : 0;
+    return v ? std::max<uint64_t>(v, 1ull << 17) : 64ull << 20;
+}
+
 int kc_write(kc_ctx* c, const char* path) {
     if (!c || !path) return KC_ERR_ARG;
     if (c->cfg.min_abundance == 0) return KC_OK;  // parallel_parser.hpp:1536 / 858
-    uint64_t* rec = nullptr;
-    uint64_t n = 0;
-    int rc = kc_dump(c, &rec, &n);
+    int rc = kc_sync(c);
     if (rc) return rc;
-    FILE* f = std::fopen(path, "wb");
-    if (!f) { kc_free(rec); return c->fail(KC_ERR_IO, std::string("cannot open ") + path); }
-    const int k = c->cfg.k, W = c->W;
-    const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    const uint64_t block = 1 << 16;
-    std::vector<std::string> bufs(nt);
-    static const char sym[4] = {'A', 'C', 'G', 'T'};
-    for (uint64_t b0 = 0; b0 < n; b0 += block * nt) {
-        std::vector<std::thread> th;
-        for (unsigned t = 0; t < nt; t++) {
-            th.emplace_back([&, t]() {
-                std::string& s = bufs[t];
-                s.clear();
-                const uint64_t lo = b0 + t * block, hi = std::min(n, lo + block);
-                if (lo >= hi) return;
-                s.reserve((hi - lo) * (k + 8));
-                char line[160];
-                for (uint64_t i = lo; i < hi; i++) {
-                    const uint64_t* r = rec + i * (W + 1);
-                    for (int j = 0; j < k; j++) {
-                        const int bit = 2 * (k - 1 - j);
-                        line[j] = sym[(r[W - 1 - bit / 64] >> (bit % 64)) & 3];
-                    }
-                    int len = k + std::snprintf(line + k, sizeof(line) - k, " %llu\n", (unsigned long long)r[W]);
-                    s.append(line, len);
-                }
-            });
+    if (!c->d_table) return c->fail(KC_ERR_STATE, "no table");
+    const TableView tv = table_view(c);
+    const int cm = c->cfg.mode == 0 ? 0 : 1;
+    const uint64_t a = c->cfg.min_abundance;
+    const uint64_t nblk = (c->nbuckets + TEXT_T - 1) / TEXT_T;
+    uint32_t* d_bb = nullptr;
+    uint64_t *d_off = nullptr, *d_bsum = nullptr;
+    uint8_t* d_txt[2] = {nullptr, nullptr};
+    uint8_t* h_txt[2] = {nullptr, nullptr};
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    std::vector<uint64_t> off(nblk + 1);
+    std::vector<uint32_t> bb(nblk);
+    FILE* f = nullptr;
+    auto cleanup = [&]() {
+        hipStreamSynchronize(c->stream);
+        hipFree(d_bb);
+        hipFree(d_off);
+        hipFree(d_bsum);
+        for (int i = 0; i < 2; i++) {
+            hipFree(d_txt[i]);
+            if (h_txt[i]) hipHostFree(h_txt[i]);
+            if (ev[i]) hipEventDestroy(ev[i]);
         }
-        for (auto& x : th) x.join();
-        for (unsigned t = 0; t < nt; t++)
-            if (!bufs[t].empty() && std::fwrite(bufs[t].data(), 1, bufs[t].size(), f) != bufs[t].size()) {
-                std::fclose(f);
-                kc_free(rec);
-                return c->fail(KC_ERR_IO, "write failed");
-            }
+        if (f) std::fclose(f);
+    };
+    auto fail = [&](int code, const std::string& m) {
+        cleanup();
+        return c->fail(code, m);
+    };
+#define TXCHK(x)                                                                         \
+    do {                                                                                 \
+        hipError_t e_ = (x);                                                             \
+        if (e_ != hipSuccess) return fail(KC_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+    if (hipMalloc(&d_bb, nblk * 4) != hipSuccess || hipMalloc(&d_off, (nblk + 1) * 8) != hipSuccess ||
+        hipMalloc(&d_bsum, ((nblk + 4095) / 4096 + 2) * 8) != hipSuccess)
+        return fail(KC_ERR_NOMEM, "text offset allocation failed");
+    TXCHK(launch_text_bytes(tv, cm, a, c->cfg.k, d_bb, d_off, d_bsum, c->stream));
+    TXCHK(hipMemcpyAsync(off.data(), d_off, (nblk + 1) * 8, hipMemcpyDeviceToHost, c->stream));
+    TXCHK(hipMemcpyAsync(bb.data(), d_bb, nblk * 4, hipMemcpyDeviceToHost, c->stream));
+    TXCHK(hipStreamSynchronize(c->stream));
+    const uint64_t total = off[nblk];
+    f = std::fopen(path, "wb");
+    if (!f) return fail(KC_ERR_IO, std::string("cannot open ") + path);
+    // pieces: maximal runs of blocks whose text fits one piece buffer (a block's text is
+    // at most TEXT_T * S * (k + 7) bytes < 128 KiB, so every block fits)
+    const uint64_t cap = std::min<uint64_t>(text_piece_bytes(), std::max<uint64_t>(total, 1));
+    struct Piece { uint64_t b0, b1; uint32_t lds; };
+    std::vector<Piece> pieces;
+    for (uint64_t b0 = 0; b0 < nblk;) {
+        uint64_t b1 = b0;
+        uint32_t mx = 0;
+        while (b1 < nblk && off[b1 + 1] - off[b0] <= cap) mx = std::max(mx, bb[b1++]);
+        if (b1 == b0) return fail(KC_ERR_STATE, "text block larger than a piece");
+        if (off[b1] > off[b0]) pieces.push_back({b0, b1, (mx + 15) & ~15u});
+        b0 = b1;
     }
-    std::fclose(f);
-    kc_free(rec);
+    const int nbuf = pieces.size() > 1 ? 2 : 1;
+    for (int i = 0; i < nbuf && !pieces.empty(); i++) {
+        if (hipMalloc(&d_txt[i], cap) != hipSuccess || hipHostMalloc(&h_txt[i], cap, hipHostMallocDefault) != hipSuccess)
+            return fail(KC_ERR_NOMEM, "text buffer allocation failed");
+        TXCHK(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
+    }
+    for (size_t i = 0; i <= pieces.size(); i++) {
+        if (i < pieces.size()) {  // format piece i while piece i - 1 is written
+            const Piece& p = pieces[i];
+            const int q = (int)(i % nbuf);
+            const uint64_t len = off[p.b1] - off[p.b0];
+            TXCHK(launch_text(tv, cm, a, c->cfg.k, p.b0, p.b1 - p.b0, d_off, off[p.b0], d_txt[q], p.lds, c->stream));
+            TXCHK(hipMemcpyAsync(h_txt[q], d_txt[q], len, hipMemcpyDeviceToHost, c->stream));
+            TXCHK(hipEventRecord(ev[q], c->stream));
+        }
+        if (i >= 1) {
+            const Piece& p = pieces[i - 1];
+            const int q = (int)((i - 1) % nbuf);
+            const uint64_t len = off[p.b1] - off[p.b0];
+            TXCHK(hipEventSynchronize(ev[q]));
+            if (std::fwrite(h_txt[q], 1, len, f) != len) return fail(KC_ERR_IO, "write failed");
+        }
+    }
+#undef TXCHK
+    const int cl = std::fclose(f);
+    f = nullptr;
+    cleanup();
+    if (cl != 0) return c->fail(KC_ERR_IO, "write failed");
     return KC_OK;
 }
 

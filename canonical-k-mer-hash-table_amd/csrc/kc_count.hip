@@ -1173,6 +1173,125 @@ __global__ __launch_bounds__(256) void k_dump(TableView tv, int count_mode, uint
     if (lane == 0 && occ_w) atomicAdd(&ctr->occupied, (unsigned long long)occ_w);
 }
 
+// --------------------------------------------------------------------------------
+// GPU output formatting: "<CANONICAL_KMER> <T(c)>\n" for every slot
+// with T(c) >= a, in table order.  Replaces the reference's single-threaded writers
+// write_kmers_on_disk_separately_even_faster (kmer_hash_table.cpp:4318-4524: chain walk,
+// int2char, "<kmer> <count>\n") and write_kmers (2013-2050).  One workgroup formats
+// TEXT_T consecutive buckets: k_text_bytes gives its byte count, the host scans them
+// into block offsets, k_text writes the block's lines into LDS and copies them out
+// contiguously at its offset (one text stream, no per-line atomics).
+// --------------------------------------------------------------------------------
+DEV uint32_t ndigits(uint32_t t) { return t >= 10000 ? 5 : t >= 1000 ? 4 : t >= 100 ? 3 : t >= 10 ? 2 : 1; }
+
+// T(c) of each emitted slot (0 = no line: a >= 1 so an emitted T(c) is >= 1); returns
+// the bucket's text bytes
+template <int W, int S = BUCKET_WORDS / (W + 1)>
+DEV uint32_t text_bucket(const TableView& tv, uint64_t bkt, int count_mode, uint64_t a, int k,
+                         uint64_t (&bw)[BUCKET_WORDS], uint32_t (&tc)[S]) {
+    uint32_t bytes = 0;
+    if (bkt < tv.nbuckets) load_bucket(tv.buckets + bkt * BUCKET_WORDS, bw);
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+        tc[s] = 0;
+        if (bkt < tv.nbuckets && bw[s * W] != EMPTY) {
+            const uint64_t c = bw[S * W + s] & CNT_MASK;
+            const uint64_t t = count_mode == 0 ? (c & 0xFFFF) : (c < 16383 ? c : 16383);
+            if (t >= a) {
+                tc[s] = (uint32_t)t;
+                bytes += (uint32_t)k + 2 + ndigits((uint32_t)t);
+            }
+        }
+    }
+    return bytes;
+}
+
+template <int NT>
+DEV uint32_t block_excl_sum(uint32_t v, uint32_t* s_w, uint32_t& total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t incl = wave_incl_sum(v);
+    if (lane == 63) s_w[wid] = incl;
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; w++) {
+        const uint32_t x = s_w[w];
+        base += w < wid ? x : 0;
+        tot += x;
+    }
+    total = tot;
+    return base + incl - v;
+}
+
+template <int W>
+__global__ __launch_bounds__(TEXT_T) void k_text_bytes(TableView tv, int count_mode, uint64_t a, int k,
+                                                       uint32_t* __restrict__ block_bytes) {
+    constexpr int S = BUCKET_WORDS / (W + 1);
+    __shared__ uint32_t s_w[TEXT_T / 64];
+    uint64_t bw[BUCKET_WORDS];
+    uint32_t tc[S];
+    const uint32_t v = text_bucket<W>(tv, (uint64_t)blockIdx.x * TEXT_T + threadIdx.x, count_mode, a, k, bw, tc);
+    uint32_t total;
+    block_excl_sum<TEXT_T>(v, s_w, total);
+    if (threadIdx.x == 0) block_bytes[blockIdx.x] = total;
+}
+
+// blocks [blk0, blk0 + grid) write at out + off[b] - base; dynamic LDS >= the largest
+// block's bytes
+template <int W>
+__global__ __launch_bounds__(TEXT_T) void k_text(TableView tv, int count_mode, uint64_t a, int k, uint64_t blk0,
+                                                 const uint64_t* __restrict__ off, uint64_t base,
+                                                 uint8_t* __restrict__ out) {
+    constexpr int S = BUCKET_WORDS / (W + 1);
+    extern __shared__ uint8_t s_txt[];
+    __shared__ uint32_t s_w[TEXT_T / 64];
+    const uint64_t b = blk0 + blockIdx.x;
+    uint64_t bw[BUCKET_WORDS];
+    uint32_t tc[S];
+    const uint32_t v = text_bucket<W>(tv, b * TEXT_T + threadIdx.x, count_mode, a, k, bw, tc);
+    uint32_t total;
+    uint32_t pos = block_excl_sum<TEXT_T>(v, s_w, total);
+    const int c0 = k - 32 * (W - 1);  // characters in key word 0 (the others hold 32)
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+        if (!tc[s]) continue;
+        uint64_t t[W], key[W];
+#pragma unroll
+        for (int i = 0; i < W; i++) t[i] = bw[s * W + i];
+        from_tkey<W>(t, key);
+        uint8_t* p = s_txt + pos;
+#pragma unroll
+        for (int w = 0; w < W; w++) {
+            const int nc = w == 0 ? c0 : 32;
+            const uint64_t x = key[w];
+            for (int q = nc - 1; q >= 0; q--) *p++ = (uint8_t)(0x54474341u >> (8 * ((x >> (2 * q)) & 3)));
+        }
+        *p++ = ' ';
+        uint32_t cnt = tc[s];
+        const uint32_t nd = ndigits(cnt);
+        for (int d = (int)nd - 1; d >= 0; d--) {
+            p[d] = (uint8_t)('0' + cnt % 10);
+            cnt /= 10;
+        }
+        p[nd] = '\n';
+        pos += (uint32_t)k + 2 + nd;
+    }
+    __syncthreads();
+    uint8_t* o = out + (off[b] - base);
+    // copy out: byte head up to a 4-byte boundary of the destination, then dwords
+    const uint32_t head = (uint32_t)((4 - ((uintptr_t)o & 3)) & 3) < total ? (uint32_t)((4 - ((uintptr_t)o & 3)) & 3)
+                                                                            : total;
+    if (threadIdx.x < head) o[threadIdx.x] = s_txt[threadIdx.x];
+    const uint32_t nw = (total - head) / 4;
+    uint32_t* o4 = reinterpret_cast<uint32_t*>(o + head);
+    for (uint32_t i = threadIdx.x; i < nw; i += TEXT_T) {
+        const uint8_t* q = s_txt + head + 4 * i;
+        o4[i] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+    }
+    const uint32_t tail0 = head + 4 * nw;
+    if (tail0 + threadIdx.x < total) o[tail0 + threadIdx.x] = s_txt[tail0 + threadIdx.x];
+}
+
 // ================================================================================
 // launchers
 // ================================================================================
@@ -1430,6 +1549,44 @@ hipError_t launch_dump(TableView t, int count_mode, uint64_t min_abundance, uint
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
+}
+
+hipError_t launch_text_bytes(TableView t, int count_mode, uint64_t a, int k, uint32_t* block_bytes, uint64_t* off,
+                             uint64_t* bsum, hipStream_t s) {
+    const uint64_t nblk = (t.nbuckets + TEXT_T - 1) / TEXT_T;
+    if (nblk == 0 || nblk > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    switch (t.W) {
+    case 1: hipLaunchKernelGGL(k_text_bytes<1>, dim3((unsigned)nblk), dim3(TEXT_T), 0, s, t, count_mode, a, k, block_bytes); break;
+    case 2: hipLaunchKernelGGL(k_text_bytes<2>, dim3((unsigned)nblk), dim3(TEXT_T), 0, s, t, count_mode, a, k, block_bytes); break;
+    case 3: hipLaunchKernelGGL(k_text_bytes<3>, dim3((unsigned)nblk), dim3(TEXT_T), 0, s, t, count_mode, a, k, block_bytes); break;
+    case 4: hipLaunchKernelGGL(k_text_bytes<4>, dim3((unsigned)nblk), dim3(TEXT_T), 0, s, t, count_mode, a, k, block_bytes); break;
+    default: return hipErrorInvalidValue;
+    }
+    launch_scan(block_bytes, nblk, off, bsum, s);
+    return hipGetLastError();
+}
+
+template <int W>
+static hipError_t text_w(TableView t, int count_mode, uint64_t a, int k, uint64_t blk0, uint64_t nblk,
+                         const uint64_t* off, uint64_t base, uint8_t* out, size_t lds, hipStream_t s) {
+    auto kern = k_text<W>;
+    hipError_t e = set_smem(kern, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(TEXT_T), lds, s, t, count_mode, a, k, blk0, off, base, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_text(TableView t, int count_mode, uint64_t a, int k, uint64_t blk0, uint64_t nblk,
+                       const uint64_t* off, uint64_t base, uint8_t* out, size_t lds, hipStream_t s) {
+    if (nblk == 0) return hipSuccess;
+    if (nblk > 0x7FFFFFFFull || lds > 160 * 1024) return hipErrorInvalidValue;
+    switch (t.W) {
+    case 1: return text_w<1>(t, count_mode, a, k, blk0, nblk, off, base, out, lds, s);
+    case 2: return text_w<2>(t, count_mode, a, k, blk0, nblk, off, base, out, lds, s);
+    case 3: return text_w<3>(t, count_mode, a, k, blk0, nblk, off, base, out, lds, s);
+    case 4: return text_w<4>(t, count_mode, a, k, blk0, nblk, off, base, out, lds, s);
+    default: return hipErrorInvalidValue;
+    }
 }
 
 }  // namespace kc

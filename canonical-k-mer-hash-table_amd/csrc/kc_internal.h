@@ -20,6 +20,7 @@ constexpr uint64_t EMPTY = 0;              // empty slot (a stored word 0 is nev
 constexpr int BPR_BITS = 9;
 constexpr uint64_t READY = 1ULL << 62;     // multi-word slot published flag, in the count word
 constexpr uint64_t CNT_MASK = READY - 1;
+constexpr int TEXT_T = 256;                // buckets per workgroup of the text formatter
 constexpr int MAX_NH = 10;                 // -f >= 0.001  =>  ceil(-ln f / ln 2) <= 10
 constexpr uint8_t SYM_BREAK = 4;
 
@@ -138,6 +139,14 @@ hipError_t launch_insert_counts(const uint64_t* rec, uint64_t n, bool partitione
                                 PartBufs pb, int fresh, hipStream_t s);
 hipError_t launch_dump(TableView t, int count_mode, uint64_t min_abundance, uint64_t* out, DevCounters* ctr,
                        hipStream_t s);
+// GPU text formatting (kc_write): bytes of each TEXT_T-bucket block into block_bytes and
+// their exclusive scan into off (off[nblocks] = total; bsum: (nblocks + 4095) / 4096 + 2
+// words of scratch); then k_text for blocks [blk0, blk0 + nblk) into out (offset base),
+// lds >= the largest of those blocks' bytes
+hipError_t launch_text_bytes(TableView t, int count_mode, uint64_t a, int k, uint32_t* block_bytes, uint64_t* off,
+                             uint64_t* bsum, hipStream_t s);
+hipError_t launch_text(TableView t, int count_mode, uint64_t a, int k, uint64_t blk0, uint64_t nblk,
+                       const uint64_t* off, uint64_t base, uint8_t* out, size_t lds, hipStream_t s);
 hipError_t launch_synth(uint8_t* dst, uint64_t first_read, uint64_t n_reads, uint64_t seed, uint64_t genome_len,
                         uint32_t read_len, uint32_t wrap, double err_rate, double n_rate, hipStream_t s);
 

@@ -82,6 +82,10 @@ def test_golden_case_host_chunks(case, golden_input, tmp_path, insert_path):
             assert sorted_digest_lines(lines) == (case["sorted_sha256"], case["lines"])
         if case["distinct"] is not None and not o["bf_enable"]:
             assert st["distinct"] == case["distinct"]
+        # the device text formatter (kc_write) gives the same lines as the records
+        out = tmp_path / "out.txt"
+        kc.write(str(out))
+        assert sorted(open(out).read().splitlines()) == sorted(lines)
 
 
 @pytest.mark.parametrize("name,k,args", [
@@ -216,3 +220,31 @@ def test_segment_overflow_falls_back_to_exact(name, k, args, golden_input, tmp_p
     out = tmp_path / "oracle.txt"
     oracle_count(path, k, args, out)
     assert sorted_digest_lines(lines) == sorted_digest_file(out)
+
+
+@pytest.mark.parametrize("piece", [0, 1 << 17])
+def test_device_text_writer_at_scale(piece, monkeypatch, tmp_path):
+    """kc_write formats on the device in pieces (KC_TEXT_PIECE forces small ones, so the
+    double-buffered copy-out runs many times): one line per distinct k-mer, the counts
+    sum to the windows, and the lines equal the decoded records."""
+    torch = pytest.importorskip("torch")
+    if piece:
+        monkeypatch.setenv("KC_TEXT_PIECE", str(piece))
+    lib = ka.load_library()
+    N, L, G = 20_000, 150, 1_000_000
+    nbytes = lib.kc_synth_bytes(0, N, L, 0)
+    img = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    assert lib.kc_synth_device(img.data_ptr(), 0, N, 7, G, L, 0, 0.01, 0.001, 0) == 0
+    torch.cuda.synchronize()
+    host = bytes(img.cpu().numpy())
+    for k, mode in ((31, 2), (51, 0), (100, 2)):
+        chunks = ka.plan_chunks(host, k, ka.FMT_FASTA)
+        with ka.KmerCounter(ka.Config(k=k, mode=mode, min_abundance=1, table_slots=8_000_000)) as kc:
+            kc.count_device(img.data_ptr(), chunks, ka.FMT_FASTA)
+            st = kc.finish()
+            out = tmp_path / f"w{k}.txt"
+            kc.write(str(out))
+            text = open(out).read().splitlines()
+            assert len(text) == st["distinct"]
+            assert sum(int(l.rsplit(" ", 1)[1]) for l in text) == st["windows"]
+            assert sorted(text) == kc.lines()
