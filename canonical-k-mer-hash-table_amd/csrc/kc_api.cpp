@@ -344,8 +344,7 @@ static int flush_host(kc_ctx* c) {
 
 static int add_host_chunk(kc_ctx* c, const uint8_t* buf, size_t len, int fmt, int bh, int pass) {
     if (!buf && len) return c->fail(KC_ERR_ARG, "null buffer");
-    if (fmt == KC_FMT_FASTQ) return c->fail(KC_ERR_UNSUPPORTED, "Input file format not supported.");
-    if (fmt != KC_FMT_FASTA && fmt != KC_FMT_PLAIN) return c->fail(KC_ERR_ARG, "unknown format");
+    if (fmt != KC_FMT_FASTA && fmt != KC_FMT_FASTQ && fmt != KC_FMT_PLAIN) return c->fail(KC_ERR_ARG, "unknown format");
     if (len == 0) return KC_OK;
     const uint64_t need = round_up(len, TILE);
     if (need > c->batch_bytes) return c->fail(KC_ERR_ARG, "chunk larger than the staging batch");
@@ -378,8 +377,7 @@ static int add_host_chunk(kc_ctx* c, const uint8_t* buf, size_t len, int fmt, in
 
 static int device_pass(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, size_t n, int fmt, int pass,
                        hipStream_t s) {
-    if (fmt == KC_FMT_FASTQ) return c->fail(KC_ERR_UNSUPPORTED, "Input file format not supported.");
-    if (fmt != KC_FMT_FASTA && fmt != KC_FMT_PLAIN) return c->fail(KC_ERR_ARG, "unknown format");
+    if (fmt != KC_FMT_FASTA && fmt != KC_FMT_FASTQ && fmt != KC_FMT_PLAIN) return c->fail(KC_ERR_ARG, "unknown format");
     int rc = flush_host(c);  // keep order with staged host chunks
     if (rc) return rc;
     if (s != c->stream) {
@@ -595,8 +593,7 @@ int kc_count_device(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, size_
 int kc_route_device(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, size_t n, int fmt, uint32_t nshards,
                     uint64_t* dev_out, uint64_t out_capacity, uint64_t* counts, void* sp) {
     if (!c || !counts || !dev_out || nshards == 0 || (!img && n) || (!chunks && n)) return KC_ERR_ARG;
-    if (fmt == KC_FMT_FASTQ) return c->fail(KC_ERR_UNSUPPORTED, "Input file format not supported.");
-    if (fmt != KC_FMT_FASTA && fmt != KC_FMT_PLAIN) return c->fail(KC_ERR_ARG, "unknown format");
+    if (fmt != KC_FMT_FASTA && fmt != KC_FMT_FASTQ && fmt != KC_FMT_PLAIN) return c->fail(KC_ERR_ARG, "unknown format");
     if (c->cfg.bf_enable) return c->fail(KC_ERR_UNSUPPORTED, "sharded counting with the Bloom filter is not supported");
     hipStream_t s = pick_stream(c, sp);
     int rc = flush_host(c);
@@ -1040,8 +1037,40 @@ int kc_plan_chunks(const uint8_t* image, uint64_t size, int k, uint64_t chunk_si
                    uint64_t* n_out) {
     if (!out || !n_out || k < 1 || (!image && size)) return KC_ERR_ARG;
     if (chunk_size == 0) chunk_size = 10ull << 20;  // main.cpp:387
-    const unsigned char start = fmt == KC_FMT_FASTA ? '>' : fmt == KC_FMT_FASTQ ? '@' : 0;
     std::vector<kc_chunk> v;
+    if (fmt == KC_FMT_FASTQ) {
+        // FASTQ (extension; the reference rejects it): chunks of whole 4-line records, no
+        // overlap (a k-mer never spans records).  A record starts at a line that begins
+        // with '@' and whose second next line begins with '+' (a quality line starting
+        // with '@' is followed two lines later by a sequence line, never by '+').
+        auto line_after = [&](uint64_t p) -> uint64_t {  // start of the line after the one at p
+            const void* q = std::memchr(image + p, '\n', size - p);
+            return q ? (uint64_t)((const uint8_t*)q - image) + 1 : size;
+        };
+        auto is_record = [&](uint64_t p) {
+            if (p >= size || image[p] != '@') return false;
+            const uint64_t l2 = line_after(line_after(p));
+            return l2 < size && image[l2] == '+';
+        };
+        uint64_t pos = 0;
+        while (pos < size) {
+            uint64_t end = size;
+            if (size - pos > chunk_size) {
+                end = 0;
+                // last record start in (pos, pos + chunk_size]: walk back over line starts
+                for (uint64_t q = pos + chunk_size; q > pos; q--)
+                    if (image[q - 1] == '\n' && is_record(q)) { end = q; break; }
+                if (!end) {  // one record longer than a chunk: cut after it
+                    end = size;
+                    for (uint64_t q = line_after(pos); q < size; q = line_after(q))
+                        if (is_record(q)) { end = q; break; }
+                }
+            }
+            v.push_back(kc_chunk{pos, end - pos, 0, 0});
+            pos = end;
+        }
+    } else {
+    const unsigned char start = fmt == KC_FMT_FASTA ? '>' : 0;
     // io_worker: loop while rem >= k, each chunk min(chunk_size, rem) bytes, then
     // read_chunk_from_file with its k = k-1 (parallel_parser.hpp:1246-1285).
     const int64_t back = (int64_t)k - 1;
@@ -1071,6 +1100,7 @@ int kc_plan_chunks(const uint8_t* image, uint64_t size, int k, uint64_t chunk_si
         if (adv == 0) break;
         rem -= adv;
         pos += (uint64_t)adv;
+    }
     }
     kc_chunk* r = (kc_chunk*)std::malloc(std::max<size_t>(1, v.size()) * sizeof(kc_chunk));
     if (!r) return KC_ERR_NOMEM;

@@ -261,10 +261,6 @@ int main(int argc, char** argv) {
     std::cout << "  output file:              " << a.output << std::endl;
     std::cout << "  device:                   MI355X (HIP device " << a.device << ")" << std::endl;
 
-    if (fmt == KC_FMT_FASTQ) {  // parallel_parser.hpp:1216-1225
-        std::cout << "Input file format not supported.";
-        return 0;
-    }
     if (a.k > 127) {
         std::cerr << "k-mer length above 127 is not supported by this build" << std::endl;
         return 1;

@@ -1,6 +1,6 @@
 // kc_tokenize.hip -- bytes -> symbol stream, and the device read generator.
 //
-//   k_tile_summary  per 4 KiB tile: FASTA newline count + last header marker
+//   k_tile_summary  per 4 KiB tile: FASTA/FASTQ newline count + last FASTA header marker
 //   k_tscan_*       two-level scan: stream offsets + header state entering each tile
 //   k_emit          per tile: bytes -> symbol codes (0..3 base, 4 break); FASTA
 //                   newlines are removed (they do not reset the window,
@@ -12,6 +12,13 @@
 // The tokenizer restates the per-byte loop of hash_kmers (parallel_parser.hpp:
 // 1373-1465 FASTA, 1322-1372 plain) as a scan: the FASTA header state at a byte is
 // the last of {'>' -> 1, '\n' -> 0, chunk start -> broken_header} at or before it.
+//
+// FASTQ (an extension: the reference rejects it, parallel_parser.hpp:1216-1225): chunks
+// hold whole 4-line records (kc_plan_chunks), so the line of a byte is (newlines
+// before it in the batch) mod 4; only line 1 (the sequence) yields symbols, every
+// other byte and every newline is a break -- the counts equal those of the plain-text
+// file of the sequence lines.  The newline count rides in bits 40.. of the tile scan's
+// symbol sum (only its value mod 4 is used; a batch holds < 2^40 symbols).
 #include "kc_common.h"
 #include "kc_synth.h"
 
@@ -87,14 +94,17 @@ __global__ __launch_bounds__(TILE_THREADS) void k_tile_summary(const uint8_t* __
     const uint32_t my0 = tid * 16;
     const uint32_t vh = valid > my0 ? valid - my0 : 0;
     uint32_t nl = 0, mk = 0;
-    if (fmt == FMT_FASTA && vh) {
+    if (fmt != FMT_PLAIN && vh) {
         uint32_t w[4];
         load16(src + cd.src_off + rel + my0, avail - my0, w);
         const uint32_t vmask = vh >= 16 ? 0xFFFFu : ((1u << vh) - 1);
-        const uint32_t nlm = eq_mask16(w, 0x0A0A0A0Au) & vmask, gtm = eq_mask16(w, 0x3E3E3E3Eu) & vmask;
+        const uint32_t nlm = eq_mask16(w, 0x0A0A0A0Au) & vmask;
         nl = __builtin_popcount(nlm);
-        const uint32_t any = nlm | gtm;
-        if (any) mk = (gtm >> (31 - __builtin_clz(any))) & 1 ? 2u : 1u;
+        if (fmt == FMT_FASTA) {
+            const uint32_t gtm = eq_mask16(w, 0x3E3E3E3Eu) & vmask;
+            const uint32_t any = nlm | gtm;
+            if (any) mk = (gtm >> (31 - __builtin_clz(any))) & 1 ? 2u : 1u;
+        }
     }
     // block reductions: sum of nl, last marker
     for (int d = 32; d >= 1; d >>= 1) nl += __shfl_xor(nl, d, 64);
@@ -121,12 +131,18 @@ __global__ __launch_bounds__(TILE_THREADS) void k_tile_summary(const uint8_t* __
 // --------------------------------------------------------------------------------
 // tile scan, two levels:
 //   kept(t)  = valid - (FASTA ? nl : 0) + first   (one break symbol per chunk start)
+//              (+ nl << 40 for FASTQ: the line count rides along)
 //   hs_in(t) = first ? bh : hs_out(t-1);  hs_out = marker ? (marker == '>') : hs_in
 // The header-state recurrence is a "last defining tile" scan (a chunk start or a
 // marker defines the state): transform code 0 = identity, 1 = state 0, 2 = state 1.
 // --------------------------------------------------------------------------------
 constexpr int TSCAN = 1024;
-DEV uint32_t tile_kept(const TileInfo& ti, int fmt) { return ti.valid - (fmt == FMT_FASTA ? ti.nl : 0) + ti.first; }
+constexpr int FQ_SHIFT = 40;
+constexpr uint64_t FQ_MASK = (1ULL << FQ_SHIFT) - 1;
+DEV uint64_t tile_kept(const TileInfo& ti, int fmt) {
+    const uint64_t kept = ti.valid - (fmt == FMT_FASTA ? ti.nl : 0) + ti.first;
+    return fmt == FMT_FASTQ ? kept + ((uint64_t)ti.nl << FQ_SHIFT) : kept;
+}
 DEV uint32_t tile_tr(const TileInfo& ti) { return ti.marker ? (ti.marker == 2 ? 2u : 1u) : (ti.first ? (ti.bh ? 2u : 1u) : 0u); }
 
 // block-wide inclusive scans over 1024 threads (sum, last non-zero)
@@ -190,7 +206,7 @@ __global__ __launch_bounds__(TSCAN) void k_tscan_block(const TileInfo* __restric
 }
 
 // single workgroup: exclusive scan of the block aggregates -> block prefixes
-__global__ __launch_bounds__(TSCAN) void k_tscan_top(TileOut* __restrict__ agg, uint64_t nblk,
+__global__ __launch_bounds__(TSCAN) void k_tscan_top(TileOut* __restrict__ agg, uint64_t nblk, int fmt,
                                                     DevCounters* __restrict__ ctr) {
     __shared__ unsigned long long s_carry;
     __shared__ uint32_t s_tr;
@@ -226,7 +242,7 @@ __global__ __launch_bounds__(TSCAN) void k_tscan_top(TileOut* __restrict__ agg, 
         }
         __syncthreads();
     }
-    if (threadIdx.x == 0) ctr->stream_len = s_carry;
+    if (threadIdx.x == 0) ctr->stream_len = fmt == FMT_FASTQ ? (s_carry & FQ_MASK) : s_carry;
 }
 
 // --------------------------------------------------------------------------------
@@ -246,12 +262,13 @@ __global__ __launch_bounds__(TILE_THREADS) void k_emit(const uint8_t* __restrict
     __shared__ unsigned long long s_pk[NW];
     __shared__ uint32_t s_bk[NW];
     __shared__ uint32_t s_wsum[TILE_THREADS / 64];
-    __shared__ uint32_t s_wmk[TILE_THREADS / 64];
+    __shared__ uint32_t s_wmk[TILE_THREADS / 64];  // FASTA: last marker per wave; FASTQ: newlines per wave
     const uint64_t t = blockIdx.x;
     const TileInfo ti = tiles[t];
     const TileOut to = touts[t];
     const TileOut bp = bpre[t / TSCAN];
-    const uint64_t g0 = bp.out_off + to.out_off;  // global index of the tile's first symbol
+    const uint64_t gsum = bp.out_off + to.out_off;
+    const uint64_t g0 = fmt == FMT_FASTQ ? (gsum & FQ_MASK) : gsum;  // global index of the tile's first symbol
     uint32_t hs_in = to.hs_in ? (to.hs_in == 2 ? 1u : 0u) : bp.hs_in;
     if (ti.first) hs_in = ti.bh;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -297,6 +314,26 @@ __global__ __launch_bounds__(TILE_THREADS) void k_emit(const uint8_t* __restrict
             D = (D | (D << s2)) & 0xFFFFu;
         }
         hdr = (D & V) | (~D & (state ? 0xFFFFu : 0u));
+    } else if (fmt == FMT_FASTQ) {
+        // line of my first byte: newlines before the tile + before me in the tile, mod 4
+        const uint32_t nl = __builtin_popcount(nlm);
+        const uint32_t incl = wave_incl_sum(nl);
+        if (lane == 63) s_wmk[wid] = incl;
+        __syncthreads();
+        uint32_t line = (uint32_t)(gsum >> FQ_SHIFT) + incl - nl;
+        for (int ww = 0; ww < wid; ww++) line += s_wmk[ww];
+        // bytes on a line other than the sequence line (line 1) are breaks
+        uint32_t seq = 0, m = nlm, b0 = 0;
+        line &= 3;
+        while (true) {
+            const uint32_t e = m ? (uint32_t)__builtin_ctz(m) : 16u;
+            if (line == 1) seq |= ((1u << e) - 1) & ~((1u << b0) - 1);
+            if (!m) break;
+            b0 = e + 1;
+            line = (line + 1) & 3;
+            m &= m - 1;
+        }
+        hdr = ~seq & 0xFFFFu;
     }
     const uint32_t keptm = fasta ? (vmask & ~nlm) : vmask;
     uint32_t brk = (hdr | ~acgt) & 0xFFFFu;
@@ -406,7 +443,7 @@ hipError_t launch_tokenize(const uint8_t* src, uint64_t ntiles, const ChunkDesc*
     hipLaunchKernelGGL(k_tile_summary, dim3((unsigned)ntiles), dim3(TILE_THREADS), 0, s, src, d_chunks, n_chunks,
                        fmt, tiles);
     hipLaunchKernelGGL(k_tscan_block, dim3((unsigned)nblk), dim3(TSCAN), 0, s, tiles, ntiles, fmt, touts, tblk);
-    hipLaunchKernelGGL(k_tscan_top, dim3(1), dim3(TSCAN), 0, s, tblk, nblk, ctr);
+    hipLaunchKernelGGL(k_tscan_top, dim3(1), dim3(TSCAN), 0, s, tblk, nblk, fmt, ctr);
     hipLaunchKernelGGL(k_emit, dim3((unsigned)ntiles), dim3(TILE_THREADS), 0, s, src, tiles, touts, tblk, fmt,
                        sv.pk, sv.bk);
     return hipGetLastError();

@@ -348,8 +348,6 @@ def count_file(path: str, k: int, mode: int = 2, min_abundance: int = 2, table_s
     with open(path, "rb") as f:
         image = f.read()
     fmt = detect_format(path, image[0] if image else 0)
-    if fmt == FMT_FASTQ:
-        raise KcError(-7, "Input file format not supported.")
     chunks = plan_chunks(image, k, fmt, chunk_size)
     if not batch_bytes:  # a small input gets a stage of its own size (one batch, little pinned memory)
         staged = 4096 + sum((ln + 4095) // 4096 * 4096 for _, ln, _ in chunks)

@@ -248,3 +248,34 @@ def test_device_text_writer_at_scale(piece, monkeypatch, tmp_path):
             assert len(text) == st["distinct"]
             assert sum(int(l.rsplit(" ", 1)[1]) for l in text) == st["windows"]
             assert sorted(text) == kc.lines()
+
+
+@pytest.mark.parametrize("k", [5, 31, 51])
+def test_fastq_equals_plain_sequence_lines(k, tmp_path):
+    """FASTQ input (an extension: the reference rejects it) counts exactly the k-mers of
+    its sequence lines: the same as the plain one-sequence-per-line file, which the
+    oracle (pinned by the golden fixtures) counts.  Host chunks with small chunk sizes,
+    the device-image path, and the CLI."""
+    torch = pytest.importorskip("torch")
+    from test_host import make_fastq
+    fq, pl = make_fastq(4000)
+    fqp, plp = tmp_path / "r.fastq", tmp_path / "r.txt"
+    fqp.write_bytes(fq)
+    plp.write_bytes(pl)
+    exp = tmp_path / "exp.txt"
+    oracle_count(str(plp), k, ["-a", "1"], exp)
+    want = sorted_digest_file(exp)
+    kc, st = ka.count_file(str(fqp), k, min_abundance=1, table_slots=1 << 22, chunk_size=5000)
+    with kc:
+        assert sorted_digest_lines(kc.lines()) == want
+    chunks = ka.plan_chunks(fq, k, ka.FMT_FASTQ, 20000)
+    dev = torch.frombuffer(bytearray(fq), dtype=torch.uint8).cuda()
+    with ka.KmerCounter(ka.Config(k=k, min_abundance=1, table_slots=1 << 22, batch_bytes=1 << 16)) as kc:
+        kc.count_device(dev.data_ptr(), chunks, ka.FMT_FASTQ, torch.cuda.current_stream().cuda_stream)
+        kc.finish()
+        assert sorted_digest_lines(kc.lines()) == want
+    out = tmp_path / "cli.txt"
+    r = subprocess.run([CLI, str(fqp), str(k), "-t", "3", "-a", "1", "-s", "4000000", "-o", str(out)],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert sorted_digest_file(out) == want

@@ -115,7 +115,35 @@ def test_cli_format_checks(tmp_path):
     r = run_cli(bad, 5, "-s", 100)
     assert r.returncode == 1 and "ill-formed" in r.stderr
     fq = tmp_path / "r.fq"
-    fq.write_bytes(b"@r1\nACGT\n+\nIIII\n")
+    fq.write_bytes(b"ACGT\n")  # FASTQ must start with '@' (FASTQ input is an extension, test_gpu_parity)
     r = run_cli(fq, 3, "-s", 100, "-o", tmp_path / "out.txt")
-    assert r.returncode == 0 and "Input file format not supported." in r.stdout
+    assert r.returncode == 1 and "ill-formed" in r.stderr
     assert not (tmp_path / "out.txt").exists()
+
+
+def make_fastq(n, seed=5, maxlen=300):
+    """4-line FASTQ records with N's, lowercase, and quality lines that begin with '@'
+    or '+' (the cases a naive record finder gets wrong); returns (fastq, plain) bytes,
+    plain = the sequence lines only (what the FASTQ counts must equal)."""
+    import random
+    rng = random.Random(seed)
+    fq, pl = [], []
+    for i in range(n):
+        L = rng.randint(0, maxlen)
+        seq = "".join(rng.choice("ACGTACGTACGTacgtN") for _ in range(L))
+        qual = "".join(rng.choice("@+!#IJ") for _ in range(L))
+        fq.append(f"@read{i} x\n{seq}\n+{'' if i % 2 else 'read' + str(i)}\n{qual}\n")
+        pl.append(seq + "\n")
+    return "".join(fq).encode(), "".join(pl).encode()
+
+
+def test_fastq_chunks_are_whole_records():
+    fq, _ = make_fastq(3000)
+    for cs in (0, 997, 4096, 100003):
+        ch = ka.plan_chunks(fq, 31, ka.FMT_FASTQ, cs)
+        assert ch[0][0] == 0 and sum(ln for _, ln, _ in ch) == len(fq)
+        pos = 0
+        for off, ln, bh in ch:
+            assert off == pos and bh == 0
+            assert fq[off:off + 1] == b"@" and fq[off:off + ln].count(b"\n") % 4 == 0
+            pos = off + ln
