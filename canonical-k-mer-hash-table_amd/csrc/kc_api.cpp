@@ -89,6 +89,7 @@ struct kc_ctx {
     uint32_t* d_bloom = nullptr;
     uint64_t bf_bits = 0;
     int nh = 0, nh_gate = 0;
+    int bloom_blocked = 1;  // KC_BLOOM_LAYOUT=reference: the reference's independent positions
     bool bloom_final = false;
 
     uint64_t n_chunks = 0, n_bytes = 0;
@@ -142,6 +143,13 @@ static void bloom_sizes(uint64_t U, double fpr, uint64_t* bits, int* nh, int* nh
     *bits = b;
     *nh = int(std::ceil(hf));
     *nh_gate = int(uint64_t(hf));
+}
+
+// blocked layout: 512-bit blocks holding 256 positions of both filters
+static uint64_t bloom_blocks(uint64_t bits) { return std::max<uint64_t>(1, bits / 256); }
+static uint64_t bloom_words(const kc_ctx* c) {
+    const uint64_t w = std::max<uint64_t>(1, (2 * c->bf_bits + 31) / 32);
+    return c->bloom_blocked ? std::max<uint64_t>(w, 16 * bloom_blocks(c->bf_bits)) : w;
 }
 
 static int alloc_table(kc_ctx* c, uint64_t min_slots) {
@@ -299,7 +307,8 @@ static int run_batch(kc_ctx* c, const uint8_t* src, uint64_t used, uint64_t nchu
                               used + nchunks, c->d_ctr, s));
     if (c->profiling) HIPCHK(c, hipEventRecord(ev[2], s));
     TableView tv = table_view(c);
-    BloomView bv{c->d_bloom, c->bf_bits ? c->bf_bits - 1 : 0, c->nh, c->nh_gate};
+    BloomView bv{c->d_bloom, c->bf_bits ? c->bf_bits - 1 : 0, c->nh, c->nh_gate, c->bloom_blocked,
+                 bloom_blocks(c->bf_bits) - 1};
     int mode;
     if (pass == 1) mode = 1;
     else mode = (c->cfg.bf_enable && c->cfg.mode != 1) ? 2 : 0;  // -m 1 -b ignores the filter (main.cpp:482-489)
@@ -500,7 +509,9 @@ int kc_create(const kc_config* cfg, kc_ctx** out) {
     if (cfg->bf_enable) {
         bloom_sizes(cfg->est_unique, cfg->fpr, &c->bf_bits, &c->nh, &c->nh_gate);
         if (c->nh > MAX_NH) return bail(KC_ERR_ARG, "too many Bloom hash functions");
-        const uint64_t words = std::max<uint64_t>(1, (2 * c->bf_bits + 31) / 32);
+        const char* lay = std::getenv("KC_BLOOM_LAYOUT");
+        c->bloom_blocked = !(lay && !std::strcmp(lay, "reference"));
+        const uint64_t words = bloom_words(c);
         if (hipMalloc(&c->d_bloom, words * 4) != hipSuccess)
             return bail(KC_ERR_NOMEM, "Bloom filter allocation failed");
         if (hipMemsetAsync(c->d_bloom, 0, words * 4, c->stream) != hipSuccess) return bail(KC_ERR_HIP, "memset");
@@ -838,8 +849,7 @@ int kc_reset(kc_ctx* c) {
         c->table_fresh = true;
     }
     if (c->d_bloom) {
-        const uint64_t words = std::max<uint64_t>(1, (2 * c->bf_bits + 31) / 32);
-        HIPCHK(c, hipMemsetAsync(c->d_bloom, 0, words * 4, c->stream));
+        HIPCHK(c, hipMemsetAsync(c->d_bloom, 0, bloom_words(c) * 4, c->stream));
         if (c->bloom_final) {  // back to the Bloom pass: the table is sized again after it
             hipFree(c->d_table);
             hipFree(c->pb.hist2);

@@ -108,6 +108,37 @@ struct BloomLocal {
     uint32_t new_first, new_second, failed;
 };
 
+// Word and bit (of the filter-1 bit; filter 2 is the next bit) of the first n hash
+// functions of a root.
+//  reference layout (mybitarray + calculate_hashes, double_bloomfilter.hpp:276-281):
+//    h_j = XXH64(root, seed_j) & (bits - 1): n independent random words.
+//  blocked layout (bf.blocked, the default): all n positions lie in one 512-bit block
+//    (one 64-byte line: 256 positions of both filters), block = XXH64(root, seed_0) &
+//    (blocks - 1), position j = byte j of XXH64(root, seed_1) (byte j - 8 of
+//    XXH64(root, seed_2) for j >= 8).  One random line per k-mer instead of n.
+template <int N>
+DEV void bloom_slots(const BloomView& bf, uint64_t root, int n, uint64_t (&widx)[N], uint32_t (&bpos)[N]) {
+    if (bf.blocked) {
+        const uint64_t blk = xxh64_u64(root, c_bf_seeds[0]) & bf.bmask;
+        const uint64_t h1 = xxh64_u64(root, c_bf_seeds[1]);
+        const uint64_t h2 = n > 8 ? xxh64_u64(root, c_bf_seeds[2]) : 0;
+#pragma unroll
+        for (int j = 0; j < N; j++) {
+            const uint32_t p = (uint32_t)(((j < 8 ? h1 : h2) >> (8 * (j & 7))) & 255);
+            widx[j] = blk * 16 + (p >> 4);
+            bpos[j] = 2 * (p & 15);
+        }
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < N; j++)
+        if (j < n) {
+            const uint64_t bit = 2 * (xxh64_u64(root, c_bf_seeds[j]) & bf.mask);
+            widx[j] = bit >> 5;
+            bpos[j] = (uint32_t)(bit & 31);
+        }
+}
+
 // insertion_process (double_bloomfilter.hpp:371-413); a "set" counts as ours only if
 // our atomicOr flipped the bit (MyAtomicBitArrayFT::set, mybitarray.hpp:87-125)
 DEV void bloom_insert(const BloomView& bf, uint64_t root, BloomLocal& loc) {
@@ -115,16 +146,10 @@ DEV void bloom_insert(const BloomView& bf, uint64_t root, BloomLocal& loc) {
     uint32_t bpos[MAX_NH];
     uint32_t view[MAX_NH];
     int s1 = 0, s2 = 0;
+    bloom_slots(bf, root, bf.nh, widx, bpos);
 #pragma unroll
-    for (int j = 0; j < MAX_NH; j++) {
-        if (j < bf.nh) {
-            const uint64_t hv = xxh64_u64(root, c_bf_seeds[j]) & bf.mask;
-            const uint64_t bit = 2 * hv;
-            widx[j] = bit >> 5;
-            bpos[j] = (uint32_t)(bit & 31);
-            view[j] = bf.bits[widx[j]];
-        }
-    }
+    for (int j = 0; j < MAX_NH; j++)
+        if (j < bf.nh) view[j] = bf.bits[widx[j]];
 #pragma unroll
     for (int j = 0; j < MAX_NH; j++)
         if (j < bf.nh) {
@@ -167,13 +192,13 @@ DEV void bloom_insert(const BloomView& bf, uint64_t root, BloomLocal& loc) {
 
 // pass-2 gate: all of the first trunc(hf) filter-2 bits set (parallel_parser.hpp:2436-2441)
 DEV bool bloom_gate(const BloomView& bf, uint64_t root) {
+    uint64_t widx[MAX_NH];
+    uint32_t bpos[MAX_NH];
+    bloom_slots(bf, root, bf.nh_gate, widx, bpos);
     bool all = true;
 #pragma unroll
     for (int j = 0; j < MAX_NH; j++)
-        if (j < bf.nh_gate) {
-            const uint64_t bit = 2 * (xxh64_u64(root, c_bf_seeds[j]) & bf.mask) + 1;
-            all &= (bf.bits[bit >> 5] >> (bit & 31)) & 1;
-        }
+        if (j < bf.nh_gate) all &= (bf.bits[widx[j]] >> (bpos[j] + 1)) & 1;
     return all;
 }
 

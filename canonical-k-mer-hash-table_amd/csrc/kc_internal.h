@@ -106,6 +106,8 @@ struct BloomView {
     uint64_t mask;          // nbits - 1
     int nh;                 // ceil(hf): pass-1 hashes
     int nh_gate;            // trunc(hf): pass-2 gate hashes
+    int blocked;            // 1: one 512-bit block per k-mer (kc_count.hip bloom_slots)
+    uint64_t bmask;         // blocks - 1 (blocks = max(1, nbits / 256))
 };
 
 inline int words_for_k(int k) { return k / 32 + 1; }          // spare top bit for EMPTY

@@ -69,6 +69,19 @@ def insert_path(request, monkeypatch):
 
 @pytest.mark.parametrize("case", CASES, ids=_case_id)
 def test_golden_case_host_chunks(case, golden_input, tmp_path, insert_path):
+    check_golden_case(case, golden_input, tmp_path)
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if "-b" in c["args"]], ids=_case_id)
+def test_golden_bloom_cases_reference_layout(case, golden_input, tmp_path, monkeypatch):
+    """The Bloom filter with the reference's bit positions (one XXH64 per hash function,
+    KC_BLOOM_LAYOUT=reference) instead of the default one-line-per-k-mer blocked layout:
+    same results (the filter only gates; counts >= 2 are exact either way)."""
+    monkeypatch.setenv("KC_BLOOM_LAYOUT", "reference")
+    check_golden_case(case, golden_input, tmp_path)
+
+
+def check_golden_case(case, golden_input, tmp_path):
     path = golden_input(case["input"])
     o = parse_ref_args(case["args"])
     kc, st = ka.count_file(path, case["k"], mode=o["mode"], min_abundance=o["min_abundance"],
