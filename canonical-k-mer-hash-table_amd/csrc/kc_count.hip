@@ -405,9 +405,14 @@ struct OutSeg {
 // LDS and write each bin as one contiguous run at gbase[bin].  The rank of a key inside
 // its bin comes back from the histogram atomic, so one LDS atomic per key suffices.
 // Returns true if a segmented run did not fit.
-template <int W, int RUNW, class Bin, class Out, int NT = COUNT_THREADS>
-DEV bool scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const Out& o, const uint64_t (&tk)[RUNW][W],
-                      const bool (&ok)[RUNW], uint64_t* __restrict__ out) {
+struct NoMid {
+    DEV void operator()() const {}
+};
+// mid(): called once the tile's keys are in LDS (tk / ok are dead from there on: a caller
+// may load its next tile into them)
+template <int W, int RUNW, class Bin, class Out, int NT = COUNT_THREADS, class Mid = NoMid>
+DEV bool scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const Out& o, uint64_t (&tk)[RUNW][W],
+                      bool (&ok)[RUNW], uint64_t* __restrict__ out, Mid&& mid = Mid()) {
     const int tid = threadIdx.x;
     uint32_t rank[RUNW];
 #pragma unroll
@@ -421,6 +426,7 @@ DEV bool scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const Out& o
 #pragma unroll
             for (int w = 0; w < W; w++) l.keys[slot * W + w] = tk[j][w];
         }
+    mid();
     __syncthreads();
     const uint32_t n = l.start[F - 1] + l.hist[F - 1];
     bool over = false;
@@ -747,8 +753,11 @@ __global__ __launch_bounds__(COUNT_THREADS, 4) void k_p2(TableView tv, PartBufs 
 template <int W, int NT>
 constexpr size_t p2f_smem(uint32_t F, uint32_t nseg_max) { return part_smem<W, NT>(F) + (size_t)(nseg_max + 1) * 4; }
 
+#ifndef KC_PREFETCH
+#define KC_PREFETCH 1
+#endif
 template <int W, int NT>
-__global__ __launch_bounds__(NT, 1024 / NT) void k_p2f(TableView tv, PartBufs pb, DevCounters* __restrict__ ctr) {
+__global__ __launch_bounds__(NT, 2048 / NT) void k_p2f(TableView tv, PartBufs pb, DevCounters* __restrict__ ctr) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int RUNW = run_w<W>(), TW = NT * RUNW;
     if (ctr->part_overflow) return;  // level 1 overflowed: the exact pipeline redoes the batch
@@ -771,17 +780,21 @@ __global__ __launch_bounds__(NT, 1024 / NT) void k_p2f(TableView tv, PartBufs pb
     block_excl_scan_lds<NT>(pre, pre, nseg + 1);  // in place; pre[nseg] = total
     const uint32_t total = pre[nseg];
     bool over = false;
-    uint32_t cs = 0;  // segment cursor of this thread
-    for (uint32_t t0 = 0; t0 < total; t0 += TW) {
-        uint64_t tk[RUNW][W];
-        bool ok[RUNW];
+    // segment cursor of this thread (its indices grow monotonically): segment cs holds
+    // [cb, nb) of the virtual run, both bounds kept in registers
+    uint32_t cs = 0, cb = 0, nb = nseg ? pre[1] : 0;
+    auto load_tile = [&](uint32_t t0, uint64_t (&tk)[RUNW][W], bool (&ok)[RUNW]) {
 #pragma unroll
         for (int q = 0; q < RUNW; q++) {
             const uint32_t i = t0 + tid + q * NT;
             ok[q] = i < total;
             if (ok[q]) {
-                while (pre[cs + 1] <= i) cs++;
-                const uint64_t* src = pb.keys1 + ((seg0 + cs) * pb.cap1 + (i - pre[cs])) * W;
+                while (nb <= i) {
+                    cs++;
+                    cb = nb;
+                    nb = pre[cs + 1];
+                }
+                const uint64_t* src = pb.keys1 + ((seg0 + cs) * pb.cap1 + (i - cb)) * W;
 #pragma unroll
                 for (int w = 0; w < W; w++) tk[q][w] = src[w];
             } else {
@@ -789,7 +802,18 @@ __global__ __launch_bounds__(NT, 1024 / NT) void k_p2f(TableView tv, PartBufs pb
                 for (int w = 0; w < W; w++) tk[q][w] = 0;
             }
         }
-        over |= scatter_tile<W, RUNW, BinRegion, OutSeg, NT>(l, F, bin, o, tk, ok, pb.keys2);
+    };
+    uint64_t tk[RUNW][W];
+    bool ok[RUNW];
+    if (total) load_tile(0, tk, ok);
+    for (uint32_t t0 = 0; t0 < total; t0 += TW) {
+        // the next tile is loaded into the same registers as soon as this tile's keys sit
+        // in LDS, so its loads overlap this tile's write-out (barriers wait for LDS only)
+        const bool more = t0 + TW < total;
+        over |= scatter_tile<W, RUNW, BinRegion, OutSeg, NT>(l, F, bin, o, tk, ok, pb.keys2, [&]() {
+            if (KC_PREFETCH && more) load_tile(t0 + TW, tk, ok);
+        });
+        if (!KC_PREFETCH && more) load_tile(t0 + TW, tk, ok);
     }
     for (uint32_t b = tid; b < F; b += NT)
         pb.hist2[((uint64_t)c * F + b) * pb.B2 + j] = (uint32_t)(l.gbase[b] - o.start(b));
@@ -839,7 +863,7 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
     constexpr int S = BUCKET_WORDS / (W + 1);
     // keys loaded per thread before inserting (memory-level parallelism); 1024-thread
     // groups already keep 8 waves per SIMD in flight
-    constexpr int KB = NT >= 1024 ? (W >= 3 ? 2 : 4) : 8;
+    constexpr int KB = NT >= 1024 ? (W >= 2 ? 2 : 4) : 8;
     if constexpr (SEG) {
         if (ctr->part_overflow) return;
     } else {
@@ -892,18 +916,23 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
         }
     }
     uint32_t n_fail = 0;
-    uint32_t cs = 0;  // SEG: segment cursor of this thread (indices grow monotonically)
-    for (uint64_t base = start; base < end; base += (uint64_t)KB * NT) {
-        uint64_t kk[KB][W];
-        uint64_t add[KB];
+    // SEG: segment cursor of this thread (indices grow monotonically): segment cs holds
+    // [cb, nb), both bounds in registers
+    uint32_t cs = 0, cb = 0, nb = 0;
+    if constexpr (SEG) nb = s_pre[1];
+    auto load_items = [&](uint64_t base, uint64_t (&kk)[KB][W], uint64_t (&add)[KB]) {
 #pragma unroll
         for (int q = 0; q < KB; q++) {
             const uint64_t i = base + threadIdx.x + (uint64_t)q * NT;
             const uint64_t* src = nullptr;
             if (i < end) {
                 if constexpr (SEG) {
-                    while (s_pre[cs + 1] <= i) cs++;
-                    src = pb.keys2 + ((r * pb.B2 + cs) * pb.cap2 + (i - s_pre[cs])) * IW;
+                    while (nb <= i) {
+                        cs++;
+                        cb = nb;
+                        nb = s_pre[cs + 1];
+                    }
+                    src = pb.keys2 + ((r * pb.B2 + cs) * pb.cap2 + (i - cb)) * IW;
                 } else {
                     src = pb.keys2 + i * IW;
                 }
@@ -913,6 +942,17 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
             if constexpr (CNT) add[q] = src ? src[W] & CNT_MASK : 0;
             else add[q] = 1;
         }
+    };
+    uint64_t kk[KB][W];
+    uint64_t add[KB];
+    if (start < end) load_items(start, kk, add);
+    for (uint64_t base = start; base < end; base += (uint64_t)KB * NT) {
+        // the next items' loads are issued before this batch's inserts
+        uint64_t nkk[KB][W];
+        uint64_t nadd[KB];
+        const uint64_t nbase = base + (uint64_t)KB * NT;
+        const bool more = KC_PREFETCH && W <= 2 && nbase < end;  // W > 2: no spare registers
+        if (more) load_items(nbase, nkk, nadd);
 #pragma unroll
         for (int q = 0; q < KB; q++) {
             if (base + threadIdx.x + (uint64_t)q * NT >= end) continue;
@@ -1065,6 +1105,16 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
                 }
             }
             if (!done) n_fail++;
+        }
+        if (more) {
+#pragma unroll
+            for (int q = 0; q < KB; q++) {
+                add[q] = nadd[q];
+#pragma unroll
+                for (int w = 0; w < W; w++) kk[q][w] = nkk[q][w];
+            }
+        } else if (nbase < end) {
+            load_items(nbase, kk, add);
         }
     }
     __syncthreads();
