@@ -268,12 +268,27 @@ def main():
     win_per_launch = windows_step / per_step
     bytes_per_launch = sym_per_launch + win_per_launch * ((1 + u) * K + 8)
     count_ms = tm["count_ms"] / launches
+    units_per_step = per_step
+    if args.unique:
+        # Bloom configs: the unit is one Bloom pass + one counting pass over
+        # the same batch: a second sym_B, ceil(hf) 8-byte filter-word RMWs (pass 1) and
+        # trunc(hf) 4-byte tests (pass 2) per window, the table term for the windows that
+        # pass the gate
+        hf = -math.log(0.01) / math.log(2)  # -f 0.01 (the Config default)
+        nh, nh_gate = math.ceil(hf), int(hf)
+        p_gate = st["inserted"] / max(1, windows_step)
+        pairs = max(1, launches // 2)
+        bytes_per_launch = (2 * nbytes / args.steps + windows_step * (8 * nh + 4 * nh_gate)
+                            + windows_step * p_gate * ((1 + u) * K + 8)) * args.steps / pairs
+        count_ms = tm["count_ms"] / pairs
+        units_per_step = pairs / args.steps
     achieved = bytes_per_launch / (count_ms * 1e-3) / 1e9
     traffic = load_traffic(workload)
     if dist:
         kname = "local count pass + merge insert of the received {key, count} records"
     elif args.unique:
-        kname = "Bloom pass (k_count<W,1>) + gated counting pass (k_p1, k_p2f, k_p3)"
+        kname = ("Bloom pass 1 (k_p1 -> k_p2f -> k_b3: LDS-resident filter regions) + counting pass "
+                 "(k_p1, k_p2f, k_p3 with the gate at level 3), one of each per batch")
     else:
         kname = "count pass: k_p1 (segmented scatter), k_p2f, k_p3 (partitioned insert)"
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -289,7 +304,7 @@ def main():
                    "table": tbl, "batches_per_step": per_step,
                    "parallelism": f"hash-prefix shard x{world}" if dist else "single"},
         "roofline": roofline,
-        "hbm_gbs_step": round(bytes_per_launch * per_step / (step_ms * 1e-3) / 1e9, 2),
+        "hbm_gbs_step": round(bytes_per_launch * units_per_step / (step_ms * 1e-3) / 1e9, 2),
         "kernel_ms": {"gather": round(tm["gather_ms"] / launches, 4), "tokenize": round(tm["tokenize_ms"] / launches, 4),
                       "count": round(count_ms, 4)},
         "image_bytes": nbytes, "stage_bytes": sum(c[1] for c in chunks),

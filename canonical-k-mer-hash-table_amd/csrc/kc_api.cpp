@@ -71,10 +71,13 @@ struct kc_ctx {
     uint32_t F1 = 1, F2 = 1;
     int f2bits = 0;
 
-    // partitioned insert buffers
-    PartBufs pb{};
-    uint32_t pb_nblk1_cap = 0;
-    uint64_t pb_k1_cap = 0, pb_k2_cap = 0;  // keys the level-1 / level-2 buffers hold
+    // partitioned insert buffers (pb: the table's levels; pbf: the Bloom pass's, same key
+    // buffers, own histograms)
+    PartBufs pb{}, pbf{};
+    uint32_t pb_nblk1_cap = 0, pbf_nblk1_cap = 0;
+    uint64_t* d_keys1 = nullptr;
+    uint64_t* d_keys2 = nullptr;
+    uint64_t k1_words = 0, k2_words = 0;  // u64 words the level-1 / level-2 key buffers hold
     bool table_fresh = false;  // the table is all zero (allocated / reset, nothing inserted since)
     // kc_reset defers the table memset: a fresh level-3 pass writes every region anyway;
     // any other use of the table zeroes it first (materialize_zero)
@@ -91,6 +94,8 @@ struct kc_ctx {
     int nh = 0, nh_gate = 0;
     int bloom_blocked = 1;  // KC_BLOOM_LAYOUT=reference: the reference's independent positions
     bool bloom_final = false;
+    bool bloom_fresh = false;  // the filter is all zero (allocated / reset, nothing inserted since)
+    TableView bgeo{};          // blocked layout: the filter's region geometry (k_b3 regions)
 
     uint64_t n_chunks = 0, n_bytes = 0;
 
@@ -206,25 +211,34 @@ static int materialize_zero(kc_ctx* c, hipStream_t s) {
 // 8 standard deviations plus 32, from the batch's symbol bound (>= its windows).  A
 // batch whose keys still overflow a segment (e.g. one k-mer repeated millions of times
 // inside one workgroup's range) is redone on the exact layout by the device itself.
-static int ensure_part(kc_ctx* c, uint64_t syms, bool seg) {
+// geometry of a partitioned pass: F1 coarse bins x F2 regions each (R regions), IW
+// u64 words per item
+struct PartGeo {
+    uint32_t F1, F2;
+    uint64_t R;
+    int IW;
+};
+static PartGeo table_geo(const kc_ctx* c) { return PartGeo{c->F1, c->F2, c->R, c->W}; }
+
+static int ensure_part_geo(kc_ctx* c, uint64_t syms, bool seg, const PartGeo& g, PartBufs& pb, uint32_t& nblk1_cap) {
     const uint64_t tile = (uint64_t)COUNT_THREADS * run_width(c->W);
     const uint32_t nblk1 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(2048, (syms + tile - 1) / tile));
-    const uint32_t B2 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(64, 2048 / c->F1));
-    if (!c->pb.hist1 || nblk1 > c->pb_nblk1_cap) {
-        hipFree(c->pb.hist1);
-        hipFree(c->pb.off1);
-        c->pb.hist1 = nullptr;
-        c->pb.off1 = nullptr;
+    const uint32_t B2 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(64, 2048 / g.F1));
+    if (!pb.hist1 || nblk1 > nblk1_cap) {
+        hipFree(pb.hist1);
+        hipFree(pb.off1);
+        pb.hist1 = nullptr;
+        pb.off1 = nullptr;
         const uint32_t cap = 2048;
-        if (hipMalloc(&c->pb.hist1, (size_t)c->F1 * cap * 4) != hipSuccess ||
-            hipMalloc(&c->pb.off1, ((size_t)c->F1 * cap + 1) * 8) != hipSuccess)
+        if (hipMalloc(&pb.hist1, (size_t)g.F1 * cap * 4) != hipSuccess ||
+            hipMalloc(&pb.off1, ((size_t)g.F1 * cap + 1) * 8) != hipSuccess)
             return c->fail(KC_ERR_NOMEM, "partition histogram allocation failed");
-        c->pb_nblk1_cap = cap;
+        nblk1_cap = cap;
     }
-    if (!c->pb.hist2) {
-        const size_t n2 = (size_t)c->R * B2, n1 = (size_t)c->F1 * 2048;
-        if (hipMalloc(&c->pb.hist2, n2 * 4) != hipSuccess || hipMalloc(&c->pb.off2, (n2 + 1) * 8) != hipSuccess ||
-            hipMalloc(&c->pb.bsum, ((std::max(n1, n2) + 4095) / 4096 + 2) * 8) != hipSuccess)
+    if (!pb.hist2) {
+        const size_t n2 = (size_t)g.R * B2, n1 = (size_t)g.F1 * 2048;
+        if (hipMalloc(&pb.hist2, n2 * 4) != hipSuccess || hipMalloc(&pb.off2, (n2 + 1) * 8) != hipSuccess ||
+            hipMalloc(&pb.bsum, ((std::max(n1, n2) + 4095) / 4096 + 2) * 8) != hipSuccess)
             return c->fail(KC_ERR_NOMEM, "partition histogram allocation failed");
     }
     uint64_t cap1 = 0, cap2 = 0;
@@ -233,34 +247,40 @@ static int ensure_part(kc_ctx* c, uint64_t syms, bool seg) {
         const uint64_t t1 = (uint64_t)p1_tile(c->W);  // k_p1<..., OutSeg> rounds block ranges to its tile
         const uint64_t per1 = ((syms + nblk1 - 1) / nblk1 + t1 - 1) / t1 * t1;  // windows per level-1 block
         const uint64_t nseg = (nblk1 + B2 - 1) / B2;                               // level-1 segments per p2 block
-        cap1 = capacity((double)per1 / c->F1);
-        cap2 = capacity((double)nseg * per1 / c->F1 / c->F2);
+        cap1 = capacity((double)per1 / g.F1);
+        cap2 = capacity((double)nseg * per1 / g.F1 / g.F2);
         if (const char* v = std::getenv("KC_SEG_CAP")) cap1 = cap2 = std::max<uint64_t>(1, std::strtoull(v, 0, 10));
         // the segment walks index a virtual run with 32-bit offsets
         if (nseg * cap1 >= (1ULL << 31) || (uint64_t)B2 * cap2 >= (1ULL << 31)) cap1 = cap2 = 0;
     }
-    const uint64_t need1 = std::max<uint64_t>(syms, (uint64_t)c->F1 * nblk1 * cap1);
-    const uint64_t need2 = std::max<uint64_t>(syms, c->R * B2 * cap2);
+    const uint64_t need1 = std::max<uint64_t>(syms, (uint64_t)g.F1 * nblk1 * cap1) * g.IW;
+    const uint64_t need2 = std::max<uint64_t>(syms, g.R * B2 * cap2) * g.IW;
     auto grow = [&](uint64_t** buf, uint64_t* have, uint64_t need) -> int {
         if (need <= *have) return KC_OK;
         hipFree(*buf);
         *buf = nullptr;
         *have = 0;
-        const size_t bytes = (size_t)need * c->W * 8;
+        const size_t bytes = (size_t)need * 8;
         if (hipMalloc(buf, bytes) != hipSuccess)
             return c->fail(KC_ERR_NOMEM, "partition key buffer allocation failed (" + std::to_string(bytes) + " bytes)");
         *have = need;
         return KC_OK;
     };
-    int rc = grow(&c->pb.keys1, &c->pb_k1_cap, need1);
+    int rc = grow(&c->d_keys1, &c->k1_words, need1);
     if (rc) return rc;
-    rc = grow(&c->pb.keys2, &c->pb_k2_cap, need2);
+    rc = grow(&c->d_keys2, &c->k2_words, need2);
     if (rc) return rc;
-    c->pb.nblk1 = nblk1;
-    c->pb.B2 = B2;
-    c->pb.cap1 = cap1;
-    c->pb.cap2 = cap2;
+    pb.keys1 = c->d_keys1;
+    pb.keys2 = c->d_keys2;
+    pb.nblk1 = nblk1;
+    pb.B2 = B2;
+    pb.cap1 = cap1;
+    pb.cap2 = cap2;
     return KC_OK;
+}
+// the table's levels
+static int ensure_part(kc_ctx* c, uint64_t syms, bool seg) {
+    return ensure_part_geo(c, syms, seg, table_geo(c), c->pb, c->pb_nblk1_cap);
 }
 
 // Insert path per batch: the partitioned pipeline moves ~(4W+1)*8 bytes per window
@@ -272,6 +292,17 @@ static bool use_partitioned(const kc_ctx* c, uint64_t syms) {
     if (env && (!std::strcmp(env, "partitioned") || !std::strcmp(env, "exact"))) return true;
     const double table_bytes = (double)c->nbuckets * 128.0;
     return (double)syms * 275.0 > (double)syms * (4.0 * c->W + 1) * 8.0 + 2.0 * table_bytes;
+}
+
+// Bloom pass 1 (blocked layout): the partitioned pass moves one u64 per window three
+// times plus two sweeps of the filter; the direct pass costs a scattered 64-byte line
+// RMW with up to ceil(hf) device-scope atomics per window.
+static bool use_partitioned_bloom(const kc_ctx* c, uint64_t syms) {
+    const char* env = std::getenv("KC_INSERT_PATH");
+    if (env && !std::strcmp(env, "direct")) return false;
+    if (env && (!std::strcmp(env, "partitioned") || !std::strcmp(env, "exact"))) return true;
+    const double filter_bytes = (double)bloom_words(c) * 4.0;
+    return (double)syms * 275.0 > (double)syms * 5.0 * 8.0 + 2.0 * filter_bytes;
 }
 
 // The device entry points run on the caller's stream, ordered after the work already
@@ -308,12 +339,19 @@ static int run_batch(kc_ctx* c, const uint8_t* src, uint64_t used, uint64_t nchu
     if (c->profiling) HIPCHK(c, hipEventRecord(ev[2], s));
     TableView tv = table_view(c);
     BloomView bv{c->d_bloom, c->bf_bits ? c->bf_bits - 1 : 0, c->nh, c->nh_gate, c->bloom_blocked,
-                 bloom_blocks(c->bf_bits) - 1};
+                 bloom_blocks(c->bf_bits)};
     int mode;
     if (pass == 1) mode = 1;
     else mode = (c->cfg.bf_enable && c->cfg.mode != 1) ? 2 : 0;  // -m 1 -b ignores the filter (main.cpp:482-489)
     const uint64_t syms = used + nchunks;
-    if (mode != 1 && use_partitioned(c, syms)) {
+    if (mode == 1 && c->bloom_blocked && use_partitioned_bloom(c, syms)) {
+        const char* env = std::getenv("KC_INSERT_PATH");
+        int rc = ensure_part_geo(c, syms, !(env && !std::strcmp(env, "exact")),
+                                 PartGeo{c->bgeo.F1, c->bgeo.F2, c->bgeo.R, 1}, c->pbf, c->pbf_nblk1_cap);
+        if (rc) return rc;
+        HIPCHK(c, launch_bloom_partitioned(sv, c->cfg.k, c->W, bv, c->bgeo, c->d_ctr, c->pbf, c->bloom_fresh, s));
+        c->bloom_fresh = false;
+    } else if (mode != 1 && use_partitioned(c, syms)) {
         const char* env = std::getenv("KC_INSERT_PATH");
         int rc = ensure_part(c, syms, !(env && !std::strcmp(env, "exact")));
         if (rc) return rc;
@@ -325,6 +363,7 @@ static int run_batch(kc_ctx* c, const uint8_t* src, uint64_t used, uint64_t nchu
             if (rc) return rc;
         }
         HIPCHK(c, launch_count(sv, syms, c->cfg.k, mode, tv, bv, c->d_ctr, s));
+        if (mode == 1) c->bloom_fresh = false;
     }
     if (mode != 1) c->table_fresh = false;
     if (c->profiling) {
@@ -509,12 +548,28 @@ int kc_create(const kc_config* cfg, kc_ctx** out) {
     if (cfg->bf_enable) {
         bloom_sizes(cfg->est_unique, cfg->fpr, &c->bf_bits, &c->nh, &c->nh_gate);
         if (c->nh > MAX_NH) return bail(KC_ERR_ARG, "too many Bloom hash functions");
+        if (bloom_blocks(c->bf_bits) > (1ULL << 32)) return bail(KC_ERR_ARG, "Bloom filter too large (-u)");
         const char* lay = std::getenv("KC_BLOOM_LAYOUT");
         c->bloom_blocked = !(lay && !std::strcmp(lay, "reference"));
         const uint64_t words = bloom_words(c);
         if (hipMalloc(&c->d_bloom, words * 4) != hipSuccess)
             return bail(KC_ERR_NOMEM, "Bloom filter allocation failed");
         if (hipMemsetAsync(c->d_bloom, 0, words * 4, c->stream) != hipSuccess) return bail(KC_ERR_HIP, "memset");
+        c->bloom_fresh = true;
+        if (c->bloom_blocked) {
+            // filter regions of up to BF_BLOCKS_PER_REGION (1024) blocks = 64 KiB, F1 x F2 as
+            // for the table (all powers of two here)
+            const uint64_t nb = bloom_blocks(c->bf_bits);
+            const uint64_t R = std::max<uint64_t>(1, nb / 1024);
+            int rbits = 0;
+            while ((1ULL << rbits) < R) rbits++;
+            const int f1bits = std::min(10, (rbits + 1) / 2);
+            c->bgeo.R = R;
+            c->bgeo.f2bits = rbits - f1bits;
+            c->bgeo.F2 = 1u << c->bgeo.f2bits;
+            c->bgeo.F1 = (uint32_t)(R >> c->bgeo.f2bits);
+            c->bgeo.W = 1;
+        }
     } else {
         int rc = alloc_table(c, cfg->table_slots);
         if (rc) return bail(rc, "");
@@ -547,8 +602,13 @@ void kc_destroy(kc_ctx* c) {
     hipFree(c->pb.hist2);
     hipFree(c->pb.off2);
     hipFree(c->pb.bsum);
-    hipFree(c->pb.keys1);
-    hipFree(c->pb.keys2);
+    hipFree(c->d_keys1);
+    hipFree(c->d_keys2);
+    hipFree(c->pbf.hist1);
+    hipFree(c->pbf.off1);
+    hipFree(c->pbf.hist2);
+    hipFree(c->pbf.off2);
+    hipFree(c->pbf.bsum);
     hipFree(c->d_rhist);
     hipFree(c->d_roff);
     hipFree(c->d_rbsum);
@@ -850,6 +910,7 @@ int kc_reset(kc_ctx* c) {
     }
     if (c->d_bloom) {
         HIPCHK(c, hipMemsetAsync(c->d_bloom, 0, bloom_words(c) * 4, c->stream));
+        c->bloom_fresh = true;
         if (c->bloom_final) {  // back to the Bloom pass: the table is sized again after it
             hipFree(c->d_table);
             hipFree(c->pb.hist2);

@@ -108,28 +108,99 @@ struct BloomLocal {
     uint32_t new_first, new_second, failed;
 };
 
-// Word and bit (of the filter-1 bit; filter 2 is the next bit) of the first n hash
-// functions of a root.
-//  reference layout (mybitarray + calculate_hashes, double_bloomfilter.hpp:276-281):
-//    h_j = XXH64(root, seed_j) & (bits - 1): n independent random words.
-//  blocked layout (bf.blocked, the default): all n positions lie in one 512-bit block
-//    (one 64-byte line: 256 positions of both filters), block = XXH64(root, seed_0) &
-//    (blocks - 1), position j = byte j of XXH64(root, seed_1) (byte j - 8 of
-//    XXH64(root, seed_2) for j >= 8).  One random line per k-mer instead of n.
-template <int N>
-DEV void bloom_slots(const BloomView& bf, uint64_t root, int n, uint64_t (&widx)[N], uint32_t (&bpos)[N]) {
-    if (bf.blocked) {
-        const uint64_t blk = xxh64_u64(root, c_bf_seeds[0]) & bf.bmask;
-        const uint64_t h1 = xxh64_u64(root, c_bf_seeds[1]);
-        const uint64_t h2 = n > 8 ? xxh64_u64(root, c_bf_seeds[2]) : 0;
+// Two layouts of the k-mer's positions:
+//  reference (KC_BLOOM_LAYOUT=reference; mybitarray + calculate_hashes,
+//    double_bloomfilter.hpp:276-281): h_j = XXH64(root, seed_j) & (bits - 1), root = the
+//    strand-symmetric Rabin-Karp hash mod 2^54: n independent random words.
+//  blocked (the default): all positions lie in one 512-bit block (one 64-byte line: 256
+//    positions of both filters).  The block is picked by the top bits of the k-mer's table
+//    key word 0 t0 (kc_common.h to_tkey, a bijective mix of the canonical key): block =
+//    ((t0 >> 32) * blocks) >> 32, the same hash prefix as the table's region index, so a
+//    filter region of BF_BLOCKS_PER_REGION blocks is one contiguous 64 KiB slice that the
+//    partitioned Bloom pass holds in LDS (k_b3) and the table's level 3 reads gate bits
+//    from (k_p3<..., GATE>).  Position j = byte j of bmix(t0, 1) (byte j - 8 of
+//    bmix(t0, 2) for j >= 8).  The filter only gates, so either layout gives the
+//    reference's counts for every k-mer seen at least twice.
+constexpr int BF_BLOCK_WORDS = 16;               // 512 bits
+constexpr int BF_BLOCKS_PER_REGION = 1024;       // 64 KiB of filter per LDS region
+DEV uint64_t bloom_block(uint64_t t0, uint64_t nblocks) { return ((t0 >> 32) * nblocks) >> 32; }
+DEV uint64_t bmix(uint64_t t0, uint64_t s) {  // splitmix64 finalizer of t0 ^ seed
+    uint64_t x = t0 ^ (s * 0xD6E8FEB86659FD93ULL);
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+    return x ^ (x >> 31);
+}
+// positions j < n of the blocked layout: word of the block and filter-1 bit mask; dup[j]:
+// position j repeats an earlier one (a k-mer's own bit counts once)
+DEV void blocked_positions(uint64_t t0, int n, uint32_t (&word)[MAX_NH], uint32_t (&m1)[MAX_NH],
+                           bool (&dup)[MAX_NH]) {
+    const uint64_t h1 = bmix(t0, 1), h2 = n > 8 ? bmix(t0, 2) : 0;
+    uint32_t p[MAX_NH];
 #pragma unroll
-        for (int j = 0; j < N; j++) {
-            const uint32_t p = (uint32_t)(((j < 8 ? h1 : h2) >> (8 * (j & 7))) & 255);
-            widx[j] = blk * 16 + (p >> 4);
-            bpos[j] = 2 * (p & 15);
-        }
-        return;
+    for (int j = 0; j < MAX_NH; j++) {
+        p[j] = (uint32_t)(((j < 8 ? h1 : h2) >> (8 * (j & 7))) & 255);
+        word[j] = p[j] >> 4;
+        m1[j] = 1u << (2 * (p[j] & 15));
+        bool d = false;
+#pragma unroll
+        for (int i = 0; i < j; i++) d |= p[i] == p[j];
+        dup[j] = d || j >= n;
     }
+}
+
+// insertion_process (double_bloomfilter.hpp:371-413) on one block of the blocked layout;
+// `blk` is the block in HBM (direct pass) or in LDS (k_b3).  A "set" counts as ours only
+// if our atomicOr flipped the bit (MyAtomicBitArrayFT::set, mybitarray.hpp:87-125).
+DEV void block_insert(uint32_t* blk, uint64_t t0, int nh, BloomLocal& loc) {
+    uint32_t word[MAX_NH], m1[MAX_NH], view[MAX_NH];
+    bool dup[MAX_NH];
+    blocked_positions(t0, nh, word, m1, dup);
+    int n = 0, s1 = 0, s2 = 0;
+#pragma unroll
+    for (int j = 0; j < MAX_NH; j++)
+        if (!dup[j]) {
+            view[j] = blk[word[j]];
+            n++;
+            s1 += (view[j] & m1[j]) != 0;
+            s2 += (view[j] & (m1[j] << 1)) != 0;
+        }
+    if (s2 == n) return;  // in the second filter already
+    bool to_second = true;
+    if (s1 != n) {
+        int mine = 0;
+#pragma unroll
+        for (int j = 0; j < MAX_NH; j++)
+            if (!dup[j] && !(view[j] & m1[j])) mine += !(atomicOr(blk + word[j], m1[j]) & m1[j]);
+        if (mine == n - s1) { loc.new_first++; to_second = false; }
+        else loc.failed++;
+    }
+    if (to_second) {
+        int mine = 0;
+#pragma unroll
+        for (int j = 0; j < MAX_NH; j++)
+            if (!dup[j] && !(view[j] & (m1[j] << 1)))
+                mine += !(atomicOr(blk + word[j], m1[j] << 1) & (m1[j] << 1));
+        if (mine == n - s2) loc.new_second++;
+    }
+}
+
+// pass-2 gate on one block: all of the first trunc(hf) filter-2 bits set
+// (parallel_parser.hpp:2436-2441)
+DEV bool block_gate(const uint32_t* blk, uint64_t t0, int nh_gate) {
+    uint32_t word[MAX_NH], m1[MAX_NH];
+    bool dup[MAX_NH];
+    blocked_positions(t0, nh_gate, word, m1, dup);
+    bool all = true;
+#pragma unroll
+    for (int j = 0; j < MAX_NH; j++)
+        if (j < nh_gate) all &= (blk[word[j]] & (m1[j] << 1)) != 0;
+    return all;
+}
+
+// reference layout: word and bit (of the filter-1 bit; filter 2 is the next bit) of the
+// first n hash functions of a root
+template <int N>
+DEV void ref_slots(const BloomView& bf, uint64_t root, int n, uint64_t (&widx)[N], uint32_t (&bpos)[N]) {
 #pragma unroll
     for (int j = 0; j < N; j++)
         if (j < n) {
@@ -139,14 +210,22 @@ DEV void bloom_slots(const BloomView& bf, uint64_t root, int n, uint64_t (&widx)
         }
 }
 
-// insertion_process (double_bloomfilter.hpp:371-413); a "set" counts as ours only if
-// our atomicOr flipped the bit (MyAtomicBitArrayFT::set, mybitarray.hpp:87-125)
-DEV void bloom_insert(const BloomView& bf, uint64_t root, BloomLocal& loc) {
+DEV uint32_t* bloom_block_ptr(const BloomView& bf, uint64_t t0) {
+    return bf.bits + bloom_block(t0, bf.nblocks) * BF_BLOCK_WORDS;
+}
+
+// insertion_process on the HBM filter (direct pass 1): root for the reference layout, the
+// table key word t0 for the blocked one
+DEV void bloom_insert(const BloomView& bf, uint64_t root, uint64_t t0, BloomLocal& loc) {
+    if (bf.blocked) {
+        block_insert(bloom_block_ptr(bf, t0), t0, bf.nh, loc);
+        return;
+    }
     uint64_t widx[MAX_NH];
     uint32_t bpos[MAX_NH];
     uint32_t view[MAX_NH];
     int s1 = 0, s2 = 0;
-    bloom_slots(bf, root, bf.nh, widx, bpos);
+    ref_slots(bf, root, bf.nh, widx, bpos);
 #pragma unroll
     for (int j = 0; j < MAX_NH; j++)
         if (j < bf.nh) view[j] = bf.bits[widx[j]];
@@ -190,11 +269,11 @@ DEV void bloom_insert(const BloomView& bf, uint64_t root, BloomLocal& loc) {
     }
 }
 
-// pass-2 gate: all of the first trunc(hf) filter-2 bits set (parallel_parser.hpp:2436-2441)
-DEV bool bloom_gate(const BloomView& bf, uint64_t root) {
+DEV bool bloom_gate(const BloomView& bf, uint64_t root, uint64_t t0) {
+    if (bf.blocked) return block_gate(bloom_block_ptr(bf, t0), t0, bf.nh_gate);
     uint64_t widx[MAX_NH];
     uint32_t bpos[MAX_NH];
-    bloom_slots(bf, root, bf.nh_gate, widx, bpos);
+    ref_slots(bf, root, bf.nh_gate, widx, bpos);
     bool all = true;
 #pragma unroll
     for (int j = 0; j < MAX_NH; j++)
@@ -295,13 +374,13 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_count(PackedView sv, int k, T
         } else {
             tile_rolled<W>(sv, t0, t1, rk, [&](const uint64_t (&fwd)[W], const uint64_t (&rc)[W], uint64_t root) {
                 n_win++;
+                uint64_t key[W], tk[W];
+                canonical<W>(fwd, rc, key);
+                to_tkey<W>(key, tk);
                 if constexpr (MODE == 1) {
-                    bloom_insert(bf, root, bl);
+                    bloom_insert(bf, root, tk[0], bl);
                 } else {
-                    if (!bloom_gate(bf, root)) return;
-                    uint64_t key[W], tk[W];
-                    canonical<W>(fwd, rc, key);
-                    to_tkey<W>(key, tk);
+                    if (!bloom_gate(bf, root, tk[0])) return;
                     n_ins++;
                     if (!table_insert<W>(tv, tk)) n_fail++;
                 }
@@ -455,7 +534,13 @@ DEV bool scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const Out& o
 // gated kernels (the exact fallback of a segmented batch) run only if *gate != 0
 DEV bool gated_off(const unsigned long long* gate) { return gate && *gate == 0; }
 
+// words per level-1 output key: the Bloom pass (MODE 3) moves table key word 0 only
+constexpr int p1_out_words(int W, int MODE) { return MODE == 3 ? 1 : W; }
+
 // Level 1: windows of a contiguous symbol range -> coarse bins (region >> f2bits).
+// MODE 0: count; 2: count behind the Bloom gate on the rolled root (reference layout);
+// 3: Bloom pass 1, blocked layout (keys = t0, bins = filter regions); 4: count, gated
+// at level 3 (blocked layout).
 // SCATTER = false: histogram only ([bin][block] into hist1); true: write the keys,
 // exact layout (offsets off1) or segmented (Out = OutSeg: single pass, the segment
 // fill counts go to hist1).  `count`: add windows / inserted to the counters (off for
@@ -468,6 +553,8 @@ __global__ __launch_bounds__(NT, 4) void k_p1(PackedView sv, int k, BloomView bf
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int RUNW = run_w<W>(), TW = NT * RUNW;
     constexpr bool COUNTS = !SCATTER || Out::kSeg;
+    constexpr bool ROLLED = MODE == 2;       // gate on the rolled root (reference layout)
+    constexpr int OW = p1_out_words(W, MODE);  // words per output key
     if (gated_off(gate)) return;
     if (gate && !SCATTER && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&ctr->part_fallbacks, 1ULL);
     const PartLds l = part_lds(smem, F);
@@ -490,25 +577,27 @@ __global__ __launch_bounds__(NT, 4) void k_p1(PackedView sv, int k, BloomView bf
     uint32_t n_win = 0, n_ins = 0;
     for (uint64_t t0 = lo; t0 < hi; t0 += TW) {
         const uint64_t t1 = min(t0 + TW, hi);
-        uint64_t tk[RUNW][W];
+        uint64_t tk[RUNW][OW];
         bool ok[RUNW];
-        if constexpr (MODE == 0) {
+        if constexpr (!ROLLED) {
             const uint64_t r0 = t0 + (uint64_t)tid * RUNW;
 #pragma unroll
             for (int j = 0; j < RUNW; j++) ok[j] = false;
             if (r0 < t1)
                 run_windows<W, RUNW>(sv, r0, t1, rk,
                                      [&](int j, bool valid, const uint64_t (&fwd)[W], const uint64_t (&rc)[W]) {
-                    uint64_t key[W];
+                    uint64_t key[W], t[W];
                     canonical<W>(fwd, rc, key);
-                    to_tkey<W>(key, tk[j]);
+                    to_tkey<W>(key, t);
+#pragma unroll
+                    for (int w = 0; w < OW; w++) tk[j][w] = t[w];
                     ok[j] = valid;
                 });
             if constexpr (COUNTS) {
 #pragma unroll
                 for (int j = 0; j < RUNW; j++) {
                     n_win += ok[j];
-                    n_ins += ok[j];
+                    n_ins += MODE == 0 ? ok[j] : 0;  // MODE 4: level 3 counts the gated insertions
                 }
             }
         } else {
@@ -516,13 +605,12 @@ __global__ __launch_bounds__(NT, 4) void k_p1(PackedView sv, int k, BloomView bf
 #pragma unroll
             for (int j = 0; j < RUNW; j++) ok[j] = false;
             tile_rolled<W>(sv, t0, t1, rk, [&](const uint64_t (&fwd)[W], const uint64_t (&rc)[W], uint64_t root) {
-                (void)fwd;
                 if constexpr (COUNTS) n_win++;
-                if (!bloom_gate(bf, root)) return;
-                if constexpr (COUNTS) n_ins++;
                 uint64_t key[W], t[W];
                 canonical<W>(fwd, rc, key);
                 to_tkey<W>(key, t);
+                if (!bloom_gate(bf, root, t[0])) return;
+                if constexpr (COUNTS) n_ins++;
                 // at most run_w windows per run: append into the first free register slot
 #pragma unroll
                 for (int j = 0; j < RUNW; j++)
@@ -535,7 +623,7 @@ __global__ __launch_bounds__(NT, 4) void k_p1(PackedView sv, int k, BloomView bf
             });
         }
         if constexpr (SCATTER) {
-            over |= scatter_tile<W, RUNW, Bin, Out, NT>(l, F, bin, ob, tk, ok, out);
+            over |= scatter_tile<OW, RUNW, Bin, Out, NT>(l, F, bin, ob, tk, ok, out);
         } else {
 #pragma unroll
             for (int j = 0; j < RUNW; j++)
@@ -551,9 +639,15 @@ __global__ __launch_bounds__(NT, 4) void k_p1(PackedView sv, int k, BloomView bf
             pb.hist1[(uint64_t)b * pb.nblk1 + blockIdx.x] = (uint32_t)(l.gbase[b] - ob.start(b));
         if (over) atomicOr(&ctr->part_overflow, 1ULL);
     }
-    // routing (owner bins) counts windows here and insertions at the owner
+    // routing (owner bins) counts windows here and insertions at the owner; the Bloom
+    // pass counts its windows apart
     if constexpr (COUNTS)
-        if (count) block_add4(n_win, Bin::kOwner ? 0 : n_ins, 0, 0, &ctr->windows, &ctr->inserted, nullptr, nullptr);
+        if (count) {
+            if constexpr (MODE == 3)
+                block_add4(n_win, 0, 0, 0, &ctr->bf_windows, nullptr, nullptr, nullptr);
+            else
+                block_add4(n_win, Bin::kOwner ? 0 : n_ins, 0, 0, &ctr->windows, &ctr->inserted, nullptr, nullptr);
+        }
 }
 
 // Level 1 over a key array (keys received from other shards): [0, n) split over nblk1
@@ -851,11 +945,16 @@ DEV uint32_t zero_byte_mask8(uint64_t x) {
 // leaves the table alone when the batch overflowed; an exact one can be gated.
 // CNT: items are {W key words, count} records (shard merge) and add their count.
 // fresh: the table is known to be all zero (just reset), so the region is not read.
+// GATE: Bloom pass 2 on the blocked layout: an item is inserted only if its filter-2 bits
+// are set (parallel_parser.hpp:2436-2441).  The blocks of a region's keys form one
+// contiguous slice of the filter (bloom_block and region_of share the hash prefix), so
+// the gate reads stay within a few KiB that L2 keeps.
 constexpr int P3_THREADS = 1024;  // two 64 KiB regions per CU: 8 waves per SIMD
-template <int W, bool SEG, bool CNT>
+template <int W, bool SEG, bool CNT, bool GATE = false>
 __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView tv, PartBufs pb,
                                                                   DevCounters* __restrict__ ctr,
-                                                                  const unsigned long long* gate, int fresh) {
+                                                                  const unsigned long long* gate, int fresh,
+                                                                  BloomView bf) {
     constexpr int NT = P3_THREADS;
     constexpr int IW = CNT ? W + 1 : W;  // words per item
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -915,7 +1014,7 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
             __syncthreads();
         }
     }
-    uint32_t n_fail = 0;
+    uint32_t n_fail = 0, n_ins = 0;
     // SEG: segment cursor of this thread (indices grow monotonically): segment cs holds
     // [cb, nb), both bounds in registers
     uint32_t cs = 0, cb = 0, nb = 0;
@@ -953,9 +1052,16 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
         const uint64_t nbase = base + (uint64_t)KB * NT;
         const bool more = KC_PREFETCH && W <= 2 && nbase < end;  // W > 2: no spare registers
         if (more) load_items(nbase, nkk, nadd);
+        bool pass[KB];
+#pragma unroll
+        for (int q = 0; q < KB; q++) {  // the gate reads of all KB items are issued together
+            pass[q] = base + threadIdx.x + (uint64_t)q * NT < end;
+            if constexpr (GATE) pass[q] = pass[q] && block_gate(bloom_block_ptr(bf, kk[q][0]), kk[q][0], bf.nh_gate);
+            n_ins += pass[q];
+        }
 #pragma unroll
         for (int q = 0; q < KB; q++) {
-            if (base + threadIdx.x + (uint64_t)q * NT >= end) continue;
+            if (!pass[q]) continue;
             const uint64_t k0 = kk[q][0];
             uint32_t b = bucket_in_region(k0, tv.R);
             bool done = false;
@@ -1120,6 +1226,99 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
     __syncthreads();
     for (int i = threadIdx.x; i < N4; i += NT) g4[i] = l4[lds_chunk(i >> 3, i & 7)];
     if (n_fail) atomicAdd(&ctr->overflow, (unsigned long long)n_fail);
+    if constexpr (GATE) {  // the gated insertions (level 1 counted the windows)
+        unsigned long long x = n_ins;
+        for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+        if ((threadIdx.x & 63) == 0 && x) atomicAdd(&ctr->inserted, x);
+    }
+}
+
+// Bloom pass 1, level 3 (blocked layout): one workgroup per filter region of `bpr`
+// blocks (64 KiB): the region -> LDS (zero-filled when the filter is fresh), the
+// reference's insertion_process for every key of the region with LDS atomics
+// (block_insert), the region back to HBM.  Replaces one scattered device-scope atomic per
+// bit (the direct pass) with two sequential sweeps of the filter per batch.
+// SEG: the region's keys are its B2 level-2 segments (fills in hist2); otherwise the
+// contiguous run [off2[r * B2], off2[(r + 1) * B2]).
+constexpr int B3_THREADS = 1024;  // two 64 KiB regions per CU
+template <bool SEG>
+__global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView bf, uint32_t bpr, PartBufs pb,
+                                                                  DevCounters* __restrict__ ctr,
+                                                                  const unsigned long long* gate, int fresh) {
+    constexpr int NT = B3_THREADS, KB = 4;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ uint32_t s_pre[65];
+    if constexpr (SEG) {
+        if (ctr->part_overflow) return;
+    } else {
+        if (gated_off(gate)) return;
+    }
+    uint32_t* lf = reinterpret_cast<uint32_t*>(smem);
+    const uint64_t r = blockIdx.x;
+    uint64_t start, end;
+    if constexpr (SEG) {
+        if (threadIdx.x == 0) {
+            uint32_t acc = 0;
+            for (uint32_t j = 0; j < pb.B2; j++) {
+                s_pre[j] = acc;
+                acc += pb.hist2[r * pb.B2 + j];
+            }
+            s_pre[pb.B2] = acc;
+        }
+        __syncthreads();
+        start = 0;
+        end = s_pre[pb.B2];
+    } else {
+        start = pb.off2[r * pb.B2];
+        end = pb.off2[(r + 1) * pb.B2];
+    }
+    if (start == end) return;  // the region keeps its bits (a fresh filter is zero already)
+    const uint32_t n4 = bpr * BF_BLOCK_WORDS / 4;
+    uint4* g4 = reinterpret_cast<uint4*>(bf.bits + r * bpr * BF_BLOCK_WORDS);
+    uint4* l4 = reinterpret_cast<uint4*>(lf);
+    for (uint32_t i = threadIdx.x; i < n4; i += NT) l4[i] = fresh ? make_uint4(0, 0, 0, 0) : g4[i];
+    __syncthreads();
+    const uint64_t blk0 = r * bpr;
+    BloomLocal bl = {0, 0, 0};
+    uint32_t cs = 0, cb = 0, nb = 0;  // SEG: segment cursor (indices grow monotonically)
+    if constexpr (SEG) nb = s_pre[1];
+    for (uint64_t base = start; base < end; base += (uint64_t)KB * NT) {
+        uint64_t t0[KB];
+#pragma unroll
+        for (int q = 0; q < KB; q++) {
+            const uint64_t i = base + threadIdx.x + (uint64_t)q * NT;
+            t0[q] = EMPTY;
+            if (i < end) {
+                if constexpr (SEG) {
+                    while (nb <= i) {
+                        cs++;
+                        cb = nb;
+                        nb = s_pre[cs + 1];
+                    }
+                    t0[q] = pb.keys2[(r * pb.B2 + cs) * pb.cap2 + (i - cb)];
+                } else {
+                    t0[q] = pb.keys2[i];
+                }
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < KB; q++)
+            if (base + threadIdx.x + (uint64_t)q * NT < end) {
+                const uint32_t lb = (uint32_t)(bloom_block(t0[q], bf.nblocks) - blk0);
+                block_insert(lf + lb * BF_BLOCK_WORDS, t0[q], bf.nh, bl);
+            }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n4; i += NT) g4[i] = l4[i];
+    unsigned long long v[3] = {bl.new_first, bl.new_second, bl.failed};
+#pragma unroll
+    for (int c = 0; c < 3; c++)
+        for (int d = 32; d >= 1; d >>= 1) v[c] += __shfl_xor(v[c], d, 64);
+    if ((threadIdx.x & 63) == 0) {
+        if (v[0]) atomicAdd(&ctr->new_in_first, v[0]);
+        if (v[1]) atomicAdd(&ctr->new_in_second, v[1]);
+        if (v[2]) atomicAdd(&ctr->failed_in_first, v[2]);
+    }
 }
 
 // exclusive scan of n u32 -> u64 (out has n+1 entries), three passes:
@@ -1413,23 +1612,20 @@ static hipError_t set_smem(K kernel, size_t bytes) {
 
 static BinRegion coarse_bins(const TableView& t) { return BinRegion{t.R, t.f2bits, 0, 1}; }
 
-template <int W, bool SEG, bool CNT = false>
+template <int W, bool SEG, bool CNT = false, bool GATE = false>
 static hipError_t launch_p3(TableView t, DevCounters* ctr, PartBufs pb, const unsigned long long* gate, int fresh,
-                            hipStream_t s) {
+                            hipStream_t s, BloomView bf = BloomView{}) {
     const size_t sm3 = (size_t)BPR * BUCKET_WORDS * 8 + (KC_P3_TAGS ? (size_t)BPR * 8 : 0);
-    auto p3 = k_p3<W, SEG, CNT>;
+    auto p3 = k_p3<W, SEG, CNT, GATE>;
     hipError_t e = set_smem(p3, sm3);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(p3, dim3((unsigned)t.R), dim3(P3_THREADS), sm3, s, t, pb, ctr, gate, fresh);
+    hipLaunchKernelGGL(p3, dim3((unsigned)t.R), dim3(P3_THREADS), sm3, s, t, pb, ctr, gate, fresh, bf);
     return hipGetLastError();
 }
 
-// levels 2 and 3 on the exact layout (after an exact level 1); `gate` as in k_p1.
-// CNT: the items are {W key words, count} records (W + 1 words each).
-template <int W, bool CNT = false>
-static hipError_t part_levels23(TableView t, DevCounters* ctr, PartBufs pb, hipStream_t s,
-                                const unsigned long long* gate = nullptr, int fresh = 0) {
-    constexpr int IW = CNT ? W + 1 : W;
+// level 2 on the exact layout (after an exact level 1): items of IW words; `gate` as in k_p1
+template <int IW>
+static hipError_t part_level2_exact(TableView t, PartBufs pb, hipStream_t s, const unsigned long long* gate) {
     const size_t sm2 = part_smem<IW>(t.F2), sm2h = hist_smem(t.F2);
     hipError_t e;
     if ((e = set_smem(k_p2<IW, false>, sm2h)) != hipSuccess) return e;
@@ -1437,7 +1633,29 @@ static hipError_t part_levels23(TableView t, DevCounters* ctr, PartBufs pb, hipS
     hipLaunchKernelGGL((k_p2<IW, false>), dim3(t.F1 * pb.B2), dim3(COUNT_THREADS), sm2h, s, t, pb, gate);
     launch_scan(pb.hist2, t.R * pb.B2, pb.off2, pb.bsum, s, gate);
     hipLaunchKernelGGL((k_p2<IW, true>), dim3(t.F1 * pb.B2), dim3(COUNT_THREADS), sm2, s, t, pb, gate);
-    return launch_p3<W, false, CNT>(t, ctr, pb, gate, fresh, s);
+    return hipGetLastError();
+}
+
+// levels 2 and 3 on the exact layout (after an exact level 1); `gate` as in k_p1.
+// CNT: the items are {W key words, count} records (W + 1 words each).  GATE: Bloom gate
+// at level 3 (bf).
+template <int W, bool CNT = false, bool GATE = false>
+static hipError_t part_levels23(TableView t, DevCounters* ctr, PartBufs pb, hipStream_t s,
+                                const unsigned long long* gate = nullptr, int fresh = 0, BloomView bf = BloomView{}) {
+    hipError_t e = part_level2_exact<CNT ? W + 1 : W>(t, pb, s, gate);
+    if (e != hipSuccess) return e;
+    return launch_p3<W, false, CNT, GATE>(t, ctr, pb, gate, fresh, s, bf);
+}
+
+template <bool SEG>
+static hipError_t launch_b3(BloomView bf, TableView ft, DevCounters* ctr, PartBufs pb, const unsigned long long* gate,
+                            int fresh, hipStream_t s) {
+    const uint32_t bpr = (uint32_t)(bf.nblocks / ft.R);
+    const size_t sm = (size_t)bpr * BF_BLOCK_WORDS * 4;
+    hipError_t e = set_smem(k_b3<SEG>, sm);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_b3<SEG>, dim3((unsigned)ft.R), dim3(B3_THREADS), sm, s, bf, bpr, pb, ctr, gate, fresh);
+    return hipGetLastError();
 }
 
 // level 1 from the symbol stream, exact layout: windows -> F bins by `bin`, keys into `out`
@@ -1445,7 +1663,7 @@ template <int W, int MODE, class Bin>
 static hipError_t part_level1(PackedView sym, int k, BloomView bf, DevCounters* ctr, PartBufs pb, uint32_t F,
                               Bin bin, uint64_t* out, hipStream_t s, const unsigned long long* gate = nullptr) {
     const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
-    const size_t sm1 = part_smem<W>(F), sm1h = hist_smem(F);
+    const size_t sm1 = part_smem<p1_out_words(W, MODE)>(F), sm1h = hist_smem(F);
     hipError_t e;
     auto kh = k_p1<W, MODE, false, Bin, OutExact>;
     auto ks = k_p1<W, MODE, true, Bin, OutExact>;
@@ -1467,10 +1685,11 @@ static hipError_t part_level1(PackedView sym, int k, BloomView bf, DevCounters* 
 template <int W, int MODE>
 static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf, DevCounters* ctr, PartBufs pb,
                                 int fresh, hipStream_t s) {
+    constexpr bool GATE3 = MODE == 4;
     if (pb.cap1 == 0) {
         hipError_t e = part_level1<W, MODE>(sym, k, bf, ctr, pb, t.F1, coarse_bins(t), pb.keys1, s);
         if (e != hipSuccess) return e;
-        return part_levels23<W>(t, ctr, pb, s, nullptr, fresh);
+        return part_levels23<W, false, GATE3>(t, ctr, pb, s, nullptr, fresh, bf);
     }
     hipError_t e;
     const unsigned long long* gate = &ctr->part_overflow;
@@ -1489,21 +1708,74 @@ static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf
     hipLaunchKernelGGL(k1, dim3(pb.nblk1), dim3(scatter_threads<W>()), sm1, s, sym, k, bf, ctr, pb, t.F1, coarse_bins(t),
                        pb.keys1, pk, pkm1, o1, (const unsigned long long*)nullptr, 1);
     hipLaunchKernelGGL((k_p2f<W, scatter_threads<W>()>), dim3(t.F1 * pb.B2), dim3(scatter_threads<W>()), sm2, s, t, pb, ctr);
-    if ((e = launch_p3<W, true>(t, ctr, pb, nullptr, fresh, s)) != hipSuccess) return e;
+    if ((e = launch_p3<W, true, false, GATE3>(t, ctr, pb, nullptr, fresh, s, bf)) != hipSuccess) return e;
     if ((e = part_level1<W, MODE>(sym, k, bf, ctr, pb, t.F1, coarse_bins(t), pb.keys1, s, gate)) != hipSuccess)
         return e;
-    return part_levels23<W>(t, ctr, pb, s, gate, fresh);
+    return part_levels23<W, false, GATE3>(t, ctr, pb, s, gate, fresh, bf);
 }
 
+// mode 2 (counting behind the Bloom gate): blocked layout -> gate at level 3 (MODE 4),
+// reference layout -> gate on the rolled root at level 1 (MODE 2)
+template <int W>
+static hipError_t count_part_w(PackedView sym, int k, int mode, TableView t, BloomView bf, DevCounters* ctr,
+                               PartBufs pb, int fresh, hipStream_t s) {
+    if (mode != 2) return launch_part_w<W, 0>(sym, k, t, bf, ctr, pb, fresh, s);
+    if (bf.blocked) return launch_part_w<W, 4>(sym, k, t, bf, ctr, pb, fresh, s);
+    return launch_part_w<W, 2>(sym, k, t, bf, ctr, pb, fresh, s);
+}
 hipError_t launch_count_partitioned(PackedView sym, uint64_t sym_bound, int k, int mode, TableView t,
                                     BloomView bf, DevCounters* ctr, PartBufs pb, int fresh, hipStream_t s) {
     (void)sym_bound;
-    const bool gate = mode == 2;
     switch (t.W) {
-    case 1: return gate ? launch_part_w<1, 2>(sym, k, t, bf, ctr, pb, fresh, s) : launch_part_w<1, 0>(sym, k, t, bf, ctr, pb, fresh, s);
-    case 2: return gate ? launch_part_w<2, 2>(sym, k, t, bf, ctr, pb, fresh, s) : launch_part_w<2, 0>(sym, k, t, bf, ctr, pb, fresh, s);
-    case 3: return gate ? launch_part_w<3, 2>(sym, k, t, bf, ctr, pb, fresh, s) : launch_part_w<3, 0>(sym, k, t, bf, ctr, pb, fresh, s);
-    case 4: return gate ? launch_part_w<4, 2>(sym, k, t, bf, ctr, pb, fresh, s) : launch_part_w<4, 0>(sym, k, t, bf, ctr, pb, fresh, s);
+    case 1: return count_part_w<1>(sym, k, mode, t, bf, ctr, pb, fresh, s);
+    case 2: return count_part_w<2>(sym, k, mode, t, bf, ctr, pb, fresh, s);
+    case 3: return count_part_w<3>(sym, k, mode, t, bf, ctr, pb, fresh, s);
+    case 4: return count_part_w<4>(sym, k, mode, t, bf, ctr, pb, fresh, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+// Bloom pass 1 on the blocked layout, partitioned: windows -> table key word 0 -> coarse
+// bins -> filter regions (ft: R = filter regions, F1 x F2) -> k_b3 (LDS-resident filter
+// regions).  Segmented single passes with the exact pipeline behind the overflow gate,
+// as for the table.
+template <int W>
+static hipError_t bloom_part_w(PackedView sym, int k, BloomView bf, TableView ft, DevCounters* ctr, PartBufs pb,
+                               int fresh, hipStream_t s) {
+    if (pb.cap1 == 0) {
+        hipError_t e = part_level1<W, 3>(sym, k, bf, ctr, pb, ft.F1, coarse_bins(ft), pb.keys1, s);
+        if (e != hipSuccess) return e;
+        if ((e = part_level2_exact<1>(ft, pb, s, nullptr)) != hipSuccess) return e;
+        return launch_b3<false>(bf, ft, ctr, pb, nullptr, fresh, s);
+    }
+    hipError_t e;
+    const unsigned long long* gate = &ctr->part_overflow;
+    if ((e = hipMemsetAsync(&ctr->part_overflow, 0, sizeof(ctr->part_overflow), s)) != hipSuccess) return e;
+    const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
+    constexpr int NT = scatter_threads<W>();
+    auto k1 = k_p1<W, 3, true, BinRegion, OutSeg, NT>;
+    const size_t sm1 = part_smem<1, NT>(ft.F1), sm2 = p2f_smem<1, NT>(ft.F2, (pb.nblk1 + pb.B2 - 1) / pb.B2);
+    if ((e = set_smem(k1, sm1)) != hipSuccess) return e;
+    if ((e = set_smem(k_p2f<1, NT>, sm2)) != hipSuccess) return e;
+    const OutSeg o1{(uint64_t)pb.nblk1 * pb.cap1, 0, pb.cap1};
+    hipLaunchKernelGGL(k1, dim3(pb.nblk1), dim3(NT), sm1, s, sym, k, bf, ctr, pb, ft.F1, coarse_bins(ft), pb.keys1, pk,
+                       pkm1, o1, (const unsigned long long*)nullptr, 1);
+    hipLaunchKernelGGL((k_p2f<1, NT>), dim3(ft.F1 * pb.B2), dim3(NT), sm2, s, ft, pb, ctr);
+    if ((e = launch_b3<true>(bf, ft, ctr, pb, nullptr, fresh, s)) != hipSuccess) return e;
+    if ((e = part_level1<W, 3>(sym, k, bf, ctr, pb, ft.F1, coarse_bins(ft), pb.keys1, s, gate)) != hipSuccess)
+        return e;
+    if ((e = part_level2_exact<1>(ft, pb, s, gate)) != hipSuccess) return e;
+    return launch_b3<false>(bf, ft, ctr, pb, gate, fresh, s);
+}
+hipError_t launch_bloom_partitioned(PackedView sym, int k, int W, BloomView bf, TableView ft, DevCounters* ctr,
+                                    PartBufs pb, int fresh, hipStream_t s) {
+    if (!bf.blocked || ft.R == 0 || bf.nblocks % ft.R || bf.nblocks / ft.R > BF_BLOCKS_PER_REGION)
+        return hipErrorInvalidValue;
+    switch (W) {
+    case 1: return bloom_part_w<1>(sym, k, bf, ft, ctr, pb, fresh, s);
+    case 2: return bloom_part_w<2>(sym, k, bf, ft, ctr, pb, fresh, s);
+    case 3: return bloom_part_w<3>(sym, k, bf, ft, ctr, pb, fresh, s);
+    case 4: return bloom_part_w<4>(sym, k, bf, ft, ctr, pb, fresh, s);
     default: return hipErrorInvalidValue;
     }
 }

@@ -106,8 +106,8 @@ struct BloomView {
     uint64_t mask;          // nbits - 1
     int nh;                 // ceil(hf): pass-1 hashes
     int nh_gate;            // trunc(hf): pass-2 gate hashes
-    int blocked;            // 1: one 512-bit block per k-mer (kc_count.hip bloom_slots)
-    uint64_t bmask;         // blocks - 1 (blocks = max(1, nbits / 256))
+    int blocked;            // 1: one 512-bit block per k-mer (kc_count.hip, blocked layout)
+    uint64_t nblocks;       // blocks (a power of two: max(1, nbits / 256))
 };
 
 inline int words_for_k(int k) { return k / 32 + 1; }          // spare top bit for EMPTY
@@ -121,10 +121,16 @@ hipError_t launch_tokenize(const uint8_t* src, uint64_t ntiles, const ChunkDesc*
 // mode: 0 count all windows, 1 Bloom pass 1, 2 count windows passing the Bloom gate
 hipError_t launch_count(PackedView sv, uint64_t sym_bound, int k, int mode, TableView t, BloomView bf,
                         DevCounters* ctr, hipStream_t s);
-// partitioned insert for modes 0 and 2 (same table, same result as launch_count)
+// partitioned insert for modes 0 and 2 (same table, same result as launch_count; mode 2
+// gates at level 3 on the blocked Bloom layout, at level 1 on the reference layout)
 // fresh: the table is all zero (just allocated or reset): level 3 does not read it
 hipError_t launch_count_partitioned(PackedView sv, uint64_t sym_bound, int k, int mode, TableView t,
                                     BloomView bf, DevCounters* ctr, PartBufs pb, int fresh, hipStream_t s);
+// Bloom pass 1 on the blocked layout, partitioned: ft = the filter's region geometry
+// (R = filter regions of nblocks / R <= 1024 blocks, F1 x F2 as for the table; no buckets);
+// fresh: the filter is all zero (level 3 does not read it)
+hipError_t launch_bloom_partitioned(PackedView sv, int k, int W, BloomView bf, TableView ft, DevCounters* ctr,
+                                    PartBufs pb, int fresh, hipStream_t s);
 int run_width(int W);  // windows rolled per thread in the partitioned kernels
 int p1_tile(int W);    // windows per tile of the segmented level-1 kernel
 // hash-prefix sharding: windows -> table keys grouped by owner (offsets in pb.off1)

@@ -292,3 +292,54 @@ def test_fastq_equals_plain_sequence_lines(k, tmp_path):
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert sorted_digest_file(out) == want
+
+
+@pytest.mark.parametrize("k", [31, 51])
+def test_bloom_at_scale_equals_exact_solid_kmers(k, insert_path):
+    """Bloom filter (-b, blocked layout) on a larger device-generated input: pass 1 runs
+    the partitioned LDS filter (k_b3) or the direct one, pass 2 gates at level 3 (or in
+    the direct kernel).  The filter only gates, so every k-mer seen >= 2 times has its
+    exact count (the same records as counting without the filter at -a 2), every
+    window is seen by both passes, and at most the windows are inserted."""
+    torch = pytest.importorskip("torch")
+    lib = ka.load_library()
+    N, L, G = 300_000, 150, 3_000_000
+    nbytes = lib.kc_synth_bytes(0, N, L, 0)
+    img = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    assert lib.kc_synth_device(img.data_ptr(), 0, N, 11, G, L, 0, 0.002, 0.0, 0) == 0
+    torch.cuda.synchronize()
+    host = bytes(img.cpu().numpy())
+    chunks = ka.plan_chunks(host, k, ka.FMT_FASTA)
+    with ka.KmerCounter(ka.Config(k=k, min_abundance=2, table_slots=20_000_000)) as kc:
+        kc.count_device(img.data_ptr(), chunks, ka.FMT_FASTA)
+        kc.finish()
+        want = kc.dump()
+    with ka.KmerCounter(ka.Config(k=k, min_abundance=2, bf_enable=True, est_unique=8_000_000,
+                                  fpr=0.01)) as kc:
+        kc.bloom_device(img.data_ptr(), chunks, ka.FMT_FASTA)
+        n2 = kc.bloom_finalize()
+        kc.count_device(img.data_ptr(), chunks, ka.FMT_FASTA)
+        st = kc.finish()
+        got = kc.dump()
+    windows = N * (L - k + 1)
+    assert st["windows"] == windows and st["bf_windows"] == windows
+    assert st["inserted"] <= windows and n2 > 0
+    a = want[np.lexsort(want[:, :-1].T[::-1])]
+    b = got[np.lexsort(got[:, :-1].T[::-1])]
+    assert np.array_equal(a, b)
+
+
+def test_bloom_segment_overflow_falls_back_to_exact(golden_input, tmp_path, monkeypatch):
+    """Forced tiny segments in the partitioned Bloom pass and the gated count pass: the
+    device redoes both on the exact layout and the result is still the reference's."""
+    monkeypatch.setenv("KC_INSERT_PATH", "partitioned")
+    monkeypatch.setenv("KC_SEG_CAP", "8")
+    path = golden_input("reads_w60.fasta")
+    args = ["-b", "-u", "200000", "-a", "2"]
+    kc, st = ka.count_file(path, 31, min_abundance=2, bf_enable=True, est_unique=200000, fpr=0.01)
+    with kc:
+        assert st["part_fallbacks"] >= 2
+        lines = kc.lines()
+    out = tmp_path / "oracle.txt"
+    oracle_count(path, 31, args, out)
+    assert sorted_digest_lines(lines) == sorted_digest_file(out)
