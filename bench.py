@@ -308,7 +308,7 @@ def main():
         "kernel_ms": {"gather": round(tm["gather_ms"] / launches, 4), "tokenize": round(tm["tokenize_ms"] / launches, 4),
                       "count": round(count_ms, 4)},
         "image_bytes": nbytes, "stage_bytes": sum(c[1] for c in chunks),
-        "windows_per_step_per_gpu": windows_step, "distinct_per_gpu": st["distinct"],
+        "windows_per_step_per_gpu": windows_step, "distinct_per_gpu": st["distinct"], "table_slots": st["table_slots"],
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -111,90 +111,110 @@ struct BloomLocal {
 // Two layouts of the k-mer's positions:
 //  reference (KC_BLOOM_LAYOUT=reference; mybitarray + calculate_hashes,
 //    double_bloomfilter.hpp:276-281): h_j = XXH64(root, seed_j) & (bits - 1), root = the
-//    strand-symmetric Rabin-Karp hash mod 2^54: n independent random words.
-//  blocked (the default): all positions lie in one 512-bit block (one 64-byte line: 256
-//    positions of both filters).  The block is picked by the top bits of the k-mer's table
-//    key word 0 t0 (kc_common.h to_tkey, a bijective mix of the canonical key): block =
+//    strand-symmetric Rabin-Karp hash mod 2^54: n independent random words, filter-1 bit
+//    of h at 2h and filter-2 bit at 2h+1 (MyAtomicBitArrayFT, mybitarray.hpp:30-125).
+//  blocked (the default): a split-block filter.  Each k-mer owns one 64-byte block of 16
+//    words: words 0-7 hold filter 1, words 8-15 filter 2 (the same 2 x 256 bits per block
+//    as the interleaved bit array).  Position j sets bit b_j = bits 5j..5j+4 of
+//    bmix(t0) in word j mod 8 of each filter, so the positions of one k-mer lie in
+//    distinct words (no repeats for ceil(hf) <= 8) and a test is two 16-byte reads and
+//    a shift per position.  The block is picked by the top bits of the k-mer's table key
+//    word 0 t0 (kc_common.h to_tkey, a bijective mix of the canonical key): block =
 //    ((t0 >> 32) * blocks) >> 32, the same hash prefix as the table's region index, so a
 //    filter region of BF_BLOCKS_PER_REGION blocks is one contiguous 64 KiB slice that the
-//    partitioned Bloom pass holds in LDS (k_b3) and the table's level 3 reads gate bits
-//    from (k_p3<..., GATE>).  Position j = byte j of bmix(t0, 1) (byte j - 8 of
-//    bmix(t0, 2) for j >= 8).  The filter only gates, so either layout gives the
-//    reference's counts for every k-mer seen at least twice.
-constexpr int BF_BLOCK_WORDS = 16;               // 512 bits
+//    partitioned Bloom pass holds in LDS (k_b3), and the filter-2 words of a table
+//    region's keys are one contiguous slice its level 3 copies to LDS for the gate
+//    (k_p3<..., GATE>).  The filter only gates, so either layout gives the reference's
+//    counts for every k-mer seen at least twice.
+constexpr int BF_BLOCK_WORDS = 16;               // 512 bits: filter 1 in words 0-7, filter 2 in 8-15
 constexpr int BF_BLOCKS_PER_REGION = 1024;       // 64 KiB of filter per LDS region
-DEV uint64_t bloom_block(uint64_t t0, uint64_t nblocks) { return ((t0 >> 32) * nblocks) >> 32; }
-DEV uint64_t bmix(uint64_t t0, uint64_t s) {  // splitmix64 finalizer of t0 ^ seed
-    uint64_t x = t0 ^ (s * 0xD6E8FEB86659FD93ULL);
-    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
-    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+// ((t0 >> 32) * nblocks) >> 32 for the power-of-two block count: a shift (the count is
+// uniform, so its log2 is scalar work)
+DEV uint64_t bloom_block(uint64_t t0, uint64_t nblocks) { return (t0 >> 32) >> (32 - __builtin_ctzll(nblocks)); }
+// position hash: t0 is already a strong mix of the key (to_tkey), one multiply-fold
+// spreads its low bits (which vary inside a block) over all position fields
+DEV uint64_t bmix(uint64_t t0) {
+    const uint64_t x = (t0 ^ 0xD6E8FEB86659FD93ULL) * 0xBF58476D1CE4E5B9ULL;
     return x ^ (x >> 31);
 }
-// positions j < n of the blocked layout: word of the block and filter-1 bit mask; dup[j]:
-// position j repeats an earlier one (a k-mer's own bit counts once)
-DEV void blocked_positions(uint64_t t0, int n, uint32_t (&word)[MAX_NH], uint32_t (&m1)[MAX_NH],
-                           bool (&dup)[MAX_NH]) {
-    const uint64_t h1 = bmix(t0, 1), h2 = n > 8 ? bmix(t0, 2) : 0;
-    uint32_t p[MAX_NH];
+// bit of position j (word j & 7 of a filter): 5-bit fields, six per 32-bit half of h (no
+// field straddles the halves, so each is one bit-field extract)
+DEV uint32_t sb_bit(uint64_t h, int j) {
+    return j < 6 ? ((uint32_t)h >> (5 * j)) & 31 : ((uint32_t)(h >> 32) >> (5 * (j - 6))) & 31;
+}
+// the 8 words of one filter of a block (16-byte aligned) into registers
+DEV void load8(const uint32_t* p, uint32_t (&w)[8]) {
+    const uint4 a = reinterpret_cast<const uint4*>(p)[0], b = reinterpret_cast<const uint4*>(p)[1];
+    w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+    w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+}
+// all of the first n positions set in the 8 words f (one filter of a block): the bits of
+// all MAX_NH positions gathered branch-free (two extracts and a shift-or each), then masked
+DEV bool sb_all(const uint32_t (&f)[8], uint64_t h, int n) {
+    uint32_t got = 0;
 #pragma unroll
-    for (int j = 0; j < MAX_NH; j++) {
-        p[j] = (uint32_t)(((j < 8 ? h1 : h2) >> (8 * (j & 7))) & 255);
-        word[j] = p[j] >> 4;
-        m1[j] = 1u << (2 * (p[j] & 15));
-        bool d = false;
-#pragma unroll
-        for (int i = 0; i < j; i++) d |= p[i] == p[j];
-        dup[j] = d || j >= n;
-    }
+    for (int j = 0; j < MAX_NH; j++) got |= ((f[j & 7] >> sb_bit(h, j)) & 1) << j;
+    const uint32_t need = (1u << n) - 1;
+    return (got & need) == need;
 }
 
 // insertion_process (double_bloomfilter.hpp:371-413) on one block of the blocked layout;
 // `blk` is the block in HBM (direct pass) or in LDS (k_b3).  A "set" counts as ours only
 // if our atomicOr flipped the bit (MyAtomicBitArrayFT::set, mybitarray.hpp:87-125).
+// Positions j >= 8 share word j - 8 and count once if they repeat its bit.
 DEV void block_insert(uint32_t* blk, uint64_t t0, int nh, BloomLocal& loc) {
-    uint32_t word[MAX_NH], m1[MAX_NH], view[MAX_NH];
-    bool dup[MAX_NH];
-    blocked_positions(t0, nh, word, m1, dup);
+    const uint64_t h = bmix(t0);
+    uint32_t f1[8], f2[8];
+    load8(blk + 8, f2);
+    if (sb_all(f2, h, nh)) return;  // in the second filter already
+    load8(blk, f1);
     int n = 0, s1 = 0, s2 = 0;
+    bool dup[MAX_NH];
 #pragma unroll
-    for (int j = 0; j < MAX_NH; j++)
+    for (int j = 0; j < MAX_NH; j++) {
+        dup[j] = j >= nh || (j >= 8 && sb_bit(h, j) == sb_bit(h, j - 8));
         if (!dup[j]) {
-            view[j] = blk[word[j]];
             n++;
-            s1 += (view[j] & m1[j]) != 0;
-            s2 += (view[j] & (m1[j] << 1)) != 0;
+            s1 += (f1[j & 7] >> sb_bit(h, j)) & 1;
+            s2 += (f2[j & 7] >> sb_bit(h, j)) & 1;
         }
-    if (s2 == n) return;  // in the second filter already
+    }
     bool to_second = true;
     if (s1 != n) {
         int mine = 0;
 #pragma unroll
-        for (int j = 0; j < MAX_NH; j++)
-            if (!dup[j] && !(view[j] & m1[j])) mine += !(atomicOr(blk + word[j], m1[j]) & m1[j]);
+        for (int j = 0; j < MAX_NH; j++) {
+            const uint32_t m = 1u << sb_bit(h, j);
+            if (!dup[j] && !(f1[j & 7] & m)) mine += !(atomicOr(blk + (j & 7), m) & m);
+        }
         if (mine == n - s1) { loc.new_first++; to_second = false; }
         else loc.failed++;
     }
     if (to_second) {
         int mine = 0;
 #pragma unroll
-        for (int j = 0; j < MAX_NH; j++)
-            if (!dup[j] && !(view[j] & (m1[j] << 1)))
-                mine += !(atomicOr(blk + word[j], m1[j] << 1) & (m1[j] << 1));
+        for (int j = 0; j < MAX_NH; j++) {
+            const uint32_t m = 1u << sb_bit(h, j);
+            if (!dup[j] && !(f2[j & 7] & m)) mine += !(atomicOr(blk + 8 + (j & 7), m) & m);
+        }
         if (mine == n - s2) loc.new_second++;
     }
 }
 
-// pass-2 gate on one block: all of the first trunc(hf) filter-2 bits set
-// (parallel_parser.hpp:2436-2441)
-DEV bool block_gate(const uint32_t* blk, uint64_t t0, int nh_gate) {
-    uint32_t word[MAX_NH], m1[MAX_NH];
-    bool dup[MAX_NH];
-    blocked_positions(t0, nh_gate, word, m1, dup);
-    bool all = true;
-#pragma unroll
-    for (int j = 0; j < MAX_NH; j++)
-        if (j < nh_gate) all &= (blk[word[j]] & (m1[j] << 1)) != 0;
-    return all;
+// pass-2 gate: all of the first trunc(hf) filter-2 bits set (parallel_parser.hpp:
+// 2436-2441); f2 = the block's 8 filter-2 words (HBM, or the LDS slice of k_p3)
+DEV bool block_gate(const uint32_t* f2, uint64_t t0, int nh_gate) {
+    uint32_t w[8];
+    load8(f2, w);
+    return sb_all(w, bmix(t0), nh_gate);
+}
+// blocks [lo, hi] hold the filter of table region r's keys (region_of and bloom_block
+// are monotone in the same 32-bit hash prefix)
+DEV void region_blocks(uint64_t r, uint64_t R, uint64_t nblocks, uint64_t& lo, uint64_t& hi) {
+    const uint64_t h_lo = ((r << 32) + R - 1) / R;                               // first prefix of r
+    const uint64_t h_hi = min((((r + 1) << 32) + R - 1) / R, 1ULL << 32) - 1;   // last prefix of r
+    lo = (h_lo * nblocks) >> 32;
+    hi = (h_hi * nblocks) >> 32;
 }
 
 // reference layout: word and bit (of the filter-1 bit; filter 2 is the next bit) of the
@@ -270,7 +290,7 @@ DEV void bloom_insert(const BloomView& bf, uint64_t root, uint64_t t0, BloomLoca
 }
 
 DEV bool bloom_gate(const BloomView& bf, uint64_t root, uint64_t t0) {
-    if (bf.blocked) return block_gate(bloom_block_ptr(bf, t0), t0, bf.nh_gate);
+    if (bf.blocked) return block_gate(bloom_block_ptr(bf, t0) + 8, t0, bf.nh_gate);
     uint64_t widx[MAX_NH];
     uint32_t bpos[MAX_NH];
     ref_slots(bf, root, bf.nh_gate, widx, bpos);
@@ -1014,6 +1034,20 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
             __syncthreads();
         }
     }
+    // GATE with an LDS slice: the filter-2 bits of the region's blocks, 8 words per block
+    uint32_t* gs = reinterpret_cast<uint32_t*>(tg + (KC_P3_TAGS ? BPR : 0));
+    uint64_t gblo = 0;
+    if constexpr (GATE) {
+        if (bf.slice_blocks) {
+            uint64_t ghi;
+            region_blocks(r, tv.R, bf.nblocks, gblo, ghi);
+            const uint32_t n4 = (uint32_t)(ghi - gblo + 1) * 2;  // filter-2 halves of the blocks, as uint4
+            const uint4* src = reinterpret_cast<const uint4*>(bf.bits + gblo * BF_BLOCK_WORDS);
+            uint4* dst = reinterpret_cast<uint4*>(gs);
+            for (uint32_t i = threadIdx.x; i < n4; i += NT) dst[i] = src[(i >> 1) * 4 + 2 + (i & 1)];
+            __syncthreads();
+        }
+    }
     uint32_t n_fail = 0, n_ins = 0;
     // SEG: segment cursor of this thread (indices grow monotonically): segment cs holds
     // [cb, nb), both bounds in registers
@@ -1056,7 +1090,13 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
 #pragma unroll
         for (int q = 0; q < KB; q++) {  // the gate reads of all KB items are issued together
             pass[q] = base + threadIdx.x + (uint64_t)q * NT < end;
-            if constexpr (GATE) pass[q] = pass[q] && block_gate(bloom_block_ptr(bf, kk[q][0]), kk[q][0], bf.nh_gate);
+            if constexpr (GATE) {
+                const uint64_t t0 = kk[q][0];
+                if (bf.slice_blocks)
+                    pass[q] = pass[q] && block_gate(gs + (bloom_block(t0, bf.nblocks) - gblo) * 8, t0, bf.nh_gate);
+                else
+                    pass[q] = pass[q] && block_gate(bloom_block_ptr(bf, t0) + 8, t0, bf.nh_gate);
+            }
             n_ins += pass[q];
         }
 #pragma unroll
@@ -1279,6 +1319,8 @@ __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView b
     for (uint32_t i = threadIdx.x; i < n4; i += NT) l4[i] = fresh ? make_uint4(0, 0, 0, 0) : g4[i];
     __syncthreads();
     const uint64_t blk0 = r * bpr;
+    const int lane = threadIdx.x & 63;
+    uint64_t* wq = reinterpret_cast<uint64_t*>(smem + (size_t)bpr * BF_BLOCK_WORDS * 4) + (threadIdx.x >> 6) * 64;
     BloomLocal bl = {0, 0, 0};
     uint32_t cs = 0, cb = 0, nb = 0;  // SEG: segment cursor (indices grow monotonically)
     if constexpr (SEG) nb = s_pre[1];
@@ -1301,12 +1343,33 @@ __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView b
                 }
             }
         }
+        // fast path: a k-mer whose filter-2 bits are all set changes nothing (most
+        // occurrences of a k-mer seen before); the others are packed into the wave's queue
+        // so the insertion path runs on dense lanes instead of once per item slot
+        bool slow[KB];
+        uint32_t pre[KB], rank[KB], total = 0;
 #pragma unroll
-        for (int q = 0; q < KB; q++)
-            if (base + threadIdx.x + (uint64_t)q * NT < end) {
-                const uint32_t lb = (uint32_t)(bloom_block(t0[q], bf.nblocks) - blk0);
-                block_insert(lf + lb * BF_BLOCK_WORDS, t0[q], bf.nh, bl);
+        for (int q = 0; q < KB; q++) {
+            slow[q] = base + threadIdx.x + (uint64_t)q * NT < end &&
+                      !block_gate(lf + (uint32_t)(bloom_block(t0[q], bf.nblocks) - blk0) * BF_BLOCK_WORDS + 8, t0[q],
+                                  bf.nh);
+            const uint64_t bal = __ballot(slow[q]);
+            pre[q] = total;
+            rank[q] = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+            total += (uint32_t)__popcll(bal);
+        }
+        for (uint32_t r0 = 0; r0 < total; r0 += 64) {
+#pragma unroll
+            for (int q = 0; q < KB; q++)
+                if (slow[q] && pre[q] + rank[q] - r0 < 64) wq[pre[q] + rank[q] - r0] = t0[q];
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's queue writes land
+            if (lane < total - r0) {
+                const uint64_t t = wq[lane];
+                const uint32_t lb = (uint32_t)(bloom_block(t, bf.nblocks) - blk0);
+                block_insert(lf + lb * BF_BLOCK_WORDS, t, bf.nh, bl);
             }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // queue reads done before reuse
+        }
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < n4; i += NT) g4[i] = l4[i];
@@ -1615,7 +1678,14 @@ static BinRegion coarse_bins(const TableView& t) { return BinRegion{t.R, t.f2bit
 template <int W, bool SEG, bool CNT = false, bool GATE = false>
 static hipError_t launch_p3(TableView t, DevCounters* ctr, PartBufs pb, const unsigned long long* gate, int fresh,
                             hipStream_t s, BloomView bf = BloomView{}) {
-    const size_t sm3 = (size_t)BPR * BUCKET_WORDS * 8 + (KC_P3_TAGS ? (size_t)BPR * 8 : 0);
+    size_t sm3 = (size_t)BPR * BUCKET_WORDS * 8 + (KC_P3_TAGS ? (size_t)BPR * 8 : 0);
+    if (GATE) {
+        // the filter-2 slice goes to LDS if two workgroups still fit a CU (80 KiB each)
+        const uint64_t maxb = bf.nblocks / t.R + 2;
+        const size_t room = 80 * 1024 - sm3 - 512;
+        bf.slice_blocks = maxb * 32 <= room ? (uint32_t)maxb : 0;
+        sm3 += (size_t)bf.slice_blocks * 32;
+    }
     auto p3 = k_p3<W, SEG, CNT, GATE>;
     hipError_t e = set_smem(p3, sm3);
     if (e != hipSuccess) return e;
@@ -1651,7 +1721,7 @@ template <bool SEG>
 static hipError_t launch_b3(BloomView bf, TableView ft, DevCounters* ctr, PartBufs pb, const unsigned long long* gate,
                             int fresh, hipStream_t s) {
     const uint32_t bpr = (uint32_t)(bf.nblocks / ft.R);
-    const size_t sm = (size_t)bpr * BF_BLOCK_WORDS * 4;
+    const size_t sm = (size_t)bpr * BF_BLOCK_WORDS * 4 + (size_t)(B3_THREADS / 64) * 64 * 8;  // + wave queues
     hipError_t e = set_smem(k_b3<SEG>, sm);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_b3<SEG>, dim3((unsigned)ft.R), dim3(B3_THREADS), sm, s, bf, bpr, pb, ctr, gate, fresh);

@@ -108,6 +108,8 @@ struct BloomView {
     int nh_gate;            // trunc(hf): pass-2 gate hashes
     int blocked;            // 1: one 512-bit block per k-mer (kc_count.hip, blocked layout)
     uint64_t nblocks;       // blocks (a power of two: max(1, nbits / 256))
+    uint32_t slice_blocks;  // gated level 3: LDS capacity for a table region's filter-2 slice
+                            // (blocks; 0 = the gate reads HBM)
 };
 
 inline int words_for_k(int k) { return k / 32 + 1; }          // spare top bit for EMPTY

@@ -1,6 +1,11 @@
+# one GPU iteration: bash tools/gpu_iter.sh "<pytest -k expr or ALL>" [bench configs...]
+# pytest (GPU tests) -> bench.py per config -> kernel-trace profile of the first config
 set -o pipefail
+K=$1; shift
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "bloom or Bloom or -b" > gpurun_out/gpu_bloom.log 2>&1 && \
-timeout -k 10 200 python bench.py --config C3 --no-cpu-baseline > gpurun_out/bench_c3.json 2> gpurun_out/bench_c3.err && \
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 && \
-timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/bench_c2.json 2> gpurun_out/bench_c2.err
+if [ "$K" = "ALL" ]; then KARG=(); else KARG=(-k "$K"); fi
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread "${KARG[@]}" > gpurun_out/gpu_tests.log 2>&1 || exit 1
+for c in "$@"; do
+  timeout -k 10 200 python bench.py --config $c --no-cpu-baseline > gpurun_out/bench_$c.json 2> gpurun_out/bench_$c.err || exit 1
+done
+if [ $# -gt 0 ]; then bash tools/gpu_prof.sh $1 --config $1; fi
