@@ -214,7 +214,9 @@ def main():
                     bf_enable=bool(args.unique), est_unique=args.unique)
     if dist:
         from kaarme_amd.sharded import ShardedCounter
-        counter = ShardedCounter(cfg, dist)
+        # strong presets: a rank's local table must hold its own input's distinct k-mers,
+        # which its 1/world share of -s does not bound
+        counter = ShardedCounter(cfg, dist, local_slots=min(args.slots or 0, windows_expected) if strong else 0)
     else:
         counter = ka.KmerCounter(cfg)
 

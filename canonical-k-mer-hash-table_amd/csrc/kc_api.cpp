@@ -66,6 +66,7 @@ struct kc_ctx {
 
     // table
     uint64_t* d_table = nullptr;
+    uint64_t table_cap_bytes = 0;  // allocation size (a Bloom job re-sizes the table per pass)
     uint64_t nbuckets = 0;
     uint64_t R = 0;
     uint32_t F1 = 1, F2 = 1;
@@ -176,8 +177,15 @@ static int alloc_table(kc_ctx* c, uint64_t min_slots) {
     c->R = (uint64_t)c->F1 * c->F2;
     c->nbuckets = c->R * BPR;
     const size_t bytes = c->nbuckets * BUCKET_WORDS * sizeof(uint64_t);
-    hipError_t e = hipMalloc(&c->d_table, bytes);
-    if (e != hipSuccess) return c->fail(KC_ERR_NOMEM, "table allocation failed (" + std::to_string(bytes) + " bytes)");
+    if (!c->d_table || bytes > c->table_cap_bytes) {  // else: reuse the previous allocation
+        hipFree(c->d_table);
+        c->d_table = nullptr;
+        c->table_cap_bytes = 0;
+        hipError_t e = hipMalloc(&c->d_table, bytes);
+        if (e != hipSuccess)
+            return c->fail(KC_ERR_NOMEM, "table allocation failed (" + std::to_string(bytes) + " bytes)");
+        c->table_cap_bytes = bytes;
+    }
     HIPCHK(c, hipMemsetAsync(c->d_table, 0, bytes, c->stream));
     c->table_fresh = true;
     return KC_OK;
@@ -651,13 +659,13 @@ int kc_bloom_finalize(kc_ctx* c, uint64_t* new_in_second) {
 
 int kc_count_chunk(kc_ctx* c, const uint8_t* buf, size_t len, int fmt, int bh) {
     if (!c) return KC_ERR_ARG;
-    if (!c->d_table) return c->fail(KC_ERR_STATE, "kc_bloom_finalize must precede the counting pass");
+    if (!c->nbuckets) return c->fail(KC_ERR_STATE, "kc_bloom_finalize must precede the counting pass");
     return add_host_chunk(c, buf, len, fmt, bh, 0);
 }
 
 int kc_count_device(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, size_t n, int fmt, void* s) {
     if (!c || (!img && n) || (!chunks && n)) return KC_ERR_ARG;
-    if (!c->d_table) return c->fail(KC_ERR_STATE, "kc_bloom_finalize must precede the counting pass");
+    if (!c->nbuckets) return c->fail(KC_ERR_STATE, "kc_bloom_finalize must precede the counting pass");
     return device_pass(c, img, chunks, n, fmt, 0, pick_stream(c, s));
 }
 
@@ -721,7 +729,7 @@ int kc_route_device(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, size_
 int kc_route_table_device(kc_ctx* c, uint32_t nshards, uint64_t* dev_out, uint64_t out_capacity, uint64_t* counts,
                           void* sp) {
     if (!c || !counts || nshards == 0 || nshards > 64) return KC_ERR_ARG;
-    if (!c->d_table) return c->fail(KC_ERR_STATE, "no table");
+    if (!c->nbuckets) return c->fail(KC_ERR_STATE, "no table");
     hipStream_t s = pick_stream(c, sp);
     int rc = flush_host(c);
     if (rc) return rc;
@@ -776,7 +784,7 @@ int kc_route_table_device(kc_ctx* c, uint32_t nshards, uint64_t* dev_out, uint64
 
 int kc_insert_counts_device(kc_ctx* c, const uint64_t* recs, uint64_t n, void* sp) {
     if (!c || (!recs && n)) return KC_ERR_ARG;
-    if (!c->d_table) return c->fail(KC_ERR_STATE, "no table");
+    if (!c->nbuckets) return c->fail(KC_ERR_STATE, "no table");
     hipStream_t s = pick_stream(c, sp);
     int rc = flush_host(c);
     if (rc) return rc;
@@ -815,7 +823,7 @@ int kc_insert_counts_device(kc_ctx* c, const uint64_t* recs, uint64_t n, void* s
 
 int kc_insert_keys_device(kc_ctx* c, const uint64_t* keys, uint64_t n, void* sp) {
     if (!c || (!keys && n)) return KC_ERR_ARG;
-    if (!c->d_table) return c->fail(KC_ERR_STATE, "no table");
+    if (!c->nbuckets) return c->fail(KC_ERR_STATE, "no table");
     hipStream_t s = pick_stream(c, sp);
     int rc = flush_host(c);
     if (rc) return rc;
@@ -881,7 +889,7 @@ int kc_finish(kc_ctx* c, kc_stats* st) {
         st->part_fallbacks = h.part_fallbacks;
         st->bytes = c->n_bytes;
         // occupied slots
-        if (c->d_table) {
+        if (c->nbuckets) {
             HIPCHK(c, hipMemsetAsync(&c->d_ctr->occupied, 0, 8, c->stream));
             HIPCHK(c, hipMemsetAsync(&c->d_ctr->dump_n, 0, 8, c->stream));
             TableView tv = table_view(c);
@@ -912,14 +920,13 @@ int kc_reset(kc_ctx* c) {
         HIPCHK(c, hipMemsetAsync(c->d_bloom, 0, bloom_words(c) * 4, c->stream));
         c->bloom_fresh = true;
         if (c->bloom_final) {  // back to the Bloom pass: the table is sized again after it
-            hipFree(c->d_table);
+            // (its allocation is kept for reuse; the region histograms follow the new size)
             hipFree(c->pb.hist2);
             hipFree(c->pb.off2);
             hipFree(c->pb.bsum);
             c->pb.hist2 = nullptr;
             c->pb.off2 = nullptr;
             c->pb.bsum = nullptr;
-            c->d_table = nullptr;
             c->nbuckets = 0;
             c->bloom_final = false;
         }
@@ -972,7 +979,7 @@ int kc_dump(kc_ctx* c, uint64_t** records, uint64_t* n_records) {
     *n_records = 0;
     int rc = kc_sync(c);
     if (rc) return rc;
-    if (!c->d_table) return c->fail(KC_ERR_STATE, "no table");
+    if (!c->nbuckets) return c->fail(KC_ERR_STATE, "no table");
     TableView tv = table_view(c);
     const int cm = c->cfg.mode == 0 ? 0 : 1;
     const uint64_t a = c->cfg.min_abundance;
@@ -1016,7 +1023,7 @@ int kc_write(kc_ctx* c, const char* path) {
     if (c->cfg.min_abundance == 0) return KC_OK;  // parallel_parser.hpp:1536 / 858
     int rc = kc_sync(c);
     if (rc) return rc;
-    if (!c->d_table) return c->fail(KC_ERR_STATE, "no table");
+    if (!c->nbuckets) return c->fail(KC_ERR_STATE, "no table");
     const TableView tv = table_view(c);
     const int cm = c->cfg.mode == 0 ? 0 : 1;
     const uint64_t a = c->cfg.min_abundance;

@@ -107,9 +107,15 @@ class DeviceEngine:
     """The HIP engine of one rank: a local table counting the rank's input and an owner
     table holding the merged counts of the k-mers this rank owns."""
 
-    def __init__(self, cfg: Config):
-        self.cfg = cfg
-        self.kc = KmerCounter(cfg)      # local table (also used by the per-window route path)
+    def __init__(self, cfg: Config, local_slots: int = 0):
+        import dataclasses
+
+        self.cfg = cfg  # the owner table: this rank's share of -s
+        # the local table must hold every distinct k-mer of this rank's input, which the
+        # owner share does not bound (a rank sees ~all k-mers of the genome at low
+        # per-rank coverage): local_slots, e.g. min(-s total, this rank's windows)
+        local = dataclasses.replace(cfg, table_slots=max(cfg.table_slots, local_slots))
+        self.kc = KmerCounter(local)    # local table (also used by the per-window route path)
         self.owner = None               # created on first use
         self.W = words_for_k(cfg.k)
         self.device = "cuda"
@@ -166,14 +172,20 @@ class DeviceEngine:
 class ShardedCounter:
     """KmerCounter-compatible front end whose table is sharded over the process group."""
 
-    def __init__(self, cfg: Config, dist, engine=None, group=None):
+    def __init__(self, cfg: Config, dist, engine=None, group=None, local_slots: int = 0):
+        """cfg.table_slots = this rank's owner share of -s, also the local table's size
+        unless local_slots is larger.  local_slots must bound the distinct k-mers of this
+        rank's own input: when each rank holds a small share of a large genome (strong
+        scaling, e.g. C4), pass min(-s total, this rank's windows)."""
         self.cfg = cfg
         self.dist = dist
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.W = words_for_k(cfg.k)
-        self.engine = engine if engine is not None else DeviceEngine(cfg)
+        if engine is None:
+            engine = DeviceEngine(cfg, local_slots)
+        self.engine = engine
         self.device = getattr(self.engine, "device", "cpu")
         self._pending = False
         self._stream = 0
