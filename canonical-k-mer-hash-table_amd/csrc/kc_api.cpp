@@ -908,6 +908,14 @@ int kc_finish(kc_ctx* c, kc_stats* st) {
     return KC_OK;
 }
 
+int kc_clear_table(kc_ctx* c) {
+    if (!c) return KC_ERR_ARG;
+    if (!c->nbuckets) return c->fail(KC_ERR_STATE, "no table");
+    c->table_zero_pending = true;  // deferred: see materialize_zero
+    c->table_fresh = true;
+    return KC_OK;
+}
+
 int kc_reset(kc_ctx* c) {
     if (!c) return KC_ERR_ARG;
     int rc = kc_sync(c);

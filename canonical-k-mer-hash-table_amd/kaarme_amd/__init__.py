@@ -45,7 +45,7 @@ EXPORTS = (
     "kc_count_chunk", "kc_bloom_device", "kc_count_device", "kc_sync", "kc_finish", "kc_dump",
     "kc_write", "kc_key_words", "kc_free", "kc_plan_chunks", "kc_synth_bytes", "kc_synth_device",
     "kc_reset", "kc_profile", "kc_get_timing", "kc_route_device", "kc_insert_keys_device",
-    "kc_route_table_device", "kc_insert_counts_device",
+    "kc_route_table_device", "kc_insert_counts_device", "kc_clear_table",
 )
 
 
@@ -124,6 +124,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                                  ctypes.POINTER(U64)]),
         "kc_synth_bytes": (U64, [U64, U64, ctypes.c_uint32, ctypes.c_uint32]),
         "kc_reset": (I32, [P]),
+        "kc_clear_table": (I32, [P]),
         "kc_route_device": (I32, [P, P, ctypes.POINTER(kc_chunk), ctypes.c_size_t, I32, ctypes.c_uint32, P, U64,
                                   ctypes.POINTER(U64), P]),
         "kc_insert_keys_device": (I32, [P, P, U64, P]),
@@ -304,6 +305,10 @@ class KmerCounter:
 
     def reset(self):
         self._chk(self.lib.kc_reset(self._ctx), "kc_reset")
+
+    def clear_table(self):
+        """Empty the table, keep the job's counters (kc_clear_table)."""
+        self._chk(self.lib.kc_clear_table(self._ctx), "kc_clear_table")
 
     def profile(self, enable: bool = True):
         self._chk(self.lib.kc_profile(self._ctx, int(enable)), "kc_profile")

@@ -156,6 +156,10 @@ class DeviceEngine:
         self._rec = torch.empty(need + need // 4, dtype=torch.int64, device="cuda")
         return self._rec, self.kc.route_table_device(parts, self._rec.data_ptr(), self._rec.numel() // R, stream)
 
+    def clear_local(self):
+        """The local table was routed to its owners: empty it (its counters stay)."""
+        self.kc.clear_table()
+
     def owner_table(self) -> KmerCounter:
         if self.owner is None:
             self.owner = KmerCounter(self.cfg)
@@ -201,6 +205,9 @@ class ShardedCounter:
         """Route the local table's records to their owners (one all-to-all) and add them
         into the owner tables.  Collective: every rank calls it the same number of times."""
         recs, counts = self.engine.route_table(self.world, stream)
+        # the records hold the local counts now: a later merge must route only what is
+        # counted after this one
+        self.engine.clear_local()
         recv, n = exchange(self.dist, recs, counts, self.W + 1, self.group)
         self.engine.insert_counts(recv, n, stream)
         self._inflight = [recv]  # the receive buffer must outlive the insert

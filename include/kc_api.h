@@ -140,6 +140,13 @@ int kc_insert_counts_device(kc_ctx* ctx, const uint64_t* dev_records, uint64_t n
  * constructors again, without reallocating). */
 int kc_reset(kc_ctx* ctx);
 
+/* Empty the table only (the next pass that touches it zero-fills it first), keeping the
+ * job's counters (windows, chunks, bytes, ...).  The sharded front end calls it on a
+ * rank's local table once kc_route_table_device has copied the table out, so the next
+ * merge routes only what was counted since (the reference has one shared table and no
+ * such step: kmer_hash_table.cpp:2207-2567). */
+int kc_clear_table(kc_ctx* ctx);
+
 /* Per-kernel device time, accumulated while profiling is enabled (HIP events on
  * the stream each kernel runs on). */
 typedef struct {

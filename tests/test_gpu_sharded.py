@@ -141,3 +141,50 @@ def test_preaggregated_merge_union(tmp_path, monkeypatch, k, mode, G, path):
     out = tmp_path / "oracle.txt"
     oracle_count(str(whole), k, ["-m", str(mode), "-a", "1"], out)
     assert sorted_digest_lines(union) == sorted_digest_file(out)
+
+
+@pytest.mark.parametrize("k,mode,G", [(31, 2, 2), (51, 0, 3)])
+def test_two_merges_route_only_new_counts(tmp_path, k, mode, G):
+    """A job that merges twice (count, merge, count more, merge): after routing, the local
+    table is cleared (kc_clear_table) but keeps its window counters, so the second merge
+    routes only what was counted after the first and the owners' union is still exact."""
+    n_reads = 12000
+    per = n_reads // G
+    images = []
+    for r in range(G):
+        fa = tmp_path / f"r{r}.fasta"
+        cnt = per if r < G - 1 else n_reads - per * (G - 1)
+        subprocess.run([GEN, str(fa), str(n_reads), "150", "20000", "--first", str(r * per), "--count", str(cnt)],
+                       check=True)
+        images.append(_image(str(fa)))
+    whole = tmp_path / "all.fasta"
+    with open(whole, "wb") as f:
+        for data, _ in images:
+            f.write(data)
+    engines = [DeviceEngine(ka.Config(k=k, mode=mode, table_slots=400000, min_abundance=1)) for _ in range(G)]
+    W = engines[0].W
+    stream = torch.cuda.current_stream().cuda_stream
+    plans = [ka.plan_chunks(data, k, ka.FMT_FASTA, chunk_size=64 * 1024) for data, _ in images]
+    per_windows = [len(data.split(b"\n")) // 2 * (150 - k + 1) for data, _ in images]
+    for e in engines:
+        e.reset()
+    for phase in range(2):
+        routed = []
+        for r, (data, img) in enumerate(images):
+            ch = plans[r]
+            half = ch[: len(ch) // 2] if phase == 0 else ch[len(ch) // 2:]
+            engines[r].count(img.data_ptr(), half, ka.FMT_FASTA, stream)
+            recs, counts = engines[r].route_table(G, stream)
+            engines[r].clear_local()
+            torch.cuda.synchronize()
+            routed.append((recs[: sum(counts) * (W + 1)].clone(), counts))
+        for d in range(G):
+            recv = torch.cat([recs[sum(c[:d]) * (W + 1):(sum(c[:d]) + c[d]) * (W + 1)] for recs, c in routed])
+            engines[d].insert_counts(recv, recv.numel() // (W + 1), stream)
+            torch.cuda.synchronize()
+    for r in range(G):  # the cleared local tables kept their window counters
+        assert engines[r].kc.finish()["windows"] == per_windows[r]
+    union = set().union(*[set(e.owner_table().lines()) for e in engines])
+    out = tmp_path / "oracle.txt"
+    oracle_count(str(whole), k, ["-m", str(mode), "-a", "1"], out)
+    assert sorted_digest_lines(union) == sorted_digest_file(out)

@@ -104,6 +104,9 @@ class NumpyEngine:
         for row in rows:
             self.owner.table[from_words(row[:self.W], self.k)] += int(row[self.W])
 
+    def clear_local(self):
+        self.kc.table.clear()
+
     def owner_table(self):
         return self.owner
 
@@ -148,11 +151,16 @@ def _worker(rank, world, port, k, reads, outdir, rounds):
         per = (len(reads) + world - 1) // world
         lo, hi = rank * per, min(len(reads), (rank + 1) * per)
         step = max(1, (hi - lo + rounds - 1) // rounds)
-        for b in range(lo, hi, step):
+        batches = list(range(lo, hi, step))
+        half = len(batches) // 2
+        for b in batches[:half]:
+            sc.count_device(0, [(b, min(step, hi - b), 0)], 2)
+        sc.sync()                  # a first merge mid-job (every rank calls it)
+        for b in batches[half:]:
             sc.count_device(0, [(b, min(step, hi - b), 0)], 2)
         sc.count_device(0, [], 2)  # an empty batch changes nothing
-        sc.sync()                  # the collective merge
-        sc.sync()                  # nothing pending: no second exchange
+        sc.sync()                  # the second merge routes only what came after the first
+        sc.sync()                  # nothing pending: no third exchange
         with open(os.path.join(outdir, f"shard{rank}.json"), "w") as f:
             json.dump(dict(eng.owner.table), f)
     finally:
