@@ -88,6 +88,11 @@ struct kc_ctx {
     uint64_t* d_roff = nullptr;
     uint64_t* d_rbsum = nullptr;
     uint64_t r_cap = 0;
+    // kc_insert_counts_runs_device: group offsets, region run starts / lengths
+    uint64_t* d_gstart = nullptr;
+    uint64_t* d_mstart = nullptr;
+    uint32_t* d_mlen = nullptr;
+    uint64_t m_cap = 0;  // entries of d_mstart
 
     // bloom
     uint32_t* d_bloom = nullptr;
@@ -612,6 +617,9 @@ void kc_destroy(kc_ctx* c) {
     hipFree(c->pb.bsum);
     hipFree(c->d_keys1);
     hipFree(c->d_keys2);
+    hipFree(c->d_gstart);
+    hipFree(c->d_mstart);
+    hipFree(c->d_mlen);
     hipFree(c->pbf.hist1);
     hipFree(c->pbf.off1);
     hipFree(c->pbf.hist2);
@@ -809,6 +817,71 @@ int kc_insert_counts_device(kc_ctx* c, const uint64_t* recs, uint64_t n, void* s
         if (rc) return rc;
     }
     HIPCHK(c, launch_insert_counts(recs, n, part, table_view(c), c->d_ctr, c->pb, c->table_fresh, s));
+    c->table_fresh = c->table_zero_pending = false;
+    if (c->profiling) {
+        HIPCHK(c, hipEventRecord(ev[3], s));
+        c->ev_pending.push_back(ev);
+    }
+    if (s != c->stream) {
+        HIPCHK(c, hipEventRecord(c->xev, s));
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->xev, 0));
+    }
+    return KC_OK;
+}
+
+int kc_insert_counts_runs_device(kc_ctx* c, const uint64_t* recs, const uint64_t* group_counts, uint32_t ngroups,
+                                 void* sp) {
+    if (!c || !group_counts || ngroups == 0 || ngroups > 64) return KC_ERR_ARG;
+    if (!c->nbuckets) return c->fail(KC_ERR_STATE, "no table");
+    std::vector<uint64_t> gs(ngroups + 1, 0);
+    uint64_t maxn = 0;
+    for (uint32_t g = 0; g < ngroups; g++) {
+        gs[g + 1] = gs[g] + group_counts[g];
+        maxn = std::max(maxn, group_counts[g]);
+    }
+    const uint64_t n = gs[ngroups];
+    if (!recs && n) return KC_ERR_ARG;
+    hipStream_t s = pick_stream(c, sp);
+    int rc = flush_host(c);
+    if (rc) return rc;
+    if (n == 0) return KC_OK;
+    if (s != c->stream) {
+        HIPCHK(c, hipEventRecord(c->xev, c->stream));
+        HIPCHK(c, hipStreamWaitEvent(s, c->xev, 0));
+    }
+    const uint64_t need = (c->R + 1) * ngroups;
+    if (!c->d_gstart && hipMalloc(&c->d_gstart, 65 * 8) != hipSuccess)
+        return c->fail(KC_ERR_NOMEM, "merge buffer allocation failed");
+    if (need > c->m_cap) {
+        hipFree(c->d_mstart);
+        hipFree(c->d_mlen);
+        c->d_mstart = nullptr;
+        c->d_mlen = nullptr;
+        c->m_cap = 0;
+        if (hipMalloc(&c->d_mstart, need * 8) != hipSuccess || hipMalloc(&c->d_mlen, need * 4) != hipSuccess)
+            return c->fail(KC_ERR_NOMEM, "merge buffer allocation failed");
+        c->m_cap = need;
+    }
+    HIPCHK(c, hipMemcpyAsync(c->d_gstart, gs.data(), (ngroups + 1) * 8, hipMemcpyHostToDevice, s));
+    // the groups must be sorted by this table's region (a sender table of another geometry,
+    // or records not from kc_route_table_device, take the general merge insert)
+    unsigned long long* flag = &c->d_ctr->part_overflow;
+    HIPCHK(c, hipMemsetAsync(flag, 0, 8, s));
+    TableView tv = table_view(c);
+    HIPCHK(c, launch_check_runs(recs, c->d_gstart, ngroups, maxn, tv, flag, s));
+    unsigned long long unsorted = 0;
+    HIPCHK(c, hipMemcpyAsync(&unsorted, flag, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    if (unsorted) return kc_insert_counts_device(c, recs, n, sp);
+    std::array<hipEvent_t, 4> ev{};
+    if (c->profiling) {
+        ev[2] = c->get_event();
+        ev[3] = c->get_event();
+        HIPCHK(c, hipEventRecord(ev[2], s));
+    }
+    HIPCHK(c, launch_insert_counts_runs(recs, c->d_gstart, ngroups, tv, c->d_ctr, c->d_mlen, c->d_mstart,
+                                        c->table_fresh, s));
+    // records counted like kc_insert_counts_device: inserted += their counts
     c->table_fresh = c->table_zero_pending = false;
     if (c->profiling) {
         HIPCHK(c, hipEventRecord(ev[3], s));

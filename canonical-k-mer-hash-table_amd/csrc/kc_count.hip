@@ -982,7 +982,7 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
     constexpr int S = BUCKET_WORDS / (W + 1);
     // keys loaded per thread before inserting (memory-level parallelism); 1024-thread
     // groups already keep 8 waves per SIMD in flight
-    constexpr int KB = NT >= 1024 ? (W >= 2 ? 2 : 4) : 8;
+    constexpr int KB = NT >= 1024 ? (W >= 2 || CNT ? 2 : 4) : 8;  // (CNT items carry a count: 64 VGPRs)
     if constexpr (SEG) {
         if (ctr->part_overflow) return;
     } else {
@@ -1049,16 +1049,44 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
         }
     }
     uint32_t n_fail = 0, n_ins = 0;
+    unsigned long long n_add = 0;  // CNT: the records' counts (the runs merge counts them here)
     // SEG: segment cursor of this thread (indices grow monotonically): segment cs holds
     // [cb, nb), both bounds in registers
     uint32_t cs = 0, cb = 0, nb = 0;
     if constexpr (SEG) nb = s_pre[1];
-    auto load_items = [&](uint64_t base, uint64_t (&kk)[KB][W], uint64_t (&add)[KB]) {
+    // Runs (the merge over region-sorted groups): a sender's records sit in its table order,
+    // i.e. sorted by home bucket, and inserted in that order neighbouring lanes collide on
+    // the same buckets and banks.  The items are visited in a scrambled order instead: a
+    // bijection of [0, 2^m) (2^m >= end), slots mapping past end are idle.
+    const bool runs = SEG && pb.seg_start != nullptr;
+    uint64_t vend = end;
+    uint32_t pmask = 0, psh = 0;
+    if (runs && end > 1) {
+        const uint32_t m = 64 - __builtin_clzll(end - 1);
+        vend = 1ULL << m;
+        pmask = (uint32_t)(vend - 1);
+        psh = (m + 1) / 2;
+    }
+    auto load_items = [&](uint64_t base, uint64_t (&kk)[KB][W], uint64_t (&add)[KB], uint32_t& ok) {
+        ok = 0;
 #pragma unroll
         for (int q = 0; q < KB; q++) {
             const uint64_t i = base + threadIdx.x + (uint64_t)q * NT;
             const uint64_t* src = nullptr;
-            if (i < end) {
+            if (runs) {
+                uint32_t j = ((uint32_t)i * 0x9E3779B1u) & pmask;
+                j ^= j >> psh;
+                j = (j * 0x85EBCA77u) & pmask;
+                if (i < vend && j < end) {
+                    uint32_t lo = 0, hi = pb.B2;  // the group holding j: s_pre[lo] <= j < s_pre[lo + 1]
+                    while (hi - lo > 1) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (s_pre[mid] <= j) lo = mid;
+                        else hi = mid;
+                    }
+                    src = pb.keys2 + (pb.seg_start[r * pb.B2 + lo] + (j - s_pre[lo])) * IW;
+                }
+            } else if (i < end) {
                 if constexpr (SEG) {
                     while (nb <= i) {
                         cs++;
@@ -1070,6 +1098,7 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
                     src = pb.keys2 + i * IW;
                 }
             }
+            ok |= (src != nullptr) << q;
 #pragma unroll
             for (int w = 0; w < W; w++) kk[q][w] = src ? src[w] : 0;
             if constexpr (CNT) add[q] = src ? src[W] & CNT_MASK : 0;
@@ -1078,18 +1107,20 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
     };
     uint64_t kk[KB][W];
     uint64_t add[KB];
-    if (start < end) load_items(start, kk, add);
-    for (uint64_t base = start; base < end; base += (uint64_t)KB * NT) {
+    uint32_t okm = 0;
+    if (start < vend) load_items(start, kk, add, okm);
+    for (uint64_t base = start; base < vend; base += (uint64_t)KB * NT) {
         // the next items' loads are issued before this batch's inserts
         uint64_t nkk[KB][W];
         uint64_t nadd[KB];
+        uint32_t nokm = 0;
         const uint64_t nbase = base + (uint64_t)KB * NT;
-        const bool more = KC_PREFETCH && W <= 2 && nbase < end;  // W > 2: no spare registers
-        if (more) load_items(nbase, nkk, nadd);
+        const bool more = KC_PREFETCH && W <= 2 && nbase < vend;  // W > 2: no spare registers
+        if (more) load_items(nbase, nkk, nadd, nokm);
         bool pass[KB];
 #pragma unroll
         for (int q = 0; q < KB; q++) {  // the gate reads of all KB items are issued together
-            pass[q] = base + threadIdx.x + (uint64_t)q * NT < end;
+            pass[q] = (okm >> q) & 1;
             if constexpr (GATE) {
                 const uint64_t t0 = kk[q][0];
                 if (bf.slice_blocks)
@@ -1098,6 +1129,7 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
                     pass[q] = pass[q] && block_gate(bloom_block_ptr(bf, t0) + 8, t0, bf.nh_gate);
             }
             n_ins += pass[q];
+            if constexpr (CNT) n_add += pass[q] ? add[q] : 0;
         }
 #pragma unroll
         for (int q = 0; q < KB; q++) {
@@ -1253,23 +1285,26 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
             if (!done) n_fail++;
         }
         if (more) {
+            okm = nokm;
 #pragma unroll
             for (int q = 0; q < KB; q++) {
                 add[q] = nadd[q];
 #pragma unroll
                 for (int w = 0; w < W; w++) kk[q][w] = nkk[q][w];
             }
-        } else if (nbase < end) {
-            load_items(nbase, kk, add);
+        } else if (nbase < vend) {
+            load_items(nbase, kk, add, okm);
         }
     }
     __syncthreads();
     for (int i = threadIdx.x; i < N4; i += NT) g4[i] = l4[lds_chunk(i >> 3, i & 7)];
     if (n_fail) atomicAdd(&ctr->overflow, (unsigned long long)n_fail);
-    if constexpr (GATE) {  // the gated insertions (level 1 counted the windows)
-        unsigned long long x = n_ins;
-        for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
-        if ((threadIdx.x & 63) == 0 && x) atomicAdd(&ctr->inserted, x);
+    if constexpr (GATE || CNT) {
+        // GATE: the gated insertions (level 1 counted the windows); CNT over runs: the
+        // records' counts (the general merge insert counted them at its level 1).  One
+        // atomic per workgroup: per-wave adds to this one counter from every region's
+        // workgroup serialise at the memory-side atomic unit (milliseconds per pass)
+        block_add4(GATE ? n_ins : (pb.seg_start ? n_add : 0), 0, 0, 0, &ctr->inserted, nullptr, nullptr, nullptr);
     }
 }
 
@@ -1280,12 +1315,20 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
 // bit (the direct pass) with two sequential sweeps of the filter per batch.
 // SEG: the region's keys are its B2 level-2 segments (fills in hist2); otherwise the
 // contiguous run [off2[r * B2], off2[(r + 1) * B2]).
-constexpr int B3_THREADS = 1024;  // two 64 KiB regions per CU
+// keys per thread per round and workgroup size: 512 threads keep the insertion path within
+// its registers (72 VGPRs, no scratch spills; 1024-thread groups would be capped at 64)
+#ifndef KC_B3_KB
+#define KC_B3_KB 4
+#endif
+#ifndef KC_B3_NT
+#define KC_B3_NT 512
+#endif
+constexpr int B3_THREADS = KC_B3_NT;  // two 64 KiB regions per CU
 template <bool SEG>
 __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView bf, uint32_t bpr, PartBufs pb,
                                                                   DevCounters* __restrict__ ctr,
                                                                   const unsigned long long* gate, int fresh) {
-    constexpr int NT = B3_THREADS, KB = 4;
+    constexpr int NT = B3_THREADS, KB = KC_B3_KB;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ uint32_t s_pre[65];
     if constexpr (SEG) {
@@ -1373,15 +1416,49 @@ __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView b
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < n4; i += NT) g4[i] = l4[i];
-    unsigned long long v[3] = {bl.new_first, bl.new_second, bl.failed};
-#pragma unroll
-    for (int c = 0; c < 3; c++)
-        for (int d = 32; d >= 1; d >>= 1) v[c] += __shfl_xor(v[c], d, 64);
-    if ((threadIdx.x & 63) == 0) {
-        if (v[0]) atomicAdd(&ctr->new_in_first, v[0]);
-        if (v[1]) atomicAdd(&ctr->new_in_second, v[1]);
-        if (v[2]) atomicAdd(&ctr->failed_in_first, v[2]);
+    // one atomic per counter and workgroup (per-wave adds to one address serialise)
+    block_add4(bl.new_first, bl.new_second, bl.failed, 0, &ctr->new_in_first, &ctr->new_in_second,
+               &ctr->failed_in_first, nullptr);
+}
+
+// --------------------------------------------------------------------------------
+// shard merge over region-sorted groups (kc_insert_counts_runs_device): the records a
+// rank receives are G groups (one per sender), each in the sender's table order, i.e.
+// sorted by region when the sender's table has this table's geometry.  Region run bounds
+// per group by binary search, then one level-3 pass (k_p3<W, SEG, CNT> over the runs):
+// the partition levels of the general merge insert are not needed.
+// --------------------------------------------------------------------------------
+template <int W>
+__global__ __launch_bounds__(256) void k_check_runs(const uint64_t* __restrict__ rec, const uint64_t* __restrict__ gstart,
+                                                    uint64_t R, unsigned long long* flag) {
+    const uint32_t g = blockIdx.y;
+    const uint64_t lo = gstart[g], hi = gstart[g + 1];
+    bool bad = false;
+    for (uint64_t i = lo + 1 + (uint64_t)blockIdx.x * 256 + threadIdx.x; i < hi; i += (uint64_t)gridDim.x * 256)
+        bad |= region_of(rec[i * (W + 1)], R) < region_of(rec[(i - 1) * (W + 1)], R);
+    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1ULL);
+}
+// m_start[r * G + g] = first record of group g with region >= r (r = 0..R)
+template <int W>
+__global__ __launch_bounds__(256) void k_run_bounds(const uint64_t* __restrict__ rec,
+                                                    const uint64_t* __restrict__ gstart, uint32_t G, uint64_t R,
+                                                    uint64_t* __restrict__ m_start) {
+    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= (R + 1) * G) return;
+    const uint64_t r = t / G;
+    const uint32_t g = (uint32_t)(t % G);
+    uint64_t lo = gstart[g], hi = gstart[g + 1];  // first index in [lo, hi) with region >= r
+    while (lo < hi) {
+        const uint64_t mid = lo + (hi - lo) / 2;
+        if (region_of(rec[mid * (W + 1)], R) < r) lo = mid + 1;
+        else hi = mid;
     }
+    m_start[t] = lo;
+}
+__global__ __launch_bounds__(256) void k_run_lengths(const uint64_t* __restrict__ m_start, uint64_t RG, uint32_t G,
+                                                     uint32_t* __restrict__ m_len) {
+    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t < RG) m_len[t] = (uint32_t)(m_start[t + G] - m_start[t]);
 }
 
 // exclusive scan of n u32 -> u64 (out has n+1 entries), three passes:
@@ -1485,12 +1562,19 @@ __global__ __launch_bounds__(256) void k_dump(TableView tv, int count_mode, uint
             if (t >= min_abundance) { emit[s] = true; tv_c[s] = t; nout++; }
         }
     }
-    const int lane = threadIdx.x & 63;
-    uint32_t incl = wave_incl_sum(nout);
-    uint32_t wtot = __shfl(incl, 63, 64);
-    unsigned long long base = 0;
-    if (lane == 63 && wtot) base = atomicAdd(&ctr->dump_n, (unsigned long long)wtot);
-    base = __shfl(base, 63, 64);
+    // output positions: one atomic per workgroup (not per wave) on the shared cursor
+    __shared__ unsigned long long s_wt[4], s_base;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t incl = wave_incl_sum(nout);
+    if (lane == 63) s_wt[wid] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long tot = s_wt[0] + s_wt[1] + s_wt[2] + s_wt[3];
+        s_base = tot ? atomicAdd(&ctr->dump_n, tot) : 0;
+    }
+    __syncthreads();
+    unsigned long long base = s_base;
+    for (int w = 0; w < wid; w++) base += s_wt[w];
     uint64_t idx = base + incl - nout;
 #pragma unroll
     for (int s = 0; s < S; s++)
@@ -1505,9 +1589,7 @@ __global__ __launch_bounds__(256) void k_dump(TableView tv, int count_mode, uint
             o[W] = tv_c[s];
             idx++;
         }
-    uint32_t occ_w = occ;
-    for (int d = 32; d >= 1; d >>= 1) occ_w += __shfl_xor(occ_w, d, 64);
-    if (lane == 0 && occ_w) atomicAdd(&ctr->occupied, (unsigned long long)occ_w);
+    block_add4(occ, 0, 0, 0, &ctr->occupied, nullptr, nullptr, nullptr);
 }
 
 // --------------------------------------------------------------------------------
@@ -1682,7 +1764,7 @@ static hipError_t launch_p3(TableView t, DevCounters* ctr, PartBufs pb, const un
     if (GATE) {
         // the filter-2 slice goes to LDS if two workgroups still fit a CU (80 KiB each)
         const uint64_t maxb = bf.nblocks / t.R + 2;
-        const size_t room = 80 * 1024 - sm3 - 512;
+        const size_t room = 80 * 1024 - sm3 - 1024;  // (static LDS: segment prefix, block sums)
         bf.slice_blocks = maxb * 32 <= room ? (uint32_t)maxb : 0;
         sm3 += (size_t)bf.slice_blocks * 32;
     }
@@ -2002,6 +2084,47 @@ hipError_t launch_text(TableView t, int count_mode, uint64_t a, int k, uint64_t 
     case 2: return text_w<2>(t, count_mode, a, k, blk0, nblk, off, base, out, lds, s);
     case 3: return text_w<3>(t, count_mode, a, k, blk0, nblk, off, base, out, lds, s);
     case 4: return text_w<4>(t, count_mode, a, k, blk0, nblk, off, base, out, lds, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_check_runs(const uint64_t* rec, const uint64_t* gstart, uint32_t G, uint64_t maxn, TableView t,
+                             unsigned long long* flag, hipStream_t s) {
+    if (G == 0) return hipSuccess;
+    const dim3 grid((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(1024, (maxn + 255) / 256)), G);
+    switch (t.W) {
+    case 1: hipLaunchKernelGGL(k_check_runs<1>, grid, dim3(256), 0, s, rec, gstart, t.R, flag); break;
+    case 2: hipLaunchKernelGGL(k_check_runs<2>, grid, dim3(256), 0, s, rec, gstart, t.R, flag); break;
+    case 3: hipLaunchKernelGGL(k_check_runs<3>, grid, dim3(256), 0, s, rec, gstart, t.R, flag); break;
+    case 4: hipLaunchKernelGGL(k_check_runs<4>, grid, dim3(256), 0, s, rec, gstart, t.R, flag); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+template <int W>
+static hipError_t insert_runs_w(const uint64_t* rec, const uint64_t* gstart, uint32_t G, TableView t,
+                                DevCounters* ctr, uint32_t* m_len, uint64_t* m_start, int fresh, hipStream_t s) {
+    const uint64_t nb = (t.R + 1) * G;
+    hipLaunchKernelGGL(k_run_bounds<W>, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, rec, gstart, G, t.R,
+                       m_start);
+    hipLaunchKernelGGL(k_run_lengths, dim3((unsigned)((t.R * G + 255) / 256)), dim3(256), 0, s, m_start, t.R * G, G,
+                       m_len);
+    PartBufs pb{};
+    pb.B2 = G;
+    pb.hist2 = m_len;
+    pb.keys2 = const_cast<uint64_t*>(rec);
+    pb.seg_start = m_start;
+    return launch_p3<W, true, true>(t, ctr, pb, nullptr, fresh, s);
+}
+hipError_t launch_insert_counts_runs(const uint64_t* rec, const uint64_t* gstart, uint32_t G, TableView t,
+                                     DevCounters* ctr, uint32_t* m_len, uint64_t* m_start, int fresh, hipStream_t s) {
+    if (G == 0 || G > 64) return hipErrorInvalidValue;
+    switch (t.W) {
+    case 1: return insert_runs_w<1>(rec, gstart, G, t, ctr, m_len, m_start, fresh, s);
+    case 2: return insert_runs_w<2>(rec, gstart, G, t, ctr, m_len, m_start, fresh, s);
+    case 3: return insert_runs_w<3>(rec, gstart, G, t, ctr, m_len, m_start, fresh, s);
+    case 4: return insert_runs_w<4>(rec, gstart, G, t, ctr, m_len, m_start, fresh, s);
     default: return hipErrorInvalidValue;
     }
 }

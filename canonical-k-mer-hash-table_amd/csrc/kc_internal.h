@@ -99,6 +99,8 @@ struct PartBufs {
     uint64_t* keys1;        // coarse-binned keys (W words each)
     uint64_t* keys2;        // region-binned keys
     uint64_t cap1, cap2;    // segmented layout: keys per segment of levels 1 / 2 (0 = exact layout)
+    const uint64_t* seg_start;  // level 3 over runs at arbitrary offsets ([R][B2] first items;
+                                // nullptr = fixed-capacity segments of cap2)
 };
 
 struct BloomView {
@@ -147,6 +149,14 @@ hipError_t launch_route_table(TableView t, uint32_t parts, uint32_t* hist, uint6
                               uint64_t* out, hipStream_t s);
 hipError_t launch_insert_counts(const uint64_t* rec, uint64_t n, bool partitioned, TableView t, DevCounters* ctr,
                                 PartBufs pb, int fresh, hipStream_t s);
+// shard merge of records that arrive as G groups each sorted by this table's region
+// (kc_route_table_device order on a table of the same geometry): gstart[G+1] group
+// offsets (device).  check: flag |= 1 if some group is not sorted.  runs: region run
+// bounds per group (m_start [(R+1)][G], m_len [R][G]) and one level-3 pass over them.
+hipError_t launch_check_runs(const uint64_t* rec, const uint64_t* gstart, uint32_t G, uint64_t maxn, TableView t,
+                             unsigned long long* flag, hipStream_t s);
+hipError_t launch_insert_counts_runs(const uint64_t* rec, const uint64_t* gstart, uint32_t G, TableView t,
+                                     DevCounters* ctr, uint32_t* m_len, uint64_t* m_start, int fresh, hipStream_t s);
 hipError_t launch_dump(TableView t, int count_mode, uint64_t min_abundance, uint64_t* out, DevCounters* ctr,
                        hipStream_t s);
 // GPU text formatting (kc_write): bytes of each TEXT_T-bucket block into block_bytes and

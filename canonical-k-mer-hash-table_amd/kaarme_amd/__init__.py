@@ -45,7 +45,7 @@ EXPORTS = (
     "kc_count_chunk", "kc_bloom_device", "kc_count_device", "kc_sync", "kc_finish", "kc_dump",
     "kc_write", "kc_key_words", "kc_free", "kc_plan_chunks", "kc_synth_bytes", "kc_synth_device",
     "kc_reset", "kc_profile", "kc_get_timing", "kc_route_device", "kc_insert_keys_device",
-    "kc_route_table_device", "kc_insert_counts_device", "kc_clear_table",
+    "kc_route_table_device", "kc_insert_counts_device", "kc_clear_table", "kc_insert_counts_runs_device",
 )
 
 
@@ -125,6 +125,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "kc_synth_bytes": (U64, [U64, U64, ctypes.c_uint32, ctypes.c_uint32]),
         "kc_reset": (I32, [P]),
         "kc_clear_table": (I32, [P]),
+        "kc_insert_counts_runs_device": (I32, [P, P, ctypes.POINTER(U64), ctypes.c_uint32, P]),
         "kc_route_device": (I32, [P, P, ctypes.POINTER(kc_chunk), ctypes.c_size_t, I32, ctypes.c_uint32, P, U64,
                                   ctypes.POINTER(U64), P]),
         "kc_insert_keys_device": (I32, [P, P, U64, P]),
@@ -296,6 +297,13 @@ class KmerCounter:
     def insert_counts_device(self, rec_ptr: int, n_records: int, stream: int = 0):
         self._chk(self.lib.kc_insert_counts_device(self._ctx, ctypes.c_void_p(rec_ptr), n_records,
                                                    ctypes.c_void_p(stream or None)), "kc_insert_counts_device")
+
+    def insert_counts_runs_device(self, rec_ptr: int, group_counts: Sequence[int], stream: int = 0):
+        """Records in per-sender groups, each in kc_route_table_device order."""
+        arr = (ctypes.c_uint64 * len(group_counts))(*group_counts)
+        self._chk(self.lib.kc_insert_counts_runs_device(self._ctx, ctypes.c_void_p(rec_ptr), arr, len(group_counts),
+                                                        ctypes.c_void_p(stream or None)),
+                  "kc_insert_counts_runs_device")
 
     def key_words(self) -> int:
         return self.lib.kc_key_words(self._ctx)

@@ -36,16 +36,18 @@ from . import Config, KmerCounter, words_for_k
 EXCHANGE_CHUNK_WORDS = 1 << 24
 
 
-def exchange(dist, keys, counts: Sequence[int], W: int, group=None, chunk_words: int = EXCHANGE_CHUNK_WORDS):
+def exchange(dist, keys, counts: Sequence[int], W: int, group=None, chunk_words: int = EXCHANGE_CHUNK_WORDS,
+             with_counts: bool = False):
     """All-to-all of owner-grouped items of W int64 words each.  keys: int64 tensor
     holding sum(counts)*W words (group d = the items for rank d, in rank order).
-    Returns (received items, n received); the items from rank s follow those of s-1."""
+    Returns (received items, n received[, items received from each rank]); the items
+    from rank s follow those of s-1."""
     import torch
 
     dev = keys.device
     world = len(counts)
     if world == 1:  # nothing leaves the rank
-        return keys, int(counts[0])
+        return (keys, int(counts[0]), [int(counts[0])]) if with_counts else (keys, int(counts[0]))
     send_counts = torch.tensor(list(counts), dtype=torch.int64, device=dev)
     recv_counts = torch.empty_like(send_counts)
     dist.all_to_all_single(recv_counts, send_counts, group=group)
@@ -60,7 +62,7 @@ def exchange(dist, keys, counts: Sequence[int], W: int, group=None, chunk_words:
     if rounds == 1:
         dist.all_to_all_single(out[: total * W], keys[: sum(sw)], output_split_sizes=rw, input_split_sizes=sw,
                                group=group)
-        return out, total
+        return (out, total, recv) if with_counts else (out, total)
     so = [sum(sw[:d]) for d in range(world)]
     ro = [sum(rw[:d]) for d in range(world)]
     for r in range(rounds):
@@ -75,7 +77,7 @@ def exchange(dist, keys, counts: Sequence[int], W: int, group=None, chunk_words:
             if rin[d]:
                 out[ro[d] + lo: ro[d] + lo + rin[d]].copy_(got[pos: pos + rin[d]])
             pos += rin[d]
-    return out, total
+    return (out, total, recv) if with_counts else (out, total)
 
 
 TILE = 4096
@@ -116,6 +118,9 @@ class DeviceEngine:
         # per-rank coverage): local_slots, e.g. min(-s total, this rank's windows)
         local = dataclasses.replace(cfg, table_slots=max(cfg.table_slots, local_slots))
         self.kc = KmerCounter(local)    # local table (also used by the per-window route path)
+        # every rank's local table has the owner table's geometry: the records a rank
+        # receives are region-sorted groups, merged in one pass (kc_insert_counts_runs_device)
+        self.same_geometry = local.table_slots == cfg.table_slots
         self.owner = None               # created on first use
         self.W = words_for_k(cfg.k)
         self.device = "cuda"
@@ -165,8 +170,11 @@ class DeviceEngine:
             self.owner = KmerCounter(self.cfg)
         return self.owner
 
-    def insert_counts(self, recs, n: int, stream: int = 0):
-        self.owner_table().insert_counts_device(recs.data_ptr(), n, stream)
+    def insert_counts(self, recs, n: int, stream: int = 0, group_counts=None):
+        if group_counts is not None and self.same_geometry and 0 < len(group_counts) <= 64:
+            self.owner_table().insert_counts_runs_device(recs.data_ptr(), group_counts, stream)
+        else:
+            self.owner_table().insert_counts_device(recs.data_ptr(), n, stream)
 
     def reset(self):
         self.kc.reset()
@@ -208,8 +216,8 @@ class ShardedCounter:
         # the records hold the local counts now: a later merge must route only what is
         # counted after this one
         self.engine.clear_local()
-        recv, n = exchange(self.dist, recs, counts, self.W + 1, self.group)
-        self.engine.insert_counts(recv, n, stream)
+        recv, n, per_rank = exchange(self.dist, recs, counts, self.W + 1, self.group, with_counts=True)
+        self.engine.insert_counts(recv, n, stream, group_counts=per_rank)
         self._inflight = [recv]  # the receive buffer must outlive the insert
         self._pending = False
 

@@ -135,6 +135,14 @@ int kc_insert_keys_device(kc_ctx* ctx, const uint64_t* dev_keys, uint64_t n_keys
 int kc_route_table_device(kc_ctx* ctx, uint32_t nshards, uint64_t* dev_out, uint64_t out_capacity,
                           uint64_t* counts, void* hip_stream);
 int kc_insert_counts_device(kc_ctx* ctx, const uint64_t* dev_records, uint64_t n_records, void* hip_stream);
+/* The same for records that arrive as ngroups (<= 64) consecutive groups of
+ * group_counts[g] records (host array), one per sending rank, each in the order
+ * kc_route_table_device wrote it: sorted by region when the sender's table has this
+ * table's size.  The table is then updated in one LDS pass per region over the groups'
+ * region runs (no partition levels); groups that are not sorted take
+ * kc_insert_counts_device. */
+int kc_insert_counts_runs_device(kc_ctx* ctx, const uint64_t* dev_records, const uint64_t* group_counts,
+                                 uint32_t ngroups, void* hip_stream);
 
 /* Re-initialise the table, the Bloom filter and all counters (the table/filter
  * constructors again, without reallocating). */

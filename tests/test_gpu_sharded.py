@@ -90,13 +90,17 @@ def test_insert_rejects_non_table_keys(monkeypatch, path):
         e.kc.finish()
 
 
+@pytest.mark.parametrize("merge", ["runs", "general", "shuffled"])
 @pytest.mark.parametrize("path", ["direct", "partitioned"])
 @pytest.mark.parametrize("k,mode,G", [(31, 2, 2), (31, 0, 3), (51, 2, 4), (63, 1, 2), (127, 0, 2)])
-def test_preaggregated_merge_union(tmp_path, monkeypatch, k, mode, G, path):
+def test_preaggregated_merge_union(tmp_path, monkeypatch, k, mode, G, path, merge):
     """Pre-aggregated sharding (ShardedCounter's path): each emulated rank counts its own
     reads locally, routes its table as {key, count} records by owner, and every owner adds
     the records it receives; the owners' outputs are disjoint and their union is the
-    oracle's count of the whole input (transforms applied to the merged counts)."""
+    oracle's count of the whole input (transforms applied to the merged counts).
+    merge: runs = the region-sorted groups in one level-3 pass (kc_insert_counts_runs_device),
+    general = the partitioned merge insert, shuffled = runs on unsorted groups (the device
+    check sends them to the general insert)."""
     monkeypatch.setenv("KC_INSERT_PATH", path)  # local counting and the merge insert
     n_reads = 20000
     per = n_reads // G
@@ -129,9 +133,14 @@ def test_preaggregated_merge_union(tmp_path, monkeypatch, k, mode, G, path):
         for recs, counts in routed:
             lo = sum(counts[:d]) * (W + 1)
             parts.append(recs[lo:lo + counts[d] * (W + 1)])
+        if merge == "shuffled":
+            parts = [p.view(-1, W + 1)[torch.randperm(p.numel() // (W + 1), device=p.device)].reshape(-1)
+                     for p in parts]
         recv = torch.cat(parts)
-        engines[d].insert_counts(recv, recv.numel() // (W + 1), stream)
+        gc = [p.numel() // (W + 1) for p in parts] if merge != "general" else None
+        engines[d].insert_counts(recv, recv.numel() // (W + 1), stream, group_counts=gc)
         torch.cuda.synchronize()
+        assert engines[d].owner_table().finish()["inserted"] == int(recv.view(-1, W + 1)[:, W].sum())
     shard_lines = [set(e.owner_table().lines()) for e in engines]
     kmers = [set(l.rsplit(" ", 1)[0] for l in s) for s in shard_lines]
     for a in range(G):

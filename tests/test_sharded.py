@@ -99,7 +99,7 @@ class NumpyEngine:
         arr = np.array(flat, dtype=np.uint64).view(np.int64)
         return torch.from_numpy(arr.copy()), [len(g) // (self.W + 1) for g in groups]
 
-    def insert_counts(self, recs, n, stream=0):
+    def insert_counts(self, recs, n, stream=0, group_counts=None):
         rows = recs[: n * (self.W + 1)].numpy().view(np.uint64).reshape(n, self.W + 1)
         for row in rows:
             self.owner.table[from_words(row[:self.W], self.k)] += int(row[self.W])
