@@ -294,8 +294,8 @@ def test_fastq_equals_plain_sequence_lines(k, tmp_path):
     assert sorted_digest_file(out) == want
 
 
-@pytest.mark.parametrize("k", [31, 51])
-def test_bloom_at_scale_equals_exact_solid_kmers(k, insert_path):
+@pytest.mark.parametrize("k,fpr", [(31, 0.01), (51, 0.01), (51, 0.001), (95, 0.05)])
+def test_bloom_at_scale_equals_exact_solid_kmers(k, fpr, insert_path):
     """Bloom filter (-b, blocked layout) on a larger device-generated input: pass 1 runs
     the partitioned LDS filter (k_b3) or the direct one, pass 2 gates at level 3 (or in
     the direct kernel).  The filter only gates, so every k-mer seen >= 2 times has its
@@ -314,8 +314,9 @@ def test_bloom_at_scale_equals_exact_solid_kmers(k, insert_path):
         kc.count_device(img.data_ptr(), chunks, ka.FMT_FASTA)
         kc.finish()
         want = kc.dump()
+    # fpr 0.001: ceil(hf) = 10 positions, two per filter word for j >= 8 (repeats counted once)
     with ka.KmerCounter(ka.Config(k=k, min_abundance=2, bf_enable=True, est_unique=8_000_000,
-                                  fpr=0.01)) as kc:
+                                  fpr=fpr)) as kc:
         kc.bloom_device(img.data_ptr(), chunks, ka.FMT_FASTA)
         n2 = kc.bloom_finalize()
         kc.count_device(img.data_ptr(), chunks, ka.FMT_FASTA)

@@ -90,7 +90,7 @@ def test_insert_rejects_non_table_keys(monkeypatch, path):
         e.kc.finish()
 
 
-@pytest.mark.parametrize("merge", ["runs", "general", "shuffled"])
+@pytest.mark.parametrize("merge", ["runs", "general", "shuffled", "runs_gaps"])
 @pytest.mark.parametrize("path", ["direct", "partitioned"])
 @pytest.mark.parametrize("k,mode,G", [(31, 2, 2), (31, 0, 3), (51, 2, 4), (63, 1, 2), (127, 0, 2)])
 def test_preaggregated_merge_union(tmp_path, monkeypatch, k, mode, G, path, merge):
@@ -136,6 +136,9 @@ def test_preaggregated_merge_union(tmp_path, monkeypatch, k, mode, G, path, merg
         if merge == "shuffled":
             parts = [p.view(-1, W + 1)[torch.randperm(p.numel() // (W + 1), device=p.device)].reshape(-1)
                      for p in parts]
+        if merge == "runs_gaps":  # empty groups before, between and after the senders' groups
+            empty = parts[0][:0]
+            parts = [empty] + [x for p in parts for x in (p, empty)]
         recv = torch.cat(parts)
         gc = [p.numel() // (W + 1) for p in parts] if merge != "general" else None
         engines[d].insert_counts(recv, recv.numel() // (W + 1), stream, group_counts=gc)
