@@ -338,6 +338,14 @@ constexpr int tile_win() { return COUNT_THREADS * run_w<W>(); }
 #endif
 template <int W>
 constexpr int scatter_threads() { return W <= 2 ? KC_SCATTER_NT12 : 512; }
+// Level 2 runs one 1024-thread workgroup per CU for keys of up to two words: twice the
+// tile of level 1 (16384 one-word keys, 128 KiB of LDS) halves the barriers per key and
+// doubles the runs each bin gets per tile (C2: k_p2f 5.6 -> 5.0 ms on one box)
+#ifndef KC_P2F_NT
+#define KC_P2F_NT 0  // 0: the default below
+#endif
+template <int W>
+constexpr int p2f_threads() { return KC_P2F_NT ? KC_P2F_NT : (W <= 2 ? 1024 : 512); }
 
 // table key of the window ending at p (MODE 0 path: direct extraction)
 template <int W>
@@ -1853,13 +1861,13 @@ static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf
         return v ? (uint32_t)std::atoi(v) : 0u;
     }();
     const size_t sm1 = part_smem<W, scatter_threads<W>()>(t.F1),
-                 sm2 = p2f_smem<W, scatter_threads<W>()>(t.F2, std::max<uint32_t>(p2f_pad, (pb.nblk1 + pb.B2 - 1) / pb.B2));
+                 sm2 = p2f_smem<W, p2f_threads<W>()>(t.F2, std::max<uint32_t>(p2f_pad, (pb.nblk1 + pb.B2 - 1) / pb.B2));
     if ((e = set_smem(k1, sm1)) != hipSuccess) return e;
-    if ((e = set_smem(k_p2f<W, scatter_threads<W>()>, sm2)) != hipSuccess) return e;
+    if ((e = set_smem(k_p2f<W, p2f_threads<W>()>, sm2)) != hipSuccess) return e;
     const OutSeg o1{(uint64_t)pb.nblk1 * pb.cap1, 0, pb.cap1};
     hipLaunchKernelGGL(k1, dim3(pb.nblk1), dim3(scatter_threads<W>()), sm1, s, sym, k, bf, ctr, pb, t.F1, coarse_bins(t),
                        pb.keys1, pk, pkm1, o1, (const unsigned long long*)nullptr, 1);
-    hipLaunchKernelGGL((k_p2f<W, scatter_threads<W>()>), dim3(t.F1 * pb.B2), dim3(scatter_threads<W>()), sm2, s, t, pb, ctr);
+    hipLaunchKernelGGL((k_p2f<W, p2f_threads<W>()>), dim3(t.F1 * pb.B2), dim3(p2f_threads<W>()), sm2, s, t, pb, ctr);
     if ((e = launch_p3<W, true, false, GATE3>(t, ctr, pb, nullptr, fresh, s, bf)) != hipSuccess) return e;
     if ((e = part_level1<W, MODE>(sym, k, bf, ctr, pb, t.F1, coarse_bins(t), pb.keys1, s, gate)) != hipSuccess)
         return e;
@@ -1904,15 +1912,15 @@ static hipError_t bloom_part_w(PackedView sym, int k, BloomView bf, TableView ft
     const unsigned long long* gate = &ctr->part_overflow;
     if ((e = hipMemsetAsync(&ctr->part_overflow, 0, sizeof(ctr->part_overflow), s)) != hipSuccess) return e;
     const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
-    constexpr int NT = scatter_threads<W>();
+    constexpr int NT = scatter_threads<W>(), NT2 = p2f_threads<1>();
     auto k1 = k_p1<W, 3, true, BinRegion, OutSeg, NT>;
-    const size_t sm1 = part_smem<1, NT>(ft.F1), sm2 = p2f_smem<1, NT>(ft.F2, (pb.nblk1 + pb.B2 - 1) / pb.B2);
+    const size_t sm1 = part_smem<1, NT>(ft.F1), sm2 = p2f_smem<1, NT2>(ft.F2, (pb.nblk1 + pb.B2 - 1) / pb.B2);
     if ((e = set_smem(k1, sm1)) != hipSuccess) return e;
-    if ((e = set_smem(k_p2f<1, NT>, sm2)) != hipSuccess) return e;
+    if ((e = set_smem(k_p2f<1, NT2>, sm2)) != hipSuccess) return e;
     const OutSeg o1{(uint64_t)pb.nblk1 * pb.cap1, 0, pb.cap1};
     hipLaunchKernelGGL(k1, dim3(pb.nblk1), dim3(NT), sm1, s, sym, k, bf, ctr, pb, ft.F1, coarse_bins(ft), pb.keys1, pk,
                        pkm1, o1, (const unsigned long long*)nullptr, 1);
-    hipLaunchKernelGGL((k_p2f<1, NT>), dim3(ft.F1 * pb.B2), dim3(NT), sm2, s, ft, pb, ctr);
+    hipLaunchKernelGGL((k_p2f<1, NT2>), dim3(ft.F1 * pb.B2), dim3(NT2), sm2, s, ft, pb, ctr);
     if ((e = launch_b3<true>(bf, ft, ctr, pb, nullptr, fresh, s)) != hipSuccess) return e;
     if ((e = part_level1<W, 3>(sym, k, bf, ctr, pb, ft.F1, coarse_bins(ft), pb.keys1, s, gate)) != hipSuccess)
         return e;
