@@ -63,14 +63,15 @@ DEV uint32_t eq_mask16(const uint32_t (&w)[4], uint32_t pat) {  // bit j: byte j
     return m;
 }
 
-// chunk owning stage position pos (chunks sorted by stage_off, tiles contiguous)
-DEV int find_chunk(const ChunkDesc* __restrict__ chunks, int n, uint64_t pos) {
-    int lo = 0, hi = n - 1;
-    while (lo < hi) {
-        int mid = (lo + hi + 1) >> 1;
-        if (chunks[mid].stage_off <= pos) lo = mid; else hi = mid - 1;
-    }
-    return lo;
+// --------------------------------------------------------------------------------
+// k_tile_map: the chunk of every tile (a chunk's tiles are the TILE-aligned slots it
+// occupies in the stage), parked in tiles[t].nl for k_tile_summary, which replaces a
+// per-tile binary search over the chunk table (dependent loads, ~8 per tile) by one load
+// --------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_tile_map(const ChunkDesc* __restrict__ chunks, TileInfo* __restrict__ tiles) {
+    const ChunkDesc cd = chunks[blockIdx.x];
+    const uint64_t t0 = cd.stage_off / TILE, t1 = (cd.stage_off + cd.len + TILE - 1) / TILE;
+    for (uint64_t t = t0 + threadIdx.x; t < t1; t += 256) tiles[t].nl = blockIdx.x;
 }
 
 // --------------------------------------------------------------------------------
@@ -84,7 +85,8 @@ __global__ __launch_bounds__(TILE_THREADS) void k_tile_summary(const uint8_t* __
     __shared__ int s_c;
     const uint64_t t = blockIdx.x;
     const uint64_t base = t * TILE;
-    if (threadIdx.x == 0) s_c = find_chunk(chunks, n_chunks, base);
+    (void)n_chunks;
+    if (threadIdx.x == 0) s_c = (int)tiles[t].nl;  // k_tile_map
     __syncthreads();
     const ChunkDesc cd = chunks[s_c];
     const uint64_t rel = base - cd.stage_off;
@@ -440,6 +442,8 @@ hipError_t launch_tokenize(const uint8_t* src, uint64_t ntiles, const ChunkDesc*
     if ((e = hipMemsetAsync(sv.pk, 0, words * 8, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(sv.bk, 0, words * 4, s)) != hipSuccess) return e;
     const uint64_t nblk = (ntiles + TSCAN - 1) / TSCAN;
+    if (n_chunks <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_tile_map, dim3((unsigned)n_chunks), dim3(256), 0, s, d_chunks, tiles);
     hipLaunchKernelGGL(k_tile_summary, dim3((unsigned)ntiles), dim3(TILE_THREADS), 0, s, src, d_chunks, n_chunks,
                        fmt, tiles);
     hipLaunchKernelGGL(k_tscan_block, dim3((unsigned)nblk), dim3(TSCAN), 0, s, tiles, ntiles, fmt, touts, tblk);
