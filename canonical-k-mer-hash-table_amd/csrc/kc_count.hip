@@ -7,15 +7,21 @@
 //  direct       k_count<W,MODE>: roll windows, canonicalise, CAS-claim / atomic-add
 //               in HBM.  One scattered device-scope atomic per window, so it runs at
 //               the chip's scattered-atomic rate (~20 G/s measured); used for small
-//               batches and for Bloom pass 1 (bit-array atomics).
+//               batches (and for the Bloom passes of small batches / the reference
+//               filter layout).
 //  partitioned  keys are moved to where they are counted instead:
 //               p1  windows -> F1 coarse bins (hash prefix), LDS counting sort per tile
-//                   so every bin is written as a contiguous run;
-//               p2  each coarse bin -> its F2 regions, same scheme;
-//               p3  one workgroup per region: load the region's 64 KiB of buckets into
-//                   LDS, insert its keys with LDS atomics, write the region back.
-//               Bandwidth-bound (~(4W+1)*8 bytes of key traffic per window plus two
-//               table sweeps) instead of atomic-bound.
+//                   so every bin is written as a contiguous run (segmented, one pass);
+//               p2f each coarse bin -> its F2 regions, same scheme;
+//               p3  one workgroup per region: the region's 64 KiB of buckets in LDS
+//                   (zero-filled when the table is fresh), its keys inserted with LDS
+//                   atomics, the region written back.
+//               Bandwidth-bound (~(4W+1)*8 bytes of key traffic per window plus the
+//               table sweeps) instead of atomic-bound.  The Bloom pass runs the same
+//               levels on table key word 0 with k_b3 (64 KiB filter regions) as level
+//               3; the counting pass behind the filter gates at level 3 (k_p3<..GATE>).
+//  merge        shard records (multi-GPU) go through the partitioned levels, or, when
+//               they arrive region-sorted, straight to level 3 (k_run_bounds + k_p3).
 //
 // Table layout (both paths): 128-byte buckets, keys [S][W] u64 then counts [S] u64,
 // S = 16/(W+1).  Keys are stored as table keys (kc_common.h: word 0 = a bijective mix,
