@@ -218,9 +218,20 @@ int main(int argc, char** argv) {
     void* map = nullptr;
     if (gz) {
         gzFile g = gzdopen(dup(fd), "r");
+        if (!g) { std::cerr << "cannot open " << a.input << " as gzip\n"; return 1; }
+        gzbuffer(g, 1 << 20);
         std::vector<uint8_t> tmp(1 << 22);
         int n;
         while ((n = gzread(g, tmp.data(), (unsigned)tmp.size())) > 0) gzbuf.insert(gzbuf.end(), tmp.begin(), tmp.begin() + n);
+        int zerr = Z_OK;
+        const char* msg = gzerror(g, &zerr);
+        // corrupt or truncated stream (zlib reports a cut stream as Z_BUF_ERROR after
+        // returning what it decoded): fail instead of counting a prefix
+        if (n < 0 || (zerr != Z_OK && zerr != Z_STREAM_END)) {
+            std::cerr << "gzip input " << a.input << " is corrupt or truncated: " << (msg ? msg : "") << std::endl;
+            gzclose(g);
+            return 1;
+        }
         gzclose(g);
         image = gzbuf.data();
         isize = gzbuf.size();

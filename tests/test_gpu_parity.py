@@ -165,6 +165,31 @@ def test_cli_end_to_end(case, golden_input, tmp_path):
     assert "Time used to build hash table" in r.stdout
 
 
+@pytest.mark.parametrize("name,k,args", [("reads_w60.fasta", 31, ["-m", "2", "-a", "1", "-s", "1000000"]),
+                                         ("reads.txt", 31, ["-a", "1", "-s", "1000000"]),
+                                         ("big_reads.fasta", 31, ["-a", "2", "-s", "8000000"])])
+@pytest.mark.parametrize("members", [1, 3])
+def test_cli_gzip_input_is_counted_whole(name, k, args, members, golden_input, tmp_path):
+    """gzip input (an extension): the reference reads only part of a
+    compressed file; the drop-in CLI decompresses every member of the
+    stream and must give the uncompressed file's fixture (big_reads.fasta: > 10 MiB, so
+    the decompressed image spans several chunks)."""
+    import gzip
+
+    case = next(c for c in CASES if c["input"] == name and c["k"] == k and c["args"] == args)
+    raw = open(golden_input(name), "rb").read()
+    gz = tmp_path / (name + ".gz")
+    cuts = [len(raw) * i // members for i in range(members + 1)]
+    with open(gz, "wb") as f:  # concatenated members split at arbitrary bytes
+        for a, b in zip(cuts, cuts[1:]):
+            f.write(gzip.compress(raw[a:b], compresslevel=1))
+    out = tmp_path / "out.kaarme_counts"
+    r = subprocess.run([CLI, str(gz), str(k), "-t", "3", "-o", str(out)] + args, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "gzip compressed:          yes" in r.stdout
+    assert sorted_digest_file(out) == (case["sorted_sha256"], case["lines"])
+
+
 def test_cli_default_output_name(golden_input, tmp_path):
     path = golden_input("reads.txt")
     r = subprocess.run([CLI, path, "31", "-s", "100000", "-a", "1"], capture_output=True, text=True, cwd=tmp_path)

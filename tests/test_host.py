@@ -121,6 +121,22 @@ def test_cli_format_checks(tmp_path):
     assert not (tmp_path / "out.txt").exists()
 
 
+def test_cli_gzip_format_checks(tmp_path):
+    """gzip input: the format comes from the name without its .gz suffix and the first
+    decompressed byte; a truncated stream is an error, never a silently shorter input."""
+    import gzip
+    good = gzip.compress(b">r0\n" + b"ACGTTGCA" * 5000 + b"\n")
+    bad = tmp_path / "bad.txt.gz"
+    bad.write_bytes(gzip.compress(b">r0\nACGT\n"))  # plain text must not start with '>'
+    r = run_cli(bad, 5, "-s", 100)
+    assert r.returncode == 1 and "ill-formed" in r.stderr
+    cut = tmp_path / "cut.fasta.gz"
+    cut.write_bytes(good[: len(good) // 2])
+    r = run_cli(cut, 5, "-s", 100, "-o", tmp_path / "out.txt")
+    assert r.returncode == 1 and "corrupt or truncated" in r.stderr
+    assert not (tmp_path / "out.txt").exists()
+
+
 def make_fastq(n, seed=5, maxlen=300):
     """4-line FASTQ records with N's, lowercase, and quality lines that begin with '@'
     or '+' (the cases a naive record finder gets wrong); returns (fastq, plain) bytes,
