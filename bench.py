@@ -118,13 +118,14 @@ def cpu_baseline(args):
 
 
 def load_traffic(workload):
-    """HBM bytes per k_count launch from the committed rocprofv3 PMC summary, if any."""
+    """HBM bytes per roofline launch of this workload from the committed rocprofv3 PMC summary, if any."""
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        if d.get("workload") == workload:
+        if d.get("workload") == workload:  # single-workload layout
             return d.get("bytes_per_launch")
+        return d.get("workloads", {}).get(workload, {}).get("bytes_per_launch")
     except (OSError, ValueError):
         pass
     return None

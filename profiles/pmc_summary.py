@@ -17,7 +17,7 @@ import os
 import sys
 from collections import defaultdict
 
-COUNT_PASS = ("k_p1<", "k_p2<", "k_p2f<", "k_p3<", "k_scanA", "k_scanB", "k_scanC", "k_count<")
+COUNT_PASS = ("k_p1<", "k_p2<", "k_p2f<", "k_p3<", "k_b3<", "k_scanA", "k_scanB", "k_scanC", "k_count<")
 # FETCH_SIZE / WRITE_SIZE unit: 1023.99998 bytes per unit measured in r01_v5 against
 # k_gather's WRITE_SIZE for a known byte count (k_gather no longer exists: the tokenizer
 # reads device images in place), i.e. the counters are in KiB.
@@ -77,15 +77,30 @@ def main():
         print(f"{k[:60]:60s} {calls:5d} {rd / 1e9:9.3f} {wr / 1e9:9.3f}")
         if k.startswith(COUNT_PASS):
             total += (rd + wr) * calls / steps
+    # bench.py's roofline unit: one counting pass per staged batch, or with the Bloom
+    # filter (-b) one Bloom pass + one counting pass over the same batch
+    per_step = bench["config"].get("batches_per_step", 1.0)
+    units = per_step / 2 if " -b " in bench["config"]["workload"] else per_step
+    total /= max(units, 1e-9)
     print(f"count pass HBM bytes per launch: {total / 1e9:.3f} GB")
     if dest:
+        # one entry per workload (bench.py looks its own up); earlier entries are kept
+        try:
+            with open(dest) as f:
+                old = json.load(f)
+        except (OSError, ValueError):
+            old = {}
+        book = old.get("workloads", {})
+        if "workload" in old:  # the single-workload layout of earlier versions
+            book.setdefault(old["workload"], {c: v for c, v in old.items() if c != "workload"})
+        book[bench["config"]["workload"]] = {
+            "bytes_per_launch": int(total), "unit_bytes": unit,
+            "method": "2*FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md HBM), unit calibrated on k_gather 16-B "
+                      "stores; count-pass kernels (with -b: Bloom pass + counting pass) summed per launch",
+            "per_kernel": per_kernel}
         with open(dest, "w") as f:
-            json.dump({"workload": bench["config"]["workload"], "bytes_per_launch": int(total),
-                       "unit_bytes": unit, "method": "2*FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md HBM), "
-                       "unit calibrated on k_gather 16-B stores; count-pass kernels summed per step",
-                       "per_kernel": per_kernel}, f, indent=1)
+            json.dump({"workloads": book}, f, indent=1)
         print("wrote", dest)
-
 
 if __name__ == "__main__":
     main()
