@@ -514,6 +514,20 @@ struct OutSeg {
     DEV bool fits(uint32_t b, uint64_t dst) const { return dst < start(b) + cap; }
 };
 
+// Key-stream access policy (A/B knob, KC_NT: bit 0 = nontemporal loads of the level-1/2
+// key streams, which are read exactly once; bit 1 = nontemporal stores of the scatters)
+#ifndef KC_NT
+#define KC_NT 0
+#endif
+DEV uint64_t ks_load(const uint64_t* p) {
+    if constexpr (KC_NT & 1) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+DEV void ks_store(uint64_t* p, uint64_t v) {
+    if constexpr (KC_NT & 2) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 // Counting-sort the tile's keys (in registers: tk[j] valid where ok[j]) by bin into
 // LDS and write each bin as one contiguous run at gbase[bin].  The rank of a key inside
 // its bin comes back from the histogram atomic, so one LDS atomic per key suffices.
@@ -551,7 +565,7 @@ DEV bool scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const Out& o
         const uint64_t dst = l.gbase[b] + (i - l.start[b]);
         if (o.fits(b, dst)) {
 #pragma unroll
-            for (int w = 0; w < W; w++) out[dst * W + w] = key[w];
+            for (int w = 0; w < W; w++) ks_store(out + dst * W + w, key[w]);
         } else {
             over = true;
         }
@@ -924,7 +938,7 @@ __global__ __launch_bounds__(NT, 2048 / NT) void k_p2f(TableView tv, PartBufs pb
                 }
                 const uint64_t* src = pb.keys1 + ((seg0 + cs) * pb.cap1 + (i - cb)) * W;
 #pragma unroll
-                for (int w = 0; w < W; w++) tk[q][w] = src[w];
+                for (int w = 0; w < W; w++) tk[q][w] = ks_load(src + w);
             } else {
 #pragma unroll
                 for (int w = 0; w < W; w++) tk[q][w] = 0;
@@ -1114,7 +1128,7 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
             }
             ok |= (src != nullptr) << q;
 #pragma unroll
-            for (int w = 0; w < W; w++) kk[q][w] = src ? src[w] : 0;
+            for (int w = 0; w < W; w++) kk[q][w] = src ? ks_load(src + w) : 0;
             if constexpr (CNT) add[q] = src ? src[W] & CNT_MASK : 0;
             else add[q] = 1;
         }
