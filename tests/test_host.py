@@ -163,3 +163,18 @@ def test_fastq_chunks_are_whole_records():
             assert off == pos and bh == 0
             assert fq[off:off + 1] == b"@" and fq[off:off + ln].count(b"\n") % 4 == 0
             pos = off + ln
+
+
+def test_committed_traffic_book_covers_the_bench_workloads():
+    """bench.py's roofline.traffic comes from profiles/pmc_traffic.json, keyed by the
+    workload string of each bench line: every committed v11 bench line must find its entry."""
+    import importlib.util
+    import json
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    for name in ("c2", "c3", "c4s", "c5s"):
+        line = json.load(open(os.path.join(root, "profiles", f"r01_v11_bench_{name}.json")))
+        got = bench.load_traffic(line["config"]["workload"])
+        assert got and got > line["roofline"]["algorithmic_bytes_per_launch"] * 0.5, name
