@@ -333,8 +333,11 @@ DEV void block_add4(unsigned long long v0, unsigned long long v1, unsigned long 
 // windows of a tile
 // --------------------------------------------------------------------------------
 // per-thread windows of one tile (the tile is COUNT_THREADS * run_w windows)
+#ifndef KC_RUNW_WIDE
+#define KC_RUNW_WIDE 8  // windows per thread for keys of three or four words (A/B knob)
+#endif
 template <int W>
-constexpr int run_w() { return W == 1 ? 16 : 8; }
+constexpr int run_w() { return W == 1 ? 16 : W == 2 ? 8 : KC_RUNW_WIDE; }
 template <int W>
 constexpr int tile_win() { return COUNT_THREADS * run_w<W>(); }
 // the segmented (single-pass) level 1 runs 512-thread workgroups: 8192-window tiles, twice
