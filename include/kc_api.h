@@ -34,7 +34,7 @@ extern "C" {
 #define KC_ERR_STATE (-4)       /* call out of order (e.g. count before bloom finalize) */
 #define KC_ERR_IO (-5)          /* file error */
 #define KC_ERR_NOMEM (-6)       /* host or device allocation failed */
-#define KC_ERR_UNSUPPORTED (-7) /* e.g. FASTQ input (parallel_parser.hpp:1216-1225) */
+#define KC_ERR_UNSUPPORTED (-7) /* e.g. the Bloom filter on the sharded entry points (the reference rejects FASTQ, parallel_parser.hpp:1216-1225; here it is an extension) */
 
 /* input_mode of main.cpp:178-189 */
 #define KC_FMT_FASTA 0
