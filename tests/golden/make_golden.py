@@ -49,6 +49,9 @@ CASES = [
     ("reads_w60.fasta", 31, ["-m", "2", "-a", "1", "-s", "1000000"]),
     ("reads_w60.fasta", 51, ["-m", "0", "-a", "2", "-s", "1000000"]),
     ("reads_w60.fasta", 33, ["-m", "1", "-a", "1", "-s", "1000000"]),
+    # -m 1 -b: the Bloom pass runs, then the filter is ignored (main.cpp:482-489)
+    ("reads_w60.fasta", 33, ["-m", "1", "-b", "-u", "100000", "-a", "1"]),
+    ("reads_w60.fasta", 33, ["-m", "1", "-b", "-u", "100000", "-a", "2"]),
     ("reads_w60.fasta", 17, ["-b", "-u", "100000", "-a", "1"]),
     ("reads_w60.fasta", 51, ["-b", "-u", "100000", "-f", "0.05", "-a", "2"]),
     ("reads_w60.fasta", 1, ["-a", "1", "-s", "100"]),
