@@ -36,6 +36,13 @@ uint64_t round_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
 
 }  // namespace
 
+// entries the histogram / offset arrays of one PartBufs were allocated for
+struct PartCap {
+    uint64_t h1 = 0;  // hist1 entries (off1: h1 + 1)
+    uint64_t h2 = 0;  // hist2 entries (off2: h2 + 1)
+    uint64_t bs = 0;  // bsum entries
+};
+
 struct kc_ctx {
     kc_config cfg{};
     int W = 1, S = 8;
@@ -75,7 +82,7 @@ struct kc_ctx {
     // partitioned insert buffers (pb: the table's levels; pbf: the Bloom pass's, same key
     // buffers, own histograms)
     PartBufs pb{}, pbf{};
-    uint32_t pb_nblk1_cap = 0, pbf_nblk1_cap = 0;
+    PartCap pb_cap{}, pbf_cap{};
     uint64_t* d_keys1 = nullptr;
     uint64_t* d_keys2 = nullptr;
     uint64_t k1_words = 0, k2_words = 0;  // u64 words the level-1 / level-2 key buffers hold
@@ -233,26 +240,43 @@ struct PartGeo {
 };
 static PartGeo table_geo(const kc_ctx* c) { return PartGeo{c->F1, c->F2, c->R, c->W}; }
 
-static int ensure_part_geo(kc_ctx* c, uint64_t syms, bool seg, const PartGeo& g, PartBufs& pb, uint32_t& nblk1_cap) {
+static int ensure_part_geo(kc_ctx* c, uint64_t syms, bool seg, const PartGeo& g, PartBufs& pb, PartCap& cap,
+                           uint32_t bins1 = 0) {
     const uint64_t tile = (uint64_t)COUNT_THREADS * run_width(c->W);
     const uint32_t nblk1 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(2048, (syms + tile - 1) / tile));
     const uint32_t B2 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(64, 2048 / g.F1));
-    if (!pb.hist1 || nblk1 > nblk1_cap) {
+    // every array is sized for the geometry of THIS call (a Bloom job re-sizes the table
+    // after each Bloom pass, so F1 and R may grow between calls on one context)
+    const uint64_t n1 = (uint64_t)std::max<uint32_t>(g.F1, bins1) * 2048;  // level-1 bins x max workgroups
+    const uint64_t n2 = g.R * B2;
+    const uint64_t nbs = (std::max(n1, n2) + 4095) / 4096 + 2;
+    if (n1 > cap.h1) {
         hipFree(pb.hist1);
         hipFree(pb.off1);
         pb.hist1 = nullptr;
         pb.off1 = nullptr;
-        const uint32_t cap = 2048;
-        if (hipMalloc(&pb.hist1, (size_t)g.F1 * cap * 4) != hipSuccess ||
-            hipMalloc(&pb.off1, ((size_t)g.F1 * cap + 1) * 8) != hipSuccess)
+        cap.h1 = 0;
+        if (hipMalloc(&pb.hist1, n1 * 4) != hipSuccess || hipMalloc(&pb.off1, (n1 + 1) * 8) != hipSuccess)
             return c->fail(KC_ERR_NOMEM, "partition histogram allocation failed");
-        nblk1_cap = cap;
+        cap.h1 = n1;
     }
-    if (!pb.hist2) {
-        const size_t n2 = (size_t)g.R * B2, n1 = (size_t)g.F1 * 2048;
-        if (hipMalloc(&pb.hist2, n2 * 4) != hipSuccess || hipMalloc(&pb.off2, (n2 + 1) * 8) != hipSuccess ||
-            hipMalloc(&pb.bsum, ((std::max(n1, n2) + 4095) / 4096 + 2) * 8) != hipSuccess)
+    if (n2 > cap.h2) {
+        hipFree(pb.hist2);
+        hipFree(pb.off2);
+        pb.hist2 = nullptr;
+        pb.off2 = nullptr;
+        cap.h2 = 0;
+        if (hipMalloc(&pb.hist2, n2 * 4) != hipSuccess || hipMalloc(&pb.off2, (n2 + 1) * 8) != hipSuccess)
             return c->fail(KC_ERR_NOMEM, "partition histogram allocation failed");
+        cap.h2 = n2;
+    }
+    if (nbs > cap.bs) {
+        hipFree(pb.bsum);
+        pb.bsum = nullptr;
+        cap.bs = 0;
+        if (hipMalloc(&pb.bsum, nbs * 8) != hipSuccess)
+            return c->fail(KC_ERR_NOMEM, "partition histogram allocation failed");
+        cap.bs = nbs;
     }
     uint64_t cap1 = 0, cap2 = 0;
     if (seg) {
@@ -292,8 +316,8 @@ static int ensure_part_geo(kc_ctx* c, uint64_t syms, bool seg, const PartGeo& g,
     return KC_OK;
 }
 // the table's levels
-static int ensure_part(kc_ctx* c, uint64_t syms, bool seg) {
-    return ensure_part_geo(c, syms, seg, table_geo(c), c->pb, c->pb_nblk1_cap);
+static int ensure_part(kc_ctx* c, uint64_t syms, bool seg, uint32_t bins1 = 0) {
+    return ensure_part_geo(c, syms, seg, table_geo(c), c->pb, c->pb_cap, bins1);
 }
 
 // Insert path per batch: the partitioned pipeline moves ~(4W+1)*8 bytes per window
@@ -360,7 +384,7 @@ static int run_batch(kc_ctx* c, const uint8_t* src, uint64_t used, uint64_t nchu
     if (mode == 1 && c->bloom_blocked && use_partitioned_bloom(c, syms)) {
         const char* env = std::getenv("KC_INSERT_PATH");
         int rc = ensure_part_geo(c, syms, !(env && !std::strcmp(env, "exact")),
-                                 PartGeo{c->bgeo.F1, c->bgeo.F2, c->bgeo.R, 1}, c->pbf, c->pbf_nblk1_cap);
+                                 PartGeo{c->bgeo.F1, c->bgeo.F2, c->bgeo.R, 1}, c->pbf, c->pbf_cap);
         if (rc) return rc;
         HIPCHK(c, launch_bloom_partitioned(sv, c->cfg.k, c->W, bv, c->bgeo, c->d_ctr, c->pbf, c->bloom_fresh, s));
         c->bloom_fresh = false;
@@ -506,7 +530,11 @@ const char* kc_last_error(const kc_ctx* ctx) { return ctx ? ctx->err.c_str() : g
 int kc_create(const kc_config* cfg, kc_ctx** out) {
     if (!cfg || !out) { g_create_error = "null argument"; return KC_ERR_ARG; }
     *out = nullptr;
-    if (cfg->k < 1 || cfg->k > 127) { g_create_error = "k must be in 1..127"; return KC_ERR_ARG; }
+    if (cfg->k < 1 || cfg->k > KC_MAX_K) {
+        g_create_error = "k must be in 1.." + std::to_string(KC_MAX_K);
+        return KC_ERR_ARG;
+    }
+    static_assert(KC_MAX_K == MAX_K, "include/kc_api.h and kc_internal.h agree on the largest k");
     if (cfg->mode < 0 || cfg->mode > 2) { g_create_error = "mode must be 0, 1 or 2"; return KC_ERR_ARG; }
     if (cfg->bf_enable && (cfg->est_unique == 0 || !(cfg->fpr >= 0.001 && cfg->fpr <= 0.999))) {
         g_create_error = "bloom filter needs est_unique > 0 and 0.001 <= fpr <= 0.999";
@@ -705,10 +733,9 @@ int kc_route_device(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, size_
         HIPCHK(c, hipEventRecord(c->xev, c->stream));
         HIPCHK(c, hipStreamWaitEvent(s, c->xev, 0));
     }
-    rc = ensure_part(c, syms, false);
+    rc = ensure_part(c, syms, false, nshards);  // level-1 bins = the shards
     if (rc) return rc;
-    if ((uint64_t)nshards * c->pb.nblk1 > (uint64_t)c->F1 * c->pb_nblk1_cap)
-        return c->fail(KC_ERR_ARG, "too many shards");
+    if ((uint64_t)nshards * c->pb.nblk1 > c->pb_cap.h1) return c->fail(KC_ERR_ARG, "too many shards");
     std::array<hipEvent_t, 4> ev{};
     if (c->profiling)
         for (auto& e : ev) e = c->get_event();
@@ -1001,13 +1028,7 @@ int kc_reset(kc_ctx* c) {
         HIPCHK(c, hipMemsetAsync(c->d_bloom, 0, bloom_words(c) * 4, c->stream));
         c->bloom_fresh = true;
         if (c->bloom_final) {  // back to the Bloom pass: the table is sized again after it
-            // (its allocation is kept for reuse; the region histograms follow the new size)
-            hipFree(c->pb.hist2);
-            hipFree(c->pb.off2);
-            hipFree(c->pb.bsum);
-            c->pb.hist2 = nullptr;
-            c->pb.off2 = nullptr;
-            c->pb.bsum = nullptr;
+            // (its allocation is kept for reuse; ensure_part_geo re-sizes the histograms)
             c->nbuckets = 0;
             c->bloom_final = false;
         }
@@ -1266,6 +1287,51 @@ int kc_plan_chunks(const uint8_t* image, uint64_t size, int k, uint64_t chunk_si
     if (!v.empty()) std::memcpy(r, v.data(), v.size() * sizeof(kc_chunk));
     *out = r;
     *n_out = v.size();
+    return KC_OK;
+}
+
+int kc_xxh64(const uint64_t* values, const uint64_t* seeds, uint64_t n, uint64_t* out) {
+    if (n && (!values || !seeds || !out)) return KC_ERR_ARG;
+    if (n == 0) return KC_OK;
+    uint64_t* d = nullptr;
+    if (hipMalloc(&d, n * 3 * 8) != hipSuccess) return KC_ERR_NOMEM;
+    hipError_t e = hipMemcpy(d, values, n * 8, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d + n, seeds, n * 8, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = launch_xxh64(d, d + n, n, d + 2 * n, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(out, d + 2 * n, n * 8, hipMemcpyDeviceToHost);
+    hipFree(d);
+    return e == hipSuccess ? KC_OK : KC_ERR_HIP;
+}
+
+int kc_bloom_info(kc_ctx* c, uint64_t* n_words, uint64_t* bits, int* nh, int* nh_gate, int* layout) {
+    if (!c) return KC_ERR_ARG;
+    if (!c->d_bloom) return c->fail(KC_ERR_STATE, "no Bloom filter");
+    if (n_words) *n_words = bloom_words(c);
+    if (bits) *bits = c->bf_bits;
+    if (nh) *nh = c->nh;
+    if (nh_gate) *nh_gate = c->nh_gate;
+    if (layout) *layout = c->bloom_blocked;
+    return KC_OK;
+}
+
+int kc_bloom_read(kc_ctx* c, uint32_t* words, uint64_t n) {
+    if (!c || (!words && n)) return KC_ERR_ARG;
+    if (!c->d_bloom) return c->fail(KC_ERR_STATE, "no Bloom filter");
+    if (n > bloom_words(c)) return c->fail(KC_ERR_ARG, "more words than the filter holds");
+    int rc = kc_sync(c);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpy(words, c->d_bloom, n * 4, hipMemcpyDeviceToHost));
+    return KC_OK;
+}
+
+int kc_bloom_write(kc_ctx* c, const uint32_t* words, uint64_t n) {
+    if (!c || (!words && n)) return KC_ERR_ARG;
+    if (!c->d_bloom) return c->fail(KC_ERR_STATE, "no Bloom filter");
+    if (n > bloom_words(c)) return c->fail(KC_ERR_ARG, "more words than the filter holds");
+    int rc = kc_sync(c);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpy(c->d_bloom, words, n * 4, hipMemcpyHostToDevice));
+    c->bloom_fresh = false;
     return KC_OK;
 }
 

@@ -1,0 +1,2079 @@
+// kc_count_impl.h -- canonical k-mer insertion, Bloom passes and the table dump.
+// Included by kc_count_w.hip, which is compiled once per key width W (-DKC_W=1..8).
+//
+// The reference inserts every window with process_kmer_MT (kmer_hash_table.cpp:
+// 2207-2567): a CAS-probed table shared by all threads.  Two MI355X paths produce the
+// same table contents:
+//
+//  direct       k_count<W,MODE>: roll windows, canonicalise, CAS-claim / atomic-add
+//               in HBM.  One scattered device-scope atomic per window, so it runs at
+//               the chip's scattered-atomic rate (~20 G/s measured); used for small
+//               batches (and for the Bloom passes of small batches / the reference
+//               filter layout).
+//  partitioned  keys are moved to where they are counted instead:
+//               p1  windows -> F1 coarse bins (hash prefix), LDS counting sort per tile
+//                   so every bin is written as a contiguous run (segmented, one pass);
+//               p2f each coarse bin -> its F2 regions, same scheme;
+//               p3  one workgroup per region: the region's 64 KiB of buckets in LDS
+//                   (zero-filled when the table is fresh), its keys inserted with LDS
+//                   atomics, the region written back.
+//               Bandwidth-bound (~(4W+1)*8 bytes of key traffic per window plus the
+//               table sweeps) instead of atomic-bound.  The Bloom pass runs the same
+//               levels on table key word 0 with k_b3 (64 KiB filter regions) as level
+//               3; the counting pass behind the filter gates at level 3 (k_p3<..GATE>).
+//  merge        shard records (multi-GPU) go through the partitioned levels, or, when
+//               they arrive region-sorted, straight to level 3 (k_run_bounds + k_p3).
+//
+// Table layout (both paths): 128-byte buckets, keys [S][W] u64 then counts [S] u64,
+// S = 16/(W+1).  Keys are stored as table keys (kc_common.h: word 0 = a bijective mix,
+// never 0, so 0 is EMPTY).  A key lives in the region given by the top bits of word 0;
+// its probe sequence starts at the bucket given by the next 9 bits and wraps inside
+// the region.  W > 1 keys: word 0 claimed by CAS, other words
+// stored, then READY|1 added to the count word; readers matching word 0 wait for READY.
+#pragma once
+#include <algorithm>
+#include <cstdlib>
+
+#include "kc_common.h"
+
+namespace kc {
+
+static __constant__ uint64_t c_bf_seeds[MAX_NH] = {2411, 3253, 1061, 1129, 2269, 7309, 3491, 8237, 6359, 8779};
+
+// --------------------------------------------------------------------------------
+// direct insert of one table key into the HBM table
+// --------------------------------------------------------------------------------
+template <int W>
+DEV bool table_insert(const TableView& tv, const uint64_t (&tk)[W], uint64_t add = 1) {
+    constexpr int S = BUCKET_WORDS / (W + 1);
+    const uint64_t region = region_of(tk[0], tv.R);
+    uint32_t b = bucket_in_region(tk[0], tv.R);
+    for (int probe = 0; probe < BPR; probe++) {
+        uint64_t* bk = tv.buckets + (region * BPR + b) * BUCKET_WORDS;
+        uint64_t w0[S];
+        if constexpr (W == 1) {
+            const uint4* b4 = reinterpret_cast<const uint4*>(bk);
+#pragma unroll
+            for (int q = 0; q < S / 2; q++) {
+                uint4 v = b4[q];
+                w0[2 * q] = ((uint64_t)v.y << 32) | v.x;
+                w0[2 * q + 1] = ((uint64_t)v.w << 32) | v.z;
+            }
+        } else {
+#pragma unroll
+            for (int s = 0; s < S; s++) w0[s] = bk[s * W];
+        }
+        int s = 0;
+        while (s < S) {
+            uint64_t* kp = bk + s * W;
+            uint64_t* cp = bk + S * W + s;
+            uint64_t v0 = w0[s];
+            if (v0 == EMPTY) {
+                const uint64_t old = atomicCAS((unsigned long long*)kp, (unsigned long long)EMPTY,
+                                               (unsigned long long)tk[0]);
+                if (old == EMPTY) {
+                    if constexpr (W == 1) {
+                        atomicAdd((unsigned long long*)cp, (unsigned long long)add);
+                    } else {
+#pragma unroll
+                        for (int i = 1; i < W; i++) atomic_store_agent(kp + i, tk[i]);
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // words land before READY
+                        atomicAdd((unsigned long long*)cp, (unsigned long long)(READY + add));
+                    }
+                    return true;
+                }
+                v0 = old;
+                w0[s] = old;
+            }
+            if (v0 == tk[0]) {
+                if constexpr (W == 1) {
+                    atomicAdd((unsigned long long*)cp, (unsigned long long)add);
+                    return true;
+                } else {
+                    const uint64_t c = atomic_load_agent(cp);
+                    if (!(c & READY)) continue;  // claimed, not yet published: retry this slot
+                    asm volatile("" ::: "memory");
+                    bool eq = true;
+#pragma unroll
+                    for (int i = 1; i < W; i++) eq &= atomic_load_agent(kp + i) == tk[i];
+                    if (eq) {
+                        atomicAdd((unsigned long long*)cp, (unsigned long long)add);
+                        return true;
+                    }
+                }
+            }
+            s++;
+        }
+        b = (b + 1) & (BPR - 1);
+    }
+    return false;  // region full
+}
+
+// --------------------------------------------------------------------------------
+// Bloom filter: both filters interleaved in one bit array (filter-1 bit of h = 2h,
+// filter-2 bit = 2h+1, the MyAtomicBitArrayFT layout, mybitarray.hpp:30-125)
+// --------------------------------------------------------------------------------
+struct BloomLocal {
+    uint32_t new_first, new_second, failed;
+};
+
+// Two layouts of the k-mer's positions:
+//  reference (KC_BLOOM_LAYOUT=reference; mybitarray + calculate_hashes,
+//    double_bloomfilter.hpp:276-281): h_j = XXH64(root, seed_j) & (bits - 1), root = the
+//    strand-symmetric Rabin-Karp hash mod 2^54: n independent random words, filter-1 bit
+//    of h at 2h and filter-2 bit at 2h+1 (MyAtomicBitArrayFT, mybitarray.hpp:30-125).
+//  blocked (the default): a split-block filter.  Each k-mer owns one 64-byte block of 16
+//    words: words 0-7 hold filter 1, words 8-15 filter 2 (the same 2 x 256 bits per block
+//    as the interleaved bit array).  Position j sets bit b_j = bits 5j..5j+4 of
+//    bmix(t0) in word j mod 8 of each filter, so the positions of one k-mer lie in
+//    distinct words (no repeats for ceil(hf) <= 8) and a test is two 16-byte reads and
+//    a shift per position.  The block is picked by the top bits of the k-mer's table key
+//    word 0 t0 (kc_common.h to_tkey, a bijective mix of the canonical key): block =
+//    ((t0 >> 32) * blocks) >> 32, the same hash prefix as the table's region index, so a
+//    filter region of BF_BLOCKS_PER_REGION blocks is one contiguous 64 KiB slice that the
+//    partitioned Bloom pass holds in LDS (k_b3), and the filter-2 words of a table
+//    region's keys are one contiguous slice its level 3 copies to LDS for the gate
+//    (k_p3<..., GATE>).  The filter only gates, so either layout gives the reference's
+//    counts for every k-mer seen at least twice.
+constexpr int BF_BLOCK_WORDS = 16;               // 512 bits: filter 1 in words 0-7, filter 2 in 8-15
+// ((t0 >> 32) * nblocks) >> 32 for the power-of-two block count: a shift (the count is
+// uniform, so its log2 is scalar work)
+DEV uint64_t bloom_block(uint64_t t0, uint64_t nblocks) { return (t0 >> 32) >> (32 - __builtin_ctzll(nblocks)); }
+// position hash: t0 is already a strong mix of the key (to_tkey), one multiply-fold
+// spreads its low bits (which vary inside a block) over all position fields
+DEV uint64_t bmix(uint64_t t0) {
+    const uint64_t x = (t0 ^ 0xD6E8FEB86659FD93ULL) * 0xBF58476D1CE4E5B9ULL;
+    return x ^ (x >> 31);
+}
+// bit of position j (word j & 7 of a filter): 5-bit fields, six per 32-bit half of h (no
+// field straddles the halves, so each is one bit-field extract)
+DEV uint32_t sb_bit(uint64_t h, int j) {
+    return j < 6 ? ((uint32_t)h >> (5 * j)) & 31 : ((uint32_t)(h >> 32) >> (5 * (j - 6))) & 31;
+}
+// the 8 words of one filter of a block (16-byte aligned) into registers
+DEV void load8(const uint32_t* p, uint32_t (&w)[8]) {
+    const uint4 a = reinterpret_cast<const uint4*>(p)[0], b = reinterpret_cast<const uint4*>(p)[1];
+    w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+    w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+}
+// all of the first n positions set in the 8 words f (one filter of a block): the bits of
+// all MAX_NH positions gathered branch-free (two extracts and a shift-or each), then masked
+DEV bool sb_all(const uint32_t (&f)[8], uint64_t h, int n) {
+    uint32_t got = 0;
+#pragma unroll
+    for (int j = 0; j < MAX_NH; j++) got |= ((f[j & 7] >> sb_bit(h, j)) & 1) << j;
+    const uint32_t need = (1u << n) - 1;
+    return (got & need) == need;
+}
+
+// insertion_process (double_bloomfilter.hpp:371-413) on one block of the blocked layout;
+// `blk` is the block in HBM (direct pass) or in LDS (k_b3).  A "set" counts as ours only
+// if our atomicOr flipped the bit (MyAtomicBitArrayFT::set, mybitarray.hpp:87-125).
+// Positions j >= 8 share word j - 8 and count once if they repeat its bit.
+DEV void block_insert(uint32_t* blk, uint64_t t0, int nh, BloomLocal& loc) {
+    const uint64_t h = bmix(t0);
+    uint32_t f1[8], f2[8];
+    load8(blk + 8, f2);
+    if (sb_all(f2, h, nh)) return;  // in the second filter already
+    load8(blk, f1);
+    int n = 0, s1 = 0, s2 = 0;
+    bool dup[MAX_NH];
+#pragma unroll
+    for (int j = 0; j < MAX_NH; j++) {
+        dup[j] = j >= nh || (j >= 8 && sb_bit(h, j) == sb_bit(h, j - 8));
+        if (!dup[j]) {
+            n++;
+            s1 += (f1[j & 7] >> sb_bit(h, j)) & 1;
+            s2 += (f2[j & 7] >> sb_bit(h, j)) & 1;
+        }
+    }
+    bool to_second = true;
+    if (s1 != n) {
+        int mine = 0;
+#pragma unroll
+        for (int j = 0; j < MAX_NH; j++) {
+            const uint32_t m = 1u << sb_bit(h, j);
+            if (!dup[j] && !(f1[j & 7] & m)) mine += !(atomicOr(blk + (j & 7), m) & m);
+        }
+        if (mine == n - s1) { loc.new_first++; to_second = false; }
+        else loc.failed++;
+    }
+    if (to_second) {
+        int mine = 0;
+#pragma unroll
+        for (int j = 0; j < MAX_NH; j++) {
+            const uint32_t m = 1u << sb_bit(h, j);
+            if (!dup[j] && !(f2[j & 7] & m)) mine += !(atomicOr(blk + 8 + (j & 7), m) & m);
+        }
+        if (mine == n - s2) loc.new_second++;
+    }
+}
+
+// pass-2 gate: all of the first trunc(hf) filter-2 bits set (parallel_parser.hpp:
+// 2436-2441); f2 = the block's 8 filter-2 words (HBM, or the LDS slice of k_p3)
+DEV bool block_gate(const uint32_t* f2, uint64_t t0, int nh_gate) {
+    uint32_t w[8];
+    load8(f2, w);
+    return sb_all(w, bmix(t0), nh_gate);
+}
+// blocks [lo, hi] hold the filter of table region r's keys (region_of and bloom_block
+// are monotone in the same 32-bit hash prefix)
+DEV void region_blocks(uint64_t r, uint64_t R, uint64_t nblocks, uint64_t& lo, uint64_t& hi) {
+    const uint64_t h_lo = ((r << 32) + R - 1) / R;                               // first prefix of r
+    const uint64_t h_hi = min((((r + 1) << 32) + R - 1) / R, 1ULL << 32) - 1;   // last prefix of r
+    lo = (h_lo * nblocks) >> 32;
+    hi = (h_hi * nblocks) >> 32;
+}
+
+// reference layout: word and bit (of the filter-1 bit; filter 2 is the next bit) of the
+// first n hash functions of a root
+template <int N>
+DEV void ref_slots(const BloomView& bf, uint64_t root, int n, uint64_t (&widx)[N], uint32_t (&bpos)[N]) {
+#pragma unroll
+    for (int j = 0; j < N; j++)
+        if (j < n) {
+            const uint64_t bit = 2 * (xxh64_u64(root, c_bf_seeds[j]) & bf.mask);
+            widx[j] = bit >> 5;
+            bpos[j] = (uint32_t)(bit & 31);
+        }
+}
+
+DEV uint32_t* bloom_block_ptr(const BloomView& bf, uint64_t t0) {
+    return bf.bits + bloom_block(t0, bf.nblocks) * BF_BLOCK_WORDS;
+}
+
+// insertion_process on the HBM filter (direct pass 1): root for the reference layout, the
+// table key word t0 for the blocked one
+DEV void bloom_insert(const BloomView& bf, uint64_t root, uint64_t t0, BloomLocal& loc) {
+    if (bf.blocked) {
+        block_insert(bloom_block_ptr(bf, t0), t0, bf.nh, loc);
+        return;
+    }
+    uint64_t widx[MAX_NH];
+    uint32_t bpos[MAX_NH];
+    uint32_t view[MAX_NH];
+    int s1 = 0, s2 = 0;
+    ref_slots(bf, root, bf.nh, widx, bpos);
+#pragma unroll
+    for (int j = 0; j < MAX_NH; j++)
+        if (j < bf.nh) view[j] = bf.bits[widx[j]];
+#pragma unroll
+    for (int j = 0; j < MAX_NH; j++)
+        if (j < bf.nh) {
+            s1 += (view[j] >> bpos[j]) & 1;
+            s2 += (view[j] >> (bpos[j] + 1)) & 1;
+        }
+    if (s2 == bf.nh) return;
+    bool to_second;
+    if (s1 == bf.nh) {
+        to_second = true;
+    } else {
+        int mine = 0;
+#pragma unroll
+        for (int j = 0; j < MAX_NH; j++)
+            if (j < bf.nh) {
+                const uint32_t m = 1u << bpos[j];
+                if (!(view[j] & m)) {
+                    const uint32_t old = atomicOr(bf.bits + widx[j], m);
+                    if (!(old & m)) mine++;
+                    view[j] = old | m;
+                }
+            }
+        if (mine == bf.nh - s1) { loc.new_first++; to_second = false; }
+        else { loc.failed++; to_second = true; }
+    }
+    if (to_second) {
+        int mine = 0;
+#pragma unroll
+        for (int j = 0; j < MAX_NH; j++)
+            if (j < bf.nh) {
+                const uint32_t m = 2u << bpos[j];
+                if (!(view[j] & m)) {
+                    const uint32_t old = atomicOr(bf.bits + widx[j], m);
+                    if (!(old & m)) mine++;
+                }
+            }
+        if (mine == bf.nh - s2) loc.new_second++;
+    }
+}
+
+DEV bool bloom_gate(const BloomView& bf, uint64_t root, uint64_t t0) {
+    if (bf.blocked) return block_gate(bloom_block_ptr(bf, t0) + 8, t0, bf.nh_gate);
+    uint64_t widx[MAX_NH];
+    uint32_t bpos[MAX_NH];
+    ref_slots(bf, root, bf.nh_gate, widx, bpos);
+    bool all = true;
+#pragma unroll
+    for (int j = 0; j < MAX_NH; j++)
+        if (j < bf.nh_gate) all &= (bf.bits[widx[j]] >> (bpos[j] + 1)) & 1;
+    return all;
+}
+
+// block reduction of up to 4 counters, one atomic each per block
+DEV void block_add4(unsigned long long v0, unsigned long long v1, unsigned long long v2, unsigned long long v3,
+                    unsigned long long* d0, unsigned long long* d1, unsigned long long* d2,
+                    unsigned long long* d3) {
+    __shared__ unsigned long long s_red[4][16];  // up to 1024-thread blocks
+    unsigned long long v[4] = {v0, v1, v2, v3};
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        unsigned long long x = v[q];
+        for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+        if (lane == 0) s_red[q][wid] = x;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        unsigned long long x = 0;
+        for (int w = 0; w < (int)(blockDim.x / 64); w++) x += s_red[threadIdx.x][w];
+        unsigned long long* dst = threadIdx.x == 0 ? d0 : threadIdx.x == 1 ? d1 : threadIdx.x == 2 ? d2 : d3;
+        if (x && dst) atomicAdd(dst, x);
+    }
+}
+
+// --------------------------------------------------------------------------------
+// windows of a tile
+// --------------------------------------------------------------------------------
+// per-thread windows of one tile (the tile is COUNT_THREADS * run_w windows):
+// kc_internal.h run_width (shared with the host's partition sizing)
+template <int W>
+constexpr int run_w() { return run_width(W); }
+template <int W>
+constexpr int tile_win() { return COUNT_THREADS * run_w<W>(); }
+// the segmented (single-pass) level 1: kc_internal.h scatter_threads
+template <int W>
+constexpr int scatter_threads() { return scatter_threads_w(W); }
+// Level 2 runs one 1024-thread workgroup per CU for keys of up to two words: twice the
+// tile of level 1 (16384 one-word keys, 128 KiB of LDS) halves the barriers per key and
+// doubles the runs each bin gets per tile (C2: k_p2f 5.6 -> 5.0 ms on one box); wider
+// keys take smaller groups so that the tile still fits the LDS
+#ifndef KC_P2F_NT
+#define KC_P2F_NT 0  // 0: the default below
+#endif
+template <int W>
+constexpr int p2f_threads() { return KC_P2F_NT ? KC_P2F_NT : (W <= 2 ? 1024 : W <= 4 ? 512 : 256); }
+
+// table key of the window ending at p (MODE 0 path: direct extraction)
+template <int W>
+DEV bool window_tkey(const PackedView& sv, uint64_t p, const RollConst& rk, uint64_t (&tk)[W]) {
+    uint64_t fwd[W], rc[W], key[W];
+    if (!extract_window<W>(sv, p, rk, fwd)) return false;
+    revcomp<W>(fwd, rk, rc);
+    canonical<W>(fwd, rc, key);
+    to_tkey<W>(key, tk);
+    return true;
+}
+
+// MODE 1/2: the Bloom root (RollingHasherDual mod 2^54) is a rolled quantity, so these
+// modes roll one contiguous run of run_w windows per thread.
+template <int W, class F>
+DEV void tile_rolled(const PackedView& sv, uint64_t t0, uint64_t t1, const RollConst& rk, F&& f) {
+    constexpr int RUNW = run_w<W>();
+    const uint64_t r0 = t0 + (uint64_t)threadIdx.x * RUNW, r1 = min(r0 + RUNW, t1);
+    if (r0 < r1) {
+        const uint64_t ps = r0 >= (uint64_t)(rk.k - 1) ? r0 - (rk.k - 1) : 0;
+        roll_run<W, true>(sv, ps, r0, r1, rk, f);
+    }
+}
+
+// --------------------------------------------------------------------------------
+// k_count<W, MODE>: direct path. MODE 0 count, 1 Bloom pass 1, 2 count behind the gate
+// --------------------------------------------------------------------------------
+template <int W, int MODE>
+__global__ __launch_bounds__(COUNT_THREADS) void k_count(PackedView sv, int k, TableView tv, BloomView bf,
+                                                         DevCounters* __restrict__ ctr, uint64_t pow5_k,
+                                                         uint64_t pow5_km1) {
+    constexpr int TW = tile_win<W>();
+    const uint64_t M = ctr->stream_len;
+    const uint64_t t0 = (uint64_t)blockIdx.x * TW;
+    uint32_t n_win = 0, n_ins = 0, n_fail = 0;
+    BloomLocal bl = {0, 0, 0};
+    if (t0 < M) {
+        const uint64_t t1 = min(t0 + TW, M);
+        const RollConst rk = make_roll<W>(k, pow5_k, pow5_km1);
+        if constexpr (MODE == 0) {
+            constexpr int RUNW = run_w<W>();
+            const uint64_t r0 = t0 + (uint64_t)threadIdx.x * RUNW;
+            if (r0 < t1)
+                run_windows<W, RUNW>(sv, r0, t1, rk,
+                                     [&](int, bool valid, const uint64_t (&fwd)[W], const uint64_t (&rc)[W]) {
+                    if (!valid) return;
+                    uint64_t key[W], tk[W];
+                    canonical<W>(fwd, rc, key);
+                    to_tkey<W>(key, tk);
+                    n_win++;
+                    n_ins++;
+                    if (!table_insert<W>(tv, tk)) n_fail++;
+                });
+        } else {
+            tile_rolled<W>(sv, t0, t1, rk, [&](const uint64_t (&fwd)[W], const uint64_t (&rc)[W], uint64_t root) {
+                n_win++;
+                uint64_t key[W], tk[W];
+                canonical<W>(fwd, rc, key);
+                to_tkey<W>(key, tk);
+                if constexpr (MODE == 1) {
+                    bloom_insert(bf, root, tk[0], bl);
+                } else {
+                    if (!bloom_gate(bf, root, tk[0])) return;
+                    n_ins++;
+                    if (!table_insert<W>(tv, tk)) n_fail++;
+                }
+            });
+        }
+    }
+    if constexpr (MODE == 1)
+        block_add4(n_win, bl.new_first, bl.new_second, bl.failed, &ctr->bf_windows, &ctr->new_in_first,
+                   &ctr->new_in_second, &ctr->failed_in_first);
+    else
+        block_add4(n_win, n_ins, n_fail, 0, &ctr->windows, &ctr->inserted, &ctr->overflow, nullptr);
+}
+
+// --------------------------------------------------------------------------------
+// partitioned path
+// --------------------------------------------------------------------------------
+// LDS of a scatter pass: tilehist, tilestart, tilecur (u32 x F), gbase (u64 x F), keys
+constexpr size_t hist_smem(uint32_t F) { return ((size_t)F * 3 + 1) * 4 + 4 + (size_t)F * 8; }
+template <int W, int NT = COUNT_THREADS>
+constexpr size_t part_smem(uint32_t F) {
+    return hist_smem(F) + (size_t)NT * run_w<W>() * 8 * W;
+}
+
+// exclusive scan of an LDS u32 array of n entries by one NT-thread block
+template <int NT = COUNT_THREADS>
+DEV void block_excl_scan_lds(const uint32_t* in, uint32_t* out, uint32_t n) {
+    __shared__ uint32_t s_w[NT / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint32_t per = (n + NT - 1) / NT;
+    const uint32_t lo = min(n, tid * per), hi = min(n, lo + per);
+    uint32_t sum = 0;
+    for (uint32_t i = lo; i < hi; i++) sum += in[i];
+    const uint32_t incl = wave_incl_sum(sum);
+    if (lane == 63) s_w[wid] = incl;
+    __syncthreads();
+    uint32_t base = incl - sum;
+    for (int w = 0; w < wid; w++) base += s_w[w];
+    for (uint32_t i = lo; i < hi; i++) {
+        const uint32_t v = in[i];
+        out[i] = base;
+        base += v;
+    }
+    __syncthreads();
+}
+
+struct PartLds {
+    uint32_t* hist;
+    uint32_t* start;
+    uint32_t* cur;
+    uint64_t* gbase;
+    uint64_t* keys;
+};
+DEV PartLds part_lds(uint8_t* smem, uint32_t F) {
+    PartLds l;
+    l.hist = reinterpret_cast<uint32_t*>(smem);
+    l.start = l.hist + F;
+    l.cur = l.start + F;
+    l.gbase = reinterpret_cast<uint64_t*>(l.cur + F + (F & 1));
+    l.keys = l.gbase + F;
+    return l;
+}
+
+// bin of a table key: its region bin (table levels) or its shard owner (routing);
+// the kind is a template parameter so the table levels carry no routing branch.
+struct BinRegion {  // level-1 bin (coarse: region >> f2bits) or level-2 bin (region & mask)
+    static constexpr bool kOwner = false;
+    uint64_t R;
+    int f2bits;
+    uint32_t mask;
+    int coarse;
+    DEV uint32_t operator()(uint64_t t0) const {
+        const uint32_t r = (uint32_t)region_of(t0, R);
+        return coarse ? r >> f2bits : r & mask;
+    }
+};
+struct BinOwner {
+    static constexpr bool kOwner = true;
+    uint32_t parts;
+    DEV uint32_t operator()(uint64_t t0) const { return owner_of(t0, parts); }
+};
+
+// Where a scatter pass writes bin b.  Exact layout: one contiguous run per bin at offsets
+// from a histogram pass + scan.  Segmented layout (single pass, no histogram): a
+// fixed-capacity segment per (bin, producing workgroup); keys that would pass a
+// segment's end are dropped and raise DevCounters::part_overflow, and the exact
+// pipeline then redoes the batch (launched behind a device-side gate).
+struct OutExact {
+    static constexpr bool kSeg = false;
+    DEV bool fits(uint32_t, uint64_t) const { return true; }
+};
+struct OutSeg {
+    static constexpr bool kSeg = true;
+    uint64_t stride;  // keys between the segments of bins b and b+1
+    uint64_t base;    // first key of bin 0's segment for this workgroup
+    uint64_t cap;     // keys per segment
+    DEV uint64_t start(uint32_t b) const { return (uint64_t)b * stride + base; }
+    DEV bool fits(uint32_t b, uint64_t dst) const { return dst < start(b) + cap; }
+};
+
+// Key-stream access policy (A/B knob, KC_NT: bit 0 = nontemporal loads of the level-1/2
+// key streams, which are read exactly once; bit 1 = nontemporal stores of the scatters)
+#ifndef KC_NT
+#define KC_NT 0
+#endif
+DEV uint64_t ks_load(const uint64_t* p) {
+    if constexpr (KC_NT & 1) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+DEV void ks_store(uint64_t* p, uint64_t v) {
+    if constexpr (KC_NT & 2) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+// Counting-sort the tile's keys (in registers: tk[j] valid where ok[j]) by bin into
+// LDS and write each bin as one contiguous run at gbase[bin].  The rank of a key inside
+// its bin comes back from the histogram atomic, so one LDS atomic per key suffices.
+// Returns true if a segmented run did not fit.
+struct NoMid {
+    DEV void operator()() const {}
+};
+// mid(): called once the tile's keys are in LDS (tk / ok are dead from there on: a caller
+// may load its next tile into them)
+template <int W, int RUNW, class Bin, class Out, int NT = COUNT_THREADS, class Mid = NoMid>
+DEV bool scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const Out& o, uint64_t (&tk)[RUNW][W],
+                      bool (&ok)[RUNW], uint64_t* __restrict__ out, Mid&& mid = Mid()) {
+    const int tid = threadIdx.x;
+    uint32_t rank[RUNW];
+#pragma unroll
+    for (int j = 0; j < RUNW; j++) rank[j] = ok[j] ? atomicAdd(&l.hist[bin(tk[j][0])], 1u) : 0;
+    __syncthreads();
+    block_excl_scan_lds<NT>(l.hist, l.start, F);
+#pragma unroll
+    for (int j = 0; j < RUNW; j++)
+        if (ok[j]) {
+            const uint32_t slot = l.start[bin(tk[j][0])] + rank[j];
+#pragma unroll
+            for (int w = 0; w < W; w++) l.keys[slot * W + w] = tk[j][w];
+        }
+    mid();
+    __syncthreads();
+    const uint32_t n = l.start[F - 1] + l.hist[F - 1];
+    bool over = false;
+    for (uint32_t i = tid; i < n; i += NT) {
+        uint64_t key[W];
+#pragma unroll
+        for (int w = 0; w < W; w++) key[w] = l.keys[i * W + w];
+        const uint32_t b = bin(key[0]);
+        const uint64_t dst = l.gbase[b] + (i - l.start[b]);
+        if (o.fits(b, dst)) {
+#pragma unroll
+            for (int w = 0; w < W; w++) ks_store(out + dst * W + w, key[w]);
+        } else {
+            over = true;
+        }
+    }
+    __syncthreads();
+    for (uint32_t b = tid; b < F; b += NT) {
+        l.gbase[b] += l.hist[b];
+        l.hist[b] = 0;
+    }
+    __syncthreads();
+    return over;
+}
+
+// gated kernels (the exact fallback of a segmented batch) run only if *gate != 0
+DEV bool gated_off(const unsigned long long* gate) { return gate && *gate == 0; }
+
+// words per level-1 output key: the Bloom pass (MODE 3) moves table key word 0 only
+constexpr int p1_out_words(int W, int MODE) { return MODE == 3 ? 1 : W; }
+
+// Level 1: windows of a contiguous symbol range -> coarse bins (region >> f2bits).
+// MODE 0: count; 2: count behind the Bloom gate on the rolled root (reference layout);
+// 3: Bloom pass 1, blocked layout (keys = t0, bins = filter regions); 4: count, gated
+// at level 3 (blocked layout).
+// SCATTER = false: histogram only ([bin][block] into hist1); true: write the keys,
+// exact layout (offsets off1) or segmented (Out = OutSeg: single pass, the segment
+// fill counts go to hist1).  `count`: add windows / inserted to the counters (off for
+// the histogram pass of a fallback, whose windows the segmented pass counted already).
+template <int W, int MODE, bool SCATTER, class Bin, class Out, int NT = COUNT_THREADS>
+__global__ __launch_bounds__(NT, 4) void k_p1(PackedView sv, int k, BloomView bf,
+                                                      DevCounters* __restrict__ ctr, PartBufs pb, uint32_t F, Bin bin,
+                                                      uint64_t* __restrict__ out, uint64_t pow5_k, uint64_t pow5_km1,
+                                                      Out o, const unsigned long long* gate, int count) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int RUNW = run_w<W>(), TW = NT * RUNW;
+    constexpr bool COUNTS = !SCATTER || Out::kSeg;
+    constexpr bool ROLLED = MODE == 2;       // gate on the rolled root (reference layout)
+    constexpr int OW = p1_out_words(W, MODE);  // words per output key
+    if (gated_off(gate)) return;
+    if (gate && !SCATTER && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&ctr->part_fallbacks, 1ULL);
+    const PartLds l = part_lds(smem, F);
+    const int tid = threadIdx.x;
+    const uint64_t M = ctr->stream_len;
+    const uint64_t per = ((M + pb.nblk1 - 1) / pb.nblk1 + TW - 1) / TW * TW;
+    const uint64_t lo = min(M, (uint64_t)blockIdx.x * per), hi = min(M, lo + per);
+    Out ob = o;
+    if constexpr (Out::kSeg) ob.base = (uint64_t)blockIdx.x * o.cap;  // segment (b, block) = b * nblk1 + block
+    for (uint32_t b = tid; b < F; b += NT) {
+        l.hist[b] = 0;
+        if constexpr (SCATTER) {
+            if constexpr (Out::kSeg) l.gbase[b] = ob.start(b);
+            else l.gbase[b] = pb.off1[(uint64_t)b * pb.nblk1 + blockIdx.x];
+        }
+    }
+    __syncthreads();
+    bool over = false;
+    const RollConst rk = make_roll<W>(k, pow5_k, pow5_km1);
+    uint32_t n_win = 0, n_ins = 0;
+    for (uint64_t t0 = lo; t0 < hi; t0 += TW) {
+        const uint64_t t1 = min(t0 + TW, hi);
+        uint64_t tk[RUNW][OW];
+        bool ok[RUNW];
+        if constexpr (!ROLLED) {
+            const uint64_t r0 = t0 + (uint64_t)tid * RUNW;
+#pragma unroll
+            for (int j = 0; j < RUNW; j++) ok[j] = false;
+            if (r0 < t1)
+                run_windows<W, RUNW>(sv, r0, t1, rk,
+                                     [&](int j, bool valid, const uint64_t (&fwd)[W], const uint64_t (&rc)[W]) {
+                    uint64_t key[W], t[W];
+                    canonical<W>(fwd, rc, key);
+                    to_tkey<W>(key, t);
+#pragma unroll
+                    for (int w = 0; w < OW; w++) tk[j][w] = t[w];
+                    ok[j] = valid;
+                });
+            if constexpr (COUNTS) {
+#pragma unroll
+                for (int j = 0; j < RUNW; j++) {
+                    n_win += ok[j];
+                    n_ins += MODE == 0 ? ok[j] : 0;  // MODE 4: level 3 counts the gated insertions
+                }
+            }
+        } else {
+            // rolled run: slot j <- the j-th symbol of the thread's run (static indices)
+#pragma unroll
+            for (int j = 0; j < RUNW; j++) ok[j] = false;
+            tile_rolled<W>(sv, t0, t1, rk, [&](const uint64_t (&fwd)[W], const uint64_t (&rc)[W], uint64_t root) {
+                if constexpr (COUNTS) n_win++;
+                uint64_t key[W], t[W];
+                canonical<W>(fwd, rc, key);
+                to_tkey<W>(key, t);
+                if (!bloom_gate(bf, root, t[0])) return;
+                if constexpr (COUNTS) n_ins++;
+                // at most run_w windows per run: append into the first free register slot
+#pragma unroll
+                for (int j = 0; j < RUNW; j++)
+                    if (!ok[j]) {
+                        ok[j] = true;
+#pragma unroll
+                        for (int w = 0; w < W; w++) tk[j][w] = t[w];
+                        break;
+                    }
+            });
+        }
+        if constexpr (SCATTER) {
+            over |= scatter_tile<OW, RUNW, Bin, Out, NT>(l, F, bin, ob, tk, ok, out);
+        } else {
+#pragma unroll
+            for (int j = 0; j < RUNW; j++)
+                if (ok[j]) atomicAdd(&l.hist[bin(tk[j][0])], 1u);
+        }
+    }
+    if constexpr (!SCATTER) {
+        __syncthreads();
+        for (uint32_t b = tid; b < F; b += NT) pb.hist1[(uint64_t)b * pb.nblk1 + blockIdx.x] = l.hist[b];
+    }
+    if constexpr (Out::kSeg) {  // segment fills (the scatter's last barrier ordered gbase)
+        for (uint32_t b = tid; b < F; b += NT)
+            pb.hist1[(uint64_t)b * pb.nblk1 + blockIdx.x] = (uint32_t)(l.gbase[b] - ob.start(b));
+        if (over) atomicOr(&ctr->part_overflow, 1ULL);
+    }
+    // routing (owner bins) counts windows here and insertions at the owner; the Bloom
+    // pass counts its windows apart
+    if constexpr (COUNTS)
+        if (count) {
+            if constexpr (MODE == 3)
+                block_add4(n_win, 0, 0, 0, &ctr->bf_windows, nullptr, nullptr, nullptr);
+            else
+                block_add4(n_win, Bin::kOwner ? 0 : n_ins, 0, 0, &ctr->windows, &ctr->inserted, nullptr, nullptr);
+        }
+}
+
+// Level 1 over a key array (keys received from other shards): [0, n) split over nblk1
+// blocks, bins = the coarse bins of the table key.
+template <int W, bool SCATTER>
+__global__ __launch_bounds__(COUNT_THREADS, 4) void k_p1k(const uint64_t* __restrict__ in, uint64_t n, PartBufs pb,
+                                                       uint32_t F, BinRegion bin, DevCounters* __restrict__ ctr,
+                                                       int cnt_word) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int RUNW = run_w<W>(), TW = tile_win<W>();
+    const PartLds l = part_lds(smem, F);
+    const int tid = threadIdx.x;
+    const uint64_t per = ((n + pb.nblk1 - 1) / pb.nblk1 + TW - 1) / TW * TW;
+    const uint64_t lo = min(n, (uint64_t)blockIdx.x * per), hi = min(n, lo + per);
+    for (uint32_t b = tid; b < F; b += COUNT_THREADS) {
+        l.hist[b] = 0;
+        if constexpr (SCATTER) l.gbase[b] = pb.off1[(uint64_t)b * pb.nblk1 + blockIdx.x];
+    }
+    __syncthreads();
+    uint32_t n_inv = 0;
+    unsigned long long added = 0;  // records (cnt_word >= 0): sum of their counts
+    for (uint64_t t0 = lo; t0 < hi; t0 += TW) {
+        uint64_t tk[RUNW][W];
+        bool ok[RUNW];
+#pragma unroll
+        for (int q = 0; q < RUNW; q++) {
+            const uint64_t i = t0 + tid + (uint64_t)q * COUNT_THREADS;
+#pragma unroll
+            for (int w = 0; w < W; w++) tk[q][w] = i < hi ? in[i * W + w] : 0;
+            ok[q] = tk[q][0] != EMPTY;  // 0 is never a table key: skip (counted as invalid)
+            if constexpr (!SCATTER) {
+                n_inv += (i < hi) & !ok[q];
+#pragma unroll
+                for (int w = 0; w < W; w++)
+                    if (w == cnt_word && ok[q]) added += tk[q][w] & CNT_MASK;
+            }
+        }
+        if constexpr (SCATTER) {
+            scatter_tile<W, RUNW>(l, F, bin, OutExact{}, tk, ok, pb.keys1);
+        } else {
+#pragma unroll
+            for (int q = 0; q < RUNW; q++)
+                if (ok[q]) atomicAdd(&l.hist[bin(tk[q][0])], 1u);
+        }
+    }
+    if constexpr (!SCATTER) {
+        __syncthreads();
+        for (uint32_t b = tid; b < F; b += COUNT_THREADS) pb.hist1[(uint64_t)b * pb.nblk1 + blockIdx.x] = l.hist[b];
+        if (cnt_word < 0) added = blockIdx.x == 0 && tid == 0 ? n : 0;
+        block_add4(added, n_inv, 0, 0, &ctr->inserted, &ctr->invalid, nullptr, nullptr);
+    }
+}
+
+// direct insert of a key array (small batches)
+template <int W>
+__global__ __launch_bounds__(COUNT_THREADS) void k_insert_keys(const uint64_t* __restrict__ in, uint64_t n,
+                                                               TableView tv, DevCounters* __restrict__ ctr) {
+    uint32_t n_fail = 0, n_inv = 0;
+    const uint64_t i = (uint64_t)blockIdx.x * COUNT_THREADS + threadIdx.x;
+    if (i < n) {
+        uint64_t tk[W];
+#pragma unroll
+        for (int w = 0; w < W; w++) tk[w] = in[i * W + w];
+        if (tk[0] == EMPTY) n_inv++;  // 0 is never a table key: skip (counted as invalid)
+        else if (!table_insert<W>(tv, tk)) n_fail++;
+    }
+    block_add4(blockIdx.x == 0 && threadIdx.x == 0 ? n : 0, n_fail, n_inv, 0, &ctr->inserted, &ctr->overflow,
+               &ctr->invalid, nullptr);
+}
+
+// --------------------------------------------------------------------------------
+// shard merge (pre-aggregated sharding): a rank's table -> {table key, count} records
+// grouped by owner shard; the owner adds the counts into its own table.
+// --------------------------------------------------------------------------------
+// one 128-byte bucket into registers: eight 16-byte loads issued together
+DEV void load_bucket(const uint64_t* __restrict__ b, uint64_t (&bw)[BUCKET_WORDS]) {
+    const uint4* b4 = reinterpret_cast<const uint4*>(b);
+    uint4 v[BUCKET_WORDS / 2];
+#pragma unroll
+    for (int c = 0; c < BUCKET_WORDS / 2; c++) v[c] = b4[c];
+#pragma unroll
+    for (int c = 0; c < BUCKET_WORDS / 2; c++) {
+        bw[2 * c] = ((uint64_t)v[c].y << 32) | v[c].x;
+        bw[2 * c + 1] = ((uint64_t)v[c].w << 32) | v[c].z;
+    }
+}
+
+// SCATTER = false: per-block record counts per owner ([owner][block] into hist);
+// true: records {W table-key words, raw count} at off[owner][block] + rank.
+template <int W, bool SCATTER>
+__global__ __launch_bounds__(256) void k_route_table(TableView tv, uint32_t parts, uint32_t* __restrict__ hist,
+                                                     const uint64_t* __restrict__ off, uint64_t* __restrict__ out) {
+    constexpr int S = BUCKET_WORDS / (W + 1);
+    __shared__ uint32_t s_cnt[RT_MAX_PARTS];
+    __shared__ uint64_t s_base[RT_MAX_PARTS];
+    const uint32_t nblk = gridDim.x;
+    for (uint32_t d = threadIdx.x; d < parts; d += 256) {
+        s_cnt[d] = 0;
+        if constexpr (SCATTER) s_base[d] = off[(uint64_t)d * nblk + blockIdx.x];
+    }
+    __syncthreads();
+    const uint64_t bkt = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (bkt < tv.nbuckets) {
+        uint64_t bw[BUCKET_WORDS];
+        load_bucket(tv.buckets + bkt * BUCKET_WORDS, bw);
+#pragma unroll
+        for (int sl = 0; sl < S; sl++) {
+            const uint64_t t0 = bw[sl * W];
+            if (t0 == EMPTY) continue;
+            const uint32_t d = owner_of(t0, parts);
+            const uint32_t r = atomicAdd(&s_cnt[d], 1u);
+            if constexpr (SCATTER) {
+                uint64_t* o = out + (s_base[d] + r) * (W + 1);
+#pragma unroll
+                for (int w = 0; w < W; w++) o[w] = bw[sl * W + w];
+                o[W] = bw[S * W + sl] & CNT_MASK;
+            }
+        }
+    }
+    if constexpr (!SCATTER) {
+        __syncthreads();
+        for (uint32_t d = threadIdx.x; d < parts; d += 256) hist[(uint64_t)d * nblk + blockIdx.x] = s_cnt[d];
+    }
+}
+
+// add the counts of {W table-key words, count} records into the table (direct inserts:
+// one record per distinct key of a sending shard, far fewer than windows)
+template <int W>
+__global__ __launch_bounds__(COUNT_THREADS) void k_insert_counts(const uint64_t* __restrict__ rec, uint64_t n,
+                                                                 TableView tv, DevCounters* __restrict__ ctr) {
+    uint32_t n_fail = 0, n_inv = 0;
+    unsigned long long added = 0;
+    const uint64_t i = (uint64_t)blockIdx.x * COUNT_THREADS + threadIdx.x;
+    if (i < n) {
+        uint64_t tk[W];
+#pragma unroll
+        for (int w = 0; w < W; w++) tk[w] = rec[i * (W + 1) + w];
+        const uint64_t c = rec[i * (W + 1) + W] & CNT_MASK;
+        if (tk[0] == EMPTY) n_inv++;
+        else if (c && !table_insert<W>(tv, tk, c)) n_fail++;
+        else added = c;
+    }
+    block_add4(added, n_fail, n_inv, 0, &ctr->inserted, &ctr->overflow, &ctr->invalid, nullptr);
+}
+
+// Level 2: coarse bin c (block = c * B2 + j) -> its F2 regions (next bits of tkey[0]).
+template <int W, bool SCATTER>
+__global__ __launch_bounds__(COUNT_THREADS, 4) void k_p2(TableView tv, PartBufs pb, const unsigned long long* gate) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int RUNW = run_w<W>(), TW = tile_win<W>();
+    if (gated_off(gate)) return;
+    const uint32_t F = tv.F2;
+    const BinRegion bin{tv.R, tv.f2bits, F - 1, 0};
+    const PartLds l = part_lds(smem, F);
+    const int tid = threadIdx.x;
+    const uint32_t c = blockIdx.x / pb.B2, j = blockIdx.x % pb.B2;
+    const uint64_t cs = pb.off1[(uint64_t)c * pb.nblk1], ce = pb.off1[(uint64_t)(c + 1) * pb.nblk1];
+    const uint64_t part = (ce - cs + pb.B2 - 1) / pb.B2;
+    const uint64_t lo = min(ce, cs + j * part), hi = min(ce, lo + part);
+    const uint64_t rbase = (uint64_t)c * F;
+    for (uint32_t b = tid; b < F; b += COUNT_THREADS) {
+        l.hist[b] = 0;
+        if constexpr (SCATTER) l.gbase[b] = pb.off2[(rbase + b) * pb.B2 + j];
+    }
+    __syncthreads();
+    for (uint64_t t0 = lo; t0 < hi; t0 += TW) {
+        uint64_t tk[RUNW][W];
+        bool ok[RUNW];
+#pragma unroll
+        for (int q = 0; q < RUNW; q++) {
+            const uint64_t i = t0 + tid + (uint64_t)q * COUNT_THREADS;
+            ok[q] = i < hi;
+#pragma unroll
+            for (int w = 0; w < W; w++) tk[q][w] = ok[q] ? pb.keys1[i * W + w] : 0;
+        }
+        if constexpr (SCATTER) {
+            scatter_tile<W, RUNW>(l, F, bin, OutExact{}, tk, ok, pb.keys2);
+        } else {
+#pragma unroll
+            for (int q = 0; q < RUNW; q++)
+                if (ok[q]) atomicAdd(&l.hist[bin(tk[q][0])], 1u);
+        }
+    }
+    if constexpr (!SCATTER) {
+        __syncthreads();
+        for (uint32_t b = tid; b < F; b += COUNT_THREADS) pb.hist2[(rbase + b) * pb.B2 + j] = l.hist[b];
+    }
+}
+
+// Level 2, segmented: coarse bin c's level-1 segments of workgroups [s_lo, s_hi)
+// (block = c * B2 + j) -> segments (c * F2 + region, j) of capacity cap2, one pass.
+// The input segments are read as one virtual run (exclusive prefix of their fills in
+// LDS; each thread walks a monotone segment cursor).
+// LDS: the scatter's arrays plus the segment-fill prefix (a level-2 workgroup reads
+// ceil(nblk1 / B2) level-1 segments)
+template <int W, int NT>
+constexpr size_t p2f_smem(uint32_t F, uint32_t nseg_max) { return part_smem<W, NT>(F) + (size_t)(nseg_max + 1) * 4; }
+
+#ifndef KC_PREFETCH
+#define KC_PREFETCH 1
+#endif
+template <int W, int NT>
+__global__ __launch_bounds__(NT, 2048 / NT) void k_p2f(TableView tv, PartBufs pb, DevCounters* __restrict__ ctr) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int RUNW = run_w<W>(), TW = NT * RUNW;
+    if (ctr->part_overflow) return;  // level 1 overflowed: the exact pipeline redoes the batch
+    const uint32_t F = tv.F2;
+    const BinRegion bin{tv.R, tv.f2bits, F - 1, 0};
+    const PartLds l = part_lds(smem, F);
+    uint32_t* pre = reinterpret_cast<uint32_t*>(smem + part_smem<W, NT>(F));
+    const int tid = threadIdx.x;
+    const uint32_t c = blockIdx.x / pb.B2, j = blockIdx.x % pb.B2;
+    const uint32_t s_lo = (uint32_t)((uint64_t)j * pb.nblk1 / pb.B2);
+    const uint32_t nseg = (uint32_t)((uint64_t)(j + 1) * pb.nblk1 / pb.B2) - s_lo;
+    const uint64_t seg0 = (uint64_t)c * pb.nblk1 + s_lo;  // level-1 segment index of cursor 0
+    const OutSeg o{(uint64_t)pb.B2 * pb.cap2, ((uint64_t)c * F * pb.B2 + j) * pb.cap2, pb.cap2};
+    for (uint32_t i = tid; i <= nseg; i += NT) pre[i] = i < nseg ? pb.hist1[seg0 + i] : 0;
+    for (uint32_t b = tid; b < F; b += NT) {
+        l.hist[b] = 0;
+        l.gbase[b] = o.start(b);
+    }
+    __syncthreads();
+    block_excl_scan_lds<NT>(pre, pre, nseg + 1);  // in place; pre[nseg] = total
+    const uint32_t total = pre[nseg];
+    bool over = false;
+    // segment cursor of this thread (its indices grow monotonically): segment cs holds
+    // [cb, nb) of the virtual run, both bounds kept in registers
+    uint32_t cs = 0, cb = 0, nb = nseg ? pre[1] : 0;
+    auto load_tile = [&](uint32_t t0, uint64_t (&tk)[RUNW][W], bool (&ok)[RUNW]) {
+#pragma unroll
+        for (int q = 0; q < RUNW; q++) {
+            const uint32_t i = t0 + tid + q * NT;
+            ok[q] = i < total;
+            if (ok[q]) {
+                while (nb <= i) {
+                    cs++;
+                    cb = nb;
+                    nb = pre[cs + 1];
+                }
+                const uint64_t* src = pb.keys1 + ((seg0 + cs) * pb.cap1 + (i - cb)) * W;
+#pragma unroll
+                for (int w = 0; w < W; w++) tk[q][w] = ks_load(src + w);
+            } else {
+#pragma unroll
+                for (int w = 0; w < W; w++) tk[q][w] = 0;
+            }
+        }
+    };
+    uint64_t tk[RUNW][W];
+    bool ok[RUNW];
+    if (total) load_tile(0, tk, ok);
+    for (uint32_t t0 = 0; t0 < total; t0 += TW) {
+        // the next tile is loaded into the same registers as soon as this tile's keys sit
+        // in LDS, so its loads overlap this tile's write-out (barriers wait for LDS only)
+        const bool more = t0 + TW < total;
+        over |= scatter_tile<W, RUNW, BinRegion, OutSeg, NT>(l, F, bin, o, tk, ok, pb.keys2, [&]() {
+            if (KC_PREFETCH && more) load_tile(t0 + TW, tk, ok);
+        });
+        if (!KC_PREFETCH && more) load_tile(t0 + TW, tk, ok);
+    }
+    for (uint32_t b = tid; b < F; b += NT)
+        pb.hist2[((uint64_t)c * F + b) * pb.B2 + j] = (uint32_t)(l.gbase[b] - o.start(b));
+    if (over) atomicOr(&ctr->part_overflow, 1ULL);
+}
+
+// LDS image of a region: the 16-byte chunks of each 128-byte bucket are XOR-swizzled
+// with the bucket index so that lanes probing random buckets spread over the banks.
+// (bits 1..3 of the bucket: with bit 0 selecting the 128-byte half of a 256-byte bank row,
+// the chunk of a random bucket lands on any of the 16 bank quads)
+DEV uint32_t lds_chunk(uint32_t b, uint32_t q) { return b * 8 + (q ^ ((b >> 1) & 7)); }
+DEV uint64_t* lds_word(uint64_t* lt, uint32_t b, uint32_t word) {
+    return lt + lds_chunk(b, word >> 1) * 2 + (word & 1);
+}
+
+// 8-bit slot tags (LDS only, beside the region image): one u64 per bucket, byte s = the tag
+// of slot s, 0 = empty.  A probe reads the bucket's tags (one ds_read_b64) and the key words
+// of the slots whose tag matches, instead of every key word of the bucket.
+#ifndef KC_P3_TAGS
+#define KC_P3_TAGS 1
+#endif
+DEV uint32_t slot_tag(uint64_t t0) { return 1u + (((uint32_t)t0 & 0xFFu) * 255u >> 8); }
+// bit i set iff byte i of x is zero (exact: no borrow between bytes)
+DEV uint32_t zero_byte_mask4(uint32_t x) {
+    const uint32_t z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);  // bit 7 of each zero byte
+    return ((z >> 7) * 0x01020408u) >> 24;                                       // bits 7/15/23/31 -> 0..3
+}
+DEV uint32_t zero_byte_mask8(uint64_t x) {
+    return zero_byte_mask4((uint32_t)x) | zero_byte_mask4((uint32_t)(x >> 32)) << 4;
+}
+
+// Level 3: one workgroup per region: LDS-resident table
+// SEG: the region's keys are the B2 level-2 segments (region, j) (fills in hist2);
+// otherwise the contiguous run [off2[r * B2], off2[(r + 1) * B2]).  A segmented launch
+// leaves the table alone when the batch overflowed; an exact one can be gated.
+// CNT: items are {W key words, count} records (shard merge) and add their count.
+// fresh: the table is known to be all zero (just reset), so the region is not read.
+// GATE: Bloom pass 2 on the blocked layout: an item is inserted only if its filter-2 bits
+// are set (parallel_parser.hpp:2436-2441).  The blocks of a region's keys form one
+// contiguous slice of the filter (bloom_block and region_of share the hash prefix), so
+// the gate reads stay within a few KiB that L2 keeps.
+constexpr int P3_THREADS = 1024;  // two 64 KiB regions per CU: 8 waves per SIMD
+template <int W, bool SEG, bool CNT, bool GATE = false>
+__global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView tv, PartBufs pb,
+                                                                  DevCounters* __restrict__ ctr,
+                                                                  const unsigned long long* gate, int fresh,
+                                                                  BloomView bf) {
+    constexpr int NT = P3_THREADS;
+    constexpr int IW = CNT ? W + 1 : W;  // words per item
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ uint32_t s_pre[65];  // SEG: exclusive prefix of the B2 (<= 64) segment fills
+    constexpr int S = BUCKET_WORDS / (W + 1);
+    // keys loaded per thread before inserting (memory-level parallelism); 1024-thread
+    // groups already keep 8 waves per SIMD in flight
+    constexpr int KB = NT >= 1024 ? (W >= 2 || CNT ? 2 : 4) : 8;  // (CNT items carry a count: 64 VGPRs)
+    if constexpr (SEG) {
+        if (ctr->part_overflow) return;
+    } else {
+        if (gated_off(gate)) return;
+    }
+    uint64_t* lt = reinterpret_cast<uint64_t*>(smem);  // BPR * BUCKET_WORDS words
+    uint64_t* tg = lt + BPR * BUCKET_WORDS;             // KC_P3_TAGS: BPR tag words
+    const uint64_t r = blockIdx.x;
+    uint64_t start, end;
+    if constexpr (SEG) {
+        if (threadIdx.x == 0) {
+            uint32_t acc = 0;
+            for (uint32_t j = 0; j < pb.B2; j++) {
+                s_pre[j] = acc;
+                acc += pb.hist2[r * pb.B2 + j];
+            }
+            s_pre[pb.B2] = acc;
+        }
+        __syncthreads();
+        start = 0;
+        end = s_pre[pb.B2];
+    } else {
+        start = pb.off2[r * pb.B2];
+        end = pb.off2[(r + 1) * pb.B2];
+    }
+    // nothing to insert: leave the region untouched, unless the table is fresh (its reset may
+    // have been deferred to this pass, which then writes every region)
+    if (start == end && !fresh) return;
+    uint4* g4 = reinterpret_cast<uint4*>(tv.buckets + r * BPR * BUCKET_WORDS);
+    uint4* l4 = reinterpret_cast<uint4*>(lt);
+    constexpr int N4 = BPR * BUCKET_WORDS / 2;
+    constexpr int NT4 = KC_P3_TAGS ? BPR / 2 : 0;  // tag words, as uint4
+    if (fresh) {
+        for (int i = threadIdx.x; i < N4 + NT4; i += NT) l4[i] = make_uint4(0, 0, 0, 0);
+        __syncthreads();
+    } else {
+        for (int i = threadIdx.x; i < N4; i += NT) l4[lds_chunk(i >> 3, i & 7)] = g4[i];
+        __syncthreads();
+        if constexpr (KC_P3_TAGS) {
+            for (int bb = threadIdx.x; bb < BPR; bb += NT) {
+                uint64_t t = 0;
+#pragma unroll
+                for (int sl = 0; sl < S; sl++) {
+                    const uint64_t w0 = *lds_word(lt, bb, sl * W);
+                    if (w0 != EMPTY) t |= (uint64_t)slot_tag(w0) << (8 * sl);
+                }
+                tg[bb] = t;
+            }
+            __syncthreads();
+        }
+    }
+    // GATE with an LDS slice: the filter-2 bits of the region's blocks, 8 words per block
+    uint32_t* gs = reinterpret_cast<uint32_t*>(tg + (KC_P3_TAGS ? BPR : 0));
+    uint64_t gblo = 0;
+    if constexpr (GATE) {
+        if (bf.slice_blocks) {
+            uint64_t ghi;
+            region_blocks(r, tv.R, bf.nblocks, gblo, ghi);
+            const uint32_t n4 = (uint32_t)(ghi - gblo + 1) * 2;  // filter-2 halves of the blocks, as uint4
+            const uint4* src = reinterpret_cast<const uint4*>(bf.bits + gblo * BF_BLOCK_WORDS);
+            uint4* dst = reinterpret_cast<uint4*>(gs);
+            for (uint32_t i = threadIdx.x; i < n4; i += NT) dst[i] = src[(i >> 1) * 4 + 2 + (i & 1)];
+            __syncthreads();
+        }
+    }
+    uint32_t n_fail = 0, n_ins = 0;
+    unsigned long long n_add = 0;  // CNT: the records' counts (the runs merge counts them here)
+    // SEG: segment cursor of this thread (indices grow monotonically): segment cs holds
+    // [cb, nb), both bounds in registers
+    uint32_t cs = 0, cb = 0, nb = 0;
+    if constexpr (SEG) nb = s_pre[1];
+    // Runs (the merge over region-sorted groups): a sender's records sit in its table order,
+    // i.e. sorted by home bucket, and inserted in that order neighbouring lanes collide on
+    // the same buckets and banks.  The items are visited in a scrambled order instead: a
+    // bijection of [0, 2^m) (2^m >= end), slots mapping past end are idle.
+    const bool runs = SEG && pb.seg_start != nullptr;
+    uint64_t vend = end;
+    uint32_t pmask = 0, psh = 0;
+    if (runs && end > 1) {
+        const uint32_t m = 64 - __builtin_clzll(end - 1);
+        vend = 1ULL << m;
+        pmask = (uint32_t)(vend - 1);
+        psh = (m + 1) / 2;
+    }
+    auto load_items = [&](uint64_t base, uint64_t (&kk)[KB][W], uint64_t (&add)[KB], uint32_t& ok) {
+        ok = 0;
+#pragma unroll
+        for (int q = 0; q < KB; q++) {
+            const uint64_t i = base + threadIdx.x + (uint64_t)q * NT;
+            const uint64_t* src = nullptr;
+            if (runs) {
+                uint32_t j = ((uint32_t)i * 0x9E3779B1u) & pmask;
+                j ^= j >> psh;
+                j = (j * 0x85EBCA77u) & pmask;
+                if (i < vend && j < end) {
+                    uint32_t lo = 0, hi = pb.B2;  // the group holding j: s_pre[lo] <= j < s_pre[lo + 1]
+                    while (hi - lo > 1) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (s_pre[mid] <= j) lo = mid;
+                        else hi = mid;
+                    }
+                    src = pb.keys2 + (pb.seg_start[r * pb.B2 + lo] + (j - s_pre[lo])) * IW;
+                }
+            } else if (i < end) {
+                if constexpr (SEG) {
+                    while (nb <= i) {
+                        cs++;
+                        cb = nb;
+                        nb = s_pre[cs + 1];
+                    }
+                    src = pb.keys2 + ((r * pb.B2 + cs) * pb.cap2 + (i - cb)) * IW;
+                } else {
+                    src = pb.keys2 + i * IW;
+                }
+            }
+            ok |= (src != nullptr) << q;
+#pragma unroll
+            for (int w = 0; w < W; w++) kk[q][w] = src ? ks_load(src + w) : 0;
+            if constexpr (CNT) add[q] = src ? src[W] & CNT_MASK : 0;
+            else add[q] = 1;
+        }
+    };
+    uint64_t kk[KB][W];
+    uint64_t add[KB];
+    uint32_t okm = 0;
+    if (start < vend) load_items(start, kk, add, okm);
+    for (uint64_t base = start; base < vend; base += (uint64_t)KB * NT) {
+        // the next items' loads are issued before this batch's inserts
+        uint64_t nkk[KB][W];
+        uint64_t nadd[KB];
+        uint32_t nokm = 0;
+        const uint64_t nbase = base + (uint64_t)KB * NT;
+        const bool more = KC_PREFETCH && W <= 2 && nbase < vend;  // W > 2: no spare registers
+        if (more) load_items(nbase, nkk, nadd, nokm);
+        bool pass[KB];
+#pragma unroll
+        for (int q = 0; q < KB; q++) {  // the gate reads of all KB items are issued together
+            pass[q] = (okm >> q) & 1;
+            if constexpr (GATE) {
+                const uint64_t t0 = kk[q][0];
+                if (bf.slice_blocks)
+                    pass[q] = pass[q] && block_gate(gs + (bloom_block(t0, bf.nblocks) - gblo) * 8, t0, bf.nh_gate);
+                else
+                    pass[q] = pass[q] && block_gate(bloom_block_ptr(bf, t0) + 8, t0, bf.nh_gate);
+            }
+            n_ins += pass[q];
+            if constexpr (CNT) n_add += pass[q] ? add[q] : 0;
+        }
+#pragma unroll
+        for (int q = 0; q < KB; q++) {
+            if (!pass[q]) continue;
+            const uint64_t k0 = kk[q][0];
+            uint32_t b = bucket_in_region(k0, tv.R);
+            bool done = false;
+            if constexpr (KC_P3_TAGS) {
+                constexpr uint32_t SMASK = (1u << S) - 1;
+                const uint32_t tag = slot_tag(k0);
+                const uint64_t bc = 0x0101010101010101ULL * tag;
+                for (int probe = 0; probe < 4 * BPR && !done;) {
+                    const uint64_t tw = tg[b];
+                    uint32_t m = zero_byte_mask8(tw ^ bc) & SMASK;
+                    int slot = -1;
+                    while (m) {  // candidates: usually none (new key) or exactly the key's slot
+                        const int sl = __builtin_ctz(m);
+                        m &= m - 1;
+                        bool eq = *lds_word(lt, b, sl * W) == k0;
+#pragma unroll
+                        for (int w = 1; w < W; w++) eq &= *lds_word(lt, b, sl * W + w) == kk[q][w];
+                        if (eq) {
+                            slot = sl;
+                            break;
+                        }
+                    }
+                    uint64_t a = add[q];
+                    if (slot < 0) {
+                        const uint32_t em = zero_byte_mask8(tw) & SMASK;
+                        if (!em) {  // bucket full, key absent: next bucket
+                            b = (b + 1) & (BPR - 1);
+                            probe++;
+                            continue;
+                        }
+                        // claim the first untagged slot by its word 0; the tag is stored last, so
+                        // a tag match always finds the key's words published
+                        const int e = __builtin_ctz(em);
+                        const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long*>(lds_word(lt, b, e * W)),
+                                                       0ULL, (unsigned long long)k0);
+                        if (old == EMPTY) {
+#pragma unroll
+                            for (int w = 1; w < W; w++)
+                                __hip_atomic_store(lds_word(lt, b, e * W + w), kk[q][w], __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+                            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                            __hip_atomic_store(reinterpret_cast<uint8_t*>(tg + b) + e, (uint8_t)tag, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+                            if constexpr (W > 1) a += READY;  // the table format's published flag
+                            slot = e;
+                        } else if (W == 1 && old == k0) {
+                            slot = e;  // the same key, claimed an instant ago
+                        } else {
+                            probe++;  // claimed by another key (tag not yet stored): read again
+                            continue;
+                        }
+                    }
+                    atomicAdd(reinterpret_cast<unsigned long long*>(lds_word(lt, b, S * W + slot)),
+                              (unsigned long long)a);
+                    done = true;
+                }
+            } else if constexpr (W == 1) {
+                // branch-light probe: match / first-empty masks over the 8 slots of a bucket
+                for (int probe = 0; probe < 2 * BPR && !done;) {
+                    uint32_t eqm = 0, emm = 0;
+#pragma unroll
+                    for (int c = 0; c < 4; c++) {
+                        const uint4 v = l4[lds_chunk(b, c)];
+                        const uint64_t x0 = ((uint64_t)v.y << 32) | v.x, x1 = ((uint64_t)v.w << 32) | v.z;
+                        eqm |= (uint32_t)(x0 == k0) << (2 * c) | (uint32_t)(x1 == k0) << (2 * c + 1);
+                        emm |= (uint32_t)(x0 == 0) << (2 * c) | (uint32_t)(x1 == 0) << (2 * c + 1);
+                    }
+                    int slot = -1;
+                    if (eqm) {
+                        slot = __builtin_ctz(eqm);
+                    } else if (emm) {
+                        const int e = __builtin_ctz(emm);
+                        const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long*>(lds_word(lt, b, e)), 0ULL,
+                                                       (unsigned long long)k0);
+                        if (old == 0 || old == k0) slot = e;
+                        else { probe++; continue; }  // lost the slot to another key: re-read this bucket
+                    }
+                    if (slot >= 0) {
+                        atomicAdd(reinterpret_cast<unsigned long long*>(lds_word(lt, b, S + slot)),
+                                  (unsigned long long)add[q]);
+                        done = true;
+                    } else {
+                        b = (b + 1) & (BPR - 1);
+                        probe++;
+                    }
+                }
+            }
+            if constexpr (!KC_P3_TAGS && W > 1) {
+                // branch-light probe over a whole bucket: the count words are read first and
+                // the key words after a wait, so a READY count guarantees that the key words
+                // read after it are published (the claimer stores them before setting READY)
+                constexpr int C0 = S * W / 2;  // first 16-byte chunk holding counts
+                static_assert((S * W) % 2 == 0, "keys end on a chunk boundary");
+                for (int probe = 0; probe < 4 * BPR && !done;) {
+                    uint64_t bw[BUCKET_WORDS];
+#pragma unroll
+                    for (int c = C0; c < BUCKET_WORDS / 2; c++) {
+                        const uint4 v = l4[lds_chunk(b, c)];
+                        bw[2 * c] = ((uint64_t)v.y << 32) | v.x;
+                        bw[2 * c + 1] = ((uint64_t)v.w << 32) | v.z;
+                    }
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+                    for (int c = 0; c < C0; c++) {
+                        const uint4 v = l4[lds_chunk(b, c)];
+                        bw[2 * c] = ((uint64_t)v.y << 32) | v.x;
+                        bw[2 * c + 1] = ((uint64_t)v.w << 32) | v.z;
+                    }
+                    uint32_t eqm = 0, pend = 0, emm = 0;
+#pragma unroll
+                    for (int sl = 0; sl < S; sl++) {
+                        const bool w0eq = bw[sl * W] == k0;
+                        bool rest = true;
+#pragma unroll
+                        for (int w = 1; w < W; w++) rest &= bw[sl * W + w] == kk[q][w];
+                        const bool ready = (bw[S * W + sl] & READY) != 0;
+                        eqm |= (uint32_t)(w0eq && rest && ready) << sl;
+                        pend |= (uint32_t)(w0eq && !ready) << sl;
+                        emm |= (uint32_t)(bw[sl * W] == EMPTY) << sl;
+                    }
+                    if (eqm) {
+                        atomicAdd(reinterpret_cast<unsigned long long*>(lds_word(lt, b, S * W + __builtin_ctz(eqm))),
+                                  (unsigned long long)add[q]);
+                        done = true;
+                    } else if (pend) {
+                        probe++;  // another wave is publishing a key with this word 0: read again
+                    } else if (emm) {
+                        const int e = __builtin_ctz(emm);
+                        const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long*>(lds_word(lt, b, e * W)),
+                                                       0ULL, (unsigned long long)k0);
+                        if (old == EMPTY) {
+#pragma unroll
+                            for (int w = 1; w < W; w++)
+                                __hip_atomic_store(lds_word(lt, b, e * W + w), kk[q][w], __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+                            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                            atomicAdd(reinterpret_cast<unsigned long long*>(lds_word(lt, b, S * W + e)),
+                                      (unsigned long long)(READY + add[q]));
+                            done = true;
+                        } else {
+                            probe++;  // lost the slot: read the bucket again
+                        }
+                    } else {
+                        b = (b + 1) & (BPR - 1);  // bucket full, key absent: next bucket
+                        probe++;
+                    }
+                }
+            }
+            if (!done) n_fail++;
+        }
+        if (more) {
+            okm = nokm;
+#pragma unroll
+            for (int q = 0; q < KB; q++) {
+                add[q] = nadd[q];
+#pragma unroll
+                for (int w = 0; w < W; w++) kk[q][w] = nkk[q][w];
+            }
+        } else if (nbase < vend) {
+            load_items(nbase, kk, add, okm);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < N4; i += NT) g4[i] = l4[lds_chunk(i >> 3, i & 7)];
+    if (n_fail) atomicAdd(&ctr->overflow, (unsigned long long)n_fail);
+    if constexpr (GATE || CNT) {
+        // GATE: the gated insertions (level 1 counted the windows); CNT over runs: the
+        // records' counts (the general merge insert counted them at its level 1).  One
+        // atomic per workgroup: per-wave adds to this one counter from every region's
+        // workgroup serialise at the memory-side atomic unit (milliseconds per pass)
+        block_add4(GATE ? n_ins : (pb.seg_start ? n_add : 0), 0, 0, 0, &ctr->inserted, nullptr, nullptr, nullptr);
+    }
+}
+
+// Bloom pass 1, level 3 (blocked layout): one workgroup per filter region of `bpr`
+// blocks (64 KiB): the region -> LDS (zero-filled when the filter is fresh), the
+// reference's insertion_process for every key of the region with LDS atomics
+// (block_insert), the region back to HBM.  Replaces one scattered device-scope atomic per
+// bit (the direct pass) with two sequential sweeps of the filter per batch.
+// SEG: the region's keys are its B2 level-2 segments (fills in hist2); otherwise the
+// contiguous run [off2[r * B2], off2[(r + 1) * B2]).
+// keys per thread per round and workgroup size: 512 threads keep the insertion path within
+// its registers (72 VGPRs, no scratch spills; 1024-thread groups would be capped at 64)
+#ifndef KC_B3_KB
+#define KC_B3_KB 4
+#endif
+#ifndef KC_B3_NT
+#define KC_B3_NT 512
+#endif
+constexpr int B3_THREADS = KC_B3_NT;  // two 64 KiB regions per CU
+template <bool SEG>
+__global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView bf, uint32_t bpr, PartBufs pb,
+                                                                  DevCounters* __restrict__ ctr,
+                                                                  const unsigned long long* gate, int fresh) {
+    constexpr int NT = B3_THREADS, KB = KC_B3_KB;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ uint32_t s_pre[65];
+    if constexpr (SEG) {
+        if (ctr->part_overflow) return;
+    } else {
+        if (gated_off(gate)) return;
+    }
+    uint32_t* lf = reinterpret_cast<uint32_t*>(smem);
+    const uint64_t r = blockIdx.x;
+    uint64_t start, end;
+    if constexpr (SEG) {
+        if (threadIdx.x == 0) {
+            uint32_t acc = 0;
+            for (uint32_t j = 0; j < pb.B2; j++) {
+                s_pre[j] = acc;
+                acc += pb.hist2[r * pb.B2 + j];
+            }
+            s_pre[pb.B2] = acc;
+        }
+        __syncthreads();
+        start = 0;
+        end = s_pre[pb.B2];
+    } else {
+        start = pb.off2[r * pb.B2];
+        end = pb.off2[(r + 1) * pb.B2];
+    }
+    if (start == end) return;  // the region keeps its bits (a fresh filter is zero already)
+    const uint32_t n4 = bpr * BF_BLOCK_WORDS / 4;
+    uint4* g4 = reinterpret_cast<uint4*>(bf.bits + r * bpr * BF_BLOCK_WORDS);
+    uint4* l4 = reinterpret_cast<uint4*>(lf);
+    for (uint32_t i = threadIdx.x; i < n4; i += NT) l4[i] = fresh ? make_uint4(0, 0, 0, 0) : g4[i];
+    __syncthreads();
+    const uint64_t blk0 = r * bpr;
+    const int lane = threadIdx.x & 63;
+    uint64_t* wq = reinterpret_cast<uint64_t*>(smem + (size_t)bpr * BF_BLOCK_WORDS * 4) + (threadIdx.x >> 6) * 64;
+    BloomLocal bl = {0, 0, 0};
+    uint32_t cs = 0, cb = 0, nb = 0;  // SEG: segment cursor (indices grow monotonically)
+    if constexpr (SEG) nb = s_pre[1];
+    for (uint64_t base = start; base < end; base += (uint64_t)KB * NT) {
+        uint64_t t0[KB];
+#pragma unroll
+        for (int q = 0; q < KB; q++) {
+            const uint64_t i = base + threadIdx.x + (uint64_t)q * NT;
+            t0[q] = EMPTY;
+            if (i < end) {
+                if constexpr (SEG) {
+                    while (nb <= i) {
+                        cs++;
+                        cb = nb;
+                        nb = s_pre[cs + 1];
+                    }
+                    t0[q] = pb.keys2[(r * pb.B2 + cs) * pb.cap2 + (i - cb)];
+                } else {
+                    t0[q] = pb.keys2[i];
+                }
+            }
+        }
+        // fast path: a k-mer whose filter-2 bits are all set changes nothing (most
+        // occurrences of a k-mer seen before); the others are packed into the wave's queue
+        // so the insertion path runs on dense lanes instead of once per item slot
+        bool slow[KB];
+        uint32_t pre[KB], rank[KB], total = 0;
+#pragma unroll
+        for (int q = 0; q < KB; q++) {
+            slow[q] = base + threadIdx.x + (uint64_t)q * NT < end &&
+                      !block_gate(lf + (uint32_t)(bloom_block(t0[q], bf.nblocks) - blk0) * BF_BLOCK_WORDS + 8, t0[q],
+                                  bf.nh);
+            const uint64_t bal = __ballot(slow[q]);
+            pre[q] = total;
+            rank[q] = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+            total += (uint32_t)__popcll(bal);
+        }
+        for (uint32_t r0 = 0; r0 < total; r0 += 64) {
+#pragma unroll
+            for (int q = 0; q < KB; q++)
+                if (slow[q] && pre[q] + rank[q] - r0 < 64) wq[pre[q] + rank[q] - r0] = t0[q];
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's queue writes land
+            if (lane < total - r0) {
+                const uint64_t t = wq[lane];
+                const uint32_t lb = (uint32_t)(bloom_block(t, bf.nblocks) - blk0);
+                block_insert(lf + lb * BF_BLOCK_WORDS, t, bf.nh, bl);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // queue reads done before reuse
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n4; i += NT) g4[i] = l4[i];
+    // one atomic per counter and workgroup (per-wave adds to one address serialise)
+    block_add4(bl.new_first, bl.new_second, bl.failed, 0, &ctr->new_in_first, &ctr->new_in_second,
+               &ctr->failed_in_first, nullptr);
+}
+
+// --------------------------------------------------------------------------------
+// shard merge over region-sorted groups (kc_insert_counts_runs_device): the records a
+// rank receives are G groups (one per sender), each in the sender's table order, i.e.
+// sorted by region when the sender's table has this table's geometry.  Region run bounds
+// per group by binary search, then one level-3 pass (k_p3<W, SEG, CNT> over the runs):
+// the partition levels of the general merge insert are not needed.
+// --------------------------------------------------------------------------------
+template <int W>
+__global__ __launch_bounds__(256) void k_check_runs(const uint64_t* __restrict__ rec, const uint64_t* __restrict__ gstart,
+                                                    uint64_t R, unsigned long long* flag) {
+    const uint32_t g = blockIdx.y;
+    const uint64_t lo = gstart[g], hi = gstart[g + 1];
+    bool bad = false;
+    for (uint64_t i = lo + 1 + (uint64_t)blockIdx.x * 256 + threadIdx.x; i < hi; i += (uint64_t)gridDim.x * 256)
+        bad |= region_of(rec[i * (W + 1)], R) < region_of(rec[(i - 1) * (W + 1)], R);
+    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1ULL);
+}
+// m_start[r * G + g] = first record of group g with region >= r (r = 0..R)
+template <int W>
+__global__ __launch_bounds__(256) void k_run_bounds(const uint64_t* __restrict__ rec,
+                                                    const uint64_t* __restrict__ gstart, uint32_t G, uint64_t R,
+                                                    uint64_t* __restrict__ m_start) {
+    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= (R + 1) * G) return;
+    const uint64_t r = t / G;
+    const uint32_t g = (uint32_t)(t % G);
+    uint64_t lo = gstart[g], hi = gstart[g + 1];  // first index in [lo, hi) with region >= r
+    while (lo < hi) {
+        const uint64_t mid = lo + (hi - lo) / 2;
+        if (region_of(rec[mid * (W + 1)], R) < r) lo = mid + 1;
+        else hi = mid;
+    }
+    m_start[t] = lo;
+}
+static __global__ __launch_bounds__(256) void k_run_lengths(const uint64_t* __restrict__ m_start, uint64_t RG, uint32_t G,
+                                                     uint32_t* __restrict__ m_len) {
+    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t < RG) m_len[t] = (uint32_t)(m_start[t + G] - m_start[t]);
+}
+
+// exclusive scan of n u32 -> u64 (out has n+1 entries), three passes:
+// per-block scans of 4096 elements, a scan of the block sums, the add-back
+constexpr int SCAN_T = 1024;
+constexpr int SCAN_PER = 4;
+DEV unsigned long long block_incl_sum_1024(unsigned long long v) {
+    __shared__ unsigned long long s_w[SCAN_T / 64];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned long long o = __shfl_up(v, d, 64);
+        if (lane >= d) v += o;
+    }
+    if (lane == 63) s_w[wid] = v;
+    __syncthreads();
+    unsigned long long base = 0;
+    for (int w = 0; w < wid; w++) base += s_w[w];
+    __syncthreads();
+    return v + base;
+}
+static __global__ __launch_bounds__(SCAN_T) void k_scanA(const uint32_t* __restrict__ in, uint64_t n,
+                                                 uint64_t* __restrict__ out, uint64_t* __restrict__ bsum,
+                                                 const unsigned long long* gate) {
+    if (gated_off(gate)) return;
+    const uint64_t i0 = ((uint64_t)blockIdx.x * SCAN_T + threadIdx.x) * SCAN_PER;
+    uint32_t v[SCAN_PER];
+    unsigned long long sum = 0;
+#pragma unroll
+    for (int q = 0; q < SCAN_PER; q++) {
+        v[q] = i0 + q < n ? in[i0 + q] : 0;
+        sum += v[q];
+    }
+    const unsigned long long incl = block_incl_sum_1024(sum);
+    unsigned long long run = incl - sum;
+#pragma unroll
+    for (int q = 0; q < SCAN_PER; q++) {
+        if (i0 + q < n) out[i0 + q] = run;
+        run += v[q];
+    }
+    if (threadIdx.x == SCAN_T - 1) bsum[blockIdx.x] = incl;
+}
+static __global__ __launch_bounds__(SCAN_T) void k_scanB(uint64_t* __restrict__ bsum, uint64_t nb, uint64_t* __restrict__ out,
+                                                 uint64_t n, const unsigned long long* gate) {
+    if (gated_off(gate)) return;
+    __shared__ unsigned long long s_carry;
+    if (threadIdx.x == 0) s_carry = 0;
+    __syncthreads();
+    for (uint64_t base = 0; base < nb; base += SCAN_T) {
+        const uint64_t i = base + threadIdx.x;
+        const unsigned long long v = i < nb ? bsum[i] : 0;
+        const unsigned long long incl = block_incl_sum_1024(v);
+        const unsigned long long carry = s_carry;
+        if (i < nb) bsum[i] = carry + incl - v;
+        __syncthreads();
+        if (threadIdx.x == SCAN_T - 1) s_carry = carry + incl;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[n] = s_carry;
+}
+static __global__ __launch_bounds__(SCAN_T) void k_scanC(uint64_t* __restrict__ out, uint64_t n,
+                                                 const uint64_t* __restrict__ bsum, const unsigned long long* gate) {
+    if (gated_off(gate)) return;
+    const uint64_t i0 = ((uint64_t)blockIdx.x * SCAN_T + threadIdx.x) * SCAN_PER;
+    const uint64_t add = bsum[blockIdx.x];
+#pragma unroll
+    for (int q = 0; q < SCAN_PER; q++)
+        if (i0 + q < n) out[i0 + q] += add;
+}
+static void launch_scan(const uint32_t* in, uint64_t n, uint64_t* out, uint64_t* bsum, hipStream_t s,
+                        const unsigned long long* gate = nullptr) {
+    const uint64_t per = (uint64_t)SCAN_T * SCAN_PER;
+    const unsigned nb = (unsigned)((n + per - 1) / per);
+    hipLaunchKernelGGL(k_scanA, dim3(nb), dim3(SCAN_T), 0, s, in, n, out, bsum, gate);
+    hipLaunchKernelGGL(k_scanB, dim3(1), dim3(SCAN_T), 0, s, bsum, (uint64_t)nb, out, n, gate);
+    hipLaunchKernelGGL(k_scanC, dim3(nb), dim3(SCAN_T), 0, s, out, n, bsum, gate);
+}
+
+// --------------------------------------------------------------------------------
+// k_dump<W>: occupied slots with T(c) >= a -> records {W key words, T(c)}
+// count_mode 0: c mod 65536 (-m 0); else min(c, 16383).  out == nullptr: count only.
+// --------------------------------------------------------------------------------
+template <int W>
+__global__ __launch_bounds__(256) void k_dump(TableView tv, int count_mode, uint64_t min_abundance,
+                                              uint64_t* __restrict__ out, DevCounters* __restrict__ ctr) {
+    constexpr int S = BUCKET_WORDS / (W + 1);
+    const uint64_t bkt = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    uint32_t occ = 0, nout = 0;
+    uint64_t tv_c[S];
+    bool emit[S];
+    uint64_t bw[BUCKET_WORDS];
+    if (bkt < tv.nbuckets) load_bucket(tv.buckets + bkt * BUCKET_WORDS, bw);
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+        emit[s] = false;
+        tv_c[s] = 0;
+        if (bkt < tv.nbuckets && bw[s * W] != EMPTY) {
+            occ++;
+            const uint64_t c = bw[S * W + s] & CNT_MASK;
+            const uint64_t t = count_mode == 0 ? (c & 0xFFFF) : (c < 16383 ? c : 16383);
+            if (t >= min_abundance) { emit[s] = true; tv_c[s] = t; nout++; }
+        }
+    }
+    // output positions: one atomic per workgroup (not per wave) on the shared cursor
+    __shared__ unsigned long long s_wt[4], s_base;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t incl = wave_incl_sum(nout);
+    if (lane == 63) s_wt[wid] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long tot = s_wt[0] + s_wt[1] + s_wt[2] + s_wt[3];
+        s_base = tot ? atomicAdd(&ctr->dump_n, tot) : 0;
+    }
+    __syncthreads();
+    unsigned long long base = s_base;
+    for (int w = 0; w < wid; w++) base += s_wt[w];
+    uint64_t idx = base + incl - nout;
+#pragma unroll
+    for (int s = 0; s < S; s++)
+        if (out && emit[s]) {
+            uint64_t t[W], key[W];
+#pragma unroll
+            for (int i = 0; i < W; i++) t[i] = bw[s * W + i];
+            from_tkey<W>(t, key);
+            uint64_t* o = out + idx * (W + 1);
+#pragma unroll
+            for (int i = 0; i < W; i++) o[i] = key[i];
+            o[W] = tv_c[s];
+            idx++;
+        }
+    block_add4(occ, 0, 0, 0, &ctr->occupied, nullptr, nullptr, nullptr);
+}
+
+// --------------------------------------------------------------------------------
+// GPU output formatting: "<CANONICAL_KMER> <T(c)>\n" for every slot
+// with T(c) >= a, in table order.  Replaces the reference's single-threaded writers
+// write_kmers_on_disk_separately_even_faster (kmer_hash_table.cpp:4318-4524: chain walk,
+// int2char, "<kmer> <count>\n") and write_kmers (2013-2050).  One workgroup formats
+// TEXT_T consecutive buckets: k_text_bytes gives its byte count, the host scans them
+// into block offsets, k_text writes the block's lines into LDS and copies them out
+// contiguously at its offset (one text stream, no per-line atomics).
+// --------------------------------------------------------------------------------
+DEV uint32_t ndigits(uint32_t t) { return t >= 10000 ? 5 : t >= 1000 ? 4 : t >= 100 ? 3 : t >= 10 ? 2 : 1; }
+
+// T(c) of each emitted slot (0 = no line: a >= 1 so an emitted T(c) is >= 1); returns
+// the bucket's text bytes
+template <int W, int S = BUCKET_WORDS / (W + 1)>
+DEV uint32_t text_bucket(const TableView& tv, uint64_t bkt, int count_mode, uint64_t a, int k,
+                         uint64_t (&bw)[BUCKET_WORDS], uint32_t (&tc)[S]) {
+    uint32_t bytes = 0;
+    if (bkt < tv.nbuckets) load_bucket(tv.buckets + bkt * BUCKET_WORDS, bw);
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+        tc[s] = 0;
+        if (bkt < tv.nbuckets && bw[s * W] != EMPTY) {
+            const uint64_t c = bw[S * W + s] & CNT_MASK;
+            const uint64_t t = count_mode == 0 ? (c & 0xFFFF) : (c < 16383 ? c : 16383);
+            if (t >= a) {
+                tc[s] = (uint32_t)t;
+                bytes += (uint32_t)k + 2 + ndigits((uint32_t)t);
+            }
+        }
+    }
+    return bytes;
+}
+
+template <int NT>
+DEV uint32_t block_excl_sum(uint32_t v, uint32_t* s_w, uint32_t& total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t incl = wave_incl_sum(v);
+    if (lane == 63) s_w[wid] = incl;
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; w++) {
+        const uint32_t x = s_w[w];
+        base += w < wid ? x : 0;
+        tot += x;
+    }
+    total = tot;
+    return base + incl - v;
+}
+
+template <int W>
+__global__ __launch_bounds__(TEXT_T) void k_text_bytes(TableView tv, int count_mode, uint64_t a, int k,
+                                                       uint32_t* __restrict__ block_bytes) {
+    constexpr int S = BUCKET_WORDS / (W + 1);
+    __shared__ uint32_t s_w[TEXT_T / 64];
+    uint64_t bw[BUCKET_WORDS];
+    uint32_t tc[S];
+    const uint32_t v = text_bucket<W>(tv, (uint64_t)blockIdx.x * TEXT_T + threadIdx.x, count_mode, a, k, bw, tc);
+    uint32_t total;
+    block_excl_sum<TEXT_T>(v, s_w, total);
+    if (threadIdx.x == 0) block_bytes[blockIdx.x] = total;
+}
+
+// blocks [blk0, blk0 + grid) write at out + off[b] - base; dynamic LDS >= the largest
+// block's bytes
+template <int W>
+__global__ __launch_bounds__(TEXT_T) void k_text(TableView tv, int count_mode, uint64_t a, int k, uint64_t blk0,
+                                                 const uint64_t* __restrict__ off, uint64_t base,
+                                                 uint8_t* __restrict__ out) {
+    constexpr int S = BUCKET_WORDS / (W + 1);
+    extern __shared__ uint8_t s_txt[];
+    __shared__ uint32_t s_w[TEXT_T / 64];
+    const uint64_t b = blk0 + blockIdx.x;
+    uint64_t bw[BUCKET_WORDS];
+    uint32_t tc[S];
+    const uint32_t v = text_bucket<W>(tv, b * TEXT_T + threadIdx.x, count_mode, a, k, bw, tc);
+    uint32_t total;
+    uint32_t pos = block_excl_sum<TEXT_T>(v, s_w, total);
+    const int c0 = k - 32 * (W - 1);  // characters in key word 0 (the others hold 32)
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+        if (!tc[s]) continue;
+        uint64_t t[W], key[W];
+#pragma unroll
+        for (int i = 0; i < W; i++) t[i] = bw[s * W + i];
+        from_tkey<W>(t, key);
+        uint8_t* p = s_txt + pos;
+#pragma unroll
+        for (int w = 0; w < W; w++) {
+            const int nc = w == 0 ? c0 : 32;
+            const uint64_t x = key[w];
+            for (int q = nc - 1; q >= 0; q--) *p++ = (uint8_t)(0x54474341u >> (8 * ((x >> (2 * q)) & 3)));
+        }
+        *p++ = ' ';
+        uint32_t cnt = tc[s];
+        const uint32_t nd = ndigits(cnt);
+        for (int d = (int)nd - 1; d >= 0; d--) {
+            p[d] = (uint8_t)('0' + cnt % 10);
+            cnt /= 10;
+        }
+        p[nd] = '\n';
+        pos += (uint32_t)k + 2 + nd;
+    }
+    __syncthreads();
+    uint8_t* o = out + (off[b] - base);
+    // copy out: byte head up to a 4-byte boundary of the destination, then dwords
+    const uint32_t head = (uint32_t)((4 - ((uintptr_t)o & 3)) & 3) < total ? (uint32_t)((4 - ((uintptr_t)o & 3)) & 3)
+                                                                            : total;
+    if (threadIdx.x < head) o[threadIdx.x] = s_txt[threadIdx.x];
+    const uint32_t nw = (total - head) / 4;
+    uint32_t* o4 = reinterpret_cast<uint32_t*>(o + head);
+    for (uint32_t i = threadIdx.x; i < nw; i += TEXT_T) {
+        const uint8_t* q = s_txt + head + 4 * i;
+        o4[i] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+    }
+    const uint32_t tail0 = head + 4 * nw;
+    if (tail0 + threadIdx.x < total) o[tail0 + threadIdx.x] = s_txt[tail0 + threadIdx.x];
+}
+
+// ================================================================================
+// launchers: templates over the key width W.  This file is compiled once per W
+// (kc_count_w.hip with -DKC_W=1..8, the translation units build in parallel); the
+// W-dispatch of the C ABI's launch_* entry points is kc_count.hip.
+// ================================================================================
+static uint64_t pow5_mod54(int e) {
+    uint64_t r = 1;
+    for (int i = 0; i < e; i++) r = (r * 5) & M54;
+    return r;
+}
+
+template <int W>
+static hipError_t launch_count_w(PackedView sym, uint64_t sym_bound, int k, int mode, TableView t, BloomView bf,
+                                 DevCounters* ctr, hipStream_t s) {
+    const unsigned grid = (unsigned)((sym_bound + tile_win<W>() - 1) / tile_win<W>());
+    const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
+    if (grid == 0) return hipSuccess;
+    if (mode == 0)
+        hipLaunchKernelGGL((k_count<W, 0>), dim3(grid), dim3(COUNT_THREADS), 0, s, sym, k, t, bf, ctr, pk, pkm1);
+    else if (mode == 1)
+        hipLaunchKernelGGL((k_count<W, 1>), dim3(grid), dim3(COUNT_THREADS), 0, s, sym, k, t, bf, ctr, pk, pkm1);
+    else
+        hipLaunchKernelGGL((k_count<W, 2>), dim3(grid), dim3(COUNT_THREADS), 0, s, sym, k, t, bf, ctr, pk, pkm1);
+    return hipGetLastError();
+}
+
+template <class K>
+static hipError_t set_smem(K kernel, size_t bytes) {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)bytes);
+}
+
+static BinRegion coarse_bins(const TableView& t) { return BinRegion{t.R, t.f2bits, 0, 1}; }
+
+template <int W, bool SEG, bool CNT = false, bool GATE = false>
+static hipError_t launch_p3(TableView t, DevCounters* ctr, PartBufs pb, const unsigned long long* gate, int fresh,
+                            hipStream_t s, BloomView bf = BloomView{}) {
+    size_t sm3 = (size_t)BPR * BUCKET_WORDS * 8 + (KC_P3_TAGS ? (size_t)BPR * 8 : 0);
+    if (GATE) {
+        // the filter-2 slice goes to LDS if two workgroups still fit a CU (80 KiB each)
+        const uint64_t maxb = bf.nblocks / t.R + 2;
+        const size_t room = 80 * 1024 - sm3 - 1024;  // (static LDS: segment prefix, block sums)
+        bf.slice_blocks = maxb * 32 <= room ? (uint32_t)maxb : 0;
+        sm3 += (size_t)bf.slice_blocks * 32;
+    }
+    auto p3 = k_p3<W, SEG, CNT, GATE>;
+    hipError_t e = set_smem(p3, sm3);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(p3, dim3((unsigned)t.R), dim3(P3_THREADS), sm3, s, t, pb, ctr, gate, fresh, bf);
+    return hipGetLastError();
+}
+
+// level 2 on the exact layout (after an exact level 1): items of IW words; `gate` as in k_p1
+template <int IW>
+static hipError_t part_level2_exact(TableView t, PartBufs pb, hipStream_t s, const unsigned long long* gate) {
+    const size_t sm2 = part_smem<IW>(t.F2), sm2h = hist_smem(t.F2);
+    hipError_t e;
+    if ((e = set_smem(k_p2<IW, false>, sm2h)) != hipSuccess) return e;
+    if ((e = set_smem(k_p2<IW, true>, sm2)) != hipSuccess) return e;
+    hipLaunchKernelGGL((k_p2<IW, false>), dim3(t.F1 * pb.B2), dim3(COUNT_THREADS), sm2h, s, t, pb, gate);
+    launch_scan(pb.hist2, t.R * pb.B2, pb.off2, pb.bsum, s, gate);
+    hipLaunchKernelGGL((k_p2<IW, true>), dim3(t.F1 * pb.B2), dim3(COUNT_THREADS), sm2, s, t, pb, gate);
+    return hipGetLastError();
+}
+
+// levels 2 and 3 on the exact layout (after an exact level 1); `gate` as in k_p1.
+// CNT: the items are {W key words, count} records (W + 1 words each).  GATE: Bloom gate
+// at level 3 (bf).
+template <int W, bool CNT = false, bool GATE = false>
+static hipError_t part_levels23(TableView t, DevCounters* ctr, PartBufs pb, hipStream_t s,
+                                const unsigned long long* gate = nullptr, int fresh = 0, BloomView bf = BloomView{}) {
+    hipError_t e = part_level2_exact<CNT ? W + 1 : W>(t, pb, s, gate);
+    if (e != hipSuccess) return e;
+    return launch_p3<W, false, CNT, GATE>(t, ctr, pb, gate, fresh, s, bf);
+}
+
+template <bool SEG>
+static hipError_t launch_b3(BloomView bf, TableView ft, DevCounters* ctr, PartBufs pb, const unsigned long long* gate,
+                            int fresh, hipStream_t s) {
+    const uint32_t bpr = (uint32_t)(bf.nblocks / ft.R);
+    const size_t sm = (size_t)bpr * BF_BLOCK_WORDS * 4 + (size_t)(B3_THREADS / 64) * 64 * 8;  // + wave queues
+    hipError_t e = set_smem(k_b3<SEG>, sm);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_b3<SEG>, dim3((unsigned)ft.R), dim3(B3_THREADS), sm, s, bf, bpr, pb, ctr, gate, fresh);
+    return hipGetLastError();
+}
+
+// level 1 from the symbol stream, exact layout: windows -> F bins by `bin`, keys into `out`
+template <int W, int MODE, class Bin>
+static hipError_t part_level1(PackedView sym, int k, BloomView bf, DevCounters* ctr, PartBufs pb, uint32_t F,
+                              Bin bin, uint64_t* out, hipStream_t s, const unsigned long long* gate = nullptr) {
+    const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
+    const size_t sm1 = part_smem<p1_out_words(W, MODE)>(F), sm1h = hist_smem(F);
+    hipError_t e;
+    auto kh = k_p1<W, MODE, false, Bin, OutExact>;
+    auto ks = k_p1<W, MODE, true, Bin, OutExact>;
+    if ((e = set_smem(kh, sm1h)) != hipSuccess) return e;
+    if ((e = set_smem(ks, sm1)) != hipSuccess) return e;
+    // a gated launch is the fallback of a segmented batch, whose windows are counted
+    const int count = gate ? 0 : 1;
+    hipLaunchKernelGGL(kh, dim3(pb.nblk1), dim3(COUNT_THREADS), sm1h, s, sym, k, bf, ctr, pb, F, bin, out, pk, pkm1,
+                       OutExact{}, gate, count);
+    launch_scan(pb.hist1, (uint64_t)F * pb.nblk1, pb.off1, pb.bsum, s, gate);
+    hipLaunchKernelGGL(ks, dim3(pb.nblk1), dim3(COUNT_THREADS), sm1, s, sym, k, bf, ctr, pb, F, bin, out, pk, pkm1,
+                       OutExact{}, gate, 0);
+    return hipGetLastError();
+}
+
+// Segmented pipeline (pb.cap1 != 0): p1 -> p2f -> p3<SEG>, each a single pass; then
+// the exact pipeline behind the overflow gate (its kernels return at once unless a
+// segment overflowed, in which case the segmented p3 left the table untouched).
+template <int W, int MODE>
+static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf, DevCounters* ctr, PartBufs pb,
+                                int fresh, hipStream_t s) {
+    constexpr bool GATE3 = MODE == 4;
+    if (pb.cap1 == 0) {
+        hipError_t e = part_level1<W, MODE>(sym, k, bf, ctr, pb, t.F1, coarse_bins(t), pb.keys1, s);
+        if (e != hipSuccess) return e;
+        return part_levels23<W, false, GATE3>(t, ctr, pb, s, nullptr, fresh, bf);
+    }
+    hipError_t e;
+    const unsigned long long* gate = &ctr->part_overflow;
+    if ((e = hipMemsetAsync(&ctr->part_overflow, 0, sizeof(ctr->part_overflow), s)) != hipSuccess) return e;
+    const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
+    auto k1 = k_p1<W, MODE, true, BinRegion, OutSeg, scatter_threads<W>()>;
+    static const uint32_t p2f_pad = [] {  // A/B knob: reserve LDS as if for this many segments
+        const char* v = std::getenv("KC_P2F_SEGS");
+        return v ? (uint32_t)std::atoi(v) : 0u;
+    }();
+    const size_t sm1 = part_smem<W, scatter_threads<W>()>(t.F1),
+                 sm2 = p2f_smem<W, p2f_threads<W>()>(t.F2, std::max<uint32_t>(p2f_pad, (pb.nblk1 + pb.B2 - 1) / pb.B2));
+    if ((e = set_smem(k1, sm1)) != hipSuccess) return e;
+    if ((e = set_smem(k_p2f<W, p2f_threads<W>()>, sm2)) != hipSuccess) return e;
+    const OutSeg o1{(uint64_t)pb.nblk1 * pb.cap1, 0, pb.cap1};
+    hipLaunchKernelGGL(k1, dim3(pb.nblk1), dim3(scatter_threads<W>()), sm1, s, sym, k, bf, ctr, pb, t.F1, coarse_bins(t),
+                       pb.keys1, pk, pkm1, o1, (const unsigned long long*)nullptr, 1);
+    hipLaunchKernelGGL((k_p2f<W, p2f_threads<W>()>), dim3(t.F1 * pb.B2), dim3(p2f_threads<W>()), sm2, s, t, pb, ctr);
+    if ((e = launch_p3<W, true, false, GATE3>(t, ctr, pb, nullptr, fresh, s, bf)) != hipSuccess) return e;
+    if ((e = part_level1<W, MODE>(sym, k, bf, ctr, pb, t.F1, coarse_bins(t), pb.keys1, s, gate)) != hipSuccess)
+        return e;
+    return part_levels23<W, false, GATE3>(t, ctr, pb, s, gate, fresh, bf);
+}
+
+// mode 2 (counting behind the Bloom gate): blocked layout -> gate at level 3 (MODE 4),
+// reference layout -> gate on the rolled root at level 1 (MODE 2)
+template <int W>
+static hipError_t count_part_w(PackedView sym, int k, int mode, TableView t, BloomView bf, DevCounters* ctr,
+                               PartBufs pb, int fresh, hipStream_t s) {
+    if (mode != 2) return launch_part_w<W, 0>(sym, k, t, bf, ctr, pb, fresh, s);
+    if (bf.blocked) return launch_part_w<W, 4>(sym, k, t, bf, ctr, pb, fresh, s);
+    return launch_part_w<W, 2>(sym, k, t, bf, ctr, pb, fresh, s);
+}
+// Bloom pass 1 on the blocked layout, partitioned: windows -> table key word 0 -> coarse
+// bins -> filter regions (ft: R = filter regions, F1 x F2) -> k_b3 (LDS-resident filter
+// regions).  Segmented single passes with the exact pipeline behind the overflow gate,
+// as for the table.
+template <int W>
+static hipError_t bloom_part_w(PackedView sym, int k, BloomView bf, TableView ft, DevCounters* ctr, PartBufs pb,
+                               int fresh, hipStream_t s) {
+    if (pb.cap1 == 0) {
+        hipError_t e = part_level1<W, 3>(sym, k, bf, ctr, pb, ft.F1, coarse_bins(ft), pb.keys1, s);
+        if (e != hipSuccess) return e;
+        if ((e = part_level2_exact<1>(ft, pb, s, nullptr)) != hipSuccess) return e;
+        return launch_b3<false>(bf, ft, ctr, pb, nullptr, fresh, s);
+    }
+    hipError_t e;
+    const unsigned long long* gate = &ctr->part_overflow;
+    if ((e = hipMemsetAsync(&ctr->part_overflow, 0, sizeof(ctr->part_overflow), s)) != hipSuccess) return e;
+    const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
+    constexpr int NT = scatter_threads<W>(), NT2 = p2f_threads<1>();
+    auto k1 = k_p1<W, 3, true, BinRegion, OutSeg, NT>;
+    const size_t sm1 = part_smem<1, NT>(ft.F1), sm2 = p2f_smem<1, NT2>(ft.F2, (pb.nblk1 + pb.B2 - 1) / pb.B2);
+    if ((e = set_smem(k1, sm1)) != hipSuccess) return e;
+    if ((e = set_smem(k_p2f<1, NT2>, sm2)) != hipSuccess) return e;
+    const OutSeg o1{(uint64_t)pb.nblk1 * pb.cap1, 0, pb.cap1};
+    hipLaunchKernelGGL(k1, dim3(pb.nblk1), dim3(NT), sm1, s, sym, k, bf, ctr, pb, ft.F1, coarse_bins(ft), pb.keys1, pk,
+                       pkm1, o1, (const unsigned long long*)nullptr, 1);
+    hipLaunchKernelGGL((k_p2f<1, NT2>), dim3(ft.F1 * pb.B2), dim3(NT2), sm2, s, ft, pb, ctr);
+    if ((e = launch_b3<true>(bf, ft, ctr, pb, nullptr, fresh, s)) != hipSuccess) return e;
+    if ((e = part_level1<W, 3>(sym, k, bf, ctr, pb, ft.F1, coarse_bins(ft), pb.keys1, s, gate)) != hipSuccess)
+        return e;
+    if ((e = part_level2_exact<1>(ft, pb, s, gate)) != hipSuccess) return e;
+    return launch_b3<false>(bf, ft, ctr, pb, gate, fresh, s);
+}
+// Routing for hash-prefix sharding: windows -> table keys grouped by owner shard into
+// `out`; per-owner offsets in pb.off1 ([owner][block], exclusive, last entry = total).
+template <int W>
+static hipError_t route_w(PackedView sym, int k, DevCounters* ctr, PartBufs pb, uint32_t parts, uint64_t* out,
+                          hipStream_t s) {
+    return part_level1<W, 0>(sym, k, BloomView{}, ctr, pb, parts, BinOwner{parts}, out, s);
+}
+// Insert an array of table keys (e.g. received from other shards), or, CNT, of
+// {W key words, count} records (shard merge), partitioned through the exact pipeline.
+template <int W, bool CNT>
+static hipError_t insert_items_part(const uint64_t* items, uint64_t n, TableView t, DevCounters* ctr, PartBufs pb,
+                                    int fresh, hipStream_t s) {
+    constexpr int IW = CNT ? W + 1 : W;
+    const BinRegion bin = coarse_bins(t);
+    const size_t sm1 = part_smem<IW>(t.F1), sm1h = hist_smem(t.F1);
+    hipError_t e;
+    if ((e = set_smem(k_p1k<IW, false>, sm1h)) != hipSuccess) return e;
+    if ((e = set_smem(k_p1k<IW, true>, sm1)) != hipSuccess) return e;
+    const int cw = CNT ? W : -1;
+    hipLaunchKernelGGL((k_p1k<IW, false>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1h, s, items, n, pb, t.F1, bin, ctr,
+                       cw);
+    launch_scan(pb.hist1, (uint64_t)t.F1 * pb.nblk1, pb.off1, pb.bsum, s);
+    hipLaunchKernelGGL((k_p1k<IW, true>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1, s, items, n, pb, t.F1, bin, ctr,
+                       cw);
+    return part_levels23<W, CNT>(t, ctr, pb, s, nullptr, fresh);
+}
+
+template <int W>
+static hipError_t insert_keys_w(const uint64_t* keys, uint64_t n, bool partitioned, TableView t, DevCounters* ctr,
+                                PartBufs pb, int fresh, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    if (!partitioned) {
+        hipLaunchKernelGGL((k_insert_keys<W>), dim3((unsigned)((n + COUNT_THREADS - 1) / COUNT_THREADS)),
+                           dim3(COUNT_THREADS), 0, s, keys, n, t, ctr);
+        return hipGetLastError();
+    }
+    return insert_items_part<W, false>(keys, n, t, ctr, pb, fresh, s);
+}
+template <int W>
+static hipError_t text_w(TableView t, int count_mode, uint64_t a, int k, uint64_t blk0, uint64_t nblk,
+                         const uint64_t* off, uint64_t base, uint8_t* out, size_t lds, hipStream_t s) {
+    auto kern = k_text<W>;
+    hipError_t e = set_smem(kern, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(TEXT_T), lds, s, t, count_mode, a, k, blk0, off, base, out);
+    return hipGetLastError();
+}
+
+template <int W>
+static hipError_t insert_runs_w(const uint64_t* rec, const uint64_t* gstart, uint32_t G, TableView t,
+                                DevCounters* ctr, uint32_t* m_len, uint64_t* m_start, int fresh, hipStream_t s) {
+    const uint64_t nb = (t.R + 1) * G;
+    hipLaunchKernelGGL(k_run_bounds<W>, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, rec, gstart, G, t.R,
+                       m_start);
+    hipLaunchKernelGGL(k_run_lengths, dim3((unsigned)((t.R * G + 255) / 256)), dim3(256), 0, s, m_start, t.R * G, G,
+                       m_len);
+    PartBufs pb{};
+    pb.B2 = G;
+    pb.hist2 = m_len;
+    pb.keys2 = const_cast<uint64_t*>(rec);
+    pb.seg_start = m_start;
+    return launch_p3<W, true, true>(t, ctr, pb, nullptr, fresh, s);
+}
+// ---- the W-specific entry points (declared in kc_internal.h, dispatched by kc_count.hip) ----
+template <int W>
+hipError_t WOps<W>::count(PackedView sym, uint64_t sym_bound, int k, int mode, TableView t, BloomView bf,
+                          DevCounters* ctr, hipStream_t s) {
+    return launch_count_w<W>(sym, sym_bound, k, mode, t, bf, ctr, s);
+}
+
+template <int W>
+hipError_t WOps<W>::count_partitioned(PackedView sym, int k, int mode, TableView t, BloomView bf, DevCounters* ctr,
+                                      PartBufs pb, int fresh, hipStream_t s) {
+    return count_part_w<W>(sym, k, mode, t, bf, ctr, pb, fresh, s);
+}
+
+template <int W>
+hipError_t WOps<W>::bloom_partitioned(PackedView sym, int k, BloomView bf, TableView ft, DevCounters* ctr,
+                                      PartBufs pb, int fresh, hipStream_t s) {
+    return bloom_part_w<W>(sym, k, bf, ft, ctr, pb, fresh, s);
+}
+
+template <int W>
+hipError_t WOps<W>::route(PackedView sym, int k, DevCounters* ctr, PartBufs pb, uint32_t parts, uint64_t* out,
+                          hipStream_t s) {
+    return route_w<W>(sym, k, ctr, pb, parts, out, s);
+}
+
+template <int W>
+hipError_t WOps<W>::insert_keys(const uint64_t* keys, uint64_t n, bool partitioned, TableView t, DevCounters* ctr,
+                                PartBufs pb, int fresh, hipStream_t s) {
+    return insert_keys_w<W>(keys, n, partitioned, t, ctr, pb, fresh, s);
+}
+
+template <int W>
+hipError_t WOps<W>::route_table(TableView t, uint32_t parts, uint32_t* hist, uint64_t* off, uint64_t* bsum,
+                                uint64_t* out, hipStream_t s) {
+    const unsigned nblk = (unsigned)((t.nbuckets + 255) / 256);
+    if (!out) {
+        hipLaunchKernelGGL((k_route_table<W, false>), dim3(nblk), dim3(256), 0, s, t, parts, hist, off, out);
+        launch_scan(hist, (uint64_t)parts * nblk, off, bsum, s);
+    } else {
+        hipLaunchKernelGGL((k_route_table<W, true>), dim3(nblk), dim3(256), 0, s, t, parts, hist, off, out);
+    }
+    return hipGetLastError();
+}
+
+template <int W>
+hipError_t WOps<W>::insert_counts(const uint64_t* rec, uint64_t n, bool partitioned, TableView t, DevCounters* ctr,
+                                  PartBufs pb, int fresh, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    if (partitioned) return insert_items_part<W, true>(rec, n, t, ctr, pb, fresh, s);
+    const dim3 grid((unsigned)((n + COUNT_THREADS - 1) / COUNT_THREADS));
+    hipLaunchKernelGGL(k_insert_counts<W>, grid, dim3(COUNT_THREADS), 0, s, rec, n, t, ctr);
+    return hipGetLastError();
+}
+
+template <int W>
+hipError_t WOps<W>::check_runs(const uint64_t* rec, const uint64_t* gstart, uint32_t G, uint64_t maxn, TableView t,
+                               unsigned long long* flag, hipStream_t s) {
+    const dim3 grid((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(1024, (maxn + 255) / 256)), G);
+    hipLaunchKernelGGL(k_check_runs<W>, grid, dim3(256), 0, s, rec, gstart, t.R, flag);
+    return hipGetLastError();
+}
+
+template <int W>
+hipError_t WOps<W>::insert_counts_runs(const uint64_t* rec, const uint64_t* gstart, uint32_t G, TableView t,
+                                       DevCounters* ctr, uint32_t* m_len, uint64_t* m_start, int fresh, hipStream_t s) {
+    return insert_runs_w<W>(rec, gstart, G, t, ctr, m_len, m_start, fresh, s);
+}
+
+template <int W>
+hipError_t WOps<W>::dump(TableView t, int count_mode, uint64_t min_abundance, uint64_t* out, DevCounters* ctr,
+                         hipStream_t s) {
+    const unsigned grid = (unsigned)((t.nbuckets + 255) / 256);
+    hipLaunchKernelGGL(k_dump<W>, dim3(grid), dim3(256), 0, s, t, count_mode, min_abundance, out, ctr);
+    return hipGetLastError();
+}
+
+template <int W>
+hipError_t WOps<W>::text_bytes(TableView t, int count_mode, uint64_t a, int k, uint32_t* block_bytes, uint64_t* off,
+                               uint64_t* bsum, hipStream_t s) {
+    const uint64_t nblk = (t.nbuckets + TEXT_T - 1) / TEXT_T;
+    hipLaunchKernelGGL(k_text_bytes<W>, dim3((unsigned)nblk), dim3(TEXT_T), 0, s, t, count_mode, a, k, block_bytes);
+    launch_scan(block_bytes, nblk, off, bsum, s);
+    return hipGetLastError();
+}
+
+template <int W>
+hipError_t WOps<W>::text(TableView t, int count_mode, uint64_t a, int k, uint64_t blk0, uint64_t nblk,
+                         const uint64_t* off, uint64_t base, uint8_t* out, size_t lds, hipStream_t s) {
+    return text_w<W>(t, count_mode, a, k, blk0, nblk, off, base, out, lds, s);
+}
+
+}  // namespace kc

@@ -23,6 +23,8 @@ constexpr uint64_t CNT_MASK = READY - 1;
 constexpr int TEXT_T = 256;                // buckets per workgroup of the text formatter
 constexpr int MAX_NH = 10;                 // -f >= 0.001  =>  ceil(-ln f / ln 2) <= 10
 constexpr uint8_t SYM_BREAK = 4;
+constexpr int BF_BLOCKS_PER_REGION = 1024; // Bloom blocks (64 B) per LDS-resident filter region: 64 KiB
+constexpr uint32_t RT_MAX_PARTS = 64;      // shards of the table routing (LDS per-owner counters)
 
 // symbol-stream code for byte b outside a header (functions_strings.cpp:56-70)
 enum Fmt { FMT_FASTA = 0, FMT_FASTQ = 1, FMT_PLAIN = 2 };
@@ -114,8 +116,23 @@ struct BloomView {
                             // (blocks; 0 = the gate reads HBM)
 };
 
+constexpr int MAX_K = 255;     // largest k: eight key words (KCO_MAXW of the oracle)
+constexpr int MAX_W = 8;
 inline int words_for_k(int k) { return k / 32 + 1; }          // spare top bit for EMPTY
 inline int slots_per_bucket(int W) { return BUCKET_WORDS / (W + 1); }
+
+// Windows rolled per thread in the partitioned kernels, and the workgroup size of the
+// segmented level 1 (tile = threads x windows), by key width: wide keys take fewer
+// windows per thread and smaller groups so that the registers and the LDS tile fit.
+#ifndef KC_RUNW_WIDE
+#define KC_RUNW_WIDE 8  // windows per thread for keys of three or four words (A/B knob)
+#endif
+#ifndef KC_SCATTER_NT12
+#define KC_SCATTER_NT12 512
+#endif
+constexpr int run_width(int W) { return W == 1 ? 16 : W == 2 ? 8 : W <= 4 ? KC_RUNW_WIDE : 4; }
+constexpr int scatter_threads_w(int W) { return W <= 2 ? KC_SCATTER_NT12 : W <= 4 ? 512 : 256; }
+constexpr int p1_tile(int W) { return scatter_threads_w(W) * run_width(W); }  // windows per segmented level-1 tile
 
 // ---- launchers (kc_tokenize.hip, kc_count.hip) -------------------------------------------------
 // src: bytes the chunk descriptors' src_off point into (host stage or device image)
@@ -135,8 +152,6 @@ hipError_t launch_count_partitioned(PackedView sv, uint64_t sym_bound, int k, in
 // fresh: the filter is all zero (level 3 does not read it)
 hipError_t launch_bloom_partitioned(PackedView sv, int k, int W, BloomView bf, TableView ft, DevCounters* ctr,
                                     PartBufs pb, int fresh, hipStream_t s);
-int run_width(int W);  // windows rolled per thread in the partitioned kernels
-int p1_tile(int W);    // windows per tile of the segmented level-1 kernel
 // hash-prefix sharding: windows -> table keys grouped by owner (offsets in pb.off1)
 hipError_t launch_route(PackedView sym, int k, int W, DevCounters* ctr, PartBufs pb, uint32_t parts, uint64_t* out,
                         hipStream_t s);
@@ -167,7 +182,45 @@ hipError_t launch_text_bytes(TableView t, int count_mode, uint64_t a, int k, uin
                              uint64_t* bsum, hipStream_t s);
 hipError_t launch_text(TableView t, int count_mode, uint64_t a, int k, uint64_t blk0, uint64_t nblk,
                        const uint64_t* off, uint64_t base, uint8_t* out, size_t lds, hipStream_t s);
+hipError_t launch_xxh64(const uint64_t* v, const uint64_t* seed, uint64_t n, uint64_t* out, hipStream_t s);
 hipError_t launch_synth(uint8_t* dst, uint64_t first_read, uint64_t n_reads, uint64_t seed, uint64_t genome_len,
                         uint32_t read_len, uint32_t wrap, double err_rate, double n_rate, hipStream_t s);
+
+// ---- per-key-width entry points (kc_count_impl.h, one translation unit per W) ------------------
+template <int W>
+struct WOps {
+    static hipError_t count(PackedView sym, uint64_t sym_bound, int k, int mode, TableView t, BloomView bf,
+                            DevCounters* ctr, hipStream_t s);
+    static hipError_t count_partitioned(PackedView sym, int k, int mode, TableView t, BloomView bf, DevCounters* ctr,
+                                        PartBufs pb, int fresh, hipStream_t s);
+    static hipError_t bloom_partitioned(PackedView sym, int k, BloomView bf, TableView ft, DevCounters* ctr, PartBufs pb,
+                                        int fresh, hipStream_t s);
+    static hipError_t route(PackedView sym, int k, DevCounters* ctr, PartBufs pb, uint32_t parts, uint64_t* out,
+                            hipStream_t s);
+    static hipError_t insert_keys(const uint64_t* keys, uint64_t n, bool partitioned, TableView t, DevCounters* ctr,
+                                  PartBufs pb, int fresh, hipStream_t s);
+    static hipError_t route_table(TableView t, uint32_t parts, uint32_t* hist, uint64_t* off, uint64_t* bsum,
+                                  uint64_t* out, hipStream_t s);
+    static hipError_t insert_counts(const uint64_t* rec, uint64_t n, bool partitioned, TableView t, DevCounters* ctr,
+                                    PartBufs pb, int fresh, hipStream_t s);
+    static hipError_t check_runs(const uint64_t* rec, const uint64_t* gstart, uint32_t G, uint64_t maxn, TableView t,
+                                 unsigned long long* flag, hipStream_t s);
+    static hipError_t insert_counts_runs(const uint64_t* rec, const uint64_t* gstart, uint32_t G, TableView t,
+                                         DevCounters* ctr, uint32_t* m_len, uint64_t* m_start, int fresh, hipStream_t s);
+    static hipError_t dump(TableView t, int count_mode, uint64_t min_abundance, uint64_t* out, DevCounters* ctr,
+                           hipStream_t s);
+    static hipError_t text_bytes(TableView t, int count_mode, uint64_t a, int k, uint32_t* block_bytes, uint64_t* off,
+                                 uint64_t* bsum, hipStream_t s);
+    static hipError_t text(TableView t, int count_mode, uint64_t a, int k, uint64_t blk0, uint64_t nblk,
+                           const uint64_t* off, uint64_t base, uint8_t* out, size_t lds, hipStream_t s);
+};
+extern template struct WOps<1>;
+extern template struct WOps<2>;
+extern template struct WOps<3>;
+extern template struct WOps<4>;
+extern template struct WOps<5>;
+extern template struct WOps<6>;
+extern template struct WOps<7>;
+extern template struct WOps<8>;
 
 }  // namespace kc

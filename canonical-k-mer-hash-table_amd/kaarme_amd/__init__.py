@@ -46,6 +46,7 @@ EXPORTS = (
     "kc_write", "kc_key_words", "kc_free", "kc_plan_chunks", "kc_synth_bytes", "kc_synth_device",
     "kc_reset", "kc_profile", "kc_get_timing", "kc_route_device", "kc_insert_keys_device",
     "kc_route_table_device", "kc_insert_counts_device", "kc_clear_table", "kc_insert_counts_runs_device",
+    "kc_xxh64", "kc_bloom_info", "kc_bloom_read", "kc_bloom_write",
 )
 
 
@@ -135,6 +136,11 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "kc_get_timing": (I32, [P, ctypes.POINTER(kc_timing)]),
         "kc_synth_device": (I32, [P, U64, U64, U64, U64, ctypes.c_uint32, ctypes.c_uint32,
                                   ctypes.c_double, ctypes.c_double, P]),
+        "kc_xxh64": (I32, [P, P, U64, P]),
+        "kc_bloom_info": (I32, [P, ctypes.POINTER(U64), ctypes.POINTER(U64), ctypes.POINTER(I32),
+                                ctypes.POINTER(I32), ctypes.POINTER(I32)]),
+        "kc_bloom_read": (I32, [P, P, U64]),
+        "kc_bloom_write": (I32, [P, P, U64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -144,8 +150,24 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     return lib
 
 
+MAX_K = 255  # include/kc_api.h KC_MAX_K
+
+
 def words_for_k(k: int) -> int:
     return k // 32 + 1
+
+
+def xxh64_device(values: Sequence[int], seeds: Sequence[int]) -> List[int]:
+    """XXH64(&v, 8, seed) of each pair by the device function of the reference-layout
+    Bloom passes (kc_xxh64 test hook)."""
+    lib = load_library()
+    v = np.ascontiguousarray(values, dtype=np.uint64)
+    sd = np.ascontiguousarray(seeds, dtype=np.uint64)
+    out = np.zeros(v.size, dtype=np.uint64)
+    rc = lib.kc_xxh64(v.ctypes.data, sd.ctypes.data, v.size, out.ctypes.data)
+    if rc:
+        raise KcError(rc, "kc_xxh64")
+    return [int(x) for x in out]
 
 
 def detect_format(path: str, first_byte: int) -> int:
@@ -307,6 +329,25 @@ class KmerCounter:
 
     def key_words(self) -> int:
         return self.lib.kc_key_words(self._ctx)
+
+    # -- Bloom filter test hooks (kc_bloom_info / kc_bloom_read / kc_bloom_write)
+    def bloom_info(self) -> dict:
+        nw, bits = ctypes.c_uint64(), ctypes.c_uint64()
+        nh, ng, lay = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        self._chk(self.lib.kc_bloom_info(self._ctx, ctypes.byref(nw), ctypes.byref(bits), ctypes.byref(nh),
+                                         ctypes.byref(ng), ctypes.byref(lay)), "kc_bloom_info")
+        return {"words": nw.value, "bits": bits.value, "nh": nh.value, "nh_gate": ng.value,
+                "layout": "blocked" if lay.value else "reference"}
+
+    def bloom_read(self) -> np.ndarray:
+        n = self.bloom_info()["words"]
+        a = np.zeros(n, dtype=np.uint32)
+        self._chk(self.lib.kc_bloom_read(self._ctx, a.ctypes.data, n), "kc_bloom_read")
+        return a
+
+    def bloom_write(self, words: np.ndarray):
+        a = np.ascontiguousarray(words, dtype=np.uint32)
+        self._chk(self.lib.kc_bloom_write(self._ctx, a.ctypes.data, a.size), "kc_bloom_write")
 
     def sync(self):
         self._chk(self.lib.kc_sync(self._ctx), "kc_sync")

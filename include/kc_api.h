@@ -27,6 +27,11 @@
 extern "C" {
 #endif
 
+/* Largest k-mer length: keys of up to eight 64-bit words (the reference sizes its blocks
+   dynamically, kmer_factory.cpp:33, and accepts any k > 0, main.cpp:135; INTEGRATION.md
+   "Differences" states this bound). */
+#define KC_MAX_K 255
+
 #define KC_OK 0
 #define KC_ERR_ARG (-1)         /* invalid argument */
 #define KC_ERR_HIP (-2)         /* HIP runtime / device error */
@@ -46,7 +51,7 @@ typedef struct kc_ctx kc_ctx;
 /* Replaces the CLI-derived arguments struct (main.cpp:70-99) that main() hands to
  * the parse_input_* functors (main.cpp:468-543). */
 typedef struct {
-    int32_t k;              /* KLEN, 1..127 (the reference is wrong for k % 32 == 0) */
+    int32_t k;              /* KLEN, 1..KC_MAX_K (the reference is wrong for k % 32 == 0) */
     int32_t mode;           /* -m: 0 plain table (uint16 counts wrap), 1/2 kaarme (saturate at 16383) */
     int32_t bf_enable;      /* -b: two-pass double Bloom filter prefilter */
     int32_t device;         /* HIP device ordinal */
@@ -188,6 +193,20 @@ void kc_free(void* p);
  * main.cpp:387).  *chunks is allocated by the library (kc_free). */
 int kc_plan_chunks(const uint8_t* image, uint64_t size, int k, uint64_t chunk_size, int fmt, kc_chunk** chunks,
                    uint64_t* n_chunks);
+
+/* Test hooks for the Bloom filter (not on the reference's path).
+ * kc_xxh64: XXH64(&values[i], 8, seeds[i]) computed by the device function the
+ *   reference-layout Bloom passes use (calculate_hashes, double_bloomfilter.hpp:276-281;
+ *   xxHash v0.8.2), host arrays in and out.
+ * kc_bloom_info: the filter's geometry: words (u32) of its bit array, filter bits per
+ *   filter (main.cpp:402-418), ceil(hf) pass-1 and trunc(hf) pass-2 positions
+ *   (main.cpp:417, parallel_parser.hpp:2397), layout 1 = blocked (default), 0 = reference.
+ * kc_bloom_read / kc_bloom_write: copy the filter's words to / from the host (a write
+ *   makes the next pass read the given bits). */
+int kc_xxh64(const uint64_t* values, const uint64_t* seeds, uint64_t n, uint64_t* out);
+int kc_bloom_info(kc_ctx* ctx, uint64_t* n_words, uint64_t* bits, int* nh, int* nh_gate, int* layout);
+int kc_bloom_read(kc_ctx* ctx, uint32_t* words, uint64_t n_words);
+int kc_bloom_write(kc_ctx* ctx, const uint32_t* words, uint64_t n_words);
 
 /* Synthetic reads (bench/test input): writes the FASTA records
  * [first_read, first_read + n_reads) of the seeded generator to device memory

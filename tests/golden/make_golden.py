@@ -73,6 +73,19 @@ CASES = [
     ("big_edge.fasta", 51, ["-m", "0", "-a", "1", "-s", "8000000"]),
     ("big_reads.fasta", 31, ["-a", "2", "-s", "8000000"]),
     ("big_reads.fasta", 55, ["-b", "-u", "3000000", "-a", "2"]),
+    # k >= 128: keys of five to eight 64-bit words (kmer_factory.cpp:33 sizes the blocks by k)
+    ("reads_w60.fasta", 129, ["-a", "1", "-s", "1000000"]),
+    ("long.fasta", 129, ["-m", "0", "-a", "1", "-s", "1000000"]),
+    ("long.fasta", 131, ["-a", "1", "-s", "1000000"]),
+    ("long.fasta", 131, ["-b", "-u", "300000", "-a", "2"]),
+    ("long.fasta", 200, ["-a", "1", "-s", "1000000"]),
+    ("long.fasta", 200, ["-m", "0", "-a", "1", "-s", "1000000"]),
+    ("long.fasta", 200, ["-b", "-u", "300000", "-a", "2"]),
+    ("long.fasta", 255, ["-a", "2", "-s", "1000000"]),
+    ("long.fasta", 255, ["-m", "0", "-a", "1", "-s", "1000000"]),
+    ("long.fasta", 255, ["-b", "-u", "300000", "-f", "0.05", "-a", "2"]),
+    ("edge.fasta", 140, ["-a", "1", "-s", "1000000"]),
+    ("big_edge.fasta", 161, ["-a", "1", "-s", "8000000"]),
 ]
 
 XXH_SEEDS = [2411, 3253, 1061, 1129, 2269, 7309, 3491, 8237, 6359, 8779, 0]

@@ -371,3 +371,37 @@ def test_bloom_segment_overflow_falls_back_to_exact(golden_input, tmp_path, monk
     out = tmp_path / "oracle.txt"
     oracle_count(path, 31, args, out)
     assert sorted_digest_lines(lines) == sorted_digest_file(out)
+
+
+def _job(kc, path, k):
+    image = open(path, "rb").read()
+    fmt = ka.detect_format(path, image[0])
+    chunks = ka.plan_chunks(image, k, fmt)
+    for off, ln, bh in chunks:
+        kc.bloom_chunk(image[off:off + ln], fmt, bool(bh))
+    kc.bloom_finalize()
+    for off, ln, bh in chunks:
+        kc.count_chunk(image[off:off + ln], fmt, bool(bh))
+    kc.finish()
+    return kc.lines()
+
+
+def test_bloom_context_reused_for_a_larger_job(golden_input, tmp_path, insert_path):
+    """One Bloom context, two jobs: a small input, kc_reset, then a much larger one.  The
+    second table (2 * new_in_second slots) has more regions and more level-1 bins than
+    the first, so every partition array must follow the new geometry (the
+    level-1 histograms kept their first size)."""
+    big = [c for c in CASES if c["input"] == "big_reads.fasta" and "-b" in c["args"]][0]
+    o = parse_ref_args(big["args"])
+    small = golden_input("reads_w60.fasta")
+    with ka.KmerCounter(ka.Config(k=big["k"], mode=2, bf_enable=True, est_unique=o["est_unique"],
+                                  min_abundance=o["min_abundance"], batch_bytes=64 << 20)) as kc:
+        got = _job(kc, small, big["k"])
+        exp = tmp_path / "exp.txt"
+        oracle_count(small, big["k"], ["-a", str(o["min_abundance"])], exp)
+        assert got == sorted(open(exp).read().splitlines())
+        kc.reset()
+        lines = _job(kc, golden_input("big_reads.fasta"), big["k"])
+        assert sorted_digest_lines(lines) == (big["sorted_sha256"], big["lines"])
+        kc.reset()  # and back to a small job on the grown buffers
+        assert _job(kc, small, big["k"]) == got

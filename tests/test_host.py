@@ -16,7 +16,7 @@ HEADER = os.path.join(REPO, "include", "kc_api.h")
 
 def declared_symbols():
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"\b(kc_[a-z_]+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(kc_[a-z0-9_]+)\s*\(", txt)))
 
 
 def test_library_exports_every_declared_symbol():
@@ -107,6 +107,9 @@ def test_cli_option_semantics(golden_input, tmp_path):
     assert run_cli(tmp_path / "missing.fa", 31, "-s", 1000).returncode == 105
     assert run_cli(fa).returncode == 106
     assert run_cli("-h").returncode == 0
+    # k above KC_MAX_K (eight key words) is refused with a message (INTEGRATION.md Differences)
+    r = run_cli(fa, 256, "-s", 1000, "-o", tmp_path / "big_k.txt")
+    assert r.returncode == 1 and "above 255" in r.stderr and not (tmp_path / "big_k.txt").exists()
 
 
 def test_cli_format_checks(tmp_path):

@@ -70,3 +70,13 @@ def test_oracle_matches_live_reference(k, args, tmp_path):
     oo = tmp_path / "or.txt"
     oracle_count(str(inp), k, args, oo)
     assert sorted_digest_file(ro) == sorted_digest_file(oo)
+
+
+def test_bloom_model_xxh64_matches_golden_vectors():
+    """The test-side XXH64 of tests/bloom_model.py (used to predict device Bloom
+    positions) against the vendored xxHash v0.8.2 vectors."""
+    import json
+    import bloom_model as bm
+    from conftest import GOLDEN
+    vec = json.load(open(os.path.join(GOLDEN, "xxh64.json")))["vectors"]
+    assert all(bm.xxh64_u64(v["value"], v["seed"]) == v["xxh64"] for v in vec)
