@@ -23,6 +23,7 @@ PMC summary profiles/pmc_traffic.json when it matches the workload), cpu_baselin
 reference CLI oracle/_ref/kaarme on a bounded sample of the same workload, rank 0, N=1).
 """
 import argparse
+import ctypes
 import json
 import math
 import os
@@ -53,6 +54,10 @@ PRESETS = {
                scale="strong"),
     "C5": dict(reads=1_000_000, read_len=10_000, genome=500_000_000, k=127, slots=3_600_000_000, unique=0,
                scale="strong"),
+    # C2 with hot keys: 5 % poly-A/T reads, 3 % (CA)n reads and a 300-bp
+    # repeat in 10^4 copies of the genome (kc_synth.h skew options)
+    "C2S": dict(reads=10_000_000, read_len=150, genome=50_000_000, k=31, slots=200_000_000, unique=0, scale="weak",
+                skew=(0.05, 0.03, 300, 10_000)),
 }
 
 
@@ -81,25 +86,32 @@ def cpu_baseline(args):
     threads = max(3, min(args.cpu_threads or share + 2, 64))
     with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
         fa = os.path.join(td, "sample.fasta")
+        sk = PRESETS[args.config].get("skew")
+        skew_args = (["--homo", str(sk[0]), "--dinuc", str(sk[1]), "--repeat", str(sk[2]), str(sk[3])] if sk else [])
         subprocess.run([gen, fa, str(args.reads), str(args.read_len), str(args.genome), "-s", str(args.seed),
-                        "-e", str(args.err), "--first", "0", "--count", str(n)], check=True)
+                        "-e", str(args.err), "--first", "0", "--count", str(n)] + skew_args, check=True)
         with open(fa, "rb") as f:  # pre-warm the page cache
             while f.read(1 << 24):
                 pass
         windows = n * (args.read_len - args.k + 1)
         # distinct <= windows: never ask the reference for more slots than the sample can fill
         slots = min(args.slots, int(windows * 1.3) + 1000) if args.slots else 0
-        targs = table_args(slots, args.unique)
+        # -b -u: the estimate scaled to the sample (the filter is sized for the reads counted)
+        unique = max(1000, args.unique * n // max(1, args.reads)) if args.unique else 0
+        targs = table_args(slots, unique)
         if kind == "reference":
             cmd = [ref, fa, str(args.k), "-m", "2", "-t", str(threads), "-a", "0"] + targs
             # the reference's worker threads occasionally crash it (seen once in ~10 runs
-            # on the box: killed before its timers); one more attempt, a CPU-only rerun
+            # on the box: killed before its timers); one more attempt, a CPU-only rerun,
+            # reported as `attempts` with the failed runs' exit codes
+            failures = []
             for attempt in range(2):
                 p = subprocess.run(cmd, capture_output=True, text=True, timeout=1800)
                 m = re.search(r"Time used to build hash table: (\d+) microseconds", p.stdout)
                 mb = re.search(r"Time used to bloom filter k-mers: (\d+) microseconds", p.stdout)
                 if p.returncode == 0 and m:
                     break
+                failures.append(p.returncode)
                 log(f"cpu baseline attempt {attempt + 1} failed (exit {p.returncode}):", p.stdout[-300:],
                     p.stderr[-300:])
             else:
@@ -111,10 +123,24 @@ def cpu_baseline(args):
             subprocess.run([orc, "count", fa, str(args.k), "-a", "0"] + targs, check=True, capture_output=True)
             secs = time.perf_counter() - t0
             cores = 1
+    if kind != "reference":
+        failures = []
     return {"value": windows / secs, "unit": "k-mers/s", "cores": cores, "kind": kind,
+            "attempts": 1 + len(failures), "failed_exit_codes": failures, "cpu_model": cpu_model(),
+            "nproc": os.cpu_count(), "core_share": share,
             "sample": f"first {n} reads of the same generator ({windows} windows, k={args.k}, "
                       f"-m 2 {' '.join(targs)} -t {threads}, {secs:.2f} s counting time"
                       f"{' incl. the Bloom pass' if args.unique else ''})"}
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def load_traffic(workload):
@@ -131,57 +157,31 @@ def load_traffic(workload):
     return None
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="C2", choices=sorted(PRESETS), help="BASELINE.md workload (default C2)")
-    ap.add_argument("--reads", type=int, default=None, help="reads (per GPU for weak, total for strong presets)")
-    ap.add_argument("--read-len", type=int, default=None)
-    ap.add_argument("--genome", type=int, default=None)
-    ap.add_argument("--k", type=int, default=None)
-    ap.add_argument("--slots", type=int, default=None, help="-s (total for strong presets)")
-    ap.add_argument("--unique", type=int, default=None, help="-b -u U (Bloom filter) instead of -s")
-    ap.add_argument("--batch-mib", type=int, default=0, help="staging batch (0 = the whole image if HBM allows)")
-    ap.add_argument("--err", type=float, default=0.001)
-    ap.add_argument("--seed", type=int, default=42)
-    ap.add_argument("--cpu-sample-bases", type=int, default=150_000_000)
-    ap.add_argument("--cpu-threads", type=int, default=0, help="-t of the reference (0 = core share + 2)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--force-sharded", action="store_true",
-                    help="use the sharded (RCCL) path even at one rank (testing)")
-    args = ap.parse_args()
-    # stdout carries exactly one JSON line: libraries (RCCL prints a version banner at
-    # communicator init) write to fd 1 too, so fd 1 becomes stderr and the JSON goes to a
-    # private copy of the original stdout
-    json_out = os.fdopen(os.dup(1), "w")
-    os.dup2(2, 1)
-    preset = PRESETS[args.config]
+def resolve(args, name):
+    """args with the preset's values for every workload option left unset."""
+    r = argparse.Namespace(**vars(args))
+    r.config = name
+    preset = PRESETS[name]
     for key in ("reads", "read_len", "genome", "k", "slots", "unique"):
-        if getattr(args, key) is None:
-            setattr(args, key, preset[key])
-    if args.unique:
-        args.slots = 0
+        if getattr(r, key) is None or name != args.config:
+            setattr(r, key, preset[key])
+    if r.unique:
+        r.slots = 0
+    return r
 
-    import torch
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    torch.cuda.set_device(local)
-    dist = None
-    if world > 1 or args.force_sharded:
-        import torch.distributed as dist
-        for key, val in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29531"), ("RANK", "0"), ("WORLD_SIZE", "1")):
-            os.environ.setdefault(key, val)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+def same_image(a, b):
+    pa, pb = PRESETS[a.config], PRESETS[b.config]
+    return (a.reads, a.read_len, a.genome, pa["scale"], pa.get("skew")) == (b.reads, b.read_len, b.genome, pb["scale"],
+                                                                           pb.get("skew"))
 
-    import kaarme_amd as ka
 
-    lib = ka.load_library()
+def run_workload(args, env, image=None):
+    """Times one workload (warmup + steps of a full counting job) and returns its JSON record
+    plus the device image (reusable by a workload with the same generator parameters)."""
+    torch, ka, lib, dist = env["torch"], env["ka"], env["lib"], env["dist"]
+    rank, world, local = env["rank"], env["world"], env["local"]
+    preset = PRESETS[args.config]
     L, k = args.read_len, args.k
     W = ka.words_for_k(k)
     strong = preset["scale"] == "strong"
@@ -193,24 +193,35 @@ def main():
         first, N, slots = rank * args.reads, args.reads, args.slots
     stream = torch.cuda.current_stream()
     nbytes = lib.kc_synth_bytes(first, N, L, 0)
-    image = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-    rc = lib.kc_synth_device(image.data_ptr(), first, N, args.seed, args.genome, L, 0, args.err, 0.0,
-                             stream.cuda_stream)
-    assert rc == 0, "kc_synth_device failed"
-    torch.cuda.synchronize()
+    sk = preset.get("skew")
+    if image is None:
+        image = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+        if sk:
+            skew = ka.kc_synth_skew(sk[0], sk[1], sk[2], sk[3])
+            rc = lib.kc_synth_skew_device(image.data_ptr(), first, N, args.seed, args.genome, L, 0, args.err, 0.0,
+                                          ctypes.byref(skew), stream.cuda_stream)
+        else:
+            rc = lib.kc_synth_device(image.data_ptr(), first, N, args.seed, args.genome, L, 0, args.err, 0.0,
+                                     stream.cuda_stream)
+        assert rc == 0, "kc_synth_device failed"
+        torch.cuda.synchronize()
+    assert image.numel() == nbytes
     host = image.cpu().numpy().tobytes()  # setup only: the host chunker reads boundary bytes
     chunks = ka.plan_chunks(host, k, ka.FMT_FASTA)
     del host
     if args.batch_mib:
         cap = args.batch_mib << 20
-    else:  # as large as HBM allows (kc_api.cpp: ~26 W + 2 bytes of partition buffers per staged byte)
+    else:  # as large as HBM allows (kc_api.cpp: ~28 W + 4 bytes of partition buffers per staged byte)
         free, _ = torch.cuda.mem_get_info()
-        cap = int(0.45 * (free - nbytes)) // (26 * W + 2)
+        cap = int(0.45 * (free - nbytes)) // (28 * W + 4)
     batch = min((nbytes + len(chunks) * 4096 + (1 << 20)) // 4096 * 4096, cap // 4096 * 4096)
     windows_expected = N * (L - k + 1)
     tbl = " ".join(["-m", "2"] + table_args(slots, args.unique))
     workload = (f"{args.config}: synthetic {N} x {L} bp reads/GPU, k={k}, {tbl}" if not strong else
                 f"{args.config}: synthetic {args.reads} x {L} bp reads over {world} GPU(s), k={k}, {tbl} per GPU")
+    if sk:
+        workload += (f", skew: {sk[0]:.0%} poly-A/T reads, {sk[1]:.0%} (CA)n reads, a {sk[2]}-bp repeat x "
+                     f"{sk[3]} in the genome")
     cfg = ka.Config(k=k, mode=2, table_slots=slots, min_abundance=2, batch_bytes=batch, device=local,
                     bf_enable=bool(args.unique), est_unique=args.unique)
     if dist:
@@ -247,6 +258,7 @@ def main():
     counter.profile(False)
     tm = counter.timing()
     st = counter.finish()  # raises on table overflow
+    counter.close()
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -297,6 +309,10 @@ def main():
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": kname,
                 "kernel_ms": round(count_ms, 4), "algorithmic_bytes_per_launch": int(bytes_per_launch)}
+    if traffic:
+        # the bytes this design moves (rocprofv3 PMC, profiles/pmc_traffic.json) over the same time
+        roofline["traffic_gbs"] = round(traffic / (count_ms * 1e-3) / 1e9, 2)
+        roofline["traffic_frac"] = round(traffic / (count_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
     step_ms = elapsed / args.steps * 1e3
     out = {
         "metric": METRIC, "value": value, "unit": "k-mers/s", "n_gpus": world, "steps": args.steps,
@@ -312,10 +328,75 @@ def main():
                       "count": round(count_ms, 4)},
         "image_bytes": nbytes, "stage_bytes": sum(c[1] for c in chunks),
         "windows_per_step_per_gpu": windows_step, "distinct_per_gpu": st["distinct"], "table_slots": st["table_slots"],
+        "skew_lists": {"spilled_keys": st["spilled"], "heavy_records": st["heavy_records"],
+                       "batches_redone": st["part_fallbacks"]},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args)
+    return out, image
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="C2", choices=sorted(PRESETS), help="BASELINE.md workload (default C2)")
+    ap.add_argument("--reads", type=int, default=None, help="reads (per GPU for weak, total for strong presets)")
+    ap.add_argument("--read-len", type=int, default=None)
+    ap.add_argument("--genome", type=int, default=None)
+    ap.add_argument("--k", type=int, default=None)
+    ap.add_argument("--slots", type=int, default=None, help="-s (total for strong presets)")
+    ap.add_argument("--unique", type=int, default=None, help="-b -u U (Bloom filter) instead of -s")
+    ap.add_argument("--batch-mib", type=int, default=0, help="staging batch (0 = the whole image if HBM allows)")
+    ap.add_argument("--err", type=float, default=0.001)
+    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--cpu-sample-bases", type=int, default=150_000_000)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="-t of the reference (0 = core share + 2)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--secondary", default="C3",
+                    help="at N=1 with the default C2: also time this workload (the north star's k=51 Bloom "
+                         "config) and attach it as a second record ('none' = skip)")
+    ap.add_argument("--secondary-cpu-sample-bases", type=int, default=50_000_000)
+    ap.add_argument("--force-sharded", action="store_true",
+                    help="use the sharded (RCCL) path even at one rank (testing)")
+    args = ap.parse_args()
+    # stdout carries exactly one JSON line: libraries (RCCL prints a version banner at
+    # communicator init) write to fd 1 too, so fd 1 becomes stderr and the JSON goes to a
+    # private copy of the original stdout
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+
+    import torch
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1 or args.force_sharded:
+        import torch.distributed as dist
+        for key, val in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29531"), ("RANK", "0"), ("WORLD_SIZE", "1")):
+            os.environ.setdefault(key, val)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import kaarme_amd as ka
+
+    env = {"torch": torch, "ka": ka, "lib": ka.load_library(), "dist": dist, "rank": rank, "world": world,
+           "local": local}
+    primary = resolve(args, args.config)
+    out, image = run_workload(primary, env)
+    if world == 1 and not dist and args.config == "C2" and args.secondary != "none":
+        sec = resolve(args, args.secondary)
+        sec.cpu_sample_bases = args.secondary_cpu_sample_bases
+        rec, _ = run_workload(sec, env, image if same_image(primary, sec) else None)
+        out[sec.config.lower()] = {key: rec[key] for key in ("value", "unit", "ms_per_step", "config", "roofline",
+                                                            "kernel_ms", "windows_per_step_per_gpu",
+                                                            "distinct_per_gpu", "table_slots", "cpu_baseline")}
+    del image
     if rank == 0:
         print(json.dumps(out), file=json_out, flush=True)
     if dist:

@@ -86,7 +86,12 @@ struct kc_ctx {
     uint64_t* d_keys1 = nullptr;
     uint64_t* d_keys2 = nullptr;
     uint64_t k1_words = 0, k2_words = 0;  // u64 words the level-1 / level-2 key buffers hold
+    uint64_t* d_spill = nullptr;           // skew lists of a segmented batch (ensure_part_geo)
+    uint64_t* d_heavy = nullptr;
+    uint64_t spill_words = 0, heavy_words = 0;
     bool table_fresh = false;  // the table is all zero (allocated / reset, nothing inserted since)
+    uint64_t min_slots = 0;        // the job's -s (or 2 * new_in_second): the reference's table size
+    bool strict_capacity = false;  // KC_STRICT_CAPACITY=1: fail past the reference's capacity
     // kc_reset defers the table memset: a fresh level-3 pass writes every region anyway;
     // any other use of the table zeroes it first (materialize_zero)
     bool table_zero_pending = false;
@@ -171,6 +176,7 @@ static uint64_t bloom_words(const kc_ctx* c) {
 }
 
 static int alloc_table(kc_ctx* c, uint64_t min_slots) {
+    c->min_slots = min_slots;
     // Kaarme's table holds exactly next_prime3mod4(min_slots) slots and dies when
     // full; open addressing on the GPU keeps 25 % headroom over that.  The table is
     // R = F1 * F2 regions of BPR 128-byte buckets (a region = one LDS-resident table).
@@ -187,6 +193,7 @@ static int alloc_table(kc_ctx* c, uint64_t min_slots) {
     c->F2 = 1u << c->f2bits;
     c->F1 = (uint32_t)((regions + c->F2 - 1) / c->F2);
     c->R = (uint64_t)c->F1 * c->F2;
+    if (c->R >= (1ULL << 32)) return c->fail(KC_ERR_ARG, "table too large");  // 32-bit region index (kc_common.h)
     c->nbuckets = c->R * BPR;
     const size_t bytes = c->nbuckets * BUCKET_WORDS * sizeof(uint64_t);
     if (!c->d_table || bytes > c->table_cap_bytes) {  // else: reuse the previous allocation
@@ -307,6 +314,21 @@ static int ensure_part_geo(kc_ctx* c, uint64_t syms, bool seg, const PartGeo& g,
     if (rc) return rc;
     rc = grow(&c->d_keys2, &c->k2_words, need2);
     if (rc) return rc;
+    // skew lists of a segmented batch: keys past a segment's end (an eighth of the windows
+    // before the batch falls back to the exact layout) and {key, count} records of repeated
+    // windows (a thirty-second)
+    uint64_t spill_cap = 0, heavy_cap = 0;
+    if (cap1) {
+        spill_cap = std::max<uint64_t>(1 << 16, syms / 8);
+        heavy_cap = std::max<uint64_t>(1 << 14, syms / 32);
+        if (const char* v = std::getenv("KC_SPILL_CAP")) spill_cap = std::strtoull(v, 0, 10);  // tests
+        if ((rc = grow(&c->d_spill, &c->spill_words, spill_cap * g.IW))) return rc;
+        if ((rc = grow(&c->d_heavy, &c->heavy_words, heavy_cap * (g.IW + 1)))) return rc;
+    }
+    pb.spill = c->d_spill;
+    pb.spill_cap = spill_cap;
+    pb.heavy = c->d_heavy;
+    pb.heavy_cap = heavy_cap;
     pb.keys1 = c->d_keys1;
     pb.keys2 = c->d_keys2;
     pb.nblk1 = nblk1;
@@ -542,6 +564,7 @@ int kc_create(const kc_config* cfg, kc_ctx** out) {
     }
     kc_ctx* c = new kc_ctx();
     c->cfg = *cfg;
+    if (const char* v = std::getenv("KC_STRICT_CAPACITY")) c->strict_capacity = std::atoi(v) != 0;
     c->W = words_for_k(cfg->k);
     c->S = slots_per_bucket(c->W);
     auto bail = [&](int code, const std::string& m) {
@@ -554,14 +577,14 @@ int kc_create(const kc_config* cfg, kc_ctx** out) {
     uint64_t batch = cfg->batch_bytes;
     if (!batch) {
         // Every staged batch of the partitioned insert sweeps the table once, so batches are
-        // as large as the device allows: the partition buffers take ~26 W + 2 bytes per
-        // staged byte (two segmented key buffers + the packed stream); use ~40 % of free
+        // as large as the device allows: the partition buffers take ~28 W + 4 bytes per
+        // staged byte (two segmented key buffers, the skew lists, the packed stream); use ~40 % of free
         // HBM, within [256 MiB, 2 GiB] (the pinned host stage is two batches).
         size_t fr = 0, tot = 0;
         batch = kDefaultBatch;
         if (hipMemGetInfo(&fr, &tot) == hipSuccess)
             batch = std::min<uint64_t>(2ull << 30, std::max<uint64_t>(kDefaultBatch,
-                                                                       (uint64_t)(0.4 * fr) / (26 * c->W + 2)));
+                                                                       (uint64_t)(0.4 * fr) / (28 * c->W + 4)));
     }
     c->batch_bytes = round_up(batch, TILE);
     c->max_chunks = c->batch_bytes / TILE;
@@ -645,6 +668,8 @@ void kc_destroy(kc_ctx* c) {
     hipFree(c->pb.bsum);
     hipFree(c->d_keys1);
     hipFree(c->d_keys2);
+    hipFree(c->d_spill);
+    hipFree(c->d_heavy);
     hipFree(c->d_gstart);
     hipFree(c->d_mstart);
     hipFree(c->d_mlen);
@@ -987,6 +1012,8 @@ int kc_finish(kc_ctx* c, kc_stats* st) {
         st->failed_in_first = h.failed_in_first;
         st->chunks = c->n_chunks;
         st->part_fallbacks = h.part_fallbacks;
+        st->spilled = h.spilled;
+        st->heavy_records = h.heavy;
         st->bytes = c->n_bytes;
         // occupied slots
         if (c->nbuckets) {
@@ -1005,6 +1032,18 @@ int kc_finish(kc_ctx* c, kc_stats* st) {
                                    "(word 0 == 0) and were skipped");
     if (h.overflow) return c->fail(KC_ERR_TABLE_FULL, "Hash table is full (" + std::to_string(h.overflow) +
                                                            " k-mers could not be inserted)");
+    if (c->strict_capacity && c->nbuckets) {  // the reference's table: next_prime3mod4(min slots)
+        const uint64_t cap = kc_table_size_reference(c->min_slots);
+        TableView tv = table_view(c);
+        HIPCHK(c, hipMemsetAsync(&c->d_ctr->occupied, 0, 8, c->stream));
+        HIPCHK(c, launch_dump(tv, c->cfg.mode == 0 ? 0 : 1, ~0ULL, nullptr, c->d_ctr, c->stream));
+        unsigned long long occ = 0;
+        HIPCHK(c, hipMemcpyAsync(&occ, &c->d_ctr->occupied, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (occ > cap)
+            return c->fail(KC_ERR_TABLE_FULL, "Hash table is full (" + std::to_string(occ) + " distinct k-mers, the "
+                                              "reference's table holds " + std::to_string(cap) + ")");
+    }
     return KC_OK;
 }
 
@@ -1290,6 +1329,17 @@ int kc_plan_chunks(const uint8_t* image, uint64_t size, int k, uint64_t chunk_si
     return KC_OK;
 }
 
+uint64_t kc_table_size_reference(uint64_t at_least) {  // next_prime3mod4, functions_math.cpp:53-96
+    if (at_least <= 2) return 2;
+    uint64_t p = at_least % 2 == 0 ? at_least + 1 : at_least;
+    for (;; p += 2) {
+        bool prime = true;
+        for (uint64_t d = 3; d * d <= p; d += 2)
+            if (p % d == 0) { prime = false; break; }
+        if (prime && p % 4 == 3) return p;
+    }
+}
+
 int kc_xxh64(const uint64_t* values, const uint64_t* seeds, uint64_t n, uint64_t* out) {
     if (n && (!values || !seeds || !out)) return KC_ERR_ARG;
     if (n == 0) return KC_OK;
@@ -1346,6 +1396,15 @@ int kc_synth_device(uint8_t* dst, uint64_t first_read, uint64_t n_reads, uint64_
                     uint32_t read_len, uint32_t wrap, double err_rate, double n_rate, void* s) {
     if (!dst || genome_len < read_len || read_len == 0) return KC_ERR_ARG;
     hipError_t e = launch_synth(dst, first_read, n_reads, seed, genome_len, read_len, wrap, err_rate, n_rate,
+                                nullptr, (hipStream_t)s);
+    return e == hipSuccess ? KC_OK : KC_ERR_HIP;
+}
+
+int kc_synth_skew_device(uint8_t* dst, uint64_t first_read, uint64_t n_reads, uint64_t seed, uint64_t genome_len,
+                         uint32_t read_len, uint32_t wrap, double err_rate, double n_rate, const kc_synth_skew* skew,
+                         void* s) {
+    if (!dst || genome_len < read_len || read_len == 0) return KC_ERR_ARG;
+    hipError_t e = launch_synth(dst, first_read, n_reads, seed, genome_len, read_len, wrap, err_rate, n_rate, skew,
                                 (hipStream_t)s);
     return e == hipSuccess ? KC_OK : KC_ERR_HIP;
 }

@@ -58,7 +58,9 @@ void usage(const char* prog) {
                  "  -o,--output-file TEXT       Output file where the k-mer counts will be stored\n"
                  "  -b,--use-bfilter            Use bloom filters to discard unique k-mers\n"
                  "  -f,--bfilter-fpr FLOAT      Bloom filter false positive rate (def. 0.01)\n"
-                 "  --device INT                HIP device ordinal (def. 0)\n\n"
+                 "  --device INT                HIP device ordinal (def. 0)\n"
+                 "  --strict-capacity           fail like the reference once the distinct k-mers pass its table\n"
+                 "                              size next_prime3mod4(-s) (the device table keeps 25 % headroom)\n\n"
                  "Mandatory params:\n"
                  "  -s,--hash-tab-size UINT     Hash table size\n"
                  "  -u,--unq-kmers UINT         Estimated number of unique k-mers\n";
@@ -110,6 +112,7 @@ int parse(int argc, char** argv, Args* a) {
         };
         if (o == "-h" || o == "--help") { usage(argv[0]); return 0; }
         if (o == "-b" || o == "--use-bfilter") { a->use_bf = true; continue; }
+        if (o == "--strict-capacity") { setenv("KC_STRICT_CAPACITY", "1", 1); continue; }  // kc_api.h
         if (o.size() > 1 && o[0] == '-' && !(o.size() > 1 && std::isdigit((unsigned char)o[1]))) {
             std::string v;
             if (!next(&v)) return cli_error(kRequired, o + " requires an argument");
@@ -311,6 +314,7 @@ int main(int argc, char** argv) {
         std::exit(1);
     };
     using clk = std::chrono::high_resolution_clock;
+    uint64_t bf_new_in_second = 0;
     if (a.use_bf) {
         std::cout << "Starting parallel bloom filtering\n";
         auto t0 = clk::now();
@@ -319,6 +323,7 @@ int main(int argc, char** argv) {
                 die("bloom pass");
         uint64_t nis = 0;
         if (kc_bloom_finalize(ctx, &nis) != KC_OK) die("bloom finalize");
+        bf_new_in_second = nis;
         auto t1 = clk::now();
         std::cout << "New k-mers in second bloom filter " << nis << "\n";
         std::cout << "Time used to bloom filter k-mers: "
@@ -335,7 +340,10 @@ int main(int argc, char** argv) {
         die("counting pass");
     }
     auto t1 = clk::now();
-    std::cout << "Hash table size is: " << stt.table_slots << "\n";
+    // the reference prints its table size, next_prime3mod4(-s or 2 * new_in_second)
+    // (functions_math.cpp:90); the device table keeps 25 % headroom over it
+    const uint64_t ref_slots = kc_table_size_reference(a.use_bf ? 2 * bf_new_in_second : a.slots);
+    std::cout << "Hash table size is: " << ref_slots << "\n";
     if (a.min_abundance > 0) {
         std::cout << "Start writing k-mers in a file\n";
         if (kc_write(ctx, a.output.c_str()) != KC_OK) die("writing k-mers");
@@ -346,7 +354,8 @@ int main(int argc, char** argv) {
     std::cout << "Time used to write k-mers in a file: "
               << std::chrono::duration_cast<std::chrono::microseconds>(t2 - t1).count() << " microseconds\n";
     std::cout << "Processed k-mers: " << stt.windows << " (inserted " << stt.inserted << ")\n";
-    std::cout << "Main array slots used " << stt.distinct << " / " << stt.table_slots << "\n";
+    std::cout << "Main array slots used " << stt.distinct << " / " << ref_slots << "\n";
+    std::cout << "Device table capacity: " << stt.table_slots << " slots\n";
     kc_destroy(ctx);
     kc_free(chunks);
     if (map) munmap(map, fsize);

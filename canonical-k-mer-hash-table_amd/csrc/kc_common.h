@@ -75,9 +75,11 @@ DEV void from_tkey(const uint64_t (&t)[W], uint64_t (&key)[W]) {
 // the region, so a region is an independent table that fits in LDS.  For R = F1 * F2
 // (F2 a power of two) the level-1 bin of a key is r >> log2 F2 and its level-2 bin
 // r & (F2 - 1).  The shard owner (multi-GPU) uses the low 32 bits, independent of both.
-DEV uint64_t region_of(uint64_t t0, uint64_t R) { return ((t0 >> 32) * R) >> 32; }
+// R < 2^32 (kc_api.cpp alloc_table): one 32 x 32 -> 64-bit product gives the region (high
+// half) and the fraction (low half)
+DEV uint64_t region_of(uint64_t t0, uint64_t R) { return __umulhi((uint32_t)(t0 >> 32), (uint32_t)R); }
 DEV uint32_t bucket_in_region(uint64_t t0, uint64_t R) {
-    return (uint32_t)((t0 >> 32) * R) >> (32 - BPR_BITS);
+    return ((uint32_t)(t0 >> 32) * (uint32_t)R) >> (32 - BPR_BITS);
 }
 DEV uint32_t owner_of(uint64_t t0, uint32_t parts) { return (uint32_t)(((t0 & 0xFFFFFFFFULL) * parts) >> 32); }
 

@@ -431,8 +431,8 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_count(PackedView sv, int k, T
 // --------------------------------------------------------------------------------
 // partitioned path
 // --------------------------------------------------------------------------------
-// LDS of a scatter pass: tilehist, tilestart, tilecur (u32 x F), gbase (u64 x F), keys
-constexpr size_t hist_smem(uint32_t F) { return ((size_t)F * 3 + 1) * 4 + 4 + (size_t)F * 8; }
+// LDS of a scatter pass: hist, start, lim (u32 x F), gbase, dlt (u64 x F), then the keys
+constexpr size_t hist_smem(uint32_t F) { return ((size_t)F * 3 + 1) * 4 + 4 + (size_t)F * 16; }
 template <int W, int NT = COUNT_THREADS>
 constexpr size_t part_smem(uint32_t F) {
     return hist_smem(F) + (size_t)NT * run_w<W>() * 8 * W;
@@ -460,20 +460,25 @@ DEV void block_excl_scan_lds(const uint32_t* in, uint32_t* out, uint32_t n) {
     __syncthreads();
 }
 
+// LDS of a scatter: per bin its tile count, its first tile slot, the tile slots that
+// fit its output (lim), the destination of its next key (gbase) and, for the write-out,
+// destination minus tile slot (dlt); then the tile's keys
 struct PartLds {
     uint32_t* hist;
     uint32_t* start;
-    uint32_t* cur;
+    uint32_t* lim;
     uint64_t* gbase;
+    uint64_t* dlt;
     uint64_t* keys;
 };
 DEV PartLds part_lds(uint8_t* smem, uint32_t F) {
     PartLds l;
     l.hist = reinterpret_cast<uint32_t*>(smem);
     l.start = l.hist + F;
-    l.cur = l.start + F;
-    l.gbase = reinterpret_cast<uint64_t*>(l.cur + F + (F & 1));
-    l.keys = l.gbase + F;
+    l.lim = l.start + F;
+    l.gbase = reinterpret_cast<uint64_t*>(l.lim + F + (F & 1));
+    l.dlt = l.gbase + F;
+    l.keys = l.dlt + F;
     return l;
 }
 
@@ -486,7 +491,7 @@ struct BinRegion {  // level-1 bin (coarse: region >> f2bits) or level-2 bin (re
     uint32_t mask;
     int coarse;
     DEV uint32_t operator()(uint64_t t0) const {
-        const uint32_t r = (uint32_t)region_of(t0, R);
+        const uint32_t r = __umulhi((uint32_t)(t0 >> 32), (uint32_t)R);  // region_of
         return coarse ? r >> f2bits : r & mask;
     }
 };
@@ -503,15 +508,24 @@ struct BinOwner {
 // pipeline then redoes the batch (launched behind a device-side gate).
 struct OutExact {
     static constexpr bool kSeg = false;
-    DEV bool fits(uint32_t, uint64_t) const { return true; }
+    DEV uint64_t room(uint32_t, uint64_t) const { return ~0ULL; }  // keys bin b can still take
 };
 struct OutSeg {
     static constexpr bool kSeg = true;
     uint64_t stride;  // keys between the segments of bins b and b+1
     uint64_t base;    // first key of bin 0's segment for this workgroup
     uint64_t cap;     // keys per segment
+    // keys past a segment's end: appended to the spill list (inserted after level 3 by the
+    // exact pipeline); a full spill list raises the batch's overflow flag (whole-batch redo)
+    uint64_t* spill;
+    uint64_t spill_cap;
+    unsigned long long* spill_n;
+    unsigned long long* overflow;
     DEV uint64_t start(uint32_t b) const { return (uint64_t)b * stride + base; }
-    DEV bool fits(uint32_t b, uint64_t dst) const { return dst < start(b) + cap; }
+    DEV uint64_t room(uint32_t b, uint64_t gbase) const {
+        const uint64_t end = start(b) + cap;
+        return gbase < end ? end - gbase : 0;
+    }
 };
 
 // Key-stream access policy (A/B knob, KC_NT: bit 0 = nontemporal loads of the level-1/2
@@ -528,6 +542,35 @@ DEV void ks_store(uint64_t* p, uint64_t v) {
     else *p = v;
 }
 
+// rank of this lane among the set lanes of a wave mask
+DEV uint32_t lane_rank(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+// wave-aggregated append: the lanes with `want` get consecutive slots of a list (one atomic
+// per wave); returns the slot (or ~0 for lanes without `want`)
+DEV uint64_t wave_append(bool want, unsigned long long* counter) {
+    const uint64_t m = __ballot(want);
+    if (!m) return ~0ULL;
+    const int leader = __builtin_ctzll(m);
+    unsigned long long base = 0;
+    if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(counter, (unsigned long long)__popcll(m));
+    base = __shfl(base, leader, 64);
+    return want ? base + lane_rank(m) : ~0ULL;
+}
+template <int W>
+DEV void spill_append(const OutSeg& o, bool want, const uint64_t (&key)[W]) {
+    const uint64_t pos = wave_append(want, o.spill_n);
+    if (!want) return;
+    if (pos < o.spill_cap) {
+#pragma unroll
+        for (int w = 0; w < W; w++) o.spill[pos * W + w] = key[w];
+    } else {
+        atomicOr(o.overflow, 1ULL);
+    }
+}
+template <int W>
+DEV void spill_append(const OutExact&, bool, const uint64_t (&)[W]) {}
+
 // Counting-sort the tile's keys (in registers: tk[j] valid where ok[j]) by bin into
 // LDS and write each bin as one contiguous run at gbase[bin].  The rank of a key inside
 // its bin comes back from the histogram atomic, so one LDS atomic per key suffices.
@@ -541,7 +584,7 @@ template <int W, int RUNW, class Bin, class Out, int NT = COUNT_THREADS, class M
 DEV bool scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const Out& o, uint64_t (&tk)[RUNW][W],
                       bool (&ok)[RUNW], uint64_t* __restrict__ out, Mid&& mid = Mid()) {
     const int tid = threadIdx.x;
-    uint32_t rank[RUNW];
+    uint32_t rank[RUNW];  // (the bins are recomputed below: one multiply, fewer registers)
 #pragma unroll
     for (int j = 0; j < RUNW; j++) rank[j] = ok[j] ? atomicAdd(&l.hist[bin(tk[j][0])], 1u) : 0;
     __syncthreads();
@@ -553,30 +596,117 @@ DEV bool scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const Out& o
 #pragma unroll
             for (int w = 0; w < W; w++) l.keys[slot * W + w] = tk[j][w];
         }
+    // per bin: destination minus tile slot, and the tile slots that fit the bin's output
+    for (uint32_t b = tid; b < F; b += NT) {
+        const uint32_t st = l.start[b], h = l.hist[b];
+        const uint64_t g = l.gbase[b];
+        l.dlt[b] = g - st;
+        l.lim[b] = st + (uint32_t)min((uint64_t)h, o.room(b, g));
+    }
     mid();
     __syncthreads();
     const uint32_t n = l.start[F - 1] + l.hist[F - 1];
-    bool over = false;
     for (uint32_t i = tid; i < n; i += NT) {
         uint64_t key[W];
 #pragma unroll
         for (int w = 0; w < W; w++) key[w] = l.keys[i * W + w];
         const uint32_t b = bin(key[0]);
-        const uint64_t dst = l.gbase[b] + (i - l.start[b]);
-        if (o.fits(b, dst)) {
+        const bool fits = i < l.lim[b];
+        if (fits) {
+            const uint64_t dst = l.dlt[b] + i;
 #pragma unroll
             for (int w = 0; w < W; w++) ks_store(out + dst * W + w, key[w]);
-        } else {
-            over = true;
         }
+        if constexpr (Out::kSeg) spill_append<W>(o, !fits, key);
     }
     __syncthreads();
     for (uint32_t b = tid; b < F; b += NT) {
-        l.gbase[b] += l.hist[b];
+        l.gbase[b] += l.lim[b] - l.start[b];  // the keys written (a segment's fill never passes its end)
         l.hist[b] = 0;
     }
     __syncthreads();
-    return over;
+    return false;
+}
+
+// Repeated windows (homopolymer runs: poly-A tails, poly-G artefacts, ...).  One key
+// repeated millions of times would send all its copies into one level-2 segment and one
+// level-3 region (SURVEY 7 "hard parts"; the reference's hot spot is the increase_count CAS,
+// kmer.cpp:699).  Runs of equal keys among a thread's consecutive windows collapse to the
+// run's first window carrying the run's length, and at each window slot the lanes of the
+// wave that hold the first valid lane's key merge into that lane.  Count passes send
+// every item that counts more than one window to the heavy list as a {key words, count}
+// record (added to the table after level 3); the Bloom pass keeps two copies of a key
+// (insertion_process changes nothing after a k-mer's second insertion,
+// double_bloomfilter.hpp:371-413).  Waves without a run skip it after one ballot.
+template <int OW, int RUNW, int MODE>
+DEV void combine_repeats(uint64_t (&tk)[RUNW][OW], bool (&ok)[RUNW], const PartBufs& pb, DevCounters* ctr) {
+    uint32_t eqm = 0;  // bit j: windows j and j + 1 are valid and equal
+    bool per2 = false;  // a period-2 repeat ((CA)n): windows j and j + 2 equal
+#pragma unroll
+    for (int j = 0; j + 1 < RUNW; j++) {
+        bool e = ok[j] && ok[j + 1], e2 = j + 2 < RUNW && ok[j] && ok[j + 2];
+#pragma unroll
+        for (int w = 0; w < OW; w++) {
+            e = e && tk[j][w] == tk[j + 1][w];
+            if (j + 2 < RUNW) e2 = e2 && tk[j][w] == tk[j + 2][w];
+        }
+        eqm |= (uint32_t)e << j;
+        per2 |= e2;
+    }
+    // (the lanes of a wave hold windows 16 apart, so a period-2 run shows the same key at the
+    // same slot of every lane inside it: the wave merge below combines those)
+    if (__ballot(eqm != 0 || per2) == 0) return;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int j = 0; j < RUNW; j++) {
+        const bool interior = j > 0 && ((eqm >> (j - 1)) & 1);
+        if constexpr (MODE == 3) {
+            // keep a run's first two windows
+            if (j > 1 && ((eqm >> (j - 2)) & 3) == 3) ok[j] = false;
+            const uint64_t v = __ballot(ok[j]);
+            if (!v) continue;
+            const int leader = __builtin_ctzll(v);
+            bool match = ok[j];
+#pragma unroll
+            for (int w = 0; w < OW; w++) match = match && tk[j][w] == __shfl(tk[j][w], leader, 64);
+            const uint64_t m = __ballot(match);
+            if (match && lane_rank(m) >= 2) ok[j] = false;  // the wave keeps two copies
+        } else {
+            // items of this slot: a run's first window counts the run
+            uint32_t c = ok[j] && !interior ? 1u + (uint32_t)__builtin_ctz(~(eqm >> j)) : 0u;
+            if (interior) ok[j] = false;
+            const uint64_t v = __ballot(c != 0);
+            if (!v) continue;
+            const int leader = __builtin_ctzll(v);
+            bool match = c != 0;
+#pragma unroll
+            for (int w = 0; w < OW; w++) match = match && tk[j][w] == __shfl(tk[j][w], leader, 64);
+            const uint64_t m = __ballot(match);
+            const uint32_t cl = __shfl(c, leader, 64);
+            const bool merge = __popcll(m) >= 2 || cl >= 2;  // wave-uniform
+            uint32_t total = c;
+            if (merge) {
+                uint32_t x = match ? c : 0u;
+#pragma unroll
+                for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+                total = lane == leader ? x : (match ? 0u : c);
+            }
+            // records: the merged leader, and every other item that counts several windows
+            const bool rec = total >= 2;
+            const uint64_t pos = wave_append(rec, &ctr->heavy_n);
+            if (rec) {
+                if (pos < pb.heavy_cap) {
+                    uint64_t* r = pb.heavy + pos * (OW + 1);
+#pragma unroll
+                    for (int w = 0; w < OW; w++) r[w] = tk[j][w];
+                    r[OW] = total;
+                } else {
+                    atomicOr(&ctr->part_overflow, 1ULL);
+                }
+            }
+            if (rec || (merge && match)) ok[j] = false;
+        }
+    }
 }
 
 // gated kernels (the exact fallback of a segmented batch) run only if *gate != 0
@@ -620,7 +750,6 @@ __global__ __launch_bounds__(NT, 4) void k_p1(PackedView sv, int k, BloomView bf
         }
     }
     __syncthreads();
-    bool over = false;
     const RollConst rk = make_roll<W>(k, pow5_k, pow5_km1);
     uint32_t n_win = 0, n_ins = 0;
     for (uint64_t t0 = lo; t0 < hi; t0 += TW) {
@@ -648,6 +777,7 @@ __global__ __launch_bounds__(NT, 4) void k_p1(PackedView sv, int k, BloomView bf
                     n_ins += MODE == 0 ? ok[j] : 0;  // MODE 4: level 3 counts the gated insertions
                 }
             }
+            if constexpr (Out::kSeg && !Bin::kOwner) combine_repeats<OW, RUNW, MODE>(tk, ok, pb, ctr);
         } else {
             // rolled run: slot j <- the j-th symbol of the thread's run (static indices)
 #pragma unroll
@@ -671,7 +801,7 @@ __global__ __launch_bounds__(NT, 4) void k_p1(PackedView sv, int k, BloomView bf
             });
         }
         if constexpr (SCATTER) {
-            over |= scatter_tile<OW, RUNW, Bin, Out, NT>(l, F, bin, ob, tk, ok, out);
+            scatter_tile<OW, RUNW, Bin, Out, NT>(l, F, bin, ob, tk, ok, out);
         } else {
 #pragma unroll
             for (int j = 0; j < RUNW; j++)
@@ -685,7 +815,6 @@ __global__ __launch_bounds__(NT, 4) void k_p1(PackedView sv, int k, BloomView bf
     if constexpr (Out::kSeg) {  // segment fills (the scatter's last barrier ordered gbase)
         for (uint32_t b = tid; b < F; b += NT)
             pb.hist1[(uint64_t)b * pb.nblk1 + blockIdx.x] = (uint32_t)(l.gbase[b] - ob.start(b));
-        if (over) atomicOr(&ctr->part_overflow, 1ULL);
     }
     // routing (owner bins) counts windows here and insertions at the owner; the Bloom
     // pass counts its windows apart
@@ -700,12 +829,25 @@ __global__ __launch_bounds__(NT, 4) void k_p1(PackedView sv, int k, BloomView bf
 
 // Level 1 over a key array (keys received from other shards): [0, n) split over nblk1
 // blocks, bins = the coarse bins of the table key.
+// Item count on the device (the spill list of a segmented batch): dn != nullptr ->
+// n = min(*dn, cap), or 0 once the batch's overflow flag is up (the whole batch is redone).
+struct DevN {
+    const unsigned long long* dn;
+    uint64_t cap;
+    const unsigned long long* ovf;
+};
+DEV uint64_t item_count(uint64_t n, const DevN& d) {
+    if (!d.dn) return n;
+    return *d.ovf ? 0 : min((uint64_t)*d.dn, d.cap);
+}
+
 template <int W, bool SCATTER>
-__global__ __launch_bounds__(COUNT_THREADS, 4) void k_p1k(const uint64_t* __restrict__ in, uint64_t n, PartBufs pb,
+__global__ __launch_bounds__(COUNT_THREADS, 4) void k_p1k(const uint64_t* __restrict__ in, uint64_t n_host, PartBufs pb,
                                                        uint32_t F, BinRegion bin, DevCounters* __restrict__ ctr,
-                                                       int cnt_word) {
+                                                       int cnt_word, DevN dn) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int RUNW = run_w<W>(), TW = tile_win<W>();
+    const uint64_t n = item_count(n_host, dn);
     const PartLds l = part_lds(smem, F);
     const int tid = threadIdx.x;
     const uint64_t per = ((n + pb.nblk1 - 1) / pb.nblk1 + TW - 1) / TW * TW;
@@ -745,6 +887,7 @@ __global__ __launch_bounds__(COUNT_THREADS, 4) void k_p1k(const uint64_t* __rest
         __syncthreads();
         for (uint32_t b = tid; b < F; b += COUNT_THREADS) pb.hist1[(uint64_t)b * pb.nblk1 + blockIdx.x] = l.hist[b];
         if (cnt_word < 0) added = blockIdx.x == 0 && tid == 0 ? n : 0;
+        if (dn.dn) added = 0;  // spilled windows: counted by level 1 (or at level 3 behind the gate)
         block_add4(added, n_inv, 0, 0, &ctr->inserted, &ctr->invalid, nullptr, nullptr);
     }
 }
@@ -911,7 +1054,8 @@ __global__ __launch_bounds__(NT, 2048 / NT) void k_p2f(TableView tv, PartBufs pb
     const uint32_t s_lo = (uint32_t)((uint64_t)j * pb.nblk1 / pb.B2);
     const uint32_t nseg = (uint32_t)((uint64_t)(j + 1) * pb.nblk1 / pb.B2) - s_lo;
     const uint64_t seg0 = (uint64_t)c * pb.nblk1 + s_lo;  // level-1 segment index of cursor 0
-    const OutSeg o{(uint64_t)pb.B2 * pb.cap2, ((uint64_t)c * F * pb.B2 + j) * pb.cap2, pb.cap2};
+    const OutSeg o{(uint64_t)pb.B2 * pb.cap2, ((uint64_t)c * F * pb.B2 + j) * pb.cap2, pb.cap2,
+                   pb.spill, pb.spill_cap, &ctr->spill_n, &ctr->part_overflow};
     for (uint32_t i = tid; i <= nseg; i += NT) pre[i] = i < nseg ? pb.hist1[seg0 + i] : 0;
     for (uint32_t b = tid; b < F; b += NT) {
         l.hist[b] = 0;
@@ -920,7 +1064,6 @@ __global__ __launch_bounds__(NT, 2048 / NT) void k_p2f(TableView tv, PartBufs pb
     __syncthreads();
     block_excl_scan_lds<NT>(pre, pre, nseg + 1);  // in place; pre[nseg] = total
     const uint32_t total = pre[nseg];
-    bool over = false;
     // segment cursor of this thread (its indices grow monotonically): segment cs holds
     // [cb, nb) of the virtual run, both bounds kept in registers
     uint32_t cs = 0, cb = 0, nb = nseg ? pre[1] : 0;
@@ -951,14 +1094,13 @@ __global__ __launch_bounds__(NT, 2048 / NT) void k_p2f(TableView tv, PartBufs pb
         // the next tile is loaded into the same registers as soon as this tile's keys sit
         // in LDS, so its loads overlap this tile's write-out (barriers wait for LDS only)
         const bool more = t0 + TW < total;
-        over |= scatter_tile<W, RUNW, BinRegion, OutSeg, NT>(l, F, bin, o, tk, ok, pb.keys2, [&]() {
+        scatter_tile<W, RUNW, BinRegion, OutSeg, NT>(l, F, bin, o, tk, ok, pb.keys2, [&]() {
             if (KC_PREFETCH && more) load_tile(t0 + TW, tk, ok);
         });
         if (!KC_PREFETCH && more) load_tile(t0 + TW, tk, ok);
     }
     for (uint32_t b = tid; b < F; b += NT)
         pb.hist2[((uint64_t)c * F + b) * pb.B2 + j] = (uint32_t)(l.gbase[b] - o.start(b));
-    if (over) atomicOr(&ctr->part_overflow, 1ULL);
 }
 
 // LDS image of a region: the 16-byte chunks of each 128-byte bucket are XOR-swizzled
@@ -1846,6 +1988,71 @@ static hipError_t part_level1(PackedView sym, int k, BloomView bf, DevCounters* 
     return hipGetLastError();
 }
 
+// The skew lists of a segmented batch, after its level 3 (item counts on the device):
+//  spill: keys that overflowed a segment (W words each; the Bloom pass: word 0) through
+//         the exact pipeline (levels 1-3 by histogram offsets, no capacity limits);
+//  heavy: {key, count} records of repeated windows (count passes), added by direct
+//         inserts, behind the Bloom gate in the gated pass.
+template <int W, bool GATE>
+static hipError_t insert_spill(TableView t, BloomView bf, DevCounters* ctr, PartBufs pb, hipStream_t s) {
+    const BinRegion bin = coarse_bins(t);
+    const size_t sm1 = part_smem<W>(t.F1), sm1h = hist_smem(t.F1);
+    hipError_t e;
+    if ((e = set_smem(k_p1k<W, false>, sm1h)) != hipSuccess) return e;
+    if ((e = set_smem(k_p1k<W, true>, sm1)) != hipSuccess) return e;
+    const DevN dn{&ctr->spill_n, pb.spill_cap, &ctr->part_overflow};
+    hipLaunchKernelGGL((k_p1k<W, false>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1h, s, pb.spill, (uint64_t)0, pb,
+                       t.F1, bin, ctr, -1, dn);
+    launch_scan(pb.hist1, (uint64_t)t.F1 * pb.nblk1, pb.off1, pb.bsum, s);
+    hipLaunchKernelGGL((k_p1k<W, true>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1, s, pb.spill, (uint64_t)0, pb,
+                       t.F1, bin, ctr, -1, dn);
+    return part_levels23<W, false, GATE>(t, ctr, pb, s, nullptr, 0, bf);
+}
+
+// direct insert of the heavy records (grid-stride: the count is on the device); gated pass:
+// a record counts only if its key passes the Bloom gate, and then adds to `inserted`
+constexpr int HEAVY_BLOCKS = 512;
+template <int W, bool GATE>
+__global__ __launch_bounds__(COUNT_THREADS) void k_insert_heavy(const uint64_t* __restrict__ rec, uint64_t cap,
+                                                                TableView tv, BloomView bf,
+                                                                DevCounters* __restrict__ ctr) {
+    const uint64_t n = ctr->part_overflow ? 0 : min((uint64_t)ctr->heavy_n, cap);
+    uint32_t n_fail = 0;
+    unsigned long long added = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * COUNT_THREADS + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * COUNT_THREADS) {
+        uint64_t tk[W];
+#pragma unroll
+        for (int w = 0; w < W; w++) tk[w] = rec[i * (W + 1) + w];
+        const uint64_t c = rec[i * (W + 1) + W];
+        if constexpr (GATE) {
+            if (!block_gate(bloom_block_ptr(bf, tk[0]) + 8, tk[0], bf.nh_gate)) continue;
+            added += c;
+        }
+        if (!table_insert<W>(tv, tk, c)) n_fail++;
+    }
+    block_add4(added, n_fail, 0, 0, &ctr->inserted, &ctr->overflow, nullptr, nullptr);
+}
+template <int W, bool GATE>
+static hipError_t insert_heavy(TableView t, BloomView bf, DevCounters* ctr, PartBufs pb, hipStream_t s) {
+    hipLaunchKernelGGL((k_insert_heavy<W, GATE>), dim3(HEAVY_BLOCKS), dim3(COUNT_THREADS), 0, s, pb.heavy,
+                       pb.heavy_cap, t, bf, ctr);
+    return hipGetLastError();
+}
+
+// batch bookkeeping of the skew lists: begin = clear the batch's flag and list counts,
+// end = add the lists' lengths to the job totals
+static __global__ void k_batch_begin(DevCounters* ctr) {
+    ctr->part_overflow = 0;
+    ctr->spill_n = 0;
+    ctr->heavy_n = 0;
+}
+static __global__ void k_batch_end(DevCounters* ctr, uint64_t spill_cap, uint64_t heavy_cap) {
+    if (ctr->part_overflow) return;
+    ctr->spilled += min((uint64_t)ctr->spill_n, spill_cap);
+    ctr->heavy += min((uint64_t)ctr->heavy_n, heavy_cap);
+}
+
 // Segmented pipeline (pb.cap1 != 0): p1 -> p2f -> p3<SEG>, each a single pass; then
 // the exact pipeline behind the overflow gate (its kernels return at once unless a
 // segment overflowed, in which case the segmented p3 left the table untouched).
@@ -1860,7 +2067,7 @@ static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf
     }
     hipError_t e;
     const unsigned long long* gate = &ctr->part_overflow;
-    if ((e = hipMemsetAsync(&ctr->part_overflow, 0, sizeof(ctr->part_overflow), s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_batch_begin, dim3(1), dim3(1), 0, s, ctr);
     const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
     auto k1 = k_p1<W, MODE, true, BinRegion, OutSeg, scatter_threads<W>()>;
     static const uint32_t p2f_pad = [] {  // A/B knob: reserve LDS as if for this many segments
@@ -1871,11 +2078,19 @@ static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf
                  sm2 = p2f_smem<W, p2f_threads<W>()>(t.F2, std::max<uint32_t>(p2f_pad, (pb.nblk1 + pb.B2 - 1) / pb.B2));
     if ((e = set_smem(k1, sm1)) != hipSuccess) return e;
     if ((e = set_smem(k_p2f<W, p2f_threads<W>()>, sm2)) != hipSuccess) return e;
-    const OutSeg o1{(uint64_t)pb.nblk1 * pb.cap1, 0, pb.cap1};
+    const OutSeg o1{(uint64_t)pb.nblk1 * pb.cap1, 0, pb.cap1, pb.spill, pb.spill_cap, &ctr->spill_n,
+                    &ctr->part_overflow};
     hipLaunchKernelGGL(k1, dim3(pb.nblk1), dim3(scatter_threads<W>()), sm1, s, sym, k, bf, ctr, pb, t.F1, coarse_bins(t),
                        pb.keys1, pk, pkm1, o1, (const unsigned long long*)nullptr, 1);
     hipLaunchKernelGGL((k_p2f<W, p2f_threads<W>()>), dim3(t.F1 * pb.B2), dim3(p2f_threads<W>()), sm2, s, t, pb, ctr);
     if ((e = launch_p3<W, true, false, GATE3>(t, ctr, pb, nullptr, fresh, s, bf)) != hipSuccess) return e;
+    // the skew lists (MODE 2 rolls its windows: no heavy records); the segmented level 3
+    // wrote every region of a fresh table, so these read the table
+    if ((e = insert_spill<W, GATE3>(t, bf, ctr, pb, s)) != hipSuccess) return e;
+    if (MODE != 2 && (e = insert_heavy<W, GATE3>(t, bf, ctr, pb, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_batch_end, dim3(1), dim3(1), 0, s, ctr, pb.spill_cap, pb.heavy_cap);
+    // a full spill or heavy list: the exact pipeline redoes the batch (the segmented levels
+    // and the lists left the table untouched)
     if ((e = part_level1<W, MODE>(sym, k, bf, ctr, pb, t.F1, coarse_bins(t), pb.keys1, s, gate)) != hipSuccess)
         return e;
     return part_levels23<W, false, GATE3>(t, ctr, pb, s, gate, fresh, bf);
@@ -1905,18 +2120,35 @@ static hipError_t bloom_part_w(PackedView sym, int k, BloomView bf, TableView ft
     }
     hipError_t e;
     const unsigned long long* gate = &ctr->part_overflow;
-    if ((e = hipMemsetAsync(&ctr->part_overflow, 0, sizeof(ctr->part_overflow), s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_batch_begin, dim3(1), dim3(1), 0, s, ctr);
     const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
     constexpr int NT = scatter_threads<W>(), NT2 = p2f_threads<1>();
     auto k1 = k_p1<W, 3, true, BinRegion, OutSeg, NT>;
     const size_t sm1 = part_smem<1, NT>(ft.F1), sm2 = p2f_smem<1, NT2>(ft.F2, (pb.nblk1 + pb.B2 - 1) / pb.B2);
     if ((e = set_smem(k1, sm1)) != hipSuccess) return e;
     if ((e = set_smem(k_p2f<1, NT2>, sm2)) != hipSuccess) return e;
-    const OutSeg o1{(uint64_t)pb.nblk1 * pb.cap1, 0, pb.cap1};
+    const OutSeg o1{(uint64_t)pb.nblk1 * pb.cap1, 0, pb.cap1, pb.spill, pb.spill_cap, &ctr->spill_n,
+                    &ctr->part_overflow};
     hipLaunchKernelGGL(k1, dim3(pb.nblk1), dim3(NT), sm1, s, sym, k, bf, ctr, pb, ft.F1, coarse_bins(ft), pb.keys1, pk,
                        pkm1, o1, (const unsigned long long*)nullptr, 1);
     hipLaunchKernelGGL((k_p2f<1, NT2>), dim3(ft.F1 * pb.B2), dim3(NT2), sm2, s, ft, pb, ctr);
     if ((e = launch_b3<true>(bf, ft, ctr, pb, nullptr, fresh, s)) != hipSuccess) return e;
+    // spilled keys (table key word 0) through the exact levels into the filter regions
+    {
+        const BinRegion bin = coarse_bins(ft);
+        const size_t s1 = part_smem<1>(ft.F1), s1h = hist_smem(ft.F1);
+        if ((e = set_smem(k_p1k<1, false>, s1h)) != hipSuccess) return e;
+        if ((e = set_smem(k_p1k<1, true>, s1)) != hipSuccess) return e;
+        const DevN dn{&ctr->spill_n, pb.spill_cap, &ctr->part_overflow};
+        hipLaunchKernelGGL((k_p1k<1, false>), dim3(pb.nblk1), dim3(COUNT_THREADS), s1h, s, pb.spill, (uint64_t)0, pb,
+                           ft.F1, bin, ctr, -1, dn);
+        launch_scan(pb.hist1, (uint64_t)ft.F1 * pb.nblk1, pb.off1, pb.bsum, s);
+        hipLaunchKernelGGL((k_p1k<1, true>), dim3(pb.nblk1), dim3(COUNT_THREADS), s1, s, pb.spill, (uint64_t)0, pb,
+                           ft.F1, bin, ctr, -1, dn);
+        if ((e = part_level2_exact<1>(ft, pb, s, nullptr)) != hipSuccess) return e;
+        if ((e = launch_b3<false>(bf, ft, ctr, pb, nullptr, 0, s)) != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_batch_end, dim3(1), dim3(1), 0, s, ctr, pb.spill_cap, (uint64_t)0);
     if ((e = part_level1<W, 3>(sym, k, bf, ctr, pb, ft.F1, coarse_bins(ft), pb.keys1, s, gate)) != hipSuccess)
         return e;
     if ((e = part_level2_exact<1>(ft, pb, s, gate)) != hipSuccess) return e;
@@ -1942,12 +2174,13 @@ static hipError_t insert_items_part(const uint64_t* items, uint64_t n, TableView
     if ((e = set_smem(k_p1k<IW, true>, sm1)) != hipSuccess) return e;
     const int cw = CNT ? W : -1;
     hipLaunchKernelGGL((k_p1k<IW, false>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1h, s, items, n, pb, t.F1, bin, ctr,
-                       cw);
+                       cw, DevN{});
     launch_scan(pb.hist1, (uint64_t)t.F1 * pb.nblk1, pb.off1, pb.bsum, s);
     hipLaunchKernelGGL((k_p1k<IW, true>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1, s, items, n, pb, t.F1, bin, ctr,
-                       cw);
+                       cw, DevN{});
     return part_levels23<W, CNT>(t, ctr, pb, s, nullptr, fresh);
 }
+
 
 template <int W>
 static hipError_t insert_keys_w(const uint64_t* keys, uint64_t n, bool partitioned, TableView t, DevCounters* ctr,

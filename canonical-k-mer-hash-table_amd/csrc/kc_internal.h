@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/kc_api.h"
+
 namespace kc {
 
 // Staged-batch geometry.  Each reference chunk (text_reader.h:17-36) is placed at a
@@ -69,6 +71,12 @@ struct DevCounters {
     unsigned long long invalid;         uint64_t _p10[15];  // received keys with word 0 == 0 (skipped)
     unsigned long long part_overflow;   uint64_t _p11[15];  // a fixed-capacity segment overflowed (this batch)
     unsigned long long part_fallbacks;  uint64_t _p12[15];  // batches redone on the exact layout
+    // skew (segmented batches): keys that did not fit their segment go to a spill list, and
+    // repeated windows go to a heavy list as {key, count} records (this batch / in total)
+    unsigned long long spill_n;         uint64_t _p13[15];
+    unsigned long long heavy_n;         uint64_t _p14[15];
+    unsigned long long spilled;         uint64_t _p15[15];
+    unsigned long long heavy;           uint64_t _p16[15];
 };
 
 // The symbol stream: 32 symbols per word, symbol j of word w at bits 62-2j of pk[w]
@@ -103,6 +111,10 @@ struct PartBufs {
     uint64_t cap1, cap2;    // segmented layout: keys per segment of levels 1 / 2 (0 = exact layout)
     const uint64_t* seg_start;  // level 3 over runs at arbitrary offsets ([R][B2] first items;
                                 // nullptr = fixed-capacity segments of cap2)
+    uint64_t* spill;        // segmented batches: keys that overflowed their segment (spill_cap keys)
+    uint64_t spill_cap;
+    uint64_t* heavy;        // segmented count passes: {key words, count} records of repeated windows
+    uint64_t heavy_cap;
 };
 
 struct BloomView {
@@ -184,7 +196,8 @@ hipError_t launch_text(TableView t, int count_mode, uint64_t a, int k, uint64_t 
                        const uint64_t* off, uint64_t base, uint8_t* out, size_t lds, hipStream_t s);
 hipError_t launch_xxh64(const uint64_t* v, const uint64_t* seed, uint64_t n, uint64_t* out, hipStream_t s);
 hipError_t launch_synth(uint8_t* dst, uint64_t first_read, uint64_t n_reads, uint64_t seed, uint64_t genome_len,
-                        uint32_t read_len, uint32_t wrap, double err_rate, double n_rate, hipStream_t s);
+                        uint32_t read_len, uint32_t wrap, double err_rate, double n_rate, const kc_synth_skew* skew,
+                        hipStream_t s);
 
 // ---- per-key-width entry points (kc_count_impl.h, one translation unit per W) ------------------
 template <int W>

@@ -28,6 +28,14 @@ typedef struct {
     uint32_t wrap;         /* 0 = single-line sequence, else columns per line */
     double err_rate;       /* substitution rate */
     double n_rate;         /* rate of 'N' symbols */
+    /* skewed workloads (all 0 = the uniform SURVEY.md 8d generator): a fraction of the
+     * reads are homopolymers (poly-A, or poly-T when reverse-complemented) or (CA)n
+     * dinucleotide repeats, and the genome carries `repeat_copies` copies of one
+     * `repeat_len`-base repeat evenly spaced over it */
+    double homo_frac;
+    double dinuc_frac;
+    uint32_t repeat_len;
+    uint32_t repeat_copies;
 } kc_synth_params;
 
 KC_HD uint64_t kcs_mix(uint64_t x) {
@@ -46,20 +54,39 @@ KC_HD uint64_t kcs_mulhi(uint64_t a, uint64_t b) {
     return (uint64_t)(((unsigned __int128)a * b) >> 64);
 #endif
 }
-/* genome base p: 32 bases per 64-bit random word */
-KC_HD int kcs_genome_base(uint64_t seed, uint64_t p) {
-    return (int)((kcs_rand(seed, 1, p >> 5, 0) >> (2 * (p & 31))) & 3);
+/* genome base p: 32 bases per 64-bit random word; inside a copy of the repeat, the
+ * repeat's base (its own random stream) */
+KC_HD int kcs_genome_base(const kc_synth_params *g, uint64_t p) {
+    if (g->repeat_copies && g->repeat_len) {
+        const uint64_t spacing = g->genome_len / g->repeat_copies;
+        const uint64_t off = spacing ? p % spacing : 0;
+        if (spacing >= g->repeat_len && off < g->repeat_len && p / spacing < g->repeat_copies)
+            return (int)((kcs_rand(g->seed, 6, off >> 5, 0) >> (2 * (off & 31))) & 3);
+    }
+    return (int)((kcs_rand(g->seed, 1, p >> 5, 0) >> (2 * (p & 31))) & 3);
 }
 KC_HD uint64_t kcs_thresh(double rate) {
     if (rate <= 0.0) return 0;
     if (rate >= 1.0) return ~0ULL;
     return (uint64_t)(rate * 18446744073709551616.0);
 }
+KC_HD uint64_t kcs_thresh(double rate);
+/* read kind: 0 genome, 1 homopolymer, 2 (CA)n */
+KC_HD int kcs_read_kind(const kc_synth_params *p, uint64_t i) {
+    if (p->homo_frac <= 0.0 && p->dinuc_frac <= 0.0) return 0;
+    const uint64_t u = kcs_rand(p->seed, 7, i, 0);
+    if (u < kcs_thresh(p->homo_frac)) return 1;
+    if (u - kcs_thresh(p->homo_frac) < kcs_thresh(p->dinuc_frac)) return 2;
+    return 0;
+}
 /* base j (0..L-1) of read i, as 0..3 or 4 = 'N' */
 KC_HD int kcs_read_base(const kc_synth_params *p, uint64_t i, uint32_t j, uint64_t start, int rc,
                         uint64_t e_th, uint64_t n_th) {
-    int b = rc ? 3 - kcs_genome_base(p->seed, start + (p->read_len - 1 - j))
-               : kcs_genome_base(p->seed, start + j);
+    const int kind = kcs_read_kind(p, i);
+    int b;
+    if (kind == 1) b = rc ? 3 : 0;                                     /* poly-A / poly-T */
+    else if (kind == 2) b = ((j + (uint32_t)(start & 1)) & 1) ? 0 : 1;  /* CACA... / ACAC... */
+    else b = rc ? 3 - kcs_genome_base(p, start + (p->read_len - 1 - j)) : kcs_genome_base(p, start + j);
     if (e_th && kcs_rand(p->seed, 3, i, j) < e_th) b = (b + 1 + (int)(kcs_rand(p->seed, 4, i, j) % 3)) & 3;
     if (n_th && kcs_rand(p->seed, 5, i, j) < n_th) b = 4;
     return b;

@@ -454,8 +454,15 @@ hipError_t launch_tokenize(const uint8_t* src, uint64_t ntiles, const ChunkDesc*
 }
 
 hipError_t launch_synth(uint8_t* dst, uint64_t first_read, uint64_t n_reads, uint64_t seed, uint64_t genome_len,
-                        uint32_t read_len, uint32_t wrap, double err_rate, double n_rate, hipStream_t s) {
-    kc_synth_params p;
+                        uint32_t read_len, uint32_t wrap, double err_rate, double n_rate, const kc_synth_skew* sk,
+                        hipStream_t s) {
+    kc_synth_params p{};
+    if (sk) {
+        p.homo_frac = sk->homo_frac;
+        p.dinuc_frac = sk->dinuc_frac;
+        p.repeat_len = sk->repeat_len;
+        p.repeat_copies = sk->repeat_copies;
+    }
     p.seed = seed;
     p.genome_len = genome_len;
     p.n_reads = first_read + n_reads;

@@ -46,7 +46,7 @@ EXPORTS = (
     "kc_write", "kc_key_words", "kc_free", "kc_plan_chunks", "kc_synth_bytes", "kc_synth_device",
     "kc_reset", "kc_profile", "kc_get_timing", "kc_route_device", "kc_insert_keys_device",
     "kc_route_table_device", "kc_insert_counts_device", "kc_clear_table", "kc_insert_counts_runs_device",
-    "kc_xxh64", "kc_bloom_info", "kc_bloom_read", "kc_bloom_write",
+    "kc_xxh64", "kc_bloom_info", "kc_bloom_read", "kc_bloom_write", "kc_synth_skew_device",
 )
 
 
@@ -74,10 +74,15 @@ class kc_timing(ctypes.Structure):
                 ("launches", ctypes.c_uint64), ("symbols", ctypes.c_uint64)]
 
 
+class kc_synth_skew(ctypes.Structure):
+    _fields_ = [("homo_frac", ctypes.c_double), ("dinuc_frac", ctypes.c_double),
+                ("repeat_len", ctypes.c_uint32), ("repeat_copies", ctypes.c_uint32)]
+
+
 class kc_stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in (
         "windows", "inserted", "distinct", "table_slots", "bf_windows", "bf_bits", "new_in_first",
-        "new_in_second", "failed_in_first", "chunks", "bytes", "part_fallbacks")]
+        "new_in_second", "failed_in_first", "chunks", "bytes", "part_fallbacks", "spilled", "heavy_records")]
 
     def as_dict(self) -> dict:
         return {n: int(getattr(self, n)) for n, _ in self._fields_}
@@ -137,6 +142,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "kc_synth_device": (I32, [P, U64, U64, U64, U64, ctypes.c_uint32, ctypes.c_uint32,
                                   ctypes.c_double, ctypes.c_double, P]),
         "kc_xxh64": (I32, [P, P, U64, P]),
+        "kc_synth_skew_device": (I32, [P, U64, U64, U64, U64, ctypes.c_uint32, ctypes.c_uint32,
+                                       ctypes.c_double, ctypes.c_double, ctypes.POINTER(kc_synth_skew), P]),
         "kc_bloom_info": (I32, [P, ctypes.POINTER(U64), ctypes.POINTER(U64), ctypes.POINTER(I32),
                                 ctypes.POINTER(I32), ctypes.POINTER(I32)]),
         "kc_bloom_read": (I32, [P, P, U64]),

@@ -1,6 +1,7 @@
 /*
  * kc_gen -- CPU synthetic read generator (bench/test input tool).
  *   kc_gen OUT N L G [-s SEED] [-e ERR] [-n NRATE] [-w WRAP] [--first R0 --count RC] [--plain]
+ *          [--homo FRAC] [--dinuc FRAC] [--repeat LEN COPIES]   (skewed workloads, kc_synth.h)
  * Writes FASTA records ">r<i>\n<seq>\n" (or plain "<seq>\n" lines with --plain)
  * identical to the device generator kc_synth_device() for the same parameters.
  */
@@ -31,6 +32,12 @@ int main(int argc, char **argv) {
         else if (!strcmp(argv[i], "--first")) first = strtoull(argv[++i], 0, 10);
         else if (!strcmp(argv[i], "--count")) count = strtoull(argv[++i], 0, 10);
         else if (!strcmp(argv[i], "--plain")) plain = 1;
+        else if (!strcmp(argv[i], "--homo")) p.homo_frac = atof(argv[++i]);
+        else if (!strcmp(argv[i], "--dinuc")) p.dinuc_frac = atof(argv[++i]);
+        else if (!strcmp(argv[i], "--repeat")) {
+            p.repeat_len = (uint32_t)atoi(argv[++i]);
+            p.repeat_copies = (uint32_t)atoi(argv[++i]);
+        }
         else { fprintf(stderr, "unknown option %s\n", argv[i]); return 2; }
     }
     if (p.genome_len < p.read_len) { fprintf(stderr, "G < L\n"); return 2; }

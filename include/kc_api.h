@@ -83,7 +83,9 @@ typedef struct {
     uint64_t failed_in_first;
     uint64_t chunks;          /* chunks processed by the counting pass */
     uint64_t bytes;           /* input bytes processed by the counting pass */
-    uint64_t part_fallbacks;  /* partitioned batches redone on the exact layout (segment overflow) */
+    uint64_t part_fallbacks;  /* partitioned batches redone on the exact layout (a full skew list) */
+    uint64_t spilled;         /* keys past their segment's end, inserted through the exact levels */
+    uint64_t heavy_records;   /* {k-mer, count} records of repeated windows (homopolymer runs) */
 } kc_stats;
 
 /* Creates the device table (PointerHashTableCanonicalAV ctor,
@@ -194,6 +196,14 @@ void kc_free(void* p);
 int kc_plan_chunks(const uint8_t* image, uint64_t size, int k, uint64_t chunk_size, int fmt, kc_chunk** chunks,
                    uint64_t* n_chunks);
 
+/* The reference's table size for a minimum of `min_slots` slots: the next prime that is
+ * 3 mod 4 (next_prime3mod4, functions_math.cpp:53-96; "Hash table size is:").  The device
+ * table keeps 25 % headroom over it (open addressing inside LDS-sized regions), so a job
+ * whose distinct k-mers fall between the two succeeds where the reference exits with
+ * "Hash table is full"; with KC_STRICT_CAPACITY=1 in the environment (CLI:
+ * --strict-capacity) kc_finish returns KC_ERR_TABLE_FULL there too. */
+uint64_t kc_table_size_reference(uint64_t min_slots);
+
 /* Test hooks for the Bloom filter (not on the reference's path).
  * kc_xxh64: XXH64(&values[i], 8, seeds[i]) computed by the device function the
  *   reference-layout Bloom passes use (calculate_hashes, double_bloomfilter.hpp:276-281;
@@ -214,6 +224,18 @@ int kc_bloom_write(kc_ctx* ctx, const uint32_t* words, uint64_t n_words);
 uint64_t kc_synth_bytes(uint64_t first_read, uint64_t n_reads, uint32_t read_len, uint32_t wrap);
 int kc_synth_device(uint8_t* dev_dst, uint64_t first_read, uint64_t n_reads, uint64_t seed, uint64_t genome_len,
                     uint32_t read_len, uint32_t wrap, double err_rate, double n_rate, void* hip_stream);
+/* Skewed variant (bench workloads and skew tests; kc_gen --homo/--dinuc/--repeat):
+ * fractions of homopolymer and (CA)n reads, and a repeat of repeat_len bases present
+ * repeat_copies times in the genome. */
+typedef struct {
+    double homo_frac;
+    double dinuc_frac;
+    uint32_t repeat_len;
+    uint32_t repeat_copies;
+} kc_synth_skew;
+int kc_synth_skew_device(uint8_t* dev_dst, uint64_t first_read, uint64_t n_reads, uint64_t seed, uint64_t genome_len,
+                         uint32_t read_len, uint32_t wrap, double err_rate, double n_rate, const kc_synth_skew* skew,
+                         void* hip_stream);
 
 #ifdef __cplusplus
 }

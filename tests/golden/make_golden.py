@@ -43,6 +43,11 @@ INPUTS = {
     "big_edge.fasta": {"edge": [7, 16000, 2000, 400, 0.002, False], "commit": False},
     "big_reads.fasta": {"gen": ["150000", "150", "2000000", "-s", "9", "-e", "0.002", "-w", "60"],
                         "commit": False},
+    # skew: 5 % poly-A/T reads, 3 % (CA)n reads, a 300-bp repeat in 300 copies of the genome
+    "skew.fasta": {"gen": ["20000", "150", "300000", "-s", "11", "-e", "0.001", "--homo", "0.05", "--dinuc", "0.03",
+                           "--repeat", "300", "300"], "commit": False},
+    "big_skew.fasta": {"gen": ["100000", "150", "1000000", "-s", "12", "-e", "0.001", "--homo", "0.05",
+                               "--dinuc", "0.03", "--repeat", "300", "1000"], "commit": False},
 }
 
 CASES = [
@@ -86,6 +91,13 @@ CASES = [
     ("long.fasta", 255, ["-b", "-u", "300000", "-f", "0.05", "-a", "2"]),
     ("edge.fasta", 140, ["-a", "1", "-s", "1000000"]),
     ("big_edge.fasta", 161, ["-a", "1", "-s", "8000000"]),
+    # skew (hot keys: homopolymers, dinucleotide repeats, a high-copy repeat)
+    ("skew.fasta", 31, ["-a", "1", "-s", "4000000"]),
+    ("skew.fasta", 25, ["-m", "0", "-a", "1", "-s", "4000000"]),
+    ("skew.fasta", 51, ["-a", "2", "-s", "4000000"]),
+    ("skew.fasta", 31, ["-b", "-u", "3000000", "-a", "2"]),
+    ("big_skew.fasta", 31, ["-a", "2", "-s", "16000000"]),
+    ("big_skew.fasta", 63, ["-b", "-u", "12000000", "-a", "2"]),
 ]
 
 XXH_SEEDS = [2411, 3253, 1061, 1129, 2269, 7309, 3491, 8237, 6359, 8779, 0]

@@ -240,12 +240,17 @@ def test_counts_sum_to_windows_at_scale(insert_path):
 
 @pytest.mark.parametrize("name,k,args", [("reads_w60.fasta", 31, ["-a", "1", "-s", "1000000"]),
                                          ("reads_w60.fasta", 51, ["-m", "0", "-a", "2", "-s", "1000000"]),
-                                         ("long.fasta", 127, ["-a", "1", "-s", "1000000"])])
-def test_segment_overflow_falls_back_to_exact(name, k, args, golden_input, tmp_path, monkeypatch):
-    """Tiny forced segment capacities overflow: the device redoes the batch on the exact
-    layout (behind the overflow gate) and the result is still the reference's."""
+                                         ("long.fasta", 127, ["-a", "1", "-s", "1000000"]),
+                                         ("long.fasta", 200, ["-a", "1", "-s", "1000000"])])
+@pytest.mark.parametrize("spill", ["list", "full"])
+def test_segment_overflow_spills_or_falls_back(name, k, args, spill, golden_input, tmp_path, monkeypatch):
+    """Tiny forced segment capacities overflow.  spill=list: the keys past a segment's end
+    go to the spill list and are inserted through the exact levels after level 3;
+    spill=full: the spill list is too small too, so the device redoes the whole batch on
+    the exact layout (behind the overflow gate).  Either way the result is the reference's."""
     monkeypatch.setenv("KC_INSERT_PATH", "partitioned")
     monkeypatch.setenv("KC_SEG_CAP", "8")
+    monkeypatch.setenv("KC_SPILL_CAP", "64" if spill == "full" else str(1 << 24))
     path = golden_input(name)
     o = parse_ref_args(args)
     cfg = ka.Config(k=k, mode=o["mode"], min_abundance=o["min_abundance"], table_slots=o["table_slots"],
@@ -255,7 +260,10 @@ def test_segment_overflow_falls_back_to_exact(name, k, args, golden_input, tmp_p
         for off, ln, bh in ka.plan_chunks(data, k, ka.FMT_FASTA):
             kc.count_chunk(data[off:off + ln], ka.FMT_FASTA, bool(bh))
         st = kc.finish()
-        assert st["part_fallbacks"] >= 1
+        if spill == "full":
+            assert st["part_fallbacks"] >= 1
+        else:
+            assert st["part_fallbacks"] == 0 and st["spilled"] > 0
         lines = kc.lines()
     out = tmp_path / "oracle.txt"
     oracle_count(path, k, args, out)
@@ -357,16 +365,22 @@ def test_bloom_at_scale_equals_exact_solid_kmers(k, fpr, insert_path):
     assert np.array_equal(a, b)
 
 
-def test_bloom_segment_overflow_falls_back_to_exact(golden_input, tmp_path, monkeypatch):
-    """Forced tiny segments in the partitioned Bloom pass and the gated count pass: the
-    device redoes both on the exact layout and the result is still the reference's."""
+@pytest.mark.parametrize("spill", ["list", "full"])
+def test_bloom_segment_overflow_spills_or_falls_back(spill, golden_input, tmp_path, monkeypatch):
+    """Forced tiny segments in the partitioned Bloom pass and the gated count pass: spilled
+    keys go through the exact levels (spill=list), or both passes are redone on the exact
+    layout (spill=full); the result is still the reference's."""
     monkeypatch.setenv("KC_INSERT_PATH", "partitioned")
     monkeypatch.setenv("KC_SEG_CAP", "8")
+    monkeypatch.setenv("KC_SPILL_CAP", "64" if spill == "full" else str(1 << 24))
     path = golden_input("reads_w60.fasta")
     args = ["-b", "-u", "200000", "-a", "2"]
     kc, st = ka.count_file(path, 31, min_abundance=2, bf_enable=True, est_unique=200000, fpr=0.01)
     with kc:
-        assert st["part_fallbacks"] >= 2
+        if spill == "full":
+            assert st["part_fallbacks"] >= 2
+        else:
+            assert st["part_fallbacks"] == 0 and st["spilled"] > 0
         lines = kc.lines()
     out = tmp_path / "oracle.txt"
     oracle_count(path, 31, args, out)
@@ -405,3 +419,31 @@ def test_bloom_context_reused_for_a_larger_job(golden_input, tmp_path, insert_pa
         assert sorted_digest_lines(lines) == (big["sorted_sha256"], big["lines"])
         kc.reset()  # and back to a small job on the grown buffers
         assert _job(kc, small, big["k"]) == got
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if "skew" in c["input"]], ids=_case_id)
+@pytest.mark.parametrize("seg", ["default", "tiny"])
+def test_skewed_input_uses_the_skew_lists(case, seg, golden_input, tmp_path, monkeypatch):
+    """Hot keys (poly-A/T and (CA)n reads, a 300-bp repeat in hundreds of copies, reference
+    fixtures): the partitioned path collapses repeated windows into heavy {key, count}
+    records and spills what overflows a segment, without redoing the batch; with tiny
+    forced segments (seg=tiny) most keys take the spill list."""
+    monkeypatch.setenv("KC_INSERT_PATH", "partitioned")
+    if seg == "tiny":
+        monkeypatch.setenv("KC_SEG_CAP", "8")
+        monkeypatch.setenv("KC_SPILL_CAP", str(1 << 25))
+    path = golden_input(case["input"])
+    o = parse_ref_args(case["args"])
+    kc, st = ka.count_file(path, case["k"], mode=o["mode"], min_abundance=o["min_abundance"],
+                           table_slots=max(o["table_slots"], 1 << 16), bf_enable=o["bf_enable"],
+                           est_unique=o["est_unique"], fpr=o["fpr"])
+    with kc:
+        lines = kc.lines()
+    assert sorted_digest_lines(lines) == (case["sorted_sha256"], case["lines"])
+    # big_skew carries its repeat in 30 % of the genome: what overflows the segments may pass
+    # the spill list's capacity (an eighth of the windows), and then the batch is redone
+    if case["input"] == "skew.fasta":
+        assert st["part_fallbacks"] == 0
+    assert st["heavy_records"] > 0 or st["part_fallbacks"] > 0  # the homopolymer reads (a redone batch: none)
+    if seg == "tiny":
+        assert st["spilled"] > 0
