@@ -47,6 +47,7 @@ EXPORTS = (
     "kc_reset", "kc_profile", "kc_get_timing", "kc_route_device", "kc_insert_keys_device",
     "kc_route_table_device", "kc_insert_counts_device", "kc_clear_table", "kc_insert_counts_runs_device",
     "kc_xxh64", "kc_bloom_info", "kc_bloom_read", "kc_bloom_write", "kc_synth_skew_device",
+    "kc_table_size_reference",
 )
 
 
@@ -142,6 +143,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "kc_synth_device": (I32, [P, U64, U64, U64, U64, ctypes.c_uint32, ctypes.c_uint32,
                                   ctypes.c_double, ctypes.c_double, P]),
         "kc_xxh64": (I32, [P, P, U64, P]),
+        "kc_table_size_reference": (U64, [U64]),
         "kc_synth_skew_device": (I32, [P, U64, U64, U64, U64, ctypes.c_uint32, ctypes.c_uint32,
                                        ctypes.c_double, ctypes.c_double, ctypes.POINTER(kc_synth_skew), P]),
         "kc_bloom_info": (I32, [P, ctypes.POINTER(U64), ctypes.POINTER(U64), ctypes.POINTER(I32),
