@@ -86,9 +86,8 @@ struct kc_ctx {
     uint64_t* d_keys1 = nullptr;
     uint64_t* d_keys2 = nullptr;
     uint64_t k1_words = 0, k2_words = 0;  // u64 words the level-1 / level-2 key buffers hold
-    uint64_t* d_spill = nullptr;           // skew lists of a segmented batch (ensure_part_geo)
-    uint64_t* d_heavy = nullptr;
-    uint64_t spill_words = 0, heavy_words = 0;
+    uint64_t* d_spill = nullptr;           // skew list of a segmented batch (ensure_part_geo)
+    uint64_t spill_words = 0;
     bool table_fresh = false;  // the table is all zero (allocated / reset, nothing inserted since)
     uint64_t min_slots = 0;        // the job's -s (or 2 * new_in_second): the reference's table size
     bool strict_capacity = false;  // KC_STRICT_CAPACITY=1: fail past the reference's capacity
@@ -297,8 +296,17 @@ static int ensure_part_geo(kc_ctx* c, uint64_t syms, bool seg, const PartGeo& g,
         // the segment walks index a virtual run with 32-bit offsets
         if (nseg * cap1 >= (1ULL << 31) || (uint64_t)B2 * cap2 >= (1ULL << 31)) cap1 = cap2 = 0;
     }
-    const uint64_t need1 = std::max<uint64_t>(syms, (uint64_t)g.F1 * nblk1 * cap1) * g.IW;
-    const uint64_t need2 = std::max<uint64_t>(syms, g.R * B2 * cap2) * g.IW;
+    // the skew list of a segmented batch: {key words, count} records of keys past a segment's
+    // end and of repeated windows (Bloom pass: plain keys), an eighth of the windows before the
+    // batch falls back to the exact layout; its exact pipeline runs through the key buffers
+    uint64_t spill_cap = 0;
+    if (cap1) {
+        spill_cap = std::max<uint64_t>(1 << 16, syms / 8);
+        if (const char* v = std::getenv("KC_SPILL_CAP")) spill_cap = std::strtoull(v, 0, 10);  // tests
+    }
+    const uint64_t spill_words = spill_cap * (g.IW + 1);
+    const uint64_t need1 = std::max(std::max<uint64_t>(syms, (uint64_t)g.F1 * nblk1 * cap1) * g.IW, spill_words);
+    const uint64_t need2 = std::max(std::max<uint64_t>(syms, g.R * B2 * cap2) * g.IW, spill_words);
     auto grow = [&](uint64_t** buf, uint64_t* have, uint64_t need) -> int {
         if (need <= *have) return KC_OK;
         hipFree(*buf);
@@ -314,21 +322,9 @@ static int ensure_part_geo(kc_ctx* c, uint64_t syms, bool seg, const PartGeo& g,
     if (rc) return rc;
     rc = grow(&c->d_keys2, &c->k2_words, need2);
     if (rc) return rc;
-    // skew lists of a segmented batch: keys past a segment's end (an eighth of the windows
-    // before the batch falls back to the exact layout) and {key, count} records of repeated
-    // windows (a thirty-second)
-    uint64_t spill_cap = 0, heavy_cap = 0;
-    if (cap1) {
-        spill_cap = std::max<uint64_t>(1 << 16, syms / 8);
-        heavy_cap = std::max<uint64_t>(1 << 14, syms / 32);
-        if (const char* v = std::getenv("KC_SPILL_CAP")) spill_cap = std::strtoull(v, 0, 10);  // tests
-        if ((rc = grow(&c->d_spill, &c->spill_words, spill_cap * g.IW))) return rc;
-        if ((rc = grow(&c->d_heavy, &c->heavy_words, heavy_cap * (g.IW + 1)))) return rc;
-    }
+    if (spill_cap && (rc = grow(&c->d_spill, &c->spill_words, spill_words))) return rc;
     pb.spill = c->d_spill;
     pb.spill_cap = spill_cap;
-    pb.heavy = c->d_heavy;
-    pb.heavy_cap = heavy_cap;
     pb.keys1 = c->d_keys1;
     pb.keys2 = c->d_keys2;
     pb.nblk1 = nblk1;
@@ -669,7 +665,6 @@ void kc_destroy(kc_ctx* c) {
     hipFree(c->d_keys1);
     hipFree(c->d_keys2);
     hipFree(c->d_spill);
-    hipFree(c->d_heavy);
     hipFree(c->d_gstart);
     hipFree(c->d_mstart);
     hipFree(c->d_mlen);

@@ -431,8 +431,8 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_count(PackedView sv, int k, T
 // --------------------------------------------------------------------------------
 // partitioned path
 // --------------------------------------------------------------------------------
-// LDS of a scatter pass: hist, start, lim (u32 x F), gbase, dlt (u64 x F), then the keys
-constexpr size_t hist_smem(uint32_t F) { return ((size_t)F * 3 + 1) * 4 + 4 + (size_t)F * 16; }
+// LDS of a scatter pass: hist, start, lim, sp (u32 x F), gbase, dlt (u64 x F), then the keys
+constexpr size_t hist_smem(uint32_t F) { return (size_t)F * 32 + 16; }
 template <int W, int NT = COUNT_THREADS>
 constexpr size_t part_smem(uint32_t F) {
     return hist_smem(F) + (size_t)NT * run_w<W>() * 8 * W;
@@ -467,6 +467,7 @@ struct PartLds {
     uint32_t* hist;
     uint32_t* start;
     uint32_t* lim;
+    uint32_t* sp;  // keys past the output's end: count, then offset in the tile's spill allocation
     uint64_t* gbase;
     uint64_t* dlt;
     uint64_t* keys;
@@ -476,7 +477,8 @@ DEV PartLds part_lds(uint8_t* smem, uint32_t F) {
     l.hist = reinterpret_cast<uint32_t*>(smem);
     l.start = l.hist + F;
     l.lim = l.start + F;
-    l.gbase = reinterpret_cast<uint64_t*>(l.lim + F + (F & 1));
+    l.sp = l.lim + F;
+    l.gbase = reinterpret_cast<uint64_t*>(l.sp + F);
     l.dlt = l.gbase + F;
     l.keys = l.dlt + F;
     return l;
@@ -515,12 +517,15 @@ struct OutSeg {
     uint64_t stride;  // keys between the segments of bins b and b+1
     uint64_t base;    // first key of bin 0's segment for this workgroup
     uint64_t cap;     // keys per segment
-    // keys past a segment's end: appended to the spill list (inserted after level 3 by the
-    // exact pipeline); a full spill list raises the batch's overflow flag (whole-batch redo)
+    // keys past a segment's end: appended to the batch's skew list (inserted after level 3 by
+    // the exact pipeline); count passes append {key words, 1} records (the list also takes the
+    // heavy records of repeated windows), the Bloom pass plain keys.  A full list raises the
+    // batch's overflow flag (whole-batch redo).
     uint64_t* spill;
     uint64_t spill_cap;
     unsigned long long* spill_n;
     unsigned long long* overflow;
+    int rec;
     DEV uint64_t start(uint32_t b) const { return (uint64_t)b * stride + base; }
     DEV uint64_t room(uint32_t b, uint64_t gbase) const {
         const uint64_t end = start(b) + cap;
@@ -557,20 +562,6 @@ DEV uint64_t wave_append(bool want, unsigned long long* counter) {
     base = __shfl(base, leader, 64);
     return want ? base + lane_rank(m) : ~0ULL;
 }
-template <int W>
-DEV void spill_append(const OutSeg& o, bool want, const uint64_t (&key)[W]) {
-    const uint64_t pos = wave_append(want, o.spill_n);
-    if (!want) return;
-    if (pos < o.spill_cap) {
-#pragma unroll
-        for (int w = 0; w < W; w++) o.spill[pos * W + w] = key[w];
-    } else {
-        atomicOr(o.overflow, 1ULL);
-    }
-}
-template <int W>
-DEV void spill_append(const OutExact&, bool, const uint64_t (&)[W]) {}
-
 // Counting-sort the tile's keys (in registers: tk[j] valid where ok[j]) by bin into
 // LDS and write each bin as one contiguous run at gbase[bin].  The rank of a key inside
 // its bin comes back from the histogram atomic, so one LDS atomic per key suffices.
@@ -583,6 +574,7 @@ struct NoMid {
 template <int W, int RUNW, class Bin, class Out, int NT = COUNT_THREADS, class Mid = NoMid>
 DEV bool scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const Out& o, uint64_t (&tk)[RUNW][W],
                       bool (&ok)[RUNW], uint64_t* __restrict__ out, Mid&& mid = Mid()) {
+    __shared__ unsigned long long s_spbase;
     const int tid = threadIdx.x;
     uint32_t rank[RUNW];  // (the bins are recomputed below: one multiply, fewer registers)
 #pragma unroll
@@ -596,28 +588,53 @@ DEV bool scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const Out& o
 #pragma unroll
             for (int w = 0; w < W; w++) l.keys[slot * W + w] = tk[j][w];
         }
-    // per bin: destination minus tile slot, and the tile slots that fit the bin's output
+    // per bin: destination minus tile slot, the tile slots that fit the bin's output, and
+    // the keys past its end
+    bool spills = false;
     for (uint32_t b = tid; b < F; b += NT) {
         const uint32_t st = l.start[b], h = l.hist[b];
         const uint64_t g = l.gbase[b];
+        const uint32_t fit = (uint32_t)min((uint64_t)h, o.room(b, g));
         l.dlt[b] = g - st;
-        l.lim[b] = st + (uint32_t)min((uint64_t)h, o.room(b, g));
+        l.lim[b] = st + fit;
+        l.sp[b] = h - fit;
+        spills |= fit < h;
     }
     mid();
-    __syncthreads();
+    if constexpr (Out::kSeg) {
+        if (__syncthreads_or(spills)) {
+            // one allocation in the skew list for all the tile's spilled keys (a bin's spilled
+            // keys are the tail of its run in the tile)
+            const uint32_t last = l.sp[F - 1];
+            block_excl_scan_lds<NT>(l.sp, l.sp, F);
+            if (tid == 0) s_spbase = atomicAdd(o.spill_n, (unsigned long long)(l.sp[F - 1] + last));
+            __syncthreads();
+        }
+    } else {
+        __syncthreads();
+    }
     const uint32_t n = l.start[F - 1] + l.hist[F - 1];
     for (uint32_t i = tid; i < n; i += NT) {
         uint64_t key[W];
 #pragma unroll
         for (int w = 0; w < W; w++) key[w] = l.keys[i * W + w];
         const uint32_t b = bin(key[0]);
-        const bool fits = i < l.lim[b];
-        if (fits) {
+        const uint32_t lim = l.lim[b];
+        if (i < lim) {
             const uint64_t dst = l.dlt[b] + i;
 #pragma unroll
             for (int w = 0; w < W; w++) ks_store(out + dst * W + w, key[w]);
+        } else if constexpr (Out::kSeg) {
+            const uint64_t pos = s_spbase + l.sp[b] + (i - lim);
+            if (pos < o.spill_cap) {
+                uint64_t* r = o.spill + pos * (W + o.rec);
+#pragma unroll
+                for (int w = 0; w < W; w++) r[w] = key[w];
+                if (o.rec) r[W] = 1;
+            } else {
+                atomicOr(o.overflow, 1ULL);
+            }
         }
-        if constexpr (Out::kSeg) spill_append<W>(o, !fits, key);
     }
     __syncthreads();
     for (uint32_t b = tid; b < F; b += NT) {
@@ -628,84 +645,166 @@ DEV bool scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const Out& o
     return false;
 }
 
-// Repeated windows (homopolymer runs: poly-A tails, poly-G artefacts, ...).  One key
-// repeated millions of times would send all its copies into one level-2 segment and one
-// level-3 region (SURVEY 7 "hard parts"; the reference's hot spot is the increase_count CAS,
-// kmer.cpp:699).  Runs of equal keys among a thread's consecutive windows collapse to the
-// run's first window carrying the run's length, and at each window slot the lanes of the
-// wave that hold the first valid lane's key merge into that lane.  Count passes send
-// every item that counts more than one window to the heavy list as a {key words, count}
-// record (added to the table after level 3); the Bloom pass keeps two copies of a key
+// Repeated windows (homopolymer runs: poly-A tails, poly-G artefacts; dinucleotide
+// microsatellites).  One key repeated millions of times would send all its copies into one
+// level-2 segment and one level-3 region (SURVEY 7 "hard parts"; the reference's hot spot is
+// the increase_count CAS, kmer.cpp:699).  A window equal to a neighbour one or two windows
+// away (within the thread's run) leaves the key stream and is counted in a small LDS table
+// of the workgroup (the heavy table: HT keys with their counts); at the end of the
+// workgroup's range every entry becomes one {key, count} record of the batch's skew list,
+// inserted after level 3.  The Bloom pass keeps two copies of such a key instead
 // (insertion_process changes nothing after a k-mer's second insertion,
-// double_bloomfilter.hpp:371-413).  Waves without a run skip it after one ballot.
-template <int OW, int RUNW, int MODE>
-DEV void combine_repeats(uint64_t (&tk)[RUNW][OW], bool (&ok)[RUNW], const PartBufs& pb, DevCounters* ctr) {
-    uint32_t eqm = 0;  // bit j: windows j and j + 1 are valid and equal
-    bool per2 = false;  // a period-2 repeat ((CA)n): windows j and j + 2 equal
+// double_bloomfilter.hpp:371-413).  Waves without a repeat skip it after one ballot.
+constexpr int HT = 64;  // heavy-table entries per workgroup
+template <int OW>
+constexpr size_t heavy_smem() { return (size_t)HT * (OW + 1) * 8; }
+struct HeavyTab {
+    uint64_t* keys;  // HT x OW words (word 0 == 0: empty)
+    uint64_t* cnt;   // HT counts (READY | count once the key words are published)
+};
+template <int OW>
+DEV HeavyTab heavy_tab(uint8_t* p) {
+    HeavyTab h;
+    h.keys = reinterpret_cast<uint64_t*>(p);
+    h.cnt = h.keys + HT * OW;
+    return h;
+}
+DEV void heavy_clear(const HeavyTab& h, int words) {
+    for (int i = threadIdx.x; i < HT * words; i += blockDim.x) h.keys[i] = 0;
+}
+// add `add` windows of key into the table (all lanes of the wave call it; `active` lanes
+// insert).  Lanes whose key finds no room return true: the caller appends them to the list.
+template <int OW>
+DEV bool heavy_insert(const HeavyTab& h, const uint64_t (&key)[OW], bool active, uint64_t add) {
+    uint32_t e = (uint32_t)((key[0] * 0x9E3779B97F4A7C15ULL) >> 58) & (HT - 1);
+    int probes = 0;
+    bool done = !active, full = false;
+    while (__ballot(!done)) {
+        if (!done) {
+            uint64_t* kp = h.keys + e * OW;
+            uint64_t w0 = __hip_atomic_load(kp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            bool next = false;
+            if (w0 == EMPTY) {
+                const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long*>(kp), 0ULL,
+                                               (unsigned long long)key[0]);
+                if (old == EMPTY) {  // claimed: publish the other words, then the count
 #pragma unroll
-    for (int j = 0; j + 1 < RUNW; j++) {
-        bool e = ok[j] && ok[j + 1], e2 = j + 2 < RUNW && ok[j] && ok[j + 2];
+                    for (int w = 1; w < OW; w++)
+                        __hip_atomic_store(kp + w, key[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    atomicAdd(reinterpret_cast<unsigned long long*>(h.cnt + e), (unsigned long long)(READY + add));
+                    done = true;
+                }  // lost the slot: read it again
+            } else if (w0 == key[0]) {
+                const uint64_t c = __hip_atomic_load(h.cnt + e, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (c & READY) {
+                    bool eq = true;
 #pragma unroll
-        for (int w = 0; w < OW; w++) {
-            e = e && tk[j][w] == tk[j + 1][w];
-            if (j + 2 < RUNW) e2 = e2 && tk[j][w] == tk[j + 2][w];
-        }
-        eqm |= (uint32_t)e << j;
-        per2 |= e2;
-    }
-    // (the lanes of a wave hold windows 16 apart, so a period-2 run shows the same key at the
-    // same slot of every lane inside it: the wave merge below combines those)
-    if (__ballot(eqm != 0 || per2) == 0) return;
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int j = 0; j < RUNW; j++) {
-        const bool interior = j > 0 && ((eqm >> (j - 1)) & 1);
-        if constexpr (MODE == 3) {
-            // keep a run's first two windows
-            if (j > 1 && ((eqm >> (j - 2)) & 3) == 3) ok[j] = false;
-            const uint64_t v = __ballot(ok[j]);
-            if (!v) continue;
-            const int leader = __builtin_ctzll(v);
-            bool match = ok[j];
-#pragma unroll
-            for (int w = 0; w < OW; w++) match = match && tk[j][w] == __shfl(tk[j][w], leader, 64);
-            const uint64_t m = __ballot(match);
-            if (match && lane_rank(m) >= 2) ok[j] = false;  // the wave keeps two copies
-        } else {
-            // items of this slot: a run's first window counts the run
-            uint32_t c = ok[j] && !interior ? 1u + (uint32_t)__builtin_ctz(~(eqm >> j)) : 0u;
-            if (interior) ok[j] = false;
-            const uint64_t v = __ballot(c != 0);
-            if (!v) continue;
-            const int leader = __builtin_ctzll(v);
-            bool match = c != 0;
-#pragma unroll
-            for (int w = 0; w < OW; w++) match = match && tk[j][w] == __shfl(tk[j][w], leader, 64);
-            const uint64_t m = __ballot(match);
-            const uint32_t cl = __shfl(c, leader, 64);
-            const bool merge = __popcll(m) >= 2 || cl >= 2;  // wave-uniform
-            uint32_t total = c;
-            if (merge) {
-                uint32_t x = match ? c : 0u;
-#pragma unroll
-                for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
-                total = lane == leader ? x : (match ? 0u : c);
+                    for (int w = 1; w < OW; w++) eq &= kp[w] == key[w];
+                    if (eq) {
+                        atomicAdd(reinterpret_cast<unsigned long long*>(h.cnt + e), (unsigned long long)add);
+                        done = true;
+                    } else {
+                        next = true;
+                    }
+                }  // not published yet: read it again
+            } else {
+                next = true;
             }
-            // records: the merged leader, and every other item that counts several windows
-            const bool rec = total >= 2;
-            const uint64_t pos = wave_append(rec, &ctr->heavy_n);
-            if (rec) {
-                if (pos < pb.heavy_cap) {
-                    uint64_t* r = pb.heavy + pos * (OW + 1);
-#pragma unroll
-                    for (int w = 0; w < OW; w++) r[w] = tk[j][w];
-                    r[OW] = total;
-                } else {
-                    atomicOr(&ctr->part_overflow, 1ULL);
+            if (next) {
+                e = (e + 1) & (HT - 1);
+                if (++probes >= HT) {
+                    full = true;
+                    done = true;
                 }
             }
-            if (rec || (merge && match)) ok[j] = false;
         }
+    }
+    return full;
+}
+// append {key, count} records (count passes) or count (<= 2) plain keys (Bloom pass) to the
+// batch's skew list, one list allocation per wave
+template <int OW, int MODE>
+DEV void skew_append(const PartBufs& pb, DevCounters* ctr, bool want, const uint64_t (&key)[OW], uint64_t c) {
+    const uint32_t copies = !want ? 0u : MODE == 3 ? (c >= 2 ? 2u : 1u) : 1u;
+    uint32_t incl = wave_incl_sum(copies);
+    const uint32_t total = __shfl(incl, 63, 64);
+    if (!total) return;
+    unsigned long long base = 0;
+    if ((threadIdx.x & 63) == 0) base = atomicAdd(&ctr->spill_n, (unsigned long long)total);
+    base = __shfl(base, 0, 64);
+    for (uint32_t q = 0; q < copies; q++) {
+        const uint64_t pos = base + incl - copies + q;
+        if (pos >= pb.spill_cap) {
+            atomicOr(&ctr->part_overflow, 1ULL);
+            break;
+        }
+        uint64_t* r = pb.spill + pos * (MODE == 3 ? OW : OW + 1);
+#pragma unroll
+        for (int w = 0; w < OW; w++) r[w] = key[w];
+        if (MODE != 3) r[OW] = c;
+    }
+}
+
+template <int OW, int RUNW, int MODE, int NT>
+DEV void combine_repeats(uint64_t (&tk)[RUNW][OW], bool (&ok)[RUNW], const PartLds& l, const HeavyTab& h,
+                         const PartBufs& pb, DevCounters* ctr) {
+    // repeated windows (lane masks only in the common case): equal to the next window
+    // (homopolymer) or to the one after ((CA)n)
+    uint32_t rep = 0;
+#pragma unroll
+    for (int j = 0; j + 1 < RUNW; j++) {
+        bool e1 = ok[j] && ok[j + 1], e2 = j + 2 < RUNW && ok[j] && ok[j + 2];
+#pragma unroll
+        for (int w = 0; w < OW; w++) {
+            e1 = e1 && tk[j][w] == tk[j + 1][w];
+            if (j + 2 < RUNW) e2 = e2 && tk[j][w] == tk[j + 2][w];
+        }
+        if (e1) rep |= 3u << j;
+        if (e2) rep |= 5u << j;
+    }
+    if (__ballot(rep != 0) == 0) return;
+    // the wave's repeated windows, compacted into its share of the (idle) tile key area
+    const int lane = threadIdx.x & 63;
+    uint64_t* stage = l.keys + (size_t)(threadIdx.x >> 6) * 64 * RUNW * OW;
+    const uint32_t nrep = __builtin_popcount(rep);
+    const uint32_t incl = wave_incl_sum(nrep);
+    const uint32_t total = __shfl(incl, 63, 64);
+    uint32_t pos = incl - nrep;
+#pragma unroll
+    for (int j = 0; j < RUNW; j++)
+        if ((rep >> j) & 1) {
+#pragma unroll
+            for (int w = 0; w < OW; w++) stage[pos * OW + w] = tk[j][w];
+            pos++;
+            ok[j] = false;
+        }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    for (uint32_t i0 = 0; i0 < total; i0 += 64) {
+        const bool act = i0 + lane < total;
+        uint64_t key[OW];
+#pragma unroll
+        for (int w = 0; w < OW; w++) key[w] = act ? stage[(i0 + lane) * OW + w] : 0;
+        const bool full = heavy_insert<OW>(h, key, act, 1);
+        skew_append<OW, MODE>(pb, ctr, full, key, 1);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // stage reads done before the tile reuses it
+}
+// end of a workgroup's range: the heavy table's entries -> records of the skew list
+template <int OW, int MODE>
+DEV void heavy_flush(const HeavyTab& h, const PartBufs& pb, DevCounters* ctr) {
+    __syncthreads();
+    if (threadIdx.x < HT) {  // one wave
+        const int e = threadIdx.x;
+        uint64_t key[OW];
+#pragma unroll
+        for (int w = 0; w < OW; w++) key[w] = h.keys[e * OW + w];
+        const uint64_t c = h.cnt[e] & CNT_MASK;
+        const bool has = key[0] != EMPTY;
+        skew_append<OW, MODE>(pb, ctr, has, key, c);
+        const uint64_t nrec = __ballot(has);
+        if (threadIdx.x == 0 && nrec) atomicAdd(&ctr->heavy_n, (unsigned long long)__popcll(nrec));
     }
 }
 
@@ -736,6 +835,12 @@ __global__ __launch_bounds__(NT, 4) void k_p1(PackedView sv, int k, BloomView bf
     if (gated_off(gate)) return;
     if (gate && !SCATTER && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&ctr->part_fallbacks, 1ULL);
     const PartLds l = part_lds(smem, F);
+    constexpr bool HEAVY = Out::kSeg && !Bin::kOwner && !ROLLED;  // repeated windows -> heavy table
+    const HeavyTab ht = heavy_tab<OW>(smem + part_smem<OW, NT>(F));
+    if constexpr (HEAVY) {
+        heavy_clear(ht, OW);
+        for (int i = threadIdx.x; i < HT; i += NT) ht.cnt[i] = 0;
+    }
     const int tid = threadIdx.x;
     const uint64_t M = ctr->stream_len;
     const uint64_t per = ((M + pb.nblk1 - 1) / pb.nblk1 + TW - 1) / TW * TW;
@@ -777,7 +882,7 @@ __global__ __launch_bounds__(NT, 4) void k_p1(PackedView sv, int k, BloomView bf
                     n_ins += MODE == 0 ? ok[j] : 0;  // MODE 4: level 3 counts the gated insertions
                 }
             }
-            if constexpr (Out::kSeg && !Bin::kOwner) combine_repeats<OW, RUNW, MODE>(tk, ok, pb, ctr);
+            if constexpr (HEAVY) combine_repeats<OW, RUNW, MODE, NT>(tk, ok, l, ht, pb, ctr);
         } else {
             // rolled run: slot j <- the j-th symbol of the thread's run (static indices)
 #pragma unroll
@@ -816,6 +921,7 @@ __global__ __launch_bounds__(NT, 4) void k_p1(PackedView sv, int k, BloomView bf
         for (uint32_t b = tid; b < F; b += NT)
             pb.hist1[(uint64_t)b * pb.nblk1 + blockIdx.x] = (uint32_t)(l.gbase[b] - ob.start(b));
     }
+    if constexpr (HEAVY) heavy_flush<OW, MODE>(ht, pb, ctr);
     // routing (owner bins) counts windows here and insertions at the owner; the Bloom
     // pass counts its windows apart
     if constexpr (COUNTS)
@@ -1041,7 +1147,8 @@ constexpr size_t p2f_smem(uint32_t F, uint32_t nseg_max) { return part_smem<W, N
 #define KC_PREFETCH 1
 #endif
 template <int W, int NT>
-__global__ __launch_bounds__(NT, 2048 / NT) void k_p2f(TableView tv, PartBufs pb, DevCounters* __restrict__ ctr) {
+__global__ __launch_bounds__(NT, 2048 / NT) void k_p2f(TableView tv, PartBufs pb, DevCounters* __restrict__ ctr,
+                                                          int REC) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int RUNW = run_w<W>(), TW = NT * RUNW;
     if (ctr->part_overflow) return;  // level 1 overflowed: the exact pipeline redoes the batch
@@ -1055,7 +1162,7 @@ __global__ __launch_bounds__(NT, 2048 / NT) void k_p2f(TableView tv, PartBufs pb
     const uint32_t nseg = (uint32_t)((uint64_t)(j + 1) * pb.nblk1 / pb.B2) - s_lo;
     const uint64_t seg0 = (uint64_t)c * pb.nblk1 + s_lo;  // level-1 segment index of cursor 0
     const OutSeg o{(uint64_t)pb.B2 * pb.cap2, ((uint64_t)c * F * pb.B2 + j) * pb.cap2, pb.cap2,
-                   pb.spill, pb.spill_cap, &ctr->spill_n, &ctr->part_overflow};
+                   pb.spill, pb.spill_cap, &ctr->spill_n, &ctr->part_overflow, REC};
     for (uint32_t i = tid; i <= nseg; i += NT) pre[i] = i < nseg ? pb.hist1[seg0 + i] : 0;
     for (uint32_t b = tid; b < F; b += NT) {
         l.hist[b] = 0;
@@ -1473,7 +1580,8 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
         // records' counts (the general merge insert counted them at its level 1).  One
         // atomic per workgroup: per-wave adds to this one counter from every region's
         // workgroup serialise at the memory-side atomic unit (milliseconds per pass)
-        block_add4(GATE ? n_ins : (pb.seg_start ? n_add : 0), 0, 0, 0, &ctr->inserted, nullptr, nullptr, nullptr);
+        block_add4(GATE ? (CNT ? n_add : n_ins) : (pb.seg_start ? n_add : 0), 0, 0, 0, &ctr->inserted, nullptr, nullptr,
+                   nullptr);
     }
 }
 
@@ -1988,56 +2096,26 @@ static hipError_t part_level1(PackedView sym, int k, BloomView bf, DevCounters* 
     return hipGetLastError();
 }
 
-// The skew lists of a segmented batch, after its level 3 (item counts on the device):
-//  spill: keys that overflowed a segment (W words each; the Bloom pass: word 0) through
-//         the exact pipeline (levels 1-3 by histogram offsets, no capacity limits);
-//  heavy: {key, count} records of repeated windows (count passes), added by direct
-//         inserts, behind the Bloom gate in the gated pass.
+// The skew list of a segmented batch, after its level 3 (its length is on the device):
+// {key words, count} records -- keys that overflowed a segment (count 1) and the heavy
+// records of repeated windows -- through the exact pipeline (levels 1-3 by histogram
+// offsets, no capacity limits), behind the Bloom gate in the gated pass.  (The Bloom pass
+// spills plain table-key words: bloom_part_w.)
 template <int W, bool GATE>
 static hipError_t insert_spill(TableView t, BloomView bf, DevCounters* ctr, PartBufs pb, hipStream_t s) {
+    constexpr int IW = W + 1;
     const BinRegion bin = coarse_bins(t);
-    const size_t sm1 = part_smem<W>(t.F1), sm1h = hist_smem(t.F1);
+    const size_t sm1 = part_smem<IW>(t.F1), sm1h = hist_smem(t.F1);
     hipError_t e;
-    if ((e = set_smem(k_p1k<W, false>, sm1h)) != hipSuccess) return e;
-    if ((e = set_smem(k_p1k<W, true>, sm1)) != hipSuccess) return e;
+    if ((e = set_smem(k_p1k<IW, false>, sm1h)) != hipSuccess) return e;
+    if ((e = set_smem(k_p1k<IW, true>, sm1)) != hipSuccess) return e;
     const DevN dn{&ctr->spill_n, pb.spill_cap, &ctr->part_overflow};
-    hipLaunchKernelGGL((k_p1k<W, false>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1h, s, pb.spill, (uint64_t)0, pb,
-                       t.F1, bin, ctr, -1, dn);
+    hipLaunchKernelGGL((k_p1k<IW, false>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1h, s, pb.spill, (uint64_t)0, pb,
+                       t.F1, bin, ctr, W, dn);
     launch_scan(pb.hist1, (uint64_t)t.F1 * pb.nblk1, pb.off1, pb.bsum, s);
-    hipLaunchKernelGGL((k_p1k<W, true>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1, s, pb.spill, (uint64_t)0, pb,
-                       t.F1, bin, ctr, -1, dn);
-    return part_levels23<W, false, GATE>(t, ctr, pb, s, nullptr, 0, bf);
-}
-
-// direct insert of the heavy records (grid-stride: the count is on the device); gated pass:
-// a record counts only if its key passes the Bloom gate, and then adds to `inserted`
-constexpr int HEAVY_BLOCKS = 512;
-template <int W, bool GATE>
-__global__ __launch_bounds__(COUNT_THREADS) void k_insert_heavy(const uint64_t* __restrict__ rec, uint64_t cap,
-                                                                TableView tv, BloomView bf,
-                                                                DevCounters* __restrict__ ctr) {
-    const uint64_t n = ctr->part_overflow ? 0 : min((uint64_t)ctr->heavy_n, cap);
-    uint32_t n_fail = 0;
-    unsigned long long added = 0;
-    for (uint64_t i = (uint64_t)blockIdx.x * COUNT_THREADS + threadIdx.x; i < n;
-         i += (uint64_t)gridDim.x * COUNT_THREADS) {
-        uint64_t tk[W];
-#pragma unroll
-        for (int w = 0; w < W; w++) tk[w] = rec[i * (W + 1) + w];
-        const uint64_t c = rec[i * (W + 1) + W];
-        if constexpr (GATE) {
-            if (!block_gate(bloom_block_ptr(bf, tk[0]) + 8, tk[0], bf.nh_gate)) continue;
-            added += c;
-        }
-        if (!table_insert<W>(tv, tk, c)) n_fail++;
-    }
-    block_add4(added, n_fail, 0, 0, &ctr->inserted, &ctr->overflow, nullptr, nullptr);
-}
-template <int W, bool GATE>
-static hipError_t insert_heavy(TableView t, BloomView bf, DevCounters* ctr, PartBufs pb, hipStream_t s) {
-    hipLaunchKernelGGL((k_insert_heavy<W, GATE>), dim3(HEAVY_BLOCKS), dim3(COUNT_THREADS), 0, s, pb.heavy,
-                       pb.heavy_cap, t, bf, ctr);
-    return hipGetLastError();
+    hipLaunchKernelGGL((k_p1k<IW, true>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1, s, pb.spill, (uint64_t)0, pb,
+                       t.F1, bin, ctr, W, dn);
+    return part_levels23<W, true, GATE>(t, ctr, pb, s, nullptr, 0, bf);
 }
 
 // batch bookkeeping of the skew lists: begin = clear the batch's flag and list counts,
@@ -2047,10 +2125,10 @@ static __global__ void k_batch_begin(DevCounters* ctr) {
     ctr->spill_n = 0;
     ctr->heavy_n = 0;
 }
-static __global__ void k_batch_end(DevCounters* ctr, uint64_t spill_cap, uint64_t heavy_cap) {
+static __global__ void k_batch_end(DevCounters* ctr) {
     if (ctr->part_overflow) return;
-    ctr->spilled += min((uint64_t)ctr->spill_n, spill_cap);
-    ctr->heavy += min((uint64_t)ctr->heavy_n, heavy_cap);
+    ctr->spilled += ctr->spill_n - ctr->heavy_n;  // list entries: spilled keys + heavy records
+    ctr->heavy += ctr->heavy_n;
 }
 
 // Segmented pipeline (pb.cap1 != 0): p1 -> p2f -> p3<SEG>, each a single pass; then
@@ -2074,21 +2152,21 @@ static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf
         const char* v = std::getenv("KC_P2F_SEGS");
         return v ? (uint32_t)std::atoi(v) : 0u;
     }();
-    const size_t sm1 = part_smem<W, scatter_threads<W>()>(t.F1),
+    const size_t sm1 = part_smem<W, scatter_threads<W>()>(t.F1) + heavy_smem<W>(),
                  sm2 = p2f_smem<W, p2f_threads<W>()>(t.F2, std::max<uint32_t>(p2f_pad, (pb.nblk1 + pb.B2 - 1) / pb.B2));
     if ((e = set_smem(k1, sm1)) != hipSuccess) return e;
     if ((e = set_smem(k_p2f<W, p2f_threads<W>()>, sm2)) != hipSuccess) return e;
     const OutSeg o1{(uint64_t)pb.nblk1 * pb.cap1, 0, pb.cap1, pb.spill, pb.spill_cap, &ctr->spill_n,
-                    &ctr->part_overflow};
+                    &ctr->part_overflow, 1};
     hipLaunchKernelGGL(k1, dim3(pb.nblk1), dim3(scatter_threads<W>()), sm1, s, sym, k, bf, ctr, pb, t.F1, coarse_bins(t),
                        pb.keys1, pk, pkm1, o1, (const unsigned long long*)nullptr, 1);
-    hipLaunchKernelGGL((k_p2f<W, p2f_threads<W>()>), dim3(t.F1 * pb.B2), dim3(p2f_threads<W>()), sm2, s, t, pb, ctr);
+    hipLaunchKernelGGL((k_p2f<W, p2f_threads<W>()>), dim3(t.F1 * pb.B2), dim3(p2f_threads<W>()), sm2, s, t, pb, ctr,
+                       1);
     if ((e = launch_p3<W, true, false, GATE3>(t, ctr, pb, nullptr, fresh, s, bf)) != hipSuccess) return e;
     // the skew lists (MODE 2 rolls its windows: no heavy records); the segmented level 3
     // wrote every region of a fresh table, so these read the table
     if ((e = insert_spill<W, GATE3>(t, bf, ctr, pb, s)) != hipSuccess) return e;
-    if (MODE != 2 && (e = insert_heavy<W, GATE3>(t, bf, ctr, pb, s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_batch_end, dim3(1), dim3(1), 0, s, ctr, pb.spill_cap, pb.heavy_cap);
+    hipLaunchKernelGGL(k_batch_end, dim3(1), dim3(1), 0, s, ctr);
     // a full spill or heavy list: the exact pipeline redoes the batch (the segmented levels
     // and the lists left the table untouched)
     if ((e = part_level1<W, MODE>(sym, k, bf, ctr, pb, t.F1, coarse_bins(t), pb.keys1, s, gate)) != hipSuccess)
@@ -2124,14 +2202,15 @@ static hipError_t bloom_part_w(PackedView sym, int k, BloomView bf, TableView ft
     const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
     constexpr int NT = scatter_threads<W>(), NT2 = p2f_threads<1>();
     auto k1 = k_p1<W, 3, true, BinRegion, OutSeg, NT>;
-    const size_t sm1 = part_smem<1, NT>(ft.F1), sm2 = p2f_smem<1, NT2>(ft.F2, (pb.nblk1 + pb.B2 - 1) / pb.B2);
+    const size_t sm1 = part_smem<1, NT>(ft.F1) + heavy_smem<1>(),
+                 sm2 = p2f_smem<1, NT2>(ft.F2, (pb.nblk1 + pb.B2 - 1) / pb.B2);
     if ((e = set_smem(k1, sm1)) != hipSuccess) return e;
     if ((e = set_smem(k_p2f<1, NT2>, sm2)) != hipSuccess) return e;
     const OutSeg o1{(uint64_t)pb.nblk1 * pb.cap1, 0, pb.cap1, pb.spill, pb.spill_cap, &ctr->spill_n,
-                    &ctr->part_overflow};
+                    &ctr->part_overflow, 0};
     hipLaunchKernelGGL(k1, dim3(pb.nblk1), dim3(NT), sm1, s, sym, k, bf, ctr, pb, ft.F1, coarse_bins(ft), pb.keys1, pk,
                        pkm1, o1, (const unsigned long long*)nullptr, 1);
-    hipLaunchKernelGGL((k_p2f<1, NT2>), dim3(ft.F1 * pb.B2), dim3(NT2), sm2, s, ft, pb, ctr);
+    hipLaunchKernelGGL((k_p2f<1, NT2>), dim3(ft.F1 * pb.B2), dim3(NT2), sm2, s, ft, pb, ctr, 0);
     if ((e = launch_b3<true>(bf, ft, ctr, pb, nullptr, fresh, s)) != hipSuccess) return e;
     // spilled keys (table key word 0) through the exact levels into the filter regions
     {
@@ -2148,7 +2227,7 @@ static hipError_t bloom_part_w(PackedView sym, int k, BloomView bf, TableView ft
         if ((e = part_level2_exact<1>(ft, pb, s, nullptr)) != hipSuccess) return e;
         if ((e = launch_b3<false>(bf, ft, ctr, pb, nullptr, 0, s)) != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(k_batch_end, dim3(1), dim3(1), 0, s, ctr, pb.spill_cap, (uint64_t)0);
+    hipLaunchKernelGGL(k_batch_end, dim3(1), dim3(1), 0, s, ctr);
     if ((e = part_level1<W, 3>(sym, k, bf, ctr, pb, ft.F1, coarse_bins(ft), pb.keys1, s, gate)) != hipSuccess)
         return e;
     if ((e = part_level2_exact<1>(ft, pb, s, gate)) != hipSuccess) return e;

@@ -71,8 +71,8 @@ struct DevCounters {
     unsigned long long invalid;         uint64_t _p10[15];  // received keys with word 0 == 0 (skipped)
     unsigned long long part_overflow;   uint64_t _p11[15];  // a fixed-capacity segment overflowed (this batch)
     unsigned long long part_fallbacks;  uint64_t _p12[15];  // batches redone on the exact layout
-    // skew (segmented batches): keys that did not fit their segment go to a spill list, and
-    // repeated windows go to a heavy list as {key, count} records (this batch / in total)
+    // skew (segmented batches): entries of the batch's skew list (keys that did not fit their
+    // segment + records of repeated windows), the records among them, and the job totals
     unsigned long long spill_n;         uint64_t _p13[15];
     unsigned long long heavy_n;         uint64_t _p14[15];
     unsigned long long spilled;         uint64_t _p15[15];
@@ -111,10 +111,8 @@ struct PartBufs {
     uint64_t cap1, cap2;    // segmented layout: keys per segment of levels 1 / 2 (0 = exact layout)
     const uint64_t* seg_start;  // level 3 over runs at arbitrary offsets ([R][B2] first items;
                                 // nullptr = fixed-capacity segments of cap2)
-    uint64_t* spill;        // segmented batches: keys that overflowed their segment (spill_cap keys)
-    uint64_t spill_cap;
-    uint64_t* heavy;        // segmented count passes: {key words, count} records of repeated windows
-    uint64_t heavy_cap;
+    uint64_t* spill;        // segmented batches: the skew list ({key words, count} records of keys past
+    uint64_t spill_cap;     // a segment's end and of repeated windows; Bloom pass: keys), spill_cap entries
 };
 
 struct BloomView {
