@@ -83,14 +83,17 @@ DEV uint32_t bucket_in_region(uint64_t t0, uint64_t R) {
 }
 DEV uint32_t owner_of(uint64_t t0, uint32_t parts) { return (uint32_t)(((t0 & 0xFFFFFFFFULL) * parts) >> 32); }
 
-// wave-level inclusive scans (64 lanes)
+// wave-level inclusive scans (64 lanes).  The sum runs on DPP lane moves (no LDS
+// round trips): row_shr 1/2/4/8 inside each 16-lane row, then row_bcast:15 (rows 1 and 3
+// add the last lane of the row below) and row_bcast:31 (rows 2 and 3 add lane 31); lanes
+// with no source lane add 0.
 DEV uint32_t wave_incl_sum(uint32_t v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        uint32_t o = __shfl_up(v, d, 64);
-        if (lane >= d) v += o;
-    }
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
     return v;
 }
 DEV uint32_t wave_incl_last(uint32_t v) {  // last non-zero value up to this lane

@@ -547,6 +547,44 @@ DEV void ks_store(uint64_t* p, uint64_t v) {
     else *p = v;
 }
 
+// In-kernel phase stamps (measurement builds only, tools/probe: -DKC_STAMP=1): wave 0 of
+// each workgroup adds the cycles of every phase of the scatter into g_stamp[block][phase].
+#ifndef KC_STAMP
+#define KC_STAMP 0
+#endif
+struct Stamps {
+    unsigned long long last, acc[8];
+    DEV void init() {
+#if KC_STAMP
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(last)::"memory");
+        for (int i = 0; i < 8; i++) acc[i] = 0;
+#endif
+    }
+    DEV void mark(int i) {
+#if KC_STAMP
+        __builtin_amdgcn_sched_barrier(0);
+        unsigned long long t;
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+        __builtin_amdgcn_sched_barrier(0);
+        acc[i] += t - last;
+        last = t;
+#endif
+    }
+    DEV void flush(int part) {  // part 0: level 1, 1: level 2
+#if KC_STAMP
+        if (threadIdx.x == 0)
+            for (int i = 0; i < 8; i++) g_stamp_buf()[(part * 2048 + (blockIdx.x & 2047)) * 8 + i] += acc[i];
+#endif
+    }
+#if KC_STAMP
+    static DEV unsigned long long* g_stamp_buf();
+#endif
+};
+#if KC_STAMP
+__device__ unsigned long long g_stamp[4096 * 8];
+DEV unsigned long long* Stamps::g_stamp_buf() { return g_stamp; }
+#endif
+
 // rank of this lane among the set lanes of a wave mask
 DEV uint32_t lane_rank(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -573,14 +611,19 @@ struct NoMid {
 // may load its next tile into them)
 template <int W, int RUNW, class Bin, class Out, int NT = COUNT_THREADS, class Mid = NoMid>
 DEV bool scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const Out& o, uint64_t (&tk)[RUNW][W],
-                      bool (&ok)[RUNW], uint64_t* __restrict__ out, Mid&& mid = Mid()) {
+                      bool (&ok)[RUNW], uint64_t* __restrict__ out, Mid&& mid = Mid(), Stamps* stp = nullptr) {
     __shared__ unsigned long long s_spbase;
+    __shared__ uint32_t s_spills;  // some bin of the tile spills (set by the setup, read after a barrier)
     const int tid = threadIdx.x;
     uint32_t rank[RUNW];  // (the bins are recomputed below: one multiply, fewer registers)
+    if (KC_STAMP && stp) stp->mark(0);
+    if (Out::kSeg && tid == 0) s_spills = 0;
 #pragma unroll
     for (int j = 0; j < RUNW; j++) rank[j] = ok[j] ? atomicAdd(&l.hist[bin(tk[j][0])], 1u) : 0;
+    if (KC_STAMP && stp) stp->mark(1);
     __syncthreads();
     block_excl_scan_lds<NT>(l.hist, l.start, F);
+    if (KC_STAMP && stp) stp->mark(2);
 #pragma unroll
     for (int j = 0; j < RUNW; j++)
         if (ok[j]) {
@@ -588,6 +631,7 @@ DEV bool scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const Out& o
 #pragma unroll
             for (int w = 0; w < W; w++) l.keys[slot * W + w] = tk[j][w];
         }
+    if (KC_STAMP && stp) stp->mark(3);
     // per bin: destination minus tile slot, the tile slots that fit the bin's output, and
     // the keys past its end
     bool spills = false;
@@ -600,9 +644,12 @@ DEV bool scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const Out& o
         l.sp[b] = h - fit;
         spills |= fit < h;
     }
+    if (Out::kSeg && spills) s_spills = 1;
+    if (KC_STAMP && stp) stp->mark(4);
     mid();
+    __syncthreads();
     if constexpr (Out::kSeg) {
-        if (__syncthreads_or(spills)) {
+        if (s_spills) {
             // one allocation in the skew list for all the tile's spilled keys (a bin's spilled
             // keys are the tail of its run in the tile)
             const uint32_t last = l.sp[F - 1];
@@ -610,9 +657,8 @@ DEV bool scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const Out& o
             if (tid == 0) s_spbase = atomicAdd(o.spill_n, (unsigned long long)(l.sp[F - 1] + last));
             __syncthreads();
         }
-    } else {
-        __syncthreads();
     }
+    if (KC_STAMP && stp) stp->mark(5);
     const uint32_t n = l.start[F - 1] + l.hist[F - 1];
     for (uint32_t i = tid; i < n; i += NT) {
         uint64_t key[W];
@@ -636,12 +682,14 @@ DEV bool scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const Out& o
             }
         }
     }
+    if (KC_STAMP && stp) stp->mark(6);
     __syncthreads();
     for (uint32_t b = tid; b < F; b += NT) {
         l.gbase[b] += l.lim[b] - l.start[b];  // the keys written (a segment's fill never passes its end)
         l.hist[b] = 0;
     }
     __syncthreads();
+    if (KC_STAMP && stp) stp->mark(7);
     return false;
 }
 
@@ -857,6 +905,8 @@ __global__ __launch_bounds__(NT, 4) void k_p1(PackedView sv, int k, BloomView bf
     __syncthreads();
     const RollConst rk = make_roll<W>(k, pow5_k, pow5_km1);
     uint32_t n_win = 0, n_ins = 0;
+    Stamps stp;
+    stp.init();
     for (uint64_t t0 = lo; t0 < hi; t0 += TW) {
         const uint64_t t1 = min(t0 + TW, hi);
         uint64_t tk[RUNW][OW];
@@ -906,7 +956,7 @@ __global__ __launch_bounds__(NT, 4) void k_p1(PackedView sv, int k, BloomView bf
             });
         }
         if constexpr (SCATTER) {
-            scatter_tile<OW, RUNW, Bin, Out, NT>(l, F, bin, ob, tk, ok, out);
+            scatter_tile<OW, RUNW, Bin, Out, NT>(l, F, bin, ob, tk, ok, out, NoMid(), &stp);
         } else {
 #pragma unroll
             for (int j = 0; j < RUNW; j++)
@@ -921,6 +971,7 @@ __global__ __launch_bounds__(NT, 4) void k_p1(PackedView sv, int k, BloomView bf
         for (uint32_t b = tid; b < F; b += NT)
             pb.hist1[(uint64_t)b * pb.nblk1 + blockIdx.x] = (uint32_t)(l.gbase[b] - ob.start(b));
     }
+    if constexpr (SCATTER && Out::kSeg) stp.flush(0);
     if constexpr (HEAVY) heavy_flush<OW, MODE>(ht, pb, ctr);
     // routing (owner bins) counts windows here and insertions at the owner; the Bloom
     // pass counts its windows apart
@@ -1174,38 +1225,50 @@ __global__ __launch_bounds__(NT, 2048 / NT) void k_p2f(TableView tv, PartBufs pb
     // segment cursor of this thread (its indices grow monotonically): segment cs holds
     // [cb, nb) of the virtual run, both bounds kept in registers
     uint32_t cs = 0, cb = 0, nb = nseg ? pre[1] : 0;
+    const uint64_t* sp = pb.keys1 + seg0 * pb.cap1 * W;  // segment cs
+    // a wave takes 64 * RUNW consecutive positions of the tile (the cursor rarely moves)
+    const uint32_t wpos = (uint32_t)(tid >> 6) * (64 * RUNW) + (tid & 63);
+    // Every lane loads (past the total: the first key again) and the select is on the address,
+    // never on loaded data, so nothing waits for these loads before the tile's ranks use them
+    // (a select on the data made every prefetch wait at once: 47 % of the level-2 cycles).
     auto load_tile = [&](uint32_t t0, uint64_t (&tk)[RUNW][W], bool (&ok)[RUNW]) {
 #pragma unroll
         for (int q = 0; q < RUNW; q++) {
-            const uint32_t i = t0 + tid + q * NT;
+            const uint32_t i = t0 + wpos + q * 64;
             ok[q] = i < total;
+            const uint64_t* src = pb.keys1;
             if (ok[q]) {
-                while (nb <= i) {
-                    cs++;
-                    cb = nb;
-                    nb = pre[cs + 1];
+                if (nb <= i) {
+                    do {
+                        cs++;
+                        cb = nb;
+                        nb = pre[cs + 1];
+                    } while (nb <= i);
+                    sp = pb.keys1 + (seg0 + cs) * pb.cap1 * W;
                 }
-                const uint64_t* src = pb.keys1 + ((seg0 + cs) * pb.cap1 + (i - cb)) * W;
-#pragma unroll
-                for (int w = 0; w < W; w++) tk[q][w] = ks_load(src + w);
-            } else {
-#pragma unroll
-                for (int w = 0; w < W; w++) tk[q][w] = 0;
+                src = sp + (uint64_t)(i - cb) * W;
             }
+#pragma unroll
+            for (int w = 0; w < W; w++) tk[q][w] = ks_load(src + w);
         }
     };
     uint64_t tk[RUNW][W];
     bool ok[RUNW];
+    Stamps stp;
+    stp.init();
     if (total) load_tile(0, tk, ok);
     for (uint32_t t0 = 0; t0 < total; t0 += TW) {
         // the next tile is loaded into the same registers as soon as this tile's keys sit
         // in LDS, so its loads overlap this tile's write-out (barriers wait for LDS only)
         const bool more = t0 + TW < total;
-        scatter_tile<W, RUNW, BinRegion, OutSeg, NT>(l, F, bin, o, tk, ok, pb.keys2, [&]() {
-            if (KC_PREFETCH && more) load_tile(t0 + TW, tk, ok);
-        });
+        scatter_tile<W, RUNW, BinRegion, OutSeg, NT>(
+            l, F, bin, o, tk, ok, pb.keys2, [&]() {
+                if (KC_PREFETCH && more) load_tile(t0 + TW, tk, ok);
+            },
+            &stp);
         if (!KC_PREFETCH && more) load_tile(t0 + TW, tk, ok);
     }
+    stp.flush(1);
     for (uint32_t b = tid; b < F; b += NT)
         pb.hist2[((uint64_t)c * F + b) * pb.B2 + j] = (uint32_t)(l.gbase[b] - o.start(b));
 }

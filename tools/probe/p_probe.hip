@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "../../canonical-k-mer-hash-table_amd/csrc/kc_count_impl.h"
@@ -301,6 +302,33 @@ int main(int argc, char** argv) {
                it, ms, h.windows, (unsigned long long)expect, h.inserted, h.overflow, h.part_overflow, h.spill_n,
                h.heavy_n, expect / (ms * 1e-3) / 1e9);
     }
-    // occupied slots of the table (fresh each iteration: one pass's distinct keys)
+#if KC_STAMP
+    {  // one more pass with the phase stamps cleared first
+        static unsigned long long h[4096 * 8];
+        memset(h, 0, sizeof(h));
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamp), h, sizeof(h)));
+        DevCounters hc{};
+        hc.stream_len = M;
+        CK(hipMemcpy(ctr, &hc, sizeof(hc), hipMemcpyHostToDevice));
+        CK(WOps<1>::count_partitioned(sv, k, 0, t, BloomView{}, ctr, pb, 1, 0));
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_stamp), sizeof(h)));
+        const char* ph[8] = {"before rank (extraction / prev)", "rank atomics", "barrier+scan", "placement",
+                             "setup", "mid+barrier", "write-out", "reset+barriers"};
+        const int nb[2] = {(int)pb.nblk1, (int)(t.F1 * pb.B2)};
+        for (int part = 0; part < 2; part++) {
+            double tot = 0, a[8];
+            for (int i = 0; i < 8; i++) {
+                a[i] = 0;
+                for (int b = 0; b < std::min(nb[part], 2048); b++) a[i] += h[(part * 2048 + b) * 8 + i];
+                a[i] /= std::min(nb[part], 2048);
+                tot += a[i];
+            }
+            printf("stamps %s (cycles per workgroup, wave 0):", part ? "k_p2f" : "k_p1");
+            for (int i = 0; i < 8; i++) printf(" [%s] %.0f (%.1f%%)", ph[i], a[i], 100 * a[i] / tot);
+            printf(" total %.0f\n", tot);
+        }
+    }
+#endif
     return 0;
 }
