@@ -570,10 +570,10 @@ struct Stamps {
         last = t;
 #endif
     }
-    DEV void flush(int part) {  // part 0: level 1, 1: level 2
+    DEV void flush(int part) {  // part 0: level 1, 1: level 2, 2: level 3
 #if KC_STAMP
         if (threadIdx.x == 0)
-            for (int i = 0; i < 8; i++) g_stamp_buf()[(part * 2048 + (blockIdx.x & 2047)) * 8 + i] += acc[i];
+            for (int i = 0; i < 8; i++) atomicAdd(&g_stamp_buf()[(part * 2048 + (blockIdx.x & 2047)) * 8 + i], acc[i]);
 #endif
     }
 #if KC_STAMP
@@ -581,7 +581,7 @@ struct Stamps {
 #endif
 };
 #if KC_STAMP
-__device__ unsigned long long g_stamp[4096 * 8];
+__device__ unsigned long long g_stamp[6144 * 8];
 DEV unsigned long long* Stamps::g_stamp_buf() { return g_stamp; }
 #endif
 
@@ -1354,6 +1354,8 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
     uint4* l4 = reinterpret_cast<uint4*>(lt);
     constexpr int N4 = BPR * BUCKET_WORDS / 2;
     constexpr int NT4 = KC_P3_TAGS ? BPR / 2 : 0;  // tag words, as uint4
+    Stamps stp;
+    stp.init();
     if (fresh) {
         for (int i = threadIdx.x; i < N4 + NT4; i += NT) l4[i] = make_uint4(0, 0, 0, 0);
         __syncthreads();
@@ -1387,6 +1389,7 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
             __syncthreads();
         }
     }
+    stp.mark(0);
     uint32_t n_fail = 0, n_ins = 0;
     unsigned long long n_add = 0;  // CNT: the records' counts (the runs merge counts them here)
     // SEG: segment cursor of this thread (indices grow monotonically): segment cs holds
@@ -1635,8 +1638,12 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
             load_items(nbase, kk, add, okm);
         }
     }
+    stp.mark(1);
     __syncthreads();
+    stp.mark(2);
     for (int i = threadIdx.x; i < N4; i += NT) g4[i] = l4[lds_chunk(i >> 3, i & 7)];
+    stp.mark(3);
+    if (SEG && !CNT && !GATE) stp.flush(2);
     if (n_fail) atomicAdd(&ctr->overflow, (unsigned long long)n_fail);
     if constexpr (GATE || CNT) {
         // GATE: the gated insertions (level 1 counted the windows); CNT over runs: the

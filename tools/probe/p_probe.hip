@@ -304,7 +304,7 @@ int main(int argc, char** argv) {
     }
 #if KC_STAMP
     {  // one more pass with the phase stamps cleared first
-        static unsigned long long h[4096 * 8];
+        static unsigned long long h[6144 * 8];
         memset(h, 0, sizeof(h));
         CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamp), h, sizeof(h)));
         DevCounters hc{};
@@ -315,8 +315,19 @@ int main(int argc, char** argv) {
         CK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_stamp), sizeof(h)));
         const char* ph[8] = {"before rank (extraction / prev)", "rank atomics", "barrier+scan", "placement",
                              "setup", "mid+barrier", "write-out", "reset+barriers"};
-        const int nb[2] = {(int)pb.nblk1, (int)(t.F1 * pb.B2)};
-        for (int part = 0; part < 2; part++) {
+        const int nb[3] = {(int)pb.nblk1, (int)(t.F1 * pb.B2), 2048};
+        for (int part = 0; part < 3; part++) {
+            if (part == 2) {  // level 3: 61440 workgroups folded onto 2048 slots; phases 0-3
+                double a[4] = {0, 0, 0, 0}, tot = 0;
+                for (int b = 0; b < 2048; b++)
+                    for (int i = 0; i < 4; i++) a[i] += h[(2 * 2048 + b) * 8 + i];
+                const char* p3[4] = {"region init", "items (loads + inserts)", "barrier", "write-back"};
+                for (int i = 0; i < 4; i++) { a[i] /= (double)t.R; tot += a[i]; }
+                printf("stamps k_p3 (cycles per workgroup):");
+                for (int i = 0; i < 4; i++) printf(" [%s] %.0f (%.1f%%)", p3[i], a[i], 100 * a[i] / tot);
+                printf(" total %.0f\n", tot);
+                continue;
+            }
             double tot = 0, a[8];
             for (int i = 0; i < 8; i++) {
                 a[i] = 0;
