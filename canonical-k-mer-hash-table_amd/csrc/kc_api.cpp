@@ -114,6 +114,26 @@ struct kc_ctx {
     bool bloom_fresh = false;  // the filter is all zero (allocated / reset, nothing inserted since)
     TableView bgeo{};          // blocked layout: the filter's region geometry (k_b3 regions)
 
+    // Level-1 reuse (device path): a Bloom job whose Bloom pass is ONE batch over a device
+    // image keeps that pass's level-1 output (whole table keys in the filter's coarse bins,
+    // launch_bloom_partitioned keep); the table is then sized with the same coarse bins, and
+    // a counting pass over the same image and chunks (checked: pointer, chunk list, format
+    // and a checksum of the bytes) starts at level 2 instead of tokenizing and extracting
+    // every window again (launch_count_reuse).  KC_REUSE=0 disables it.
+    int bloom_batches = 0;            // Bloom-pass batches since the job started
+    bool reuse_kept = false;          // the (only) Bloom batch kept its level-1 output
+    bool reuse_ok = false;            // kc_bloom_finalize: kept, no skew entries, geometry fits
+    const uint8_t* reuse_img = nullptr;
+    std::vector<ChunkDesc> reuse_chunks;
+    int reuse_fmt = -1;
+    uint64_t reuse_used = 0;          // stage bytes of the batch
+    unsigned long long reuse_sum = 0; // checksum of the Bloom pass's chunk bytes
+    uint64_t reuse_windows = 0;       // windows of that batch
+    unsigned long long* d_sum = nullptr;  // CHECKSUM_SLOTS partial sums
+    uint32_t* d_keep_fill = nullptr;      // the kept level 1's segment fills ([F1][nblk1])
+    uint64_t keep_fill_cap = 0;
+    uint64_t reuse_hits = 0;          // counting passes that reused (kc_stats.reused_passes)
+
     uint64_t n_chunks = 0, n_bytes = 0;
 
     // profiling: event quadruples {start, after gather, after tokenize, after count}
@@ -174,7 +194,9 @@ static uint64_t bloom_words(const kc_ctx* c) {
     return c->bloom_blocked ? std::max<uint64_t>(w, 16 * bloom_blocks(c->bf_bits)) : w;
 }
 
-static int alloc_table(kc_ctx* c, uint64_t min_slots) {
+// pow2_f1 != 0: R = F1 x F2 with F1 = pow2_f1 (the Bloom filter's coarse bins) and F2 a power
+// of two, so the table's coarse bins are the filter's hash-prefix bins (level-1 reuse)
+static int alloc_table(kc_ctx* c, uint64_t min_slots, uint32_t pow2_f1 = 0) {
     c->min_slots = min_slots;
     // Kaarme's table holds exactly next_prime3mod4(min_slots) slots and dies when
     // full; open addressing on the GPU keeps 25 % headroom over that.  The table is
@@ -187,10 +209,18 @@ static int alloc_table(kc_ctx* c, uint64_t min_slots) {
     // (multiply-shift region index, so R is not rounded up to a power of two)
     int rbits = 0;
     while ((1ULL << rbits) < regions) rbits++;
-    const int f1bits = std::min(10, (rbits + 1) / 2);
-    c->f2bits = rbits - f1bits;
-    c->F2 = 1u << c->f2bits;
-    c->F1 = (uint32_t)((regions + c->F2 - 1) / c->F2);
+    if (pow2_f1) {
+        int f1 = 0;
+        while ((1u << f1) < pow2_f1) f1++;
+        c->f2bits = std::max(0, rbits - f1);
+        c->F2 = 1u << c->f2bits;
+        c->F1 = pow2_f1;
+    } else {
+        const int f1bits = std::min(10, (rbits + 1) / 2);
+        c->f2bits = rbits - f1bits;
+        c->F2 = 1u << c->f2bits;
+        c->F1 = (uint32_t)((regions + c->F2 - 1) / c->F2);
+    }
     c->R = (uint64_t)c->F1 * c->F2;
     if (c->R >= (1ULL << 32)) return c->fail(KC_ERR_ARG, "table too large");  // 32-bit region index (kc_common.h)
     c->nbuckets = c->R * BPR;
@@ -374,7 +404,7 @@ static hipStream_t pick_stream(kc_ctx* c, void* s) {
 // src: the bytes the chunk descriptors' src_off point into (the host stage, or a
 // device-resident image read in place)
 static int run_batch(kc_ctx* c, const uint8_t* src, uint64_t used, uint64_t nchunks, int fmt, int pass, hipStream_t s,
-                     hipEvent_t ev_start = nullptr, hipEvent_t ev_gather = nullptr) {
+                     hipEvent_t ev_start = nullptr, hipEvent_t ev_gather = nullptr, bool keep = false) {
     const uint64_t ntiles = used / TILE;
     if (ntiles == 0) return KC_OK;
     std::array<hipEvent_t, 4> ev{ev_start, ev_gather, nullptr, nullptr};
@@ -399,13 +429,34 @@ static int run_batch(kc_ctx* c, const uint8_t* src, uint64_t used, uint64_t nchu
     if (pass == 1) mode = 1;
     else mode = (c->cfg.bf_enable && c->cfg.mode != 1) ? 2 : 0;  // -m 1 -b ignores the filter (main.cpp:482-489)
     const uint64_t syms = used + nchunks;
+    if (mode == 1) {
+        c->bloom_batches++;
+        c->reuse_kept = false;
+    }
     if (mode == 1 && c->bloom_blocked && use_partitioned_bloom(c, syms)) {
         const char* env = std::getenv("KC_INSERT_PATH");
-        int rc = ensure_part_geo(c, syms, !(env && !std::strcmp(env, "exact")),
-                                 PartGeo{c->bgeo.F1, c->bgeo.F2, c->bgeo.R, 1}, c->pbf, c->pbf_cap);
+        const bool seg = !(env && !std::strcmp(env, "exact"));
+        keep = keep && seg;  // (the exact layout does not keep: its level 1 moves word 0 only)
+        int rc = ensure_part_geo(c, syms, seg, PartGeo{c->bgeo.F1, c->bgeo.F2, c->bgeo.R, keep ? c->W : 1}, c->pbf,
+                                 c->pbf_cap);
         if (rc) return rc;
-        HIPCHK(c, launch_bloom_partitioned(sv, c->cfg.k, c->W, bv, c->bgeo, c->d_ctr, c->pbf, c->bloom_fresh, s));
+        c->pbf.keep_fill = nullptr;
+        if (keep) {
+            const uint64_t nf = (uint64_t)c->bgeo.F1 * c->pbf.nblk1;
+            if (nf > c->keep_fill_cap) {
+                hipFree(c->d_keep_fill);
+                c->d_keep_fill = nullptr;
+                c->keep_fill_cap = 0;
+                if (hipMalloc(&c->d_keep_fill, nf * 4) != hipSuccess)
+                    return c->fail(KC_ERR_NOMEM, "level-1 fill copy allocation failed");
+                c->keep_fill_cap = nf;
+            }
+            c->pbf.keep_fill = c->d_keep_fill;
+        }
+        HIPCHK(c, launch_bloom_partitioned(sv, c->cfg.k, c->W, bv, c->bgeo, c->d_ctr, c->pbf, c->bloom_fresh,
+                                           keep ? 1 : 0, s));
         c->bloom_fresh = false;
+        c->reuse_kept = keep;
     } else if (mode != 1 && use_partitioned(c, syms)) {
         const char* env = std::getenv("KC_INSERT_PATH");
         int rc = ensure_part(c, syms, !(env && !std::strcmp(env, "exact")));
@@ -478,6 +529,113 @@ static int add_host_chunk(kc_ctx* c, const uint8_t* buf, size_t len, int fmt, in
     return KC_OK;
 }
 
+static bool reuse_enabled() {
+    const char* v = std::getenv("KC_REUSE");
+    return !(v && *v == '0');
+}
+
+// The counting pass from the Bloom pass's kept level-1 output (see kc_ctx, level-1 reuse).
+// Sets *done when the pass ran; otherwise (different input, changed bytes, overflow) the
+// caller runs the ordinary pass and nothing was counted.
+static int count_reused(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, size_t n, int fmt, hipStream_t s,
+                        bool* done) {
+    *done = false;
+    if (img != c->reuse_img || fmt != c->reuse_fmt) {
+        if (std::getenv("KC_REUSE_DEBUG")) std::fprintf(stderr, "reuse: another image or format\n");
+        return KC_OK;
+    }
+    std::vector<ChunkDesc> b;
+    uint64_t used = 0, max_len = 0, bytes = 0;
+    for (size_t i = 0; i < n; i++) {
+        if (chunks[i].len == 0) continue;
+        ChunkDesc d;
+        d.src_off = chunks[i].off;
+        d.stage_off = used;
+        d.len = chunks[i].len;
+        d.bh = chunks[i].broken_header ? 1 : 0;
+        d.pad = 0;
+        b.push_back(d);
+        used += round_up(chunks[i].len, TILE);
+        max_len = std::max<uint64_t>(max_len, d.len);
+        bytes += d.len;
+    }
+    if (b.size() != c->reuse_chunks.size() || used != c->reuse_used) return KC_OK;
+    for (size_t i = 0; i < b.size(); i++) {
+        const ChunkDesc &x = b[i], &y = c->reuse_chunks[i];
+        if (x.src_off != y.src_off || x.len != y.len || x.bh != y.bh) return KC_OK;
+    }
+    int rc = flush_host(c);  // keep order with staged host chunks
+    if (rc) return rc;
+    if (s != c->stream) {
+        HIPCHK(c, hipEventRecord(c->xev, c->stream));
+        HIPCHK(c, hipStreamWaitEvent(s, c->xev, 0));
+    }
+    std::array<hipEvent_t, 4> ev{nullptr, nullptr, nullptr, nullptr};
+    if (c->profiling)
+        for (auto& e : ev) e = c->get_event();
+    auto release = [&]() {
+        for (auto e : ev)
+            if (e) c->ev_pool.push_back(e);
+    };
+    if (ev[0]) {
+        HIPCHK(c, hipEventRecord(ev[0], s));
+        HIPCHK(c, hipEventRecord(ev[1], s));
+    }
+    // the bytes must be the Bloom pass's: same checksum
+    std::memcpy(c->h_desc[c->cur], b.data(), b.size() * sizeof(ChunkDesc));
+    HIPCHK(c, hipMemcpyAsync(c->d_chunks, c->h_desc[c->cur], b.size() * sizeof(ChunkDesc), hipMemcpyHostToDevice, s));
+    HIPCHK(c, launch_checksum(img, c->d_chunks, (int)b.size(), max_len, c->d_sum, s));
+    unsigned long long part[CHECKSUM_SLOTS];
+    HIPCHK(c, hipMemcpyAsync(part, c->d_sum, sizeof(part), hipMemcpyDeviceToHost, s));
+    if (ev[2]) HIPCHK(c, hipEventRecord(ev[2], s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    unsigned long long sum = 0;
+    for (auto v : part) sum += v;
+    if (sum != c->reuse_sum) {
+        if (std::getenv("KC_REUSE_DEBUG")) std::fprintf(stderr, "reuse: checksum differs\n");
+        release();
+        return KC_OK;
+    }
+    // the table's partition buffers for this batch: level 1 = the Bloom pass's output
+    const uint64_t syms = used + b.size();
+    if ((rc = ensure_part(c, syms, true))) return rc;
+    PartBufs pr = c->pb;
+    if (pr.keys1 != c->pbf.keys1 || pr.nblk1 != c->pbf.nblk1 || pr.B2 != c->pbf.B2 || pr.cap1 != c->pbf.cap1 ||
+        pr.cap1 == 0) {
+        if (std::getenv("KC_REUSE_DEBUG")) std::fprintf(stderr, "reuse: partition geometry differs\n");
+        release();
+        return KC_OK;
+    }
+    pr.hist1 = c->d_keep_fill;
+    const BloomView bv{c->d_bloom, c->bf_bits ? c->bf_bits - 1 : 0, c->nh, c->nh_gate, c->bloom_blocked,
+                       bloom_blocks(c->bf_bits)};
+    HIPCHK(c, launch_count_reuse(c->W, table_view(c), bv, c->d_ctr, pr, c->table_fresh, c->reuse_windows, s));
+    if (ev[3]) HIPCHK(c, hipEventRecord(ev[3], s));
+    unsigned long long ovf = 0;
+    HIPCHK(c, hipMemcpyAsync(&ovf, &c->d_ctr->part_overflow, sizeof(ovf), hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    if (ovf) {  // a full skew list: nothing was inserted, the ordinary pass redoes the batch
+        if (std::getenv("KC_REUSE_DEBUG")) std::fprintf(stderr, "reuse: level 2 overflowed\n");
+        release();
+        return KC_OK;
+    }
+    c->table_fresh = false;
+    c->table_zero_pending = false;  // the fresh level 3 wrote every region
+    c->n_chunks += b.size();
+    c->n_bytes += bytes;
+    c->reuse_hits++;
+    if (c->profiling) {
+        c->ev_pending.push_back(ev);
+        c->pending_symbols_bound.push_back(syms);
+    }
+    if (s != c->stream) {
+        HIPCHK(c, hipEventRecord(c->xev, s));
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->xev, 0));
+    }
+    *done = true;
+    return KC_OK;
+}
+
 static int device_pass(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, size_t n, int fmt, int pass,
                        hipStream_t s) {
     if (fmt != KC_FMT_FASTA && fmt != KC_FMT_FASTQ && fmt != KC_FMT_PLAIN) return c->fail(KC_ERR_ARG, "unknown format");
@@ -489,6 +647,17 @@ static int device_pass(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, si
     }
     std::vector<ChunkDesc> batch;
     uint64_t used = 0;
+    // level-1 reuse: the Bloom pass keeps its level-1 output if it is the job's only batch
+    bool keep = false;
+    if (pass == 1 && c->bloom_batches == 0 && reuse_enabled()) {
+        uint64_t tot = 0, cnt = 0;
+        for (size_t i = 0; i < n; i++)
+            if (chunks[i].len) {
+                tot += round_up(chunks[i].len, TILE);
+                cnt++;
+            }
+        keep = cnt > 0 && tot <= c->batch_bytes && cnt <= c->max_chunks;
+    }
     auto launch = [&]() -> int {
         if (batch.empty()) return KC_OK;
         // descriptors go through the (idle) pinned desc buffer of the current slot
@@ -504,8 +673,17 @@ static int device_pass(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, si
         }
         // the image is tokenized in place (no gather into the stage): "gather" is ~0
         if (c->profiling) HIPCHK(c, hipEventRecord(e1, s));
-        int r = run_batch(c, img, used, batch.size(), fmt, pass, s, e0, e1);
+        int r = run_batch(c, img, used, batch.size(), fmt, pass, s, e0, e1, keep);
         if (r) return r;
+        if (keep && c->reuse_kept) {  // what a counting pass must present again, and its checksum
+            c->reuse_img = img;
+            c->reuse_chunks = batch;
+            c->reuse_fmt = fmt;
+            c->reuse_used = used;
+            uint64_t max_len = 0;
+            for (auto& d : batch) max_len = std::max<uint64_t>(max_len, d.len);
+            HIPCHK(c, launch_checksum(img, c->d_chunks, (int)batch.size(), max_len, c->d_sum, s));
+        }
         HIPCHK(c, hipEventSynchronize(c->h_free[c->cur]));
         batch.clear();
         used = 0;
@@ -601,7 +779,8 @@ int kc_create(const kc_config* cfg, kc_ctx** out) {
         hipMalloc(&c->d_touts, ntiles * sizeof(TileOut)) != hipSuccess ||
         hipMalloc(&c->d_tblk, (ntiles / 1024 + 2) * sizeof(TileOut)) != hipSuccess ||
         hipMalloc(&c->d_chunks, c->max_chunks * sizeof(ChunkDesc)) != hipSuccess ||
-        hipMalloc(&c->d_ctr, sizeof(DevCounters)) != hipSuccess)
+        hipMalloc(&c->d_ctr, sizeof(DevCounters)) != hipSuccess ||
+        hipMalloc(&c->d_sum, CHECKSUM_SLOTS * sizeof(unsigned long long)) != hipSuccess)
         return bail(KC_ERR_NOMEM, "device staging allocation failed");
     if (hipMemsetAsync(c->d_ctr, 0, sizeof(DevCounters), c->stream) != hipSuccess)
         return bail(KC_ERR_HIP, "memset failed");
@@ -655,6 +834,8 @@ void kc_destroy(kc_ctx* c) {
     hipFree(c->d_tblk);
     hipFree(c->d_chunks);
     hipFree(c->d_ctr);
+    hipFree(c->d_sum);
+    hipFree(c->d_keep_fill);
     hipFree(c->d_table);
     hipFree(c->d_bloom);
     hipFree(c->pb.hist1);
@@ -707,7 +888,32 @@ int kc_bloom_finalize(kc_ctx* c, uint64_t* new_in_second) {
     HIPCHK(c, hipMemcpy(&h, c->d_ctr, sizeof(h), hipMemcpyDeviceToHost));
     if (new_in_second) *new_in_second = h.new_in_second;
     c->bloom_final = true;
-    rc = alloc_table(c, 2 * h.new_in_second);  // main.cpp:454
+    // level-1 reuse: the only Bloom batch kept its level-1 output and no key of it went to a
+    // skew list; the table takes the filter's coarse bins if its level 2 still fits the LDS
+    bool reuse = c->reuse_kept && c->bloom_batches == 1 && h.part_fallbacks == 0 && h.spilled == 0 && h.heavy == 0;
+    const uint64_t slots = 2 * h.new_in_second;  // main.cpp:454
+    if (reuse) {
+        uint64_t want = std::max<uint64_t>(slots, 64);
+        want += want / 4;
+        const uint64_t regions = std::max<uint64_t>(1, ((want + c->S - 1) / c->S + BPR - 1) / BPR);
+        uint64_t f2 = 1;
+        while (f2 * c->bgeo.F1 < regions) f2 *= 2;
+        const uint32_t nseg = (c->pbf.nblk1 + c->pbf.B2 - 1) / std::max<uint32_t>(1, c->pbf.B2);
+        reuse = p2f_lds_bytes(c->W, (uint32_t)f2, nseg) <= 160 * 1024 && f2 * c->bgeo.F1 < (1ULL << 32);
+    }
+    if (reuse) {
+        unsigned long long part[CHECKSUM_SLOTS];
+        HIPCHK(c, hipMemcpy(part, c->d_sum, sizeof(part), hipMemcpyDeviceToHost));
+        c->reuse_sum = 0;
+        for (auto v : part) c->reuse_sum += v;
+        c->reuse_windows = h.bf_windows;
+    }
+    c->reuse_ok = reuse;
+    if (std::getenv("KC_REUSE_DEBUG"))
+        std::fprintf(stderr, "reuse finalize: kept %d batches %d fallbacks %llu spilled %llu heavy %llu -> %d\n",
+                     (int)c->reuse_kept, c->bloom_batches, (unsigned long long)h.part_fallbacks,
+                     (unsigned long long)h.spilled, (unsigned long long)h.heavy, (int)reuse);
+    rc = alloc_table(c, slots, reuse ? c->bgeo.F1 : 0);
     if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return KC_OK;
@@ -722,6 +928,12 @@ int kc_count_chunk(kc_ctx* c, const uint8_t* buf, size_t len, int fmt, int bh) {
 int kc_count_device(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, size_t n, int fmt, void* s) {
     if (!c || (!img && n) || (!chunks && n)) return KC_ERR_ARG;
     if (!c->nbuckets) return c->fail(KC_ERR_STATE, "kc_bloom_finalize must precede the counting pass");
+    if (c->reuse_ok) {  // one chance: the first counting pass after the Bloom pass
+        c->reuse_ok = false;
+        bool done = false;
+        const int rc = count_reused(c, img, chunks, n, fmt, pick_stream(c, s), &done);
+        if (rc || done) return rc;
+    }
     return device_pass(c, img, chunks, n, fmt, 0, pick_stream(c, s));
 }
 
@@ -1009,6 +1221,7 @@ int kc_finish(kc_ctx* c, kc_stats* st) {
         st->part_fallbacks = h.part_fallbacks;
         st->spilled = h.spilled;
         st->heavy_records = h.heavy;
+        st->reused_passes = c->reuse_hits;
         st->bytes = c->n_bytes;
         // occupied slots
         if (c->nbuckets) {
@@ -1070,6 +1283,9 @@ int kc_reset(kc_ctx* c) {
     HIPCHK(c, hipMemsetAsync(c->d_ctr, 0, sizeof(DevCounters), c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->n_chunks = c->n_bytes = 0;
+    c->bloom_batches = 0;
+    c->reuse_kept = c->reuse_ok = false;
+    c->reuse_hits = 0;
     return KC_OK;
 }
 

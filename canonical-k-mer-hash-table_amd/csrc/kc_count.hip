@@ -31,9 +31,15 @@ hipError_t launch_count_partitioned(PackedView sym, uint64_t sym_bound, int k, i
 
 // the blocked layout's filter regions: R divides the block count, <= 1024 blocks each
 hipError_t launch_bloom_partitioned(PackedView sym, int k, int W, BloomView bf, TableView ft, DevCounters* ctr,
-                                    PartBufs pb, int fresh, hipStream_t s) {
+                                    PartBufs pb, int fresh, int keep, hipStream_t s) {
     if (!bf.blocked || ft.R == 0 || bf.nblocks % ft.R || bf.nblocks / ft.R > (uint64_t)BF_BLOCKS_PER_REGION) return hipErrorInvalidValue;
-    KC_DISPATCH_W(W, bloom_partitioned(sym, k, bf, ft, ctr, pb, fresh, s));
+    KC_DISPATCH_W(W, bloom_partitioned(sym, k, bf, ft, ctr, pb, fresh, keep, s));
+}
+
+hipError_t launch_count_reuse(int W, TableView t, BloomView bf, DevCounters* ctr, PartBufs pb, int fresh,
+                              uint64_t windows, hipStream_t s) {
+    if (!bf.blocked || pb.cap1 == 0 || t.F1 * pb.B2 == 0) return hipErrorInvalidValue;
+    KC_DISPATCH_W(W, count_reuse(t, bf, ctr, pb, fresh, windows, s));
 }
 
 hipError_t launch_route(PackedView sym, int k, int W, DevCounters* ctr, PartBufs pb, uint32_t parts, uint64_t* out,

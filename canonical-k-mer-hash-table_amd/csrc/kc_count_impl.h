@@ -347,11 +347,8 @@ constexpr int scatter_threads() { return scatter_threads_w(W); }
 // tile of level 1 (16384 one-word keys, 128 KiB of LDS) halves the barriers per key and
 // doubles the runs each bin gets per tile (C2: k_p2f 5.6 -> 5.0 ms on one box); wider
 // keys take smaller groups so that the tile still fits the LDS
-#ifndef KC_P2F_NT
-#define KC_P2F_NT 0  // 0: the default below
-#endif
 template <int W>
-constexpr int p2f_threads() { return KC_P2F_NT ? KC_P2F_NT : (W <= 2 ? 1024 : W <= 4 ? 512 : 256); }
+constexpr int p2f_threads() { return p2f_threads_w(W); }
 
 // table key of the window ending at p (MODE 0 path: direct extraction)
 template <int W>
@@ -693,6 +690,10 @@ DEV bool scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const Out& o
     return false;
 }
 
+// MODE 3 and 5 are Bloom pass 1 (MODE 5 writes the whole table key: its level-1 output is
+// kept for the counting pass, kc_api.cpp "level-1 reuse")
+constexpr bool bloom_mode(int MODE) { return MODE == 3 || MODE == 5; }
+
 // Repeated windows (homopolymer runs: poly-A tails, poly-G artefacts; dinucleotide
 // microsatellites).  One key repeated millions of times would send all its copies into one
 // level-2 segment and one level-3 region (SURVEY 7 "hard parts"; the reference's hot spot is
@@ -774,7 +775,7 @@ DEV bool heavy_insert(const HeavyTab& h, const uint64_t (&key)[OW], bool active,
 // batch's skew list, one list allocation per wave
 template <int OW, int MODE>
 DEV void skew_append(const PartBufs& pb, DevCounters* ctr, bool want, const uint64_t (&key)[OW], uint64_t c) {
-    const uint32_t copies = !want ? 0u : MODE == 3 ? (c >= 2 ? 2u : 1u) : 1u;
+    const uint32_t copies = !want ? 0u : bloom_mode(MODE) ? (c >= 2 ? 2u : 1u) : 1u;
     uint32_t incl = wave_incl_sum(copies);
     const uint32_t total = __shfl(incl, 63, 64);
     if (!total) return;
@@ -787,10 +788,10 @@ DEV void skew_append(const PartBufs& pb, DevCounters* ctr, bool want, const uint
             atomicOr(&ctr->part_overflow, 1ULL);
             break;
         }
-        uint64_t* r = pb.spill + pos * (MODE == 3 ? OW : OW + 1);
+        uint64_t* r = pb.spill + pos * (bloom_mode(MODE) ? OW : OW + 1);
 #pragma unroll
         for (int w = 0; w < OW; w++) r[w] = key[w];
-        if (MODE != 3) r[OW] = c;
+        if (!bloom_mode(MODE)) r[OW] = c;
     }
 }
 
@@ -861,6 +862,7 @@ DEV bool gated_off(const unsigned long long* gate) { return gate && *gate == 0; 
 
 // words per level-1 output key: the Bloom pass (MODE 3) moves table key word 0 only
 constexpr int p1_out_words(int W, int MODE) { return MODE == 3 ? 1 : W; }
+
 
 // Level 1: windows of a contiguous symbol range -> coarse bins (region >> f2bits).
 // MODE 0: count; 2: count behind the Bloom gate on the rolled root (reference layout);
@@ -977,7 +979,7 @@ __global__ __launch_bounds__(NT, 4) void k_p1(PackedView sv, int k, BloomView bf
     // pass counts its windows apart
     if constexpr (COUNTS)
         if (count) {
-            if constexpr (MODE == 3)
+            if constexpr (bloom_mode(MODE))
                 block_add4(n_win, 0, 0, 0, &ctr->bf_windows, nullptr, nullptr, nullptr);
             else
                 block_add4(n_win, Bin::kOwner ? 0 : n_ins, 0, 0, &ctr->windows, &ctr->inserted, nullptr, nullptr);
@@ -1001,7 +1003,7 @@ DEV uint64_t item_count(uint64_t n, const DevN& d) {
 template <int W, bool SCATTER>
 __global__ __launch_bounds__(COUNT_THREADS, 4) void k_p1k(const uint64_t* __restrict__ in, uint64_t n_host, PartBufs pb,
                                                        uint32_t F, BinRegion bin, DevCounters* __restrict__ ctr,
-                                                       int cnt_word, DevN dn) {
+                                                       int cnt_word, DevN dn, int istride) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int RUNW = run_w<W>(), TW = tile_win<W>();
     const uint64_t n = item_count(n_host, dn);
@@ -1023,7 +1025,7 @@ __global__ __launch_bounds__(COUNT_THREADS, 4) void k_p1k(const uint64_t* __rest
         for (int q = 0; q < RUNW; q++) {
             const uint64_t i = t0 + tid + (uint64_t)q * COUNT_THREADS;
 #pragma unroll
-            for (int w = 0; w < W; w++) tk[q][w] = i < hi ? in[i * W + w] : 0;
+            for (int w = 0; w < W; w++) tk[q][w] = i < hi ? in[i * istride + w] : 0;
             ok[q] = tk[q][0] != EMPTY;  // 0 is never a table key: skip (counted as invalid)
             if constexpr (!SCATTER) {
                 n_inv += (i < hi) & !ok[q];
@@ -1197,7 +1199,9 @@ constexpr size_t p2f_smem(uint32_t F, uint32_t nseg_max) { return part_smem<W, N
 #ifndef KC_PREFETCH
 #define KC_PREFETCH 1
 #endif
-template <int W, int NT>
+// IS: u64 words per level-1 item (W, or the whole table key of a kept level-1 output when
+// the Bloom pass reads only its word 0)
+template <int W, int NT, int IS = W>
 __global__ __launch_bounds__(NT, 2048 / NT) void k_p2f(TableView tv, PartBufs pb, DevCounters* __restrict__ ctr,
                                                           int REC) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -1225,7 +1229,7 @@ __global__ __launch_bounds__(NT, 2048 / NT) void k_p2f(TableView tv, PartBufs pb
     // segment cursor of this thread (its indices grow monotonically): segment cs holds
     // [cb, nb) of the virtual run, both bounds kept in registers
     uint32_t cs = 0, cb = 0, nb = nseg ? pre[1] : 0;
-    const uint64_t* sp = pb.keys1 + seg0 * pb.cap1 * W;  // segment cs
+    const uint64_t* sp = pb.keys1 + seg0 * pb.cap1 * IS;  // segment cs
     // a wave takes 64 * RUNW consecutive positions of the tile (the cursor rarely moves)
     const uint32_t wpos = (uint32_t)(tid >> 6) * (64 * RUNW) + (tid & 63);
     // Every lane loads (past the total: the first key again) and the select is on the address,
@@ -1244,9 +1248,9 @@ __global__ __launch_bounds__(NT, 2048 / NT) void k_p2f(TableView tv, PartBufs pb
                         cb = nb;
                         nb = pre[cs + 1];
                     } while (nb <= i);
-                    sp = pb.keys1 + (seg0 + cs) * pb.cap1 * W;
+                    sp = pb.keys1 + (seg0 + cs) * pb.cap1 * IS;
                 }
-                src = sp + (uint64_t)(i - cb) * W;
+                src = sp + (uint64_t)(i - cb) * IS;
             }
 #pragma unroll
             for (int w = 0; w < W; w++) tk[q][w] = ks_load(src + w);
@@ -2181,10 +2185,10 @@ static hipError_t insert_spill(TableView t, BloomView bf, DevCounters* ctr, Part
     if ((e = set_smem(k_p1k<IW, true>, sm1)) != hipSuccess) return e;
     const DevN dn{&ctr->spill_n, pb.spill_cap, &ctr->part_overflow};
     hipLaunchKernelGGL((k_p1k<IW, false>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1h, s, pb.spill, (uint64_t)0, pb,
-                       t.F1, bin, ctr, W, dn);
+                       t.F1, bin, ctr, W, dn, IW);
     launch_scan(pb.hist1, (uint64_t)t.F1 * pb.nblk1, pb.off1, pb.bsum, s);
     hipLaunchKernelGGL((k_p1k<IW, true>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1, s, pb.spill, (uint64_t)0, pb,
-                       t.F1, bin, ctr, W, dn);
+                       t.F1, bin, ctr, W, dn, IW);
     return part_levels23<W, true, GATE>(t, ctr, pb, s, nullptr, 0, bf);
 }
 
@@ -2257,7 +2261,11 @@ static hipError_t count_part_w(PackedView sym, int k, int mode, TableView t, Blo
 // bins -> filter regions (ft: R = filter regions, F1 x F2) -> k_b3 (LDS-resident filter
 // regions).  Segmented single passes with the exact pipeline behind the overflow gate,
 // as for the table.
-template <int W>
+// KEEP (level-1 reuse, kc_api.cpp): level 1 writes the whole table key (MODE 5) into the
+// coarse bins of the filter geometry, which the table of a reusing job shares (powers of
+// two: the same hash-prefix bins); the Bloom levels read word 0 of it, and the counting
+// pass starts at its level 2 on the same output.
+template <int W, bool KEEP>
 static hipError_t bloom_part_w(PackedView sym, int k, BloomView bf, TableView ft, DevCounters* ctr, PartBufs pb,
                                int fresh, hipStream_t s) {
     if (pb.cap1 == 0) {
@@ -2266,23 +2274,30 @@ static hipError_t bloom_part_w(PackedView sym, int k, BloomView bf, TableView ft
         if ((e = part_level2_exact<1>(ft, pb, s, nullptr)) != hipSuccess) return e;
         return launch_b3<false>(bf, ft, ctr, pb, nullptr, fresh, s);
     }
+    constexpr int MODE = KEEP ? 5 : 3, OW = KEEP ? W : 1;
     hipError_t e;
     const unsigned long long* gate = &ctr->part_overflow;
     hipLaunchKernelGGL(k_batch_begin, dim3(1), dim3(1), 0, s, ctr);
     const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
     constexpr int NT = scatter_threads<W>(), NT2 = p2f_threads<1>();
-    auto k1 = k_p1<W, 3, true, BinRegion, OutSeg, NT>;
-    const size_t sm1 = part_smem<1, NT>(ft.F1) + heavy_smem<1>(),
+    auto k1 = k_p1<W, MODE, true, BinRegion, OutSeg, NT>;
+    auto k2 = k_p2f<1, NT2, OW>;
+    const size_t sm1 = part_smem<OW, NT>(ft.F1) + heavy_smem<OW>(),
                  sm2 = p2f_smem<1, NT2>(ft.F2, (pb.nblk1 + pb.B2 - 1) / pb.B2);
     if ((e = set_smem(k1, sm1)) != hipSuccess) return e;
-    if ((e = set_smem(k_p2f<1, NT2>, sm2)) != hipSuccess) return e;
+    if ((e = set_smem(k2, sm2)) != hipSuccess) return e;
     const OutSeg o1{(uint64_t)pb.nblk1 * pb.cap1, 0, pb.cap1, pb.spill, pb.spill_cap, &ctr->spill_n,
                     &ctr->part_overflow, 0};
     hipLaunchKernelGGL(k1, dim3(pb.nblk1), dim3(NT), sm1, s, sym, k, bf, ctr, pb, ft.F1, coarse_bins(ft), pb.keys1, pk,
                        pkm1, o1, (const unsigned long long*)nullptr, 1);
-    hipLaunchKernelGGL((k_p2f<1, NT2>), dim3(ft.F1 * pb.B2), dim3(NT2), sm2, s, ft, pb, ctr, 0);
+    hipLaunchKernelGGL(k2, dim3(ft.F1 * pb.B2), dim3(NT2), sm2, s, ft, pb, ctr, 0);
+    if (KEEP && pb.keep_fill &&
+        (e = hipMemcpyAsync(pb.keep_fill, pb.hist1, (size_t)ft.F1 * pb.nblk1 * 4, hipMemcpyDeviceToDevice, s)) !=
+            hipSuccess)
+        return e;
     if ((e = launch_b3<true>(bf, ft, ctr, pb, nullptr, fresh, s)) != hipSuccess) return e;
-    // spilled keys (table key word 0) through the exact levels into the filter regions
+    // spilled keys (table key word 0 of OW-word entries) through the exact levels into the
+    // filter regions
     {
         const BinRegion bin = coarse_bins(ft);
         const size_t s1 = part_smem<1>(ft.F1), s1h = hist_smem(ft.F1);
@@ -2290,10 +2305,10 @@ static hipError_t bloom_part_w(PackedView sym, int k, BloomView bf, TableView ft
         if ((e = set_smem(k_p1k<1, true>, s1)) != hipSuccess) return e;
         const DevN dn{&ctr->spill_n, pb.spill_cap, &ctr->part_overflow};
         hipLaunchKernelGGL((k_p1k<1, false>), dim3(pb.nblk1), dim3(COUNT_THREADS), s1h, s, pb.spill, (uint64_t)0, pb,
-                           ft.F1, bin, ctr, -1, dn);
+                           ft.F1, bin, ctr, -1, dn, OW);
         launch_scan(pb.hist1, (uint64_t)ft.F1 * pb.nblk1, pb.off1, pb.bsum, s);
         hipLaunchKernelGGL((k_p1k<1, true>), dim3(pb.nblk1), dim3(COUNT_THREADS), s1, s, pb.spill, (uint64_t)0, pb,
-                           ft.F1, bin, ctr, -1, dn);
+                           ft.F1, bin, ctr, -1, dn, OW);
         if ((e = part_level2_exact<1>(ft, pb, s, nullptr)) != hipSuccess) return e;
         if ((e = launch_b3<false>(bf, ft, ctr, pb, nullptr, 0, s)) != hipSuccess) return e;
     }
@@ -2303,6 +2318,29 @@ static hipError_t bloom_part_w(PackedView sym, int k, BloomView bf, TableView ft
     if ((e = part_level2_exact<1>(ft, pb, s, gate)) != hipSuccess) return e;
     return launch_b3<false>(bf, ft, ctr, pb, gate, fresh, s);
 }
+
+// The counting pass of a job whose Bloom pass kept its level-1 output (pb.keys1 / hist1 /
+// cap1 / nblk1 / B2 of that pass; the table's coarse bins are the filter's): levels 2 and 3
+// behind the gate, the skew list, and the batch's windows (counted by the Bloom pass).
+static __global__ void k_add_windows(DevCounters* ctr, unsigned long long n) {
+    if (!ctr->part_overflow) ctr->windows += n;
+}
+template <int W>
+static hipError_t count_reuse_w(TableView t, BloomView bf, DevCounters* ctr, PartBufs pb, int fresh,
+                                uint64_t windows, hipStream_t s) {
+    hipError_t e;
+    hipLaunchKernelGGL(k_batch_begin, dim3(1), dim3(1), 0, s, ctr);
+    constexpr int NT = p2f_threads<W>();
+    const size_t sm2 = p2f_smem<W, NT>(t.F2, (pb.nblk1 + pb.B2 - 1) / pb.B2);
+    if ((e = set_smem(k_p2f<W, NT>, sm2)) != hipSuccess) return e;
+    hipLaunchKernelGGL((k_p2f<W, NT>), dim3(t.F1 * pb.B2), dim3(NT), sm2, s, t, pb, ctr, 1);
+    if ((e = launch_p3<W, true, false, true>(t, ctr, pb, nullptr, fresh, s, bf)) != hipSuccess) return e;
+    if ((e = insert_spill<W, true>(t, bf, ctr, pb, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_batch_end, dim3(1), dim3(1), 0, s, ctr);
+    hipLaunchKernelGGL(k_add_windows, dim3(1), dim3(1), 0, s, ctr, (unsigned long long)windows);
+    return hipGetLastError();
+}
+
 // Routing for hash-prefix sharding: windows -> table keys grouped by owner shard into
 // `out`; per-owner offsets in pb.off1 ([owner][block], exclusive, last entry = total).
 template <int W>
@@ -2323,10 +2361,10 @@ static hipError_t insert_items_part(const uint64_t* items, uint64_t n, TableView
     if ((e = set_smem(k_p1k<IW, true>, sm1)) != hipSuccess) return e;
     const int cw = CNT ? W : -1;
     hipLaunchKernelGGL((k_p1k<IW, false>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1h, s, items, n, pb, t.F1, bin, ctr,
-                       cw, DevN{});
+                       cw, DevN{}, IW);
     launch_scan(pb.hist1, (uint64_t)t.F1 * pb.nblk1, pb.off1, pb.bsum, s);
     hipLaunchKernelGGL((k_p1k<IW, true>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1, s, items, n, pb, t.F1, bin, ctr,
-                       cw, DevN{});
+                       cw, DevN{}, IW);
     return part_levels23<W, CNT>(t, ctr, pb, s, nullptr, fresh);
 }
 
@@ -2382,8 +2420,14 @@ hipError_t WOps<W>::count_partitioned(PackedView sym, int k, int mode, TableView
 
 template <int W>
 hipError_t WOps<W>::bloom_partitioned(PackedView sym, int k, BloomView bf, TableView ft, DevCounters* ctr,
-                                      PartBufs pb, int fresh, hipStream_t s) {
-    return bloom_part_w<W>(sym, k, bf, ft, ctr, pb, fresh, s);
+                                      PartBufs pb, int fresh, int keep, hipStream_t s) {
+    if (keep) return bloom_part_w<W, true>(sym, k, bf, ft, ctr, pb, fresh, s);
+    return bloom_part_w<W, false>(sym, k, bf, ft, ctr, pb, fresh, s);
+}
+template <int W>
+hipError_t WOps<W>::count_reuse(TableView t, BloomView bf, DevCounters* ctr, PartBufs pb, int fresh, uint64_t windows,
+                                hipStream_t s) {
+    return count_reuse_w<W>(t, bf, ctr, pb, fresh, windows, s);
 }
 
 template <int W>

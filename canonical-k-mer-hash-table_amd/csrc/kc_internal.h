@@ -113,6 +113,8 @@ struct PartBufs {
                                 // nullptr = fixed-capacity segments of cap2)
     uint64_t* spill;        // segmented batches: the skew list ({key words, count} records of keys past
     uint64_t spill_cap;     // a segment's end and of repeated windows; Bloom pass: keys), spill_cap entries
+    uint32_t* keep_fill;    // Bloom pass keeping its level 1 (level-1 reuse): a copy of its segment
+                            // fills ([F1][nblk1]; the skew-list pass reuses hist1)
 };
 
 struct BloomView {
@@ -143,6 +145,14 @@ inline int slots_per_bucket(int W) { return BUCKET_WORDS / (W + 1); }
 constexpr int run_width(int W) { return W == 1 ? 16 : W == 2 ? 8 : W <= 4 ? KC_RUNW_WIDE : 4; }
 constexpr int scatter_threads_w(int W) { return W <= 2 ? KC_SCATTER_NT12 : W <= 4 ? 512 : 256; }
 constexpr int p1_tile(int W) { return scatter_threads_w(W) * run_width(W); }  // windows per segmented level-1 tile
+// level 2 (k_p2f): workgroup size by key width, and its LDS for F2 regions per coarse bin
+#ifndef KC_P2F_NT
+#define KC_P2F_NT 0  // 0: the default below
+#endif
+constexpr int p2f_threads_w(int W) { return KC_P2F_NT ? KC_P2F_NT : (W <= 2 ? 1024 : W <= 4 ? 512 : 256); }
+constexpr size_t p2f_lds_bytes(int W, uint32_t F2, uint32_t nseg) {
+    return (size_t)F2 * 32 + 16 + (size_t)p2f_threads_w(W) * run_width(W) * 8 * W + ((size_t)nseg + 1) * 4;
+}
 
 // ---- launchers (kc_tokenize.hip, kc_count.hip) -------------------------------------------------
 // src: bytes the chunk descriptors' src_off point into (host stage or device image)
@@ -160,8 +170,18 @@ hipError_t launch_count_partitioned(PackedView sv, uint64_t sym_bound, int k, in
 // Bloom pass 1 on the blocked layout, partitioned: ft = the filter's region geometry
 // (R = filter regions of nblocks / R <= 1024 blocks, F1 x F2 as for the table; no buckets);
 // fresh: the filter is all zero (level 3 does not read it)
+// keep: level 1 writes whole table keys (kept for the counting pass, count_reuse)
 hipError_t launch_bloom_partitioned(PackedView sv, int k, int W, BloomView bf, TableView ft, DevCounters* ctr,
-                                    PartBufs pb, int fresh, hipStream_t s);
+                                    PartBufs pb, int fresh, int keep, hipStream_t s);
+// the counting pass from the level-1 output kept by the Bloom pass (pb: that output's
+// buffers); windows: the batch's windows (counted by the Bloom pass)
+hipError_t launch_count_reuse(int W, TableView t, BloomView bf, DevCounters* ctr, PartBufs pb, int fresh,
+                              uint64_t windows, hipStream_t s);
+// 64-bit checksum of the chunks' bytes (a promise check between two passes over one image):
+// CHECKSUM_SLOTS partial sums in out (their sum is the checksum)
+constexpr int CHECKSUM_SLOTS = 64;
+hipError_t launch_checksum(const uint8_t* src, const ChunkDesc* d_chunks, int n_chunks, uint64_t max_len,
+                           unsigned long long* out, hipStream_t s);
 // hash-prefix sharding: windows -> table keys grouped by owner (offsets in pb.off1)
 hipError_t launch_route(PackedView sym, int k, int W, DevCounters* ctr, PartBufs pb, uint32_t parts, uint64_t* out,
                         hipStream_t s);
@@ -205,7 +225,9 @@ struct WOps {
     static hipError_t count_partitioned(PackedView sym, int k, int mode, TableView t, BloomView bf, DevCounters* ctr,
                                         PartBufs pb, int fresh, hipStream_t s);
     static hipError_t bloom_partitioned(PackedView sym, int k, BloomView bf, TableView ft, DevCounters* ctr, PartBufs pb,
-                                        int fresh, hipStream_t s);
+                                        int fresh, int keep, hipStream_t s);
+    static hipError_t count_reuse(TableView t, BloomView bf, DevCounters* ctr, PartBufs pb, int fresh, uint64_t windows,
+                                  hipStream_t s);
     static hipError_t route(PackedView sym, int k, DevCounters* ctr, PartBufs pb, uint32_t parts, uint64_t* out,
                             hipStream_t s);
     static hipError_t insert_keys(const uint64_t* keys, uint64_t n, bool partitioned, TableView t, DevCounters* ctr,

@@ -16,4 +16,47 @@ hipError_t launch_xxh64(const uint64_t* v, const uint64_t* seed, uint64_t n, uin
     return hipGetLastError();
 }
 
+// Checksum of the chunks' bytes: the sum over every aligned 8-byte word w overlapping a
+// chunk of fmix64(w's chunk bytes + its address * C), bytes outside the chunk masked.
+// Two passes over one image compare their sums (kc_api.cpp level-1 reuse).
+constexpr int CK_T = 256, CK_PER = 32;  // words per thread
+constexpr int CK_SLOTS = 64;            // partial sums (the caller adds them)
+__global__ __launch_bounds__(CK_T) void k_checksum(const uint8_t* __restrict__ src, const ChunkDesc* __restrict__ ch,
+                                                   unsigned long long* __restrict__ out) {
+    const ChunkDesc d = ch[blockIdx.y];
+    const uint64_t a0 = (reinterpret_cast<uint64_t>(src) + d.src_off) & ~7ull;  // first aligned word
+    const uint64_t end = reinterpret_cast<uint64_t>(src) + d.src_off + d.len;
+    const uint64_t beg = reinterpret_cast<uint64_t>(src) + d.src_off;
+    unsigned long long h = 0;
+#pragma unroll
+    for (int q = 0; q < CK_PER; q++) {
+        const uint64_t a = a0 + 8 * ((uint64_t)blockIdx.x * CK_T * CK_PER + (uint64_t)q * CK_T + threadIdx.x);
+        if (a >= end) continue;
+        uint64_t v = *reinterpret_cast<const uint64_t*>(a);
+        if (a < beg) v &= ~0ull << (8 * (beg - a));              // little-endian: low bytes first
+        if (a + 8 > end) v &= ~0ull >> (8 * (a + 8 - end));
+        h += fmix64(v + (a - reinterpret_cast<uint64_t>(src)) * 0x9E3779B97F4A7C15ull + blockIdx.y);
+    }
+    for (int o = 32; o >= 1; o >>= 1) h += __shfl_xor(h, o, 64);
+    __shared__ unsigned long long s_h[CK_T / 64];
+    if ((threadIdx.x & 63) == 0) s_h[threadIdx.x >> 6] = h;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int w = 0; w < CK_T / 64; w++) t += s_h[w];
+        // one add per workgroup, spread over CK_SLOTS words (one word takes ~90 adds per us)
+        if (t) atomicAdd(out + ((blockIdx.x + blockIdx.y * 7) % CK_SLOTS), t);
+    }
+}
+
+hipError_t launch_checksum(const uint8_t* src, const ChunkDesc* d_chunks, int n_chunks, uint64_t max_len,
+                           unsigned long long* out, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(out, 0, CK_SLOTS * sizeof(unsigned long long), s);
+    if (e != hipSuccess || n_chunks == 0) return e;
+    const uint64_t words = max_len / 8 + 2, per = (uint64_t)CK_T * CK_PER;
+    hipLaunchKernelGGL(k_checksum, dim3((unsigned)((words + per - 1) / per), (unsigned)n_chunks), dim3(CK_T), 0, s, src,
+                       d_chunks, out);
+    return hipGetLastError();
+}
+
 }  // namespace kc

@@ -83,7 +83,8 @@ class kc_synth_skew(ctypes.Structure):
 class kc_stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in (
         "windows", "inserted", "distinct", "table_slots", "bf_windows", "bf_bits", "new_in_first",
-        "new_in_second", "failed_in_first", "chunks", "bytes", "part_fallbacks", "spilled", "heavy_records")]
+        "new_in_second", "failed_in_first", "chunks", "bytes", "part_fallbacks", "spilled", "heavy_records",
+        "reused_passes")]
 
     def as_dict(self) -> dict:
         return {n: int(getattr(self, n)) for n, _ in self._fields_}

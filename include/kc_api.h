@@ -86,6 +86,7 @@ typedef struct {
     uint64_t part_fallbacks;  /* partitioned batches redone on the exact layout (a full skew list) */
     uint64_t spilled;         /* keys past their segment's end, inserted through the exact levels */
     uint64_t heavy_records;   /* {k-mer, count} records of repeated windows (homopolymer runs) */
+    uint64_t reused_passes;   /* counting passes that started from the Bloom pass's level-1 output */
 } kc_stats;
 
 /* Creates the device table (PointerHashTableCanonicalAV ctor,
@@ -112,7 +113,13 @@ int kc_count_chunk(kc_ctx* ctx, const uint8_t* buf, size_t len, int fmt, int bro
  * (kc_plan_chunks), enqueued on hip_stream (a hipStream_t; NULL = the HIP null
  * stream) after the work already queued there, so a buffer produced on that stream
  * (e.g. by PyTorch on its current stream) is safe to pass.  The image must stay valid
- * until the work completes (kc_sync).  Every *_device entry point follows this rule. */
+ * until the work completes (kc_sync).  Every *_device entry point follows this rule.
+ * Level-1 reuse: when the Bloom pass is one staging batch, it keeps its window
+ * partition, and a counting pass given the same image pointer, chunk table and format
+ * -- and the same bytes, checked by a checksum of the chunks -- starts from that
+ * partition instead of tokenizing and canonicalising every window again (that counting
+ * call then waits for its work; kc_stats.reused_passes counts such passes).  Any
+ * difference runs the ordinary counting pass.  KC_REUSE=0 disables it. */
 int kc_bloom_device(kc_ctx* ctx, const uint8_t* dev_image, const kc_chunk* chunks, size_t n_chunks, int fmt,
                     void* hip_stream);
 int kc_count_device(kc_ctx* ctx, const uint8_t* dev_image, const kc_chunk* chunks, size_t n_chunks, int fmt,

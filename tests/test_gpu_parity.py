@@ -360,9 +360,95 @@ def test_bloom_at_scale_equals_exact_solid_kmers(k, fpr, insert_path):
     windows = N * (L - k + 1)
     assert st["windows"] == windows and st["bf_windows"] == windows
     assert st["inserted"] <= windows and n2 > 0
+    # the counting pass started from the Bloom pass's level-1 partition (same image, same
+    # chunks, one batch) on the segmented path; the direct and exact paths do not keep it
+    assert st["reused_passes"] == (1 if insert_path == "partitioned" else 0)
     a = want[np.lexsort(want[:, :-1].T[::-1])]
     b = got[np.lexsort(got[:, :-1].T[::-1])]
     assert np.array_equal(a, b)
+
+
+def _bloom_job_device(torch, img, chunks, k, count_img=None, count_chunks=None, batch_bytes=0):
+    cfg = ka.Config(k=k, min_abundance=2, bf_enable=True, est_unique=4_000_000, fpr=0.01, batch_bytes=batch_bytes)
+    with ka.KmerCounter(cfg) as kc:
+        kc.bloom_device(img.data_ptr(), chunks, ka.FMT_FASTA)
+        kc.bloom_finalize()
+        ci = img if count_img is None else count_img
+        kc.count_device(ci.data_ptr(), chunks if count_chunks is None else count_chunks, ka.FMT_FASTA)
+        st = kc.finish()
+        got = kc.dump()
+    return st, got[np.lexsort(got[:, :-1].T[::-1])]
+
+
+@pytest.mark.parametrize("change", ["none", "bytes", "chunks", "batches"])
+def test_level1_reuse_only_on_the_same_input(change, monkeypatch):
+    """Level-1 reuse (kc_api.cpp): the counting pass starts from the Bloom pass's window
+    partition only for the same image, chunk table and bytes in one batch.  Bytes changed
+    after the Bloom pass (checksum), a different chunk table, or a Bloom pass of several
+    batches run the ordinary counting pass; every variant equals the run with reuse off."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("KC_INSERT_PATH", "partitioned")
+    lib = ka.load_library()
+    N, L, G, k = 200_000, 150, 2_000_000, 51
+    nbytes = lib.kc_synth_bytes(0, N, L, 0)
+    img = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    assert lib.kc_synth_device(img.data_ptr(), 0, N, 5, G, L, 0, 0.002, 0.0, 0) == 0
+    torch.cuda.synchronize()
+    chunks = ka.plan_chunks(bytes(img.cpu().numpy()), k, ka.FMT_FASTA)
+    count_img, count_chunks, bb = None, None, 0
+    if change == "chunks":
+        count_chunks = chunks[: max(1, len(chunks) - 1)]
+    elif change == "batches":
+        bb = 16 << 20  # (a chunk is up to 10 MiB: several batches)
+    def run():
+        if change == "bytes":  # same pointer and chunks, bytes changed between the passes
+            img2 = img.clone()
+            st, got = None, None
+            cfg = ka.Config(k=k, min_abundance=2, bf_enable=True, est_unique=4_000_000, fpr=0.01)
+            with ka.KmerCounter(cfg) as kc:
+                kc.bloom_device(img2.data_ptr(), chunks, ka.FMT_FASTA)
+                kc.bloom_finalize()
+                torch.cuda.synchronize()
+                seg = img2[1000:1600]
+                seg[seg == ord("A")] = ord("C")  # the image changes between the passes
+                torch.cuda.synchronize()
+                kc.count_device(img2.data_ptr(), chunks, ka.FMT_FASTA)
+                st = kc.finish()
+                got = kc.dump()
+            return st, got[np.lexsort(got[:, :-1].T[::-1])]
+        return _bloom_job_device(torch, img, chunks, k, count_img, count_chunks, bb)
+    st, got = run()
+    assert st["reused_passes"] == (1 if change == "none" else 0)
+    monkeypatch.setenv("KC_REUSE", "0")
+    st0, want = run()
+    assert st0["reused_passes"] == 0
+    assert np.array_equal(got, want)
+    # (inserted may differ by count-1 k-mers: which first sightings pass the gate depends on
+    # the order of the Bloom insertions, nondeterministic in the reference too)
+    assert st["windows"] == st0["windows"] and st["inserted"] <= st["windows"]
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c["input"] == "skew.fasta" and "-b" in c["args"]][:1],
+                         ids=_case_id)
+def test_level1_reuse_declined_on_skewed_input(case, golden_input):
+    """Hot keys put heavy records into the Bloom pass's skew list: its partition is not the
+    whole input, so the counting pass runs in full (and matches the reference)."""
+    torch = pytest.importorskip("torch")
+    path = golden_input(case["input"])
+    o = parse_ref_args(case["args"])
+    image = open(path, "rb").read()
+    chunks = ka.plan_chunks(image, case["k"], ka.FMT_FASTA)
+    dev = torch.frombuffer(bytearray(image), dtype=torch.uint8).cuda()
+    cfg = ka.Config(k=case["k"], mode=o["mode"], min_abundance=o["min_abundance"], bf_enable=True,
+                    est_unique=o["est_unique"], fpr=o["fpr"])
+    with ka.KmerCounter(cfg) as kc:
+        kc.bloom_device(dev.data_ptr(), chunks, ka.FMT_FASTA)
+        kc.bloom_finalize()
+        kc.count_device(dev.data_ptr(), chunks, ka.FMT_FASTA)
+        st = kc.finish()
+        lines = kc.lines()
+    assert st["reused_passes"] == 0
+    assert sorted_digest_lines(lines) == (case["sorted_sha256"], case["lines"])
 
 
 @pytest.mark.parametrize("spill", ["list", "full"])
