@@ -302,8 +302,9 @@ def run_workload(args, env, image=None):
     if dist:
         kname = "local count pass + merge insert of the received {key, count} records"
     elif args.unique:
-        kname = ("Bloom pass 1 (k_p1 -> k_p2f -> k_b3: LDS-resident filter regions) + counting pass "
-                 "(k_p1, k_p2f, k_p3 with the gate at level 3), one of each per batch")
+        kname = ("Bloom pass 1 (k_p1 -> k_p2f -> k_b3: LDS-resident filter regions, whole table keys in fine "
+                 "hash-prefix bins) + counting pass from the kept partitions (k_p3 with the gate at level 3; "
+                 "kc_stats.reused_passes), one of each per batch")
     else:
         kname = "count pass: k_p1 (segmented scatter), k_p2f, k_p3 (partitioned insert)"
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

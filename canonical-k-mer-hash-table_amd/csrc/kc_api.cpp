@@ -130,8 +130,11 @@ struct kc_ctx {
     unsigned long long reuse_sum = 0; // checksum of the Bloom pass's chunk bytes
     uint64_t reuse_windows = 0;       // windows of that batch
     unsigned long long* d_sum = nullptr;  // CHECKSUM_SLOTS partial sums
-    uint32_t* d_keep_fill = nullptr;      // the kept level 1's segment fills ([F1][nblk1])
-    uint64_t keep_fill_cap = 0;
+    uint32_t* d_keep_fill = nullptr;      // the kept partitions' segment fills: level 1 [F1][nblk1]
+    uint32_t* d_keep_fill2 = nullptr;     // and level 2 [R_fine][B2]
+    uint64_t keep_fill_cap = 0, keep_fill2_cap = 0;
+    TableView fgeo{};                     // the kept partitions' fine geometry (powers of two)
+    int reuse_level = 0;                  // kc_bloom_finalize: 2 = from level 2, 1 = from level 1
     uint64_t reuse_hits = 0;          // counting passes that reused (kc_stats.reused_passes)
 
     uint64_t n_chunks = 0, n_bytes = 0;
@@ -437,24 +440,30 @@ static int run_batch(kc_ctx* c, const uint8_t* src, uint64_t used, uint64_t nchu
         const char* env = std::getenv("KC_INSERT_PATH");
         const bool seg = !(env && !std::strcmp(env, "exact"));
         keep = keep && seg;  // (the exact layout does not keep: its level 1 moves word 0 only)
-        int rc = ensure_part_geo(c, syms, seg, PartGeo{c->bgeo.F1, c->bgeo.F2, c->bgeo.R, keep ? c->W : 1}, c->pbf,
-                                 c->pbf_cap);
+        keep = keep && c->fgeo.R != 0;
+        const PartGeo g = keep ? PartGeo{c->fgeo.F1, c->fgeo.F2, c->fgeo.R, c->W}
+                               : PartGeo{c->bgeo.F1, c->bgeo.F2, c->bgeo.R, 1};
+        int rc = ensure_part_geo(c, syms, seg, g, c->pbf, c->pbf_cap);
         if (rc) return rc;
-        c->pbf.keep_fill = nullptr;
-        if (keep) {
-            const uint64_t nf = (uint64_t)c->bgeo.F1 * c->pbf.nblk1;
-            if (nf > c->keep_fill_cap) {
-                hipFree(c->d_keep_fill);
-                c->d_keep_fill = nullptr;
-                c->keep_fill_cap = 0;
-                if (hipMalloc(&c->d_keep_fill, nf * 4) != hipSuccess)
-                    return c->fail(KC_ERR_NOMEM, "level-1 fill copy allocation failed");
-                c->keep_fill_cap = nf;
-            }
+        c->pbf.keep_fill = c->pbf.keep_fill2 = nullptr;
+        if (keep) {  // copies of the kept partitions' segment fills
+            auto grow = [&](uint32_t** p, uint64_t* cap, uint64_t n) -> int {
+                if (n <= *cap) return KC_OK;
+                hipFree(*p);
+                *p = nullptr;
+                *cap = 0;
+                if (hipMalloc(p, n * 4) != hipSuccess) return c->fail(KC_ERR_NOMEM, "partition fill copy allocation failed");
+                *cap = n;
+                return KC_OK;
+            };
+            if ((rc = grow(&c->d_keep_fill, &c->keep_fill_cap, (uint64_t)c->fgeo.F1 * c->pbf.nblk1)) ||
+                (rc = grow(&c->d_keep_fill2, &c->keep_fill2_cap, c->fgeo.R * c->pbf.B2)))
+                return rc;
             c->pbf.keep_fill = c->d_keep_fill;
+            c->pbf.keep_fill2 = c->d_keep_fill2;
         }
-        HIPCHK(c, launch_bloom_partitioned(sv, c->cfg.k, c->W, bv, c->bgeo, c->d_ctr, c->pbf, c->bloom_fresh,
-                                           keep ? 1 : 0, s));
+        HIPCHK(c, launch_bloom_partitioned(sv, c->cfg.k, c->W, bv, c->bgeo, c->fgeo, c->d_ctr, c->pbf,
+                                           c->bloom_fresh, keep ? 1 : 0, s));
         c->bloom_fresh = false;
         c->reuse_kept = keep;
     } else if (mode != 1 && use_partitioned(c, syms)) {
@@ -596,20 +605,27 @@ static int count_reused(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, s
         release();
         return KC_OK;
     }
-    // the table's partition buffers for this batch: level 1 = the Bloom pass's output
+    // the table's partition buffers for this batch, with the Bloom pass's partitions as its
+    // level 1 (and level 2); the kept buffers must not have moved
     const uint64_t syms = used + b.size();
     if ((rc = ensure_part(c, syms, true))) return rc;
     PartBufs pr = c->pb;
-    if (pr.keys1 != c->pbf.keys1 || pr.nblk1 != c->pbf.nblk1 || pr.B2 != c->pbf.B2 || pr.cap1 != c->pbf.cap1 ||
-        pr.cap1 == 0) {
+    if (pr.keys1 != c->pbf.keys1 || (c->reuse_level == 2 && pr.keys2 != c->pbf.keys2) || pr.nblk1 != c->pbf.nblk1 ||
+        pr.B2 != c->pbf.B2 || pr.cap1 != c->pbf.cap1 || pr.cap1 == 0 || c->F1 != c->fgeo.F1) {
         if (std::getenv("KC_REUSE_DEBUG")) std::fprintf(stderr, "reuse: partition geometry differs\n");
         release();
         return KC_OK;
     }
     pr.hist1 = c->d_keep_fill;
+    if (c->reuse_level == 2) {  // a table region = fgeo.R / R consecutive fine bins
+        pr.hist2 = c->d_keep_fill2;
+        pr.cap2 = c->pbf.cap2;
+        pr.B2 = (uint32_t)(c->fgeo.R / c->R) * c->pbf.B2;
+    }
     const BloomView bv{c->d_bloom, c->bf_bits ? c->bf_bits - 1 : 0, c->nh, c->nh_gate, c->bloom_blocked,
                        bloom_blocks(c->bf_bits)};
-    HIPCHK(c, launch_count_reuse(c->W, table_view(c), bv, c->d_ctr, pr, c->table_fresh, c->reuse_windows, s));
+    HIPCHK(c, launch_count_reuse(c->W, table_view(c), bv, c->d_ctr, pr, c->table_fresh, c->reuse_level,
+                                 c->reuse_windows, s));
     if (ev[3]) HIPCHK(c, hipEventRecord(ev[3], s));
     unsigned long long ovf = 0;
     HIPCHK(c, hipMemcpyAsync(&ovf, &c->d_ctr->part_overflow, sizeof(ovf), hipMemcpyDeviceToHost, s));
@@ -808,6 +824,35 @@ int kc_create(const kc_config* cfg, kc_ctx** out) {
             c->bgeo.F2 = 1u << c->bgeo.f2bits;
             c->bgeo.F1 = (uint32_t)(R >> c->bgeo.f2bits);
             c->bgeo.W = 1;
+            // partition reuse: fine bins for a table of up to 2 * est_unique slots (the table
+            // of the counting pass holds 2 * new_in_second <= about 2 * -u), never coarser than
+            // the filter regions, and as fine as level 1 (two workgroups per CU), level 2 and
+            // k_b3 (segments per filter region) allow
+            {
+                uint64_t want = std::max<uint64_t>(2 * cfg->est_unique, 64);
+                want += want / 4;
+                const uint64_t regions = std::max<uint64_t>(1, ((want + c->S - 1) / c->S + BPR - 1) / BPR);
+                int fb = rbits, f1 = 0;
+                while ((1ULL << fb) < regions) fb++;
+                // (wide keys run one level-1 workgroup per CU anyway)
+                const size_t p1_cap = p1_lds_bytes(c->W, 1) <= 80 * 1024 ? 80 * 1024 : 160 * 1024;
+                for (; fb >= rbits; fb--) {
+                    f1 = std::min(fb, std::min(8, (fb + 1) / 2 + 1));
+                    while (f1 > 0 && p1_lds_bytes(c->W, 1u << f1) > p1_cap) f1--;
+                    const uint32_t F2 = 1u << (fb - f1), F1 = 1u << f1;
+                    const uint32_t B2 = std::max<uint32_t>(1, std::min<uint32_t>(64, 2048 / F1));
+                    if (p2f_lds_bytes(c->W, F2, 2048 / B2 + 1) <= 160 * 1024 &&
+                        (1ULL << (fb - rbits)) * B2 <= MAX_SEG_GROUP)
+                        break;
+                }
+                if (fb >= rbits) {
+                    c->fgeo.R = 1ULL << fb;
+                    c->fgeo.f2bits = fb - f1;
+                    c->fgeo.F2 = 1u << c->fgeo.f2bits;
+                    c->fgeo.F1 = 1u << f1;
+                    c->fgeo.W = c->W;
+                }
+            }
         }
     } else {
         int rc = alloc_table(c, cfg->table_slots);
@@ -836,6 +881,7 @@ void kc_destroy(kc_ctx* c) {
     hipFree(c->d_ctr);
     hipFree(c->d_sum);
     hipFree(c->d_keep_fill);
+    hipFree(c->d_keep_fill2);
     hipFree(c->d_table);
     hipFree(c->d_bloom);
     hipFree(c->pb.hist1);
@@ -888,18 +934,26 @@ int kc_bloom_finalize(kc_ctx* c, uint64_t* new_in_second) {
     HIPCHK(c, hipMemcpy(&h, c->d_ctr, sizeof(h), hipMemcpyDeviceToHost));
     if (new_in_second) *new_in_second = h.new_in_second;
     c->bloom_final = true;
-    // level-1 reuse: the only Bloom batch kept its level-1 output and no key of it went to a
-    // skew list; the table takes the filter's coarse bins if its level 2 still fits the LDS
+    // partition reuse: the only Bloom batch kept its partitions and no key of them went to a
+    // skew list.  The table then takes power-of-two hash-prefix bins: R_t regions with the
+    // fine geometry's coarse bins (F1); from level 2 if its regions are unions of fine bins
+    // (R_t <= R_fine, at most MAX_SEG_GROUP segments per region), else from level 1 if that
+    // level 2 fits the LDS.
     bool reuse = c->reuse_kept && c->bloom_batches == 1 && h.part_fallbacks == 0 && h.spilled == 0 && h.heavy == 0;
     const uint64_t slots = 2 * h.new_in_second;  // main.cpp:454
+    c->reuse_level = 0;
     if (reuse) {
         uint64_t want = std::max<uint64_t>(slots, 64);
         want += want / 4;
         const uint64_t regions = std::max<uint64_t>(1, ((want + c->S - 1) / c->S + BPR - 1) / BPR);
-        uint64_t f2 = 1;
-        while (f2 * c->bgeo.F1 < regions) f2 *= 2;
+        uint64_t rt = c->fgeo.F1;
+        while (rt < regions) rt *= 2;
         const uint32_t nseg = (c->pbf.nblk1 + c->pbf.B2 - 1) / std::max<uint32_t>(1, c->pbf.B2);
-        reuse = p2f_lds_bytes(c->W, (uint32_t)f2, nseg) <= 160 * 1024 && f2 * c->bgeo.F1 < (1ULL << 32);
+        if (rt <= c->fgeo.R && (c->fgeo.R / rt) * c->pbf.B2 <= MAX_SEG_GROUP)
+            c->reuse_level = 2;
+        else if (p2f_lds_bytes(c->W, (uint32_t)(rt / c->fgeo.F1), nseg) <= 160 * 1024 && rt < (1ULL << 32))
+            c->reuse_level = 1;
+        reuse = c->reuse_level != 0;
     }
     if (reuse) {
         unsigned long long part[CHECKSUM_SLOTS];
@@ -910,10 +964,10 @@ int kc_bloom_finalize(kc_ctx* c, uint64_t* new_in_second) {
     }
     c->reuse_ok = reuse;
     if (std::getenv("KC_REUSE_DEBUG"))
-        std::fprintf(stderr, "reuse finalize: kept %d batches %d fallbacks %llu spilled %llu heavy %llu -> %d\n",
+        std::fprintf(stderr, "reuse finalize: kept %d batches %d fallbacks %llu spilled %llu heavy %llu -> level %d\n",
                      (int)c->reuse_kept, c->bloom_batches, (unsigned long long)h.part_fallbacks,
-                     (unsigned long long)h.spilled, (unsigned long long)h.heavy, (int)reuse);
-    rc = alloc_table(c, slots, reuse ? c->bgeo.F1 : 0);
+                     (unsigned long long)h.spilled, (unsigned long long)h.heavy, c->reuse_level);
+    rc = alloc_table(c, slots, reuse ? c->fgeo.F1 : 0);
     if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return KC_OK;
@@ -1285,6 +1339,7 @@ int kc_reset(kc_ctx* c) {
     c->n_chunks = c->n_bytes = 0;
     c->bloom_batches = 0;
     c->reuse_kept = c->reuse_ok = false;
+    c->reuse_level = 0;
     c->reuse_hits = 0;
     return KC_OK;
 }

@@ -30,16 +30,18 @@ hipError_t launch_count_partitioned(PackedView sym, uint64_t sym_bound, int k, i
 }
 
 // the blocked layout's filter regions: R divides the block count, <= 1024 blocks each
-hipError_t launch_bloom_partitioned(PackedView sym, int k, int W, BloomView bf, TableView ft, DevCounters* ctr,
-                                    PartBufs pb, int fresh, int keep, hipStream_t s) {
+hipError_t launch_bloom_partitioned(PackedView sym, int k, int W, BloomView bf, TableView ft, TableView fg,
+                                    DevCounters* ctr, PartBufs pb, int fresh, int keep, hipStream_t s) {
     if (!bf.blocked || ft.R == 0 || bf.nblocks % ft.R || bf.nblocks / ft.R > (uint64_t)BF_BLOCKS_PER_REGION) return hipErrorInvalidValue;
-    KC_DISPATCH_W(W, bloom_partitioned(sym, k, bf, ft, ctr, pb, fresh, keep, s));
+    // the fine bins refine the filter regions (both powers of two)
+    if (keep && (fg.R < ft.R || fg.R % ft.R || (fg.R & (fg.R - 1)))) return hipErrorInvalidValue;
+    KC_DISPATCH_W(W, bloom_partitioned(sym, k, bf, ft, fg, ctr, pb, fresh, keep, s));
 }
 
-hipError_t launch_count_reuse(int W, TableView t, BloomView bf, DevCounters* ctr, PartBufs pb, int fresh,
+hipError_t launch_count_reuse(int W, TableView t, BloomView bf, DevCounters* ctr, PartBufs pb, int fresh, int level,
                               uint64_t windows, hipStream_t s) {
     if (!bf.blocked || pb.cap1 == 0 || t.F1 * pb.B2 == 0) return hipErrorInvalidValue;
-    KC_DISPATCH_W(W, count_reuse(t, bf, ctr, pb, fresh, windows, s));
+    KC_DISPATCH_W(W, count_reuse(t, bf, ctr, pb, fresh, level, windows, s));
 }
 
 hipError_t launch_route(PackedView sym, int k, int W, DevCounters* ctr, PartBufs pb, uint32_t parts, uint64_t* out,

@@ -1321,7 +1321,7 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
     constexpr int NT = P3_THREADS;
     constexpr int IW = CNT ? W + 1 : W;  // words per item
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    __shared__ uint32_t s_pre[65];  // SEG: exclusive prefix of the B2 (<= 64) segment fills
+    __shared__ uint32_t s_pre[MAX_SEG_GROUP + 1];  // SEG: exclusive prefix of the B2 segment fills
     constexpr int S = BUCKET_WORDS / (W + 1);
     // keys loaded per thread before inserting (memory-level parallelism); 1024-thread
     // groups already keep 8 waves per SIMD in flight
@@ -1678,10 +1678,11 @@ constexpr int B3_THREADS = KC_B3_NT;  // two 64 KiB regions per CU
 template <bool SEG>
 __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView bf, uint32_t bpr, PartBufs pb,
                                                                   DevCounters* __restrict__ ctr,
-                                                                  const unsigned long long* gate, int fresh) {
+                                                                  const unsigned long long* gate, int fresh, int is) {
+    // is: u64 words per item (word 0 is the table key word the filter uses)
     constexpr int NT = B3_THREADS, KB = KC_B3_KB;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    __shared__ uint32_t s_pre[65];
+    __shared__ uint32_t s_pre[MAX_SEG_GROUP + 1];
     if constexpr (SEG) {
         if (ctr->part_overflow) return;
     } else {
@@ -1731,9 +1732,9 @@ __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView b
                         cb = nb;
                         nb = s_pre[cs + 1];
                     }
-                    t0[q] = pb.keys2[(r * pb.B2 + cs) * pb.cap2 + (i - cb)];
+                    t0[q] = pb.keys2[((r * pb.B2 + cs) * pb.cap2 + (i - cb)) * is];
                 } else {
-                    t0[q] = pb.keys2[i];
+                    t0[q] = pb.keys2[i * is];
                 }
             }
         }
@@ -2108,6 +2109,7 @@ static hipError_t launch_p3(TableView t, DevCounters* ctr, PartBufs pb, const un
         sm3 += (size_t)bf.slice_blocks * 32;
     }
     auto p3 = k_p3<W, SEG, CNT, GATE>;
+    if (SEG && pb.B2 > MAX_SEG_GROUP) return hipErrorInvalidValue;
     hipError_t e = set_smem(p3, sm3);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(p3, dim3((unsigned)t.R), dim3(P3_THREADS), sm3, s, t, pb, ctr, gate, fresh, bf);
@@ -2140,12 +2142,13 @@ static hipError_t part_levels23(TableView t, DevCounters* ctr, PartBufs pb, hipS
 
 template <bool SEG>
 static hipError_t launch_b3(BloomView bf, TableView ft, DevCounters* ctr, PartBufs pb, const unsigned long long* gate,
-                            int fresh, hipStream_t s) {
+                            int fresh, hipStream_t s, int is = 1) {
     const uint32_t bpr = (uint32_t)(bf.nblocks / ft.R);
     const size_t sm = (size_t)bpr * BF_BLOCK_WORDS * 4 + (size_t)(B3_THREADS / 64) * 64 * 8;  // + wave queues
+    if (SEG && pb.B2 > MAX_SEG_GROUP) return hipErrorInvalidValue;
     hipError_t e = set_smem(k_b3<SEG>, sm);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_b3<SEG>, dim3((unsigned)ft.R), dim3(B3_THREADS), sm, s, bf, bpr, pb, ctr, gate, fresh);
+    hipLaunchKernelGGL(k_b3<SEG>, dim3((unsigned)ft.R), dim3(B3_THREADS), sm, s, bf, bpr, pb, ctr, gate, fresh, is);
     return hipGetLastError();
 }
 
@@ -2261,13 +2264,15 @@ static hipError_t count_part_w(PackedView sym, int k, int mode, TableView t, Blo
 // bins -> filter regions (ft: R = filter regions, F1 x F2) -> k_b3 (LDS-resident filter
 // regions).  Segmented single passes with the exact pipeline behind the overflow gate,
 // as for the table.
-// KEEP (level-1 reuse, kc_api.cpp): level 1 writes the whole table key (MODE 5) into the
-// coarse bins of the filter geometry, which the table of a reusing job shares (powers of
-// two: the same hash-prefix bins); the Bloom levels read word 0 of it, and the counting
-// pass starts at its level 2 on the same output.
+// KEEP (partition reuse, kc_api.cpp): levels 1 and 2 move the whole table key (MODE 5) and
+// partition by fg, a power-of-two geometry at least as fine as the filter regions ft; k_b3
+// reads word 0 of each filter region's fine bins (consecutive, B2 x R_fine / R_f segments).
+// A table of the same hash-prefix bins can then be counted from these partitions: from level
+// 2 (its regions are unions of fine bins) or from level 1 (its coarse bins are fg's).  The
+// segment fills of both levels are copied aside (the skew-list pass reuses hist1 / hist2).
 template <int W, bool KEEP>
-static hipError_t bloom_part_w(PackedView sym, int k, BloomView bf, TableView ft, DevCounters* ctr, PartBufs pb,
-                               int fresh, hipStream_t s) {
+static hipError_t bloom_part_w(PackedView sym, int k, BloomView bf, TableView ft, TableView fg, DevCounters* ctr,
+                               PartBufs pb, int fresh, hipStream_t s) {
     if (pb.cap1 == 0) {
         hipError_t e = part_level1<W, 3>(sym, k, bf, ctr, pb, ft.F1, coarse_bins(ft), pb.keys1, s);
         if (e != hipSuccess) return e;
@@ -2275,27 +2280,34 @@ static hipError_t bloom_part_w(PackedView sym, int k, BloomView bf, TableView ft
         return launch_b3<false>(bf, ft, ctr, pb, nullptr, fresh, s);
     }
     constexpr int MODE = KEEP ? 5 : 3, OW = KEEP ? W : 1;
+    const TableView& lg = KEEP ? fg : ft;  // the partition levels' geometry
     hipError_t e;
     const unsigned long long* gate = &ctr->part_overflow;
     hipLaunchKernelGGL(k_batch_begin, dim3(1), dim3(1), 0, s, ctr);
     const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
-    constexpr int NT = scatter_threads<W>(), NT2 = p2f_threads<1>();
+    constexpr int NT = scatter_threads<W>(), NT2 = p2f_threads<OW>();
     auto k1 = k_p1<W, MODE, true, BinRegion, OutSeg, NT>;
-    auto k2 = k_p2f<1, NT2, OW>;
-    const size_t sm1 = part_smem<OW, NT>(ft.F1) + heavy_smem<OW>(),
-                 sm2 = p2f_smem<1, NT2>(ft.F2, (pb.nblk1 + pb.B2 - 1) / pb.B2);
+    auto k2 = k_p2f<OW, NT2>;
+    const size_t sm1 = part_smem<OW, NT>(lg.F1) + heavy_smem<OW>(),
+                 sm2 = p2f_smem<OW, NT2>(lg.F2, (pb.nblk1 + pb.B2 - 1) / pb.B2);
     if ((e = set_smem(k1, sm1)) != hipSuccess) return e;
     if ((e = set_smem(k2, sm2)) != hipSuccess) return e;
     const OutSeg o1{(uint64_t)pb.nblk1 * pb.cap1, 0, pb.cap1, pb.spill, pb.spill_cap, &ctr->spill_n,
                     &ctr->part_overflow, 0};
-    hipLaunchKernelGGL(k1, dim3(pb.nblk1), dim3(NT), sm1, s, sym, k, bf, ctr, pb, ft.F1, coarse_bins(ft), pb.keys1, pk,
+    hipLaunchKernelGGL(k1, dim3(pb.nblk1), dim3(NT), sm1, s, sym, k, bf, ctr, pb, lg.F1, coarse_bins(lg), pb.keys1, pk,
                        pkm1, o1, (const unsigned long long*)nullptr, 1);
-    hipLaunchKernelGGL(k2, dim3(ft.F1 * pb.B2), dim3(NT2), sm2, s, ft, pb, ctr, 0);
-    if (KEEP && pb.keep_fill &&
-        (e = hipMemcpyAsync(pb.keep_fill, pb.hist1, (size_t)ft.F1 * pb.nblk1 * 4, hipMemcpyDeviceToDevice, s)) !=
-            hipSuccess)
-        return e;
-    if ((e = launch_b3<true>(bf, ft, ctr, pb, nullptr, fresh, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k2, dim3(lg.F1 * pb.B2), dim3(NT2), sm2, s, lg, pb, ctr, 0);
+    PartBufs p3 = pb;  // k_b3's view: a filter region = R_fine / R_f consecutive fine bins
+    if constexpr (KEEP) {
+        if (pb.keep_fill &&
+            ((e = hipMemcpyAsync(pb.keep_fill, pb.hist1, (size_t)fg.F1 * pb.nblk1 * 4, hipMemcpyDeviceToDevice, s)) !=
+                 hipSuccess ||
+             (e = hipMemcpyAsync(pb.keep_fill2, pb.hist2, (size_t)fg.R * pb.B2 * 4, hipMemcpyDeviceToDevice, s)) !=
+                 hipSuccess))
+            return e;
+        p3.B2 = (uint32_t)(fg.R / ft.R) * pb.B2;
+    }
+    if ((e = launch_b3<true>(bf, ft, ctr, p3, nullptr, fresh, s, OW)) != hipSuccess) return e;
     // spilled keys (table key word 0 of OW-word entries) through the exact levels into the
     // filter regions
     {
@@ -2319,23 +2331,29 @@ static hipError_t bloom_part_w(PackedView sym, int k, BloomView bf, TableView ft
     return launch_b3<false>(bf, ft, ctr, pb, gate, fresh, s);
 }
 
-// The counting pass of a job whose Bloom pass kept its level-1 output (pb.keys1 / hist1 /
-// cap1 / nblk1 / B2 of that pass; the table's coarse bins are the filter's): levels 2 and 3
-// behind the gate, the skew list, and the batch's windows (counted by the Bloom pass).
+// The counting pass of a job whose Bloom pass kept its partitions (bloom_part_w KEEP):
+// level >= 2: pb.keys2 / hist2 / cap2 are the fine bins and pb.B2 the fine bins per table
+// region times their segments (the regions are unions of fine bins): level 3 only; level 1:
+// pb.keys1 / hist1 / cap1 / nblk1 / B2 are the kept level 1 (the table's coarse bins are
+// the fine geometry's): levels 2 and 3.  Then the skew list and the batch's windows (counted
+// by the Bloom pass).
 static __global__ void k_add_windows(DevCounters* ctr, unsigned long long n) {
     if (!ctr->part_overflow) ctr->windows += n;
 }
 template <int W>
-static hipError_t count_reuse_w(TableView t, BloomView bf, DevCounters* ctr, PartBufs pb, int fresh,
+static hipError_t count_reuse_w(TableView t, BloomView bf, DevCounters* ctr, PartBufs pb, int fresh, int level,
                                 uint64_t windows, hipStream_t s) {
     hipError_t e;
     hipLaunchKernelGGL(k_batch_begin, dim3(1), dim3(1), 0, s, ctr);
-    constexpr int NT = p2f_threads<W>();
-    const size_t sm2 = p2f_smem<W, NT>(t.F2, (pb.nblk1 + pb.B2 - 1) / pb.B2);
-    if ((e = set_smem(k_p2f<W, NT>, sm2)) != hipSuccess) return e;
-    hipLaunchKernelGGL((k_p2f<W, NT>), dim3(t.F1 * pb.B2), dim3(NT), sm2, s, t, pb, ctr, 1);
+    if (level < 2) {
+        constexpr int NT = p2f_threads<W>();
+        const size_t sm2 = p2f_smem<W, NT>(t.F2, (pb.nblk1 + pb.B2 - 1) / pb.B2);
+        if ((e = set_smem(k_p2f<W, NT>, sm2)) != hipSuccess) return e;
+        hipLaunchKernelGGL((k_p2f<W, NT>), dim3(t.F1 * pb.B2), dim3(NT), sm2, s, t, pb, ctr, 1);
+    }
     if ((e = launch_p3<W, true, false, true>(t, ctr, pb, nullptr, fresh, s, bf)) != hipSuccess) return e;
-    if ((e = insert_spill<W, true>(t, bf, ctr, pb, s)) != hipSuccess) return e;
+    // (from level 2 nothing can reach the skew list: no level of this pass scatters)
+    if (level < 2 && (e = insert_spill<W, true>(t, bf, ctr, pb, s)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_batch_end, dim3(1), dim3(1), 0, s, ctr);
     hipLaunchKernelGGL(k_add_windows, dim3(1), dim3(1), 0, s, ctr, (unsigned long long)windows);
     return hipGetLastError();
@@ -2419,15 +2437,15 @@ hipError_t WOps<W>::count_partitioned(PackedView sym, int k, int mode, TableView
 }
 
 template <int W>
-hipError_t WOps<W>::bloom_partitioned(PackedView sym, int k, BloomView bf, TableView ft, DevCounters* ctr,
+hipError_t WOps<W>::bloom_partitioned(PackedView sym, int k, BloomView bf, TableView ft, TableView fg, DevCounters* ctr,
                                       PartBufs pb, int fresh, int keep, hipStream_t s) {
-    if (keep) return bloom_part_w<W, true>(sym, k, bf, ft, ctr, pb, fresh, s);
-    return bloom_part_w<W, false>(sym, k, bf, ft, ctr, pb, fresh, s);
+    if (keep) return bloom_part_w<W, true>(sym, k, bf, ft, fg, ctr, pb, fresh, s);
+    return bloom_part_w<W, false>(sym, k, bf, ft, fg, ctr, pb, fresh, s);
 }
 template <int W>
-hipError_t WOps<W>::count_reuse(TableView t, BloomView bf, DevCounters* ctr, PartBufs pb, int fresh, uint64_t windows,
-                                hipStream_t s) {
-    return count_reuse_w<W>(t, bf, ctr, pb, fresh, windows, s);
+hipError_t WOps<W>::count_reuse(TableView t, BloomView bf, DevCounters* ctr, PartBufs pb, int fresh, int level,
+                                uint64_t windows, hipStream_t s) {
+    return count_reuse_w<W>(t, bf, ctr, pb, fresh, level, windows, s);
 }
 
 template <int W>

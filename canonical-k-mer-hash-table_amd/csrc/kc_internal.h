@@ -27,6 +27,7 @@ constexpr int MAX_NH = 10;                 // -f >= 0.001  =>  ceil(-ln f / ln 2
 constexpr uint8_t SYM_BREAK = 4;
 constexpr int BF_BLOCKS_PER_REGION = 1024; // Bloom blocks (64 B) per LDS-resident filter region: 64 KiB
 constexpr uint32_t RT_MAX_PARTS = 64;      // shards of the table routing (LDS per-owner counters)
+constexpr uint32_t MAX_SEG_GROUP = 128;    // level-2 segments one level-3 workgroup reads (k_p3, k_b3)
 
 // symbol-stream code for byte b outside a header (functions_strings.cpp:56-70)
 enum Fmt { FMT_FASTA = 0, FMT_FASTQ = 1, FMT_PLAIN = 2 };
@@ -113,8 +114,8 @@ struct PartBufs {
                                 // nullptr = fixed-capacity segments of cap2)
     uint64_t* spill;        // segmented batches: the skew list ({key words, count} records of keys past
     uint64_t spill_cap;     // a segment's end and of repeated windows; Bloom pass: keys), spill_cap entries
-    uint32_t* keep_fill;    // Bloom pass keeping its level 1 (level-1 reuse): a copy of its segment
-                            // fills ([F1][nblk1]; the skew-list pass reuses hist1)
+    uint32_t* keep_fill;    // Bloom pass keeping its partitions (partition reuse): copies of the
+    uint32_t* keep_fill2;   // segment fills of levels 1 and 2 (the skew-list pass reuses hist1/2)
 };
 
 struct BloomView {
@@ -150,6 +151,10 @@ constexpr int p1_tile(int W) { return scatter_threads_w(W) * run_width(W); }  //
 #define KC_P2F_NT 0  // 0: the default below
 #endif
 constexpr int p2f_threads_w(int W) { return KC_P2F_NT ? KC_P2F_NT : (W <= 2 ? 1024 : W <= 4 ? 512 : 256); }
+// segmented level 1 (k_p1, W-word output keys + the heavy table) for F1 coarse bins
+constexpr size_t p1_lds_bytes(int W, uint32_t F1) {
+    return (size_t)F1 * 32 + 16 + (size_t)scatter_threads_w(W) * run_width(W) * 8 * W + (size_t)64 * (W + 1) * 8;
+}
 constexpr size_t p2f_lds_bytes(int W, uint32_t F2, uint32_t nseg) {
     return (size_t)F2 * 32 + 16 + (size_t)p2f_threads_w(W) * run_width(W) * 8 * W + ((size_t)nseg + 1) * 4;
 }
@@ -170,12 +175,14 @@ hipError_t launch_count_partitioned(PackedView sv, uint64_t sym_bound, int k, in
 // Bloom pass 1 on the blocked layout, partitioned: ft = the filter's region geometry
 // (R = filter regions of nblocks / R <= 1024 blocks, F1 x F2 as for the table; no buckets);
 // fresh: the filter is all zero (level 3 does not read it)
-// keep: level 1 writes whole table keys (kept for the counting pass, count_reuse)
-hipError_t launch_bloom_partitioned(PackedView sv, int k, int W, BloomView bf, TableView ft, DevCounters* ctr,
-                                    PartBufs pb, int fresh, int keep, hipStream_t s);
-// the counting pass from the level-1 output kept by the Bloom pass (pb: that output's
-// buffers); windows: the batch's windows (counted by the Bloom pass)
-hipError_t launch_count_reuse(int W, TableView t, BloomView bf, DevCounters* ctr, PartBufs pb, int fresh,
+// keep: levels 1 and 2 move whole table keys in the fine geometry fg (kept for the counting
+// pass, count_reuse); otherwise fg is unused
+hipError_t launch_bloom_partitioned(PackedView sv, int k, int W, BloomView bf, TableView ft, TableView fg,
+                                    DevCounters* ctr, PartBufs pb, int fresh, int keep, hipStream_t s);
+// the counting pass from the partitions kept by the Bloom pass (pb: their buffers), from
+// level 2 (level 2) or level 1 (level 1); windows: the batch's windows (counted by the
+// Bloom pass)
+hipError_t launch_count_reuse(int W, TableView t, BloomView bf, DevCounters* ctr, PartBufs pb, int fresh, int level,
                               uint64_t windows, hipStream_t s);
 // 64-bit checksum of the chunks' bytes (a promise check between two passes over one image):
 // CHECKSUM_SLOTS partial sums in out (their sum is the checksum)
@@ -224,10 +231,10 @@ struct WOps {
                             DevCounters* ctr, hipStream_t s);
     static hipError_t count_partitioned(PackedView sym, int k, int mode, TableView t, BloomView bf, DevCounters* ctr,
                                         PartBufs pb, int fresh, hipStream_t s);
-    static hipError_t bloom_partitioned(PackedView sym, int k, BloomView bf, TableView ft, DevCounters* ctr, PartBufs pb,
-                                        int fresh, int keep, hipStream_t s);
-    static hipError_t count_reuse(TableView t, BloomView bf, DevCounters* ctr, PartBufs pb, int fresh, uint64_t windows,
-                                  hipStream_t s);
+    static hipError_t bloom_partitioned(PackedView sym, int k, BloomView bf, TableView ft, TableView fg,
+                                        DevCounters* ctr, PartBufs pb, int fresh, int keep, hipStream_t s);
+    static hipError_t count_reuse(TableView t, BloomView bf, DevCounters* ctr, PartBufs pb, int fresh, int level,
+                                  uint64_t windows, hipStream_t s);
     static hipError_t route(PackedView sym, int k, DevCounters* ctr, PartBufs pb, uint32_t parts, uint64_t* out,
                             hipStream_t s);
     static hipError_t insert_keys(const uint64_t* keys, uint64_t n, bool partitioned, TableView t, DevCounters* ctr,

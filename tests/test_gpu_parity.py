@@ -368,8 +368,8 @@ def test_bloom_at_scale_equals_exact_solid_kmers(k, fpr, insert_path):
     assert np.array_equal(a, b)
 
 
-def _bloom_job_device(torch, img, chunks, k, count_img=None, count_chunks=None, batch_bytes=0):
-    cfg = ka.Config(k=k, min_abundance=2, bf_enable=True, est_unique=4_000_000, fpr=0.01, batch_bytes=batch_bytes)
+def _bloom_job_device(torch, img, chunks, k, count_img=None, count_chunks=None, batch_bytes=0, est_unique=4_000_000):
+    cfg = ka.Config(k=k, min_abundance=2, bf_enable=True, est_unique=est_unique, fpr=0.01, batch_bytes=batch_bytes)
     with ka.KmerCounter(cfg) as kc:
         kc.bloom_device(img.data_ptr(), chunks, ka.FMT_FASTA)
         kc.bloom_finalize()
@@ -380,12 +380,14 @@ def _bloom_job_device(torch, img, chunks, k, count_img=None, count_chunks=None, 
     return st, got[np.lexsort(got[:, :-1].T[::-1])]
 
 
-@pytest.mark.parametrize("change", ["none", "bytes", "chunks", "batches"])
+@pytest.mark.parametrize("change", ["none", "small_u", "bytes", "chunks", "batches"])
 def test_level1_reuse_only_on_the_same_input(change, monkeypatch):
-    """Level-1 reuse (kc_api.cpp): the counting pass starts from the Bloom pass's window
-    partition only for the same image, chunk table and bytes in one batch.  Bytes changed
-    after the Bloom pass (checksum), a different chunk table, or a Bloom pass of several
-    batches run the ordinary counting pass; every variant equals the run with reuse off."""
+    """Partition reuse (kc_api.cpp): the counting pass starts from the Bloom pass's window
+    partitions only for the same image, chunk table and bytes in one batch -- from level 2
+    when the table's regions are unions of the fine bins (none), from level 1 when the table
+    outgrew the bins sized from -u (small_u).  Bytes changed after the Bloom pass
+    (checksum), a different chunk table, or a Bloom pass of several batches run the ordinary
+    counting pass; every variant equals the run with reuse off."""
     torch = pytest.importorskip("torch")
     monkeypatch.setenv("KC_INSERT_PATH", "partitioned")
     lib = ka.load_library()
@@ -416,9 +418,10 @@ def test_level1_reuse_only_on_the_same_input(change, monkeypatch):
                 st = kc.finish()
                 got = kc.dump()
             return st, got[np.lexsort(got[:, :-1].T[::-1])]
-        return _bloom_job_device(torch, img, chunks, k, count_img, count_chunks, bb)
+        return _bloom_job_device(torch, img, chunks, k, count_img, count_chunks, bb,
+                                 est_unique=1_000_000 if change == "small_u" else 4_000_000)
     st, got = run()
-    assert st["reused_passes"] == (1 if change == "none" else 0)
+    assert st["reused_passes"] == (1 if change in ("none", "small_u") else 0)
     monkeypatch.setenv("KC_REUSE", "0")
     st0, want = run()
     assert st0["reused_passes"] == 0
