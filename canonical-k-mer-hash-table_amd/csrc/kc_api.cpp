@@ -624,8 +624,9 @@ static int count_reused(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, s
     }
     const BloomView bv{c->d_bloom, c->bf_bits ? c->bf_bits - 1 : 0, c->nh, c->nh_gate, c->bloom_blocked,
                        bloom_blocks(c->bf_bits)};
+    // -m 1 -b counts every window (the reference ignores its filter, main.cpp:482-489)
     HIPCHK(c, launch_count_reuse(c->W, table_view(c), bv, c->d_ctr, pr, c->table_fresh, c->reuse_level,
-                                 c->reuse_windows, s));
+                                 c->cfg.mode != 1, c->reuse_windows, s));
     if (ev[3]) HIPCHK(c, hipEventRecord(ev[3], s));
     unsigned long long ovf = 0;
     HIPCHK(c, hipMemcpyAsync(&ovf, &c->d_ctr->part_overflow, sizeof(ovf), hipMemcpyDeviceToHost, s));

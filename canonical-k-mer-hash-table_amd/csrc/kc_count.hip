@@ -39,9 +39,9 @@ hipError_t launch_bloom_partitioned(PackedView sym, int k, int W, BloomView bf, 
 }
 
 hipError_t launch_count_reuse(int W, TableView t, BloomView bf, DevCounters* ctr, PartBufs pb, int fresh, int level,
-                              uint64_t windows, hipStream_t s) {
+                              int gate, uint64_t windows, hipStream_t s) {
     if (!bf.blocked || pb.cap1 == 0 || t.F1 * pb.B2 == 0) return hipErrorInvalidValue;
-    KC_DISPATCH_W(W, count_reuse(t, bf, ctr, pb, fresh, level, windows, s));
+    KC_DISPATCH_W(W, count_reuse(t, bf, ctr, pb, fresh, level, gate, windows, s));
 }
 
 hipError_t launch_route(PackedView sym, int k, int W, DevCounters* ctr, PartBufs pb, uint32_t parts, uint64_t* out,

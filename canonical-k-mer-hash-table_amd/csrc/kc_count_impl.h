@@ -2340,7 +2340,10 @@ static hipError_t bloom_part_w(PackedView sym, int k, BloomView bf, TableView ft
 static __global__ void k_add_windows(DevCounters* ctr, unsigned long long n) {
     if (!ctr->part_overflow) ctr->windows += n;
 }
-template <int W>
+static __global__ void k_add_inserted(DevCounters* ctr, unsigned long long n) {
+    if (!ctr->part_overflow) ctr->inserted += n;
+}
+template <int W, bool GATE>
 static hipError_t count_reuse_w(TableView t, BloomView bf, DevCounters* ctr, PartBufs pb, int fresh, int level,
                                 uint64_t windows, hipStream_t s) {
     hipError_t e;
@@ -2351,9 +2354,11 @@ static hipError_t count_reuse_w(TableView t, BloomView bf, DevCounters* ctr, Par
         if ((e = set_smem(k_p2f<W, NT>, sm2)) != hipSuccess) return e;
         hipLaunchKernelGGL((k_p2f<W, NT>), dim3(t.F1 * pb.B2), dim3(NT), sm2, s, t, pb, ctr, 1);
     }
-    if ((e = launch_p3<W, true, false, true>(t, ctr, pb, nullptr, fresh, s, bf)) != hipSuccess) return e;
+    if ((e = launch_p3<W, true, false, GATE>(t, ctr, pb, nullptr, fresh, s, bf)) != hipSuccess) return e;
     // (from level 2 nothing can reach the skew list: no level of this pass scatters)
-    if (level < 2 && (e = insert_spill<W, true>(t, bf, ctr, pb, s)) != hipSuccess) return e;
+    if (level < 2 && (e = insert_spill<W, GATE>(t, bf, ctr, pb, s)) != hipSuccess) return e;
+    // ungated (-m 1 -b): every window is an insertion (level 1 counts them in an ordinary pass)
+    if (!GATE) hipLaunchKernelGGL(k_add_inserted, dim3(1), dim3(1), 0, s, ctr, (unsigned long long)windows);
     hipLaunchKernelGGL(k_batch_end, dim3(1), dim3(1), 0, s, ctr);
     hipLaunchKernelGGL(k_add_windows, dim3(1), dim3(1), 0, s, ctr, (unsigned long long)windows);
     return hipGetLastError();
@@ -2444,8 +2449,9 @@ hipError_t WOps<W>::bloom_partitioned(PackedView sym, int k, BloomView bf, Table
 }
 template <int W>
 hipError_t WOps<W>::count_reuse(TableView t, BloomView bf, DevCounters* ctr, PartBufs pb, int fresh, int level,
-                                uint64_t windows, hipStream_t s) {
-    return count_reuse_w<W>(t, bf, ctr, pb, fresh, level, windows, s);
+                                int gate, uint64_t windows, hipStream_t s) {
+    if (gate) return count_reuse_w<W, true>(t, bf, ctr, pb, fresh, level, windows, s);
+    return count_reuse_w<W, false>(t, bf, ctr, pb, fresh, level, windows, s);
 }
 
 template <int W>

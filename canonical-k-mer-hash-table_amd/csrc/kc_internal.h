@@ -180,10 +180,10 @@ hipError_t launch_count_partitioned(PackedView sv, uint64_t sym_bound, int k, in
 hipError_t launch_bloom_partitioned(PackedView sv, int k, int W, BloomView bf, TableView ft, TableView fg,
                                     DevCounters* ctr, PartBufs pb, int fresh, int keep, hipStream_t s);
 // the counting pass from the partitions kept by the Bloom pass (pb: their buffers), from
-// level 2 (level 2) or level 1 (level 1); windows: the batch's windows (counted by the
-// Bloom pass)
+// level 2 (level 2) or level 1 (level 1); gate: behind the Bloom gate (0: -m 1 -b, whose
+// filter is ignored); windows: the batch's windows (counted by the Bloom pass)
 hipError_t launch_count_reuse(int W, TableView t, BloomView bf, DevCounters* ctr, PartBufs pb, int fresh, int level,
-                              uint64_t windows, hipStream_t s);
+                              int gate, uint64_t windows, hipStream_t s);
 // 64-bit checksum of the chunks' bytes (a promise check between two passes over one image):
 // CHECKSUM_SLOTS partial sums in out (their sum is the checksum)
 constexpr int CHECKSUM_SLOTS = 64;
@@ -234,7 +234,7 @@ struct WOps {
     static hipError_t bloom_partitioned(PackedView sym, int k, BloomView bf, TableView ft, TableView fg,
                                         DevCounters* ctr, PartBufs pb, int fresh, int keep, hipStream_t s);
     static hipError_t count_reuse(TableView t, BloomView bf, DevCounters* ctr, PartBufs pb, int fresh, int level,
-                                  uint64_t windows, hipStream_t s);
+                                  int gate, uint64_t windows, hipStream_t s);
     static hipError_t route(PackedView sym, int k, DevCounters* ctr, PartBufs pb, uint32_t parts, uint64_t* out,
                             hipStream_t s);
     static hipError_t insert_keys(const uint64_t* keys, uint64_t n, bool partitioned, TableView t, DevCounters* ctr,

@@ -157,14 +157,20 @@ def test_synth_device_matches_cpu_generator(tmp_path):
                                   and not ("-b" in c["args"] and "1" == c["args"][c["args"].index("-a") + 1]
                                            and parse_ref_args(c["args"])["mode"] != 1)],
                          ids=_case_id)
-def test_cli_end_to_end(case, golden_input, tmp_path):
+@pytest.mark.parametrize("cli_path", ["device", "host"])
+def test_cli_end_to_end(case, cli_path, golden_input, tmp_path):
+    """The drop-in CLI: the input read into HBM by parallel pinned slices and counted from
+    there (device; Bloom jobs count from the Bloom pass's partitions), or staged as host
+    chunks (KC_CLI_HOST=1)."""
     path = golden_input(case["input"])
     out = tmp_path / "out.kaarme_counts"
+    env = dict(os.environ, KC_CLI_HOST="1" if cli_path == "host" else "0")
     r = subprocess.run([CLI, path, str(case["k"]), "-t", "3", "-o", str(out)] + case["args"],
-                       capture_output=True, text=True)
+                       capture_output=True, text=True, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert sorted_digest_file(out) == (case["sorted_sha256"], case["lines"])
     assert "Time used to build hash table" in r.stdout
+    assert ("Input path: device image" in r.stdout) == (cli_path == "device")
 
 
 @pytest.mark.parametrize("name,k,args", [("reads_w60.fasta", 31, ["-m", "2", "-a", "1", "-s", "1000000"]),
