@@ -129,7 +129,7 @@ struct kc_ctx {
     uint64_t reuse_used = 0;          // stage bytes of the batch
     unsigned long long reuse_sum = 0; // checksum of the Bloom pass's chunk bytes
     uint64_t reuse_windows = 0;       // windows of that batch
-    unsigned long long* d_sum = nullptr;  // CHECKSUM_SLOTS partial sums
+    unsigned long long* d_sum = nullptr;  // CHECKSUM_SLOTS partial sums (+ CHECKSUM_SLOTS for kc_bloom_estimate)
     uint32_t* d_keep_fill = nullptr;      // the kept partitions' segment fills: level 1 [F1][nblk1]
     uint32_t* d_keep_fill2 = nullptr;     // and level 2 [R_fine][B2]
     uint64_t keep_fill_cap = 0, keep_fill2_cap = 0;
@@ -797,7 +797,7 @@ int kc_create(const kc_config* cfg, kc_ctx** out) {
         hipMalloc(&c->d_tblk, (ntiles / 1024 + 2) * sizeof(TileOut)) != hipSuccess ||
         hipMalloc(&c->d_chunks, c->max_chunks * sizeof(ChunkDesc)) != hipSuccess ||
         hipMalloc(&c->d_ctr, sizeof(DevCounters)) != hipSuccess ||
-        hipMalloc(&c->d_sum, CHECKSUM_SLOTS * sizeof(unsigned long long)) != hipSuccess)
+        hipMalloc(&c->d_sum, 2 * CHECKSUM_SLOTS * sizeof(unsigned long long)) != hipSuccess)
         return bail(KC_ERR_NOMEM, "device staging allocation failed");
     if (hipMemsetAsync(c->d_ctr, 0, sizeof(DevCounters), c->stream) != hipSuccess)
         return bail(KC_ERR_HIP, "memset failed");
@@ -1650,6 +1650,81 @@ int kc_bloom_write(kc_ctx* c, const uint32_t* words, uint64_t n) {
     HIPCHK(c, hipMemcpy(c->d_bloom, words, n * 4, hipMemcpyHostToDevice));
     c->bloom_fresh = false;
     return KC_OK;
+}
+
+// Work on stream s after everything the context staged from the host (its own stream).
+static int after_host_work(kc_ctx* c, hipStream_t s) {
+    int rc = flush_host(c);
+    if (rc) return rc;
+    if (s != c->stream) {
+        HIPCHK(c, hipEventRecord(c->xev, c->stream));
+        HIPCHK(c, hipStreamWaitEvent(s, c->xev, 0));
+    }
+    return KC_OK;
+}
+
+int kc_bloom_get_device(kc_ctx* c, uint32_t* dev_dst, uint64_t first_word, uint64_t n_words, void* sp) {
+    if (!c || (!dev_dst && n_words)) return KC_ERR_ARG;
+    if (!c->d_bloom) return c->fail(KC_ERR_STATE, "no Bloom filter");
+    if (first_word > bloom_words(c) || n_words > bloom_words(c) - first_word)
+        return c->fail(KC_ERR_ARG, "word range outside the filter");
+    hipStream_t s = pick_stream(c, sp);
+    int rc = after_host_work(c, s);
+    if (rc) return rc;
+    if (n_words) HIPCHK(c, hipMemcpyAsync(dev_dst, c->d_bloom + first_word, n_words * 4, hipMemcpyDeviceToDevice, s));
+    return KC_OK;
+}
+
+int kc_bloom_merge_device(kc_ctx* c, const uint32_t* dev_parts, uint32_t nparts, uint64_t n_words, uint32_t* dev_out,
+                          void* sp) {
+    if (!c || nparts == 0 || (n_words && (!dev_parts || !dev_out))) return KC_ERR_ARG;
+    if (!c->d_bloom) return c->fail(KC_ERR_STATE, "no Bloom filter");
+    if (c->bloom_blocked && n_words % 16) return c->fail(KC_ERR_ARG, "the blocked filter merges whole 16-word blocks");
+    HIPCHK(c, launch_bloom_merge(dev_parts, nparts, n_words, c->bloom_blocked, dev_out, pick_stream(c, sp)));
+    return KC_OK;
+}
+
+// Distinct k-mers in filter 2 from its set bits (after the work queued on s): X of m bits set
+// after n insertions of h positions each, X = m (1 - e^{-hn/m}).
+static int estimate_filter2(kc_ctx* c, hipStream_t s, uint64_t* est) {
+    unsigned long long* part_d = c->d_sum + CHECKSUM_SLOTS;  // the first CHECKSUM_SLOTS hold the reuse checksum
+    HIPCHK(c, launch_bloom_popcount2(c->d_bloom, bloom_words(c), c->bloom_blocked, part_d, s));
+    unsigned long long part[CHECKSUM_SLOTS];
+    HIPCHK(c, hipMemcpyAsync(part, part_d, sizeof(part), hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    double x = 0;
+    for (auto v : part) x += (double)v;
+    const double m = c->bloom_blocked ? 256.0 * (double)bloom_blocks(c->bf_bits) : (double)c->bf_bits;
+    x = std::min(x, m - 1);
+    *est = (uint64_t)std::llround(-(m / std::max(1, c->nh)) * std::log1p(-x / m));
+    return KC_OK;
+}
+
+int kc_bloom_set_device(kc_ctx* c, const uint32_t* dev_src, uint64_t n_words, uint64_t* new_in_second, void* sp) {
+    if (!c || !dev_src) return KC_ERR_ARG;
+    if (!c->cfg.bf_enable || c->bloom_final) return c->fail(KC_ERR_STATE, "bloom pass not active");
+    if (n_words != bloom_words(c)) return c->fail(KC_ERR_ARG, "n_words must be the filter's word count");
+    hipStream_t s = pick_stream(c, sp);
+    int rc = after_host_work(c, s);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(c->d_bloom, dev_src, n_words * 4, hipMemcpyDeviceToDevice, s));
+    c->bloom_fresh = false;
+    uint64_t est = 0;
+    rc = estimate_filter2(c, s, &est);  // waits for the copy
+    if (rc) return rc;
+    // the pass-1 counter kc_bloom_finalize sizes the table from (main.cpp:454)
+    HIPCHK(c, hipMemcpy(&c->d_ctr->new_in_second, &est, 8, hipMemcpyHostToDevice));
+    if (new_in_second) *new_in_second = est;
+    return KC_OK;
+}
+
+int kc_bloom_estimate(kc_ctx* c, uint64_t* distinct_in_second, void* sp) {
+    if (!c || !distinct_in_second) return KC_ERR_ARG;
+    if (!c->d_bloom) return c->fail(KC_ERR_STATE, "no Bloom filter");
+    hipStream_t s = pick_stream(c, sp);
+    int rc = after_host_work(c, s);
+    if (rc) return rc;
+    return estimate_filter2(c, s, distinct_in_second);
 }
 
 uint64_t kc_synth_bytes(uint64_t first_read, uint64_t n_reads, uint32_t read_len, uint32_t wrap) {

@@ -189,6 +189,14 @@ hipError_t launch_count_reuse(int W, TableView t, BloomView bf, DevCounters* ctr
 constexpr int CHECKSUM_SLOTS = 64;
 hipError_t launch_checksum(const uint8_t* src, const ChunkDesc* d_chunks, int n_chunks, uint64_t max_len,
                            unsigned long long* out, hipStream_t s);
+// sharded Bloom filter: combine nparts copies (consecutive, n words each) of one word range of
+// the filter into out -- filter 1 = OR, filter 2 = OR | (filter-1 bits set in >= 2 copies);
+// blocked: the range starts at a block (16 words); else the reference's 2h / 2h+1 bit pairs
+hipError_t launch_bloom_merge(const uint32_t* parts, uint32_t nparts, uint64_t n, int blocked, uint32_t* out,
+                              hipStream_t s);
+// set filter-2 bits of the whole filter: CHECKSUM_SLOTS partial sums in out
+hipError_t launch_bloom_popcount2(const uint32_t* words, uint64_t n, int blocked, unsigned long long* out,
+                                  hipStream_t s);
 // hash-prefix sharding: windows -> table keys grouped by owner (offsets in pb.off1)
 hipError_t launch_route(PackedView sym, int k, int W, DevCounters* ctr, PartBufs pb, uint32_t parts, uint64_t* out,
                         hipStream_t s);

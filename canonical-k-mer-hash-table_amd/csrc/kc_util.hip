@@ -1,5 +1,6 @@
-// kc_util.hip -- small device helpers behind the C ABI's test hooks: the device XXH64
-// of the reference-layout Bloom passes (kc_common.h xxh64_u64) over host-given inputs.
+// kc_util.hip -- small device helpers: the device XXH64 of the reference-layout Bloom
+// passes (kc_common.h xxh64_u64) over host-given inputs (test hook), the chunk checksum of
+// the partition reuse, and the sharded Bloom filter's merge and filter-2 bit count.
 #include "kc_common.h"
 
 namespace kc {
@@ -56,6 +57,80 @@ hipError_t launch_checksum(const uint8_t* src, const ChunkDesc* d_chunks, int n_
     const uint64_t words = max_len / 8 + 2, per = (uint64_t)CK_T * CK_PER;
     hipLaunchKernelGGL(k_checksum, dim3((unsigned)((words + per - 1) / per), (unsigned)n_chunks), dim3(CK_T), 0, s, src,
                        d_chunks, out);
+    return hipGetLastError();
+}
+
+// Sharded Bloom filter (kc_bloom_merge_device).  The ranks' filters after their own Bloom
+// passes are combined so that the gate passes every k-mer the reference's one filter would
+// pass for count >= 2 (double_bloomfilter.hpp:233-246 insertion_process): a k-mer seen twice
+// on one rank has its filter-2 bits set there (OR), one seen on two ranks has its filter-1
+// bits set in two copies.  Blocked layout: thread = word w < 8 of a block, filter 1 at w,
+// filter 2 at w + 8.  Reference layout: thread = word, filter 1 = even bits, filter 2 = odd.
+__global__ __launch_bounds__(256) void k_bloom_merge(const uint32_t* __restrict__ parts, uint32_t nparts, uint64_t n,
+                                                     int blocked, uint32_t* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    uint32_t once = 0, twice = 0, f2 = 0;
+    if (blocked) {
+        if (i >= n / 2) return;
+        const uint64_t a = (i >> 3) * 16 + (i & 7);
+        for (uint32_t p = 0; p < nparts; p++) {
+            const uint32_t x = parts[p * n + a];
+            twice |= once & x;
+            once |= x;
+            f2 |= parts[p * n + a + 8];
+        }
+        out[a] = once;
+        out[a + 8] = f2 | twice;
+    } else {
+        if (i >= n) return;
+        for (uint32_t p = 0; p < nparts; p++) {
+            const uint32_t x = parts[p * n + i];
+            const uint32_t x1 = x & 0x55555555u;
+            twice |= once & x1;
+            once |= x1;
+            f2 |= x & 0xAAAAAAAAu;
+        }
+        out[i] = once | f2 | (twice << 1);
+    }
+}
+
+hipError_t launch_bloom_merge(const uint32_t* parts, uint32_t nparts, uint64_t n, int blocked, uint32_t* out,
+                              hipStream_t s) {
+    const uint64_t threads = blocked ? n / 2 : n;
+    if (threads == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_bloom_merge, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, parts, nparts, n,
+                       blocked, out);
+    return hipGetLastError();
+}
+
+constexpr int PC_PER = 16;  // words per thread
+__global__ __launch_bounds__(256) void k_bloom_popcount2(const uint32_t* __restrict__ w, uint64_t n, int blocked,
+                                                         unsigned long long* __restrict__ out) {
+    unsigned long long c = 0;
+#pragma unroll
+    for (int q = 0; q < PC_PER; q++) {
+        const uint64_t i = ((uint64_t)blockIdx.x * PC_PER + q) * 256 + threadIdx.x;
+        if (i >= n) break;
+        const uint32_t x = w[i];
+        c += blocked ? ((i & 15) >= 8 ? __popc(x) : 0) : __popc(x & 0xAAAAAAAAu);
+    }
+    for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
+    __shared__ unsigned long long s_c[4];
+    if ((threadIdx.x & 63) == 0) s_c[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long t = s_c[0] + s_c[1] + s_c[2] + s_c[3];
+        if (t) atomicAdd(out + blockIdx.x % CK_SLOTS, t);
+    }
+}
+
+hipError_t launch_bloom_popcount2(const uint32_t* words, uint64_t n, int blocked, unsigned long long* out,
+                                  hipStream_t s) {
+    hipError_t e = hipMemsetAsync(out, 0, CK_SLOTS * sizeof(unsigned long long), s);
+    if (e != hipSuccess || n == 0) return e;
+    const uint64_t per = 256ull * PC_PER;
+    hipLaunchKernelGGL(k_bloom_popcount2, dim3((unsigned)((n + per - 1) / per)), dim3(256), 0, s, words, n, blocked,
+                       out);
     return hipGetLastError();
 }
 

@@ -47,7 +47,8 @@ EXPORTS = (
     "kc_reset", "kc_profile", "kc_get_timing", "kc_route_device", "kc_insert_keys_device",
     "kc_route_table_device", "kc_insert_counts_device", "kc_clear_table", "kc_insert_counts_runs_device",
     "kc_xxh64", "kc_bloom_info", "kc_bloom_read", "kc_bloom_write", "kc_synth_skew_device",
-    "kc_table_size_reference",
+    "kc_table_size_reference", "kc_bloom_get_device", "kc_bloom_merge_device", "kc_bloom_set_device",
+    "kc_bloom_estimate",
 )
 
 
@@ -151,6 +152,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                                 ctypes.POINTER(I32), ctypes.POINTER(I32)]),
         "kc_bloom_read": (I32, [P, P, U64]),
         "kc_bloom_write": (I32, [P, P, U64]),
+        "kc_bloom_get_device": (I32, [P, P, U64, U64, P]),
+        "kc_bloom_merge_device": (I32, [P, P, ctypes.c_uint32, U64, P, P]),
+        "kc_bloom_set_device": (I32, [P, P, U64, ctypes.POINTER(U64), P]),
+        "kc_bloom_estimate": (I32, [P, ctypes.POINTER(U64), P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -358,6 +363,29 @@ class KmerCounter:
     def bloom_write(self, words: np.ndarray):
         a = np.ascontiguousarray(words, dtype=np.uint32)
         self._chk(self.lib.kc_bloom_write(self._ctx, a.ctypes.data, a.size), "kc_bloom_write")
+
+    # -- sharded Bloom filter (kc_bloom_get/merge/set_device, kc_bloom_estimate)
+    def bloom_get_device(self, dst_ptr: int, first_word: int, n_words: int, stream: int = 0):
+        self._chk(self.lib.kc_bloom_get_device(self._ctx, ctypes.c_void_p(dst_ptr), first_word, n_words,
+                                               ctypes.c_void_p(stream or None)), "kc_bloom_get_device")
+
+    def bloom_merge_device(self, parts_ptr: int, nparts: int, n_words: int, out_ptr: int, stream: int = 0):
+        self._chk(self.lib.kc_bloom_merge_device(self._ctx, ctypes.c_void_p(parts_ptr), nparts, n_words,
+                                                 ctypes.c_void_p(out_ptr), ctypes.c_void_p(stream or None)),
+                  "kc_bloom_merge_device")
+
+    def bloom_set_device(self, src_ptr: int, n_words: int, stream: int = 0) -> int:
+        """Install a whole filter; returns the new_in_second estimate the table is sized from."""
+        n = ctypes.c_uint64()
+        self._chk(self.lib.kc_bloom_set_device(self._ctx, ctypes.c_void_p(src_ptr), n_words, ctypes.byref(n),
+                                               ctypes.c_void_p(stream or None)), "kc_bloom_set_device")
+        return n.value
+
+    def bloom_estimate(self, stream: int = 0) -> int:
+        n = ctypes.c_uint64()
+        self._chk(self.lib.kc_bloom_estimate(self._ctx, ctypes.byref(n), ctypes.c_void_p(stream or None)),
+                  "kc_bloom_estimate")
+        return n.value
 
     def sync(self):
         self._chk(self.lib.kc_sync(self._ctx), "kc_sync")

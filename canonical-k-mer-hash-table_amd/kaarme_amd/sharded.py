@@ -20,6 +20,18 @@ The per-window alternative (kc_route_device + kc_insert_keys_device: route every
 window's key to its owner, no local table) stays in the C ABI and is exercised by
 tests/test_gpu_sharded.py.
 
+Bloom prefilter (-b, main.cpp:395-461 / parallel_parser.hpp:2680-2974), sharded:
+  1. every rank runs the Bloom pass over its own input into its own filter;
+  2. `bloom_finalize` combines the filters: the filter's words are cut into one slice per
+     rank, an all-to-all hands every rank the ranks' copies of its slice, the rank merges
+     them (kc_bloom_merge_device: filter 1 = OR, filter 2 = OR | filter-1 bits set in two
+     copies, so a k-mer seen twice anywhere passes the gate) and an all-gather gives every
+     rank the combined filter; kc_bloom_set_device installs it and sets new_in_second to
+     its filter-2 estimate, the same on every rank, which sizes the tables (2 x, main.cpp:454:
+     the local table whole, the owner table its 1/world share);
+  3. the counting pass is gated by the combined filter on every rank, then merged as above.
+For every k-mer with count >= 2 the owners hold the single-GPU (and reference) count.
+
 The exchange logic (:func:`exchange`) is backend-agnostic torch code: the CPU tests run
 it over ``gloo`` with a NumPy engine, the GPU path over RCCL with the HIP engine.
 """
@@ -78,6 +90,40 @@ def exchange(dist, keys, counts: Sequence[int], W: int, group=None, chunk_words:
                 out[ro[d] + lo: ro[d] + lo + rin[d]].copy_(got[pos: pos + rin[d]])
             pos += rin[d]
     return (out, total, recv) if with_counts else (out, total)
+
+
+def all_gather_words(dist, mine, world: int, group=None, chunk_words: int = 2 * EXCHANGE_CHUNK_WORDS):
+    """[world x len(mine)] = every rank's `mine` (int32 words), in pieces of at most
+    chunk_words per rank (EXCHANGE_CHUNK_WORDS bytes, as the all-to-all's rounds)."""
+    import torch
+
+    per = mine.numel()
+    full = torch.empty(world * per, dtype=mine.dtype, device=mine.device)
+    if world == 1:
+        full.copy_(mine)
+        return full
+    grid = full.view(world, per)
+    for lo in range(0, per, chunk_words):
+        hi = min(per, lo + chunk_words)
+        piece = mine[lo:hi].contiguous()
+        if hi - lo == per:
+            tmp = full
+        else:
+            tmp = torch.empty(world * (hi - lo), dtype=mine.dtype, device=mine.device)
+        try:
+            dist.all_gather_into_tensor(tmp, piece, group=group)
+        except (RuntimeError, AttributeError, NotImplementedError):  # backends without it
+            dist.all_gather(list(tmp.view(world, hi - lo).unbind(0)), piece, group=group)
+        if tmp is not full:
+            grid[:, lo:hi].copy_(tmp.view(world, hi - lo))
+    return full
+
+
+def owner_share(slots: int, world: int) -> int:
+    """Slots of one owner's table for a job whose whole table is `slots`: the 1/world share
+    plus 8 sigma of the binomial spread of hash-split keys."""
+    share = -(-slots // world)
+    return share if world == 1 else share + 8 * int(share ** 0.5) + 64
 
 
 TILE = 4096
@@ -176,9 +222,57 @@ class DeviceEngine:
         else:
             self.owner_table().insert_counts_device(recs.data_ptr(), n, stream)
 
+    # -- sharded Bloom filter
+    def bloom(self, dev_ptr: int, chunks, fmt: int, stream: int = 0):
+        self.kc.bloom_device(dev_ptr, chunks, fmt, stream)
+
+    def bloom_words(self):
+        """(filter words, merge unit in words): whole 16-word blocks, or int64 pairs."""
+        info = self.kc.bloom_info()
+        return info["words"], 16 if info["layout"] == "blocked" else 2
+
+    def bloom_copy(self, n_pad: int, stream: int = 0):
+        import torch
+
+        n = self.kc.bloom_info()["words"]
+        out = torch.zeros(n_pad, dtype=torch.int32, device="cuda")
+        self.kc.bloom_get_device(out.data_ptr(), 0, n, stream)
+        return out
+
+    def bloom_merge(self, parts, nparts: int, n: int, stream: int = 0):
+        import torch
+
+        out = torch.empty(n, dtype=torch.int32, device="cuda")
+        self.kc.bloom_merge_device(parts.data_ptr(), nparts, n, out.data_ptr(), stream)
+        return out
+
+    def bloom_install(self, full, n: int, stream: int = 0) -> int:
+        return self.kc.bloom_set_device(full.data_ptr(), n, stream)
+
+    def bloom_finalize(self, owner_slots: int) -> int:
+        """Size the local table (2 x new_in_second) and the owner table (owner_slots)."""
+        import dataclasses
+
+        nis = self.kc.bloom_finalize()
+        ocfg = dataclasses.replace(self.cfg, bf_enable=False, table_slots=owner_slots)
+        if self.owner is not None and self.owner.cfg == ocfg:
+            self.owner.reset()
+        else:
+            if self.owner is not None:
+                self.owner.close()
+            self.owner = KmerCounter(ocfg)
+        self.same_geometry = False
+        return nis
+
     def reset(self):
         self.kc.reset()
-        self.owner_table().reset()
+        if self.owner is not None:
+            self.owner.reset()
+
+    def close(self):
+        self.kc.close()
+        if self.owner is not None:
+            self.owner.close()
 
 
 class ShardedCounter:
@@ -221,10 +315,35 @@ class ShardedCounter:
         self._inflight = [recv]  # the receive buffer must outlive the insert
         self._pending = False
 
-    def bloom_device(self, *a, **kw):
-        raise NotImplementedError("the Bloom-filter prefilter is not sharded (run it on one GPU)")
+    # the Bloom pass over a device image: into this rank's own filter
+    def bloom_device(self, dev_ptr: int, chunks: List[Tuple[int, int, int]], fmt: int, stream: int = 0):
+        if not self.cfg.bf_enable:
+            raise ValueError("bloom_device needs Config(bf_enable=True)")
+        self.engine.bloom(dev_ptr, chunks, fmt, stream)
+        self._stream = stream
 
-    bloom_finalize = bloom_device
+    def bloom_finalize(self, stream: int = None) -> int:
+        """End of the Bloom pass (collective): combine the ranks' filters, install the
+        combined filter on every rank and size the tables.  Returns new_in_second (the
+        combined filter's estimate, the same on every rank)."""
+        import torch
+
+        stream = self._stream if stream is None else stream
+        n, unit = self.engine.bloom_words()
+        world = self.world
+        per = -(-max(n, 1) // (unit * world)) * unit  # words of one rank's slice
+        send = self.engine.bloom_copy(per * world, stream)
+        if world > 1:  # rank d receives every rank's copy of slice d, in rank order
+            recv, got = exchange(self.dist, send.view(torch.int64), [per // 2] * world, 1, self.group)
+            parts = recv[:got].view(torch.int32)
+        else:
+            parts = send
+        mine = self.engine.bloom_merge(parts, world, per, stream)
+        full = all_gather_words(self.dist, mine, world, self.group)
+        nis = self.engine.bloom_install(full, n, stream)
+        self.engine.bloom_finalize(owner_share(2 * nis, world))
+        self._inflight = [send, parts, mine, full]
+        return nis
 
     @property
     def kc(self) -> KmerCounter:
@@ -234,6 +353,7 @@ class ShardedCounter:
     def reset(self):
         self.engine.reset()
         self._pending = False
+        self._inflight = []
 
     def sync(self):
         """Completes the job: the (collective) merge if counts are pending, then waits."""
@@ -259,10 +379,18 @@ class ShardedCounter:
         self.sync()
         local, own = self.engine.kc.finish(), self.kc.finish()
         st = dict(own)
-        for key in ("windows", "chunks", "bytes", "bf_windows"):
+        for key in ("windows", "chunks", "bytes", "bf_windows", "bf_bits", "new_in_first", "new_in_second",
+                    "failed_in_first", "reused_passes"):
             st[key] = local[key]
         st["local_distinct"] = local["distinct"]
         return st
+
+    def close(self):
+        """Free the rank's device tables (the counter is unusable afterwards)."""
+        self._inflight = []
+        close = getattr(self.engine, "close", None)
+        if close:
+            close()
 
     def dump(self):
         return self.kc.dump()

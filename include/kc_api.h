@@ -39,7 +39,7 @@ extern "C" {
 #define KC_ERR_STATE (-4)       /* call out of order (e.g. count before bloom finalize) */
 #define KC_ERR_IO (-5)          /* file error */
 #define KC_ERR_NOMEM (-6)       /* host or device allocation failed */
-#define KC_ERR_UNSUPPORTED (-7) /* e.g. the Bloom filter on the sharded entry points (the reference rejects FASTQ, parallel_parser.hpp:1216-1225; here it is an extension) */
+#define KC_ERR_UNSUPPORTED (-7) /* the Bloom filter on the per-window routing entry point kc_route_device (the sharded Bloom pass is pre-aggregated: kc_bloom_merge_device) */
 
 /* input_mode of main.cpp:178-189 */
 #define KC_FMT_FASTA 0
@@ -157,6 +157,33 @@ int kc_insert_counts_device(kc_ctx* ctx, const uint64_t* dev_records, uint64_t n
  * kc_insert_counts_device. */
 int kc_insert_counts_runs_device(kc_ctx* ctx, const uint64_t* dev_records, const uint64_t* group_counts,
                                  uint32_t ngroups, void* hip_stream);
+
+/* Sharded Bloom filter (the reference has one filter,
+ * DoubleAtomicDoubleBloomFilter, double_bloomfilter.hpp:233-260, filled by every worker of
+ * the Bloom pass, parallel_parser.hpp:2788-2940).  Every rank runs kc_bloom_device over its
+ * own input; the ranks' filters are then combined and every rank gates its counting pass
+ * with the combined filter before the pre-aggregated merge:
+ *   kc_bloom_get_device   copies words [first_word, first_word + n_words) of the filter to
+ *                         dev_dst (after the work queued on hip_stream and the context);
+ *   kc_bloom_merge_device combines nparts copies of one word range (consecutive in
+ *                         dev_parts, n_words each; whole 16-word blocks in the blocked
+ *                         layout) into dev_out: filter 1 = OR, filter 2 = OR | (filter-1
+ *                         bits set in >= 2 copies), so every k-mer seen twice in the whole
+ *                         input passes the gate (seen twice on one rank, or on two ranks);
+ *   kc_bloom_set_device   replaces the whole filter (n_words = kc_bloom_info's count) and
+ *                         sets the pass-1 counter new_in_second, which kc_bloom_finalize
+ *                         sizes the table from (main.cpp:454), to kc_bloom_estimate of the
+ *                         new filter (also returned in *new_in_second; the same on every rank
+ *                         for the combined filter); new_in_first / failed_in_first stay the
+ *                         rank's own;
+ *   kc_bloom_estimate     the number of distinct k-mers in filter 2 estimated from its set
+ *                         bits (X of m bits, h pass-1 positions: -(m/h) ln(1 - X/m)). */
+int kc_bloom_get_device(kc_ctx* ctx, uint32_t* dev_dst, uint64_t first_word, uint64_t n_words, void* hip_stream);
+int kc_bloom_merge_device(kc_ctx* ctx, const uint32_t* dev_parts, uint32_t nparts, uint64_t n_words,
+                          uint32_t* dev_out, void* hip_stream);
+int kc_bloom_set_device(kc_ctx* ctx, const uint32_t* dev_src, uint64_t n_words, uint64_t* new_in_second,
+                        void* hip_stream);
+int kc_bloom_estimate(kc_ctx* ctx, uint64_t* distinct_in_second, void* hip_stream);
 
 /* Re-initialise the table, the Bloom filter and all counters (the table/filter
  * constructors again, without reallocating). */

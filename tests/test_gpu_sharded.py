@@ -200,3 +200,155 @@ def test_two_merges_route_only_new_counts(tmp_path, k, mode, G):
     out = tmp_path / "oracle.txt"
     oracle_count(str(whole), k, ["-m", str(mode), "-a", "1"], out)
     assert sorted_digest_lines(union) == sorted_digest_file(out)
+
+
+def merge_rule(parts, nparts, n, layout):
+    """kc_bloom_merge_device's rule (checker restatement): filter 1 = OR, filter 2 = OR |
+    filter-1 bits set in >= 2 copies; blocked = words 0-7 / 8-15 of 16-word blocks,
+    reference = even / odd bits of every word."""
+    import numpy as np
+
+    p = parts[: nparts * n].reshape(nparts, n).astype(np.uint32)
+    if layout == "blocked":
+        p = p.reshape(nparts, n // 16, 2, 8)
+        f1, f2 = p[:, :, 0], p[:, :, 1]
+    else:
+        f1, f2 = p & np.uint32(0x55555555), p & np.uint32(0xAAAAAAAA)
+    once = np.zeros_like(f1[0])
+    twice = np.zeros_like(f1[0])
+    for i in range(nparts):
+        twice |= once & f1[i]
+        once |= f1[i]
+    orf2 = np.bitwise_or.reduce(f2, axis=0)
+    if layout == "blocked":
+        return np.stack([once, orf2 | twice], axis=1).reshape(-1)
+    return (once | orf2 | (twice << np.uint32(1))).reshape(-1)
+
+
+@pytest.mark.parametrize("layout", ["blocked", "reference"])
+def test_bloom_merge_kernel(monkeypatch, layout):
+    """kc_bloom_merge_device against its restatement on random filter copies."""
+    import numpy as np
+
+    if layout == "reference":
+        monkeypatch.setenv("KC_BLOOM_LAYOUT", "reference")
+    e = DeviceEngine(ka.Config(k=31, mode=2, bf_enable=True, est_unique=100000, fpr=0.01))
+    rng = np.random.default_rng(5)
+    for nparts in (1, 2, 3, 5):
+        n = 16 * 37
+        parts = rng.integers(0, 1 << 32, size=nparts * n, dtype=np.uint64).astype(np.uint32)
+        parts &= rng.integers(0, 1 << 32, size=parts.size, dtype=np.uint64).astype(np.uint32)  # sparser
+        got = e.bloom_merge(torch.from_numpy(parts.view(np.int32)).cuda(), nparts, n).cpu().numpy().view(np.uint32)
+        torch.cuda.synchronize()
+        assert (got == merge_rule(parts, nparts, n, layout)).all()
+
+
+def _emulated_bloom_job(tmp_path, k, mode, G, n_reads, genome, est_unique):
+    """G emulated ranks through the sharded Bloom flow of ShardedCounter.bloom_finalize
+    (slices of every rank's filter -> merge at the slice's rank -> combined filter installed
+    everywhere), then the gated counting pass and the pre-aggregated merge."""
+    from kaarme_amd.sharded import owner_share
+
+    per = n_reads // G
+    images = []
+    for r in range(G):
+        fa = tmp_path / f"r{r}.fasta"
+        cnt = per if r < G - 1 else n_reads - per * (G - 1)
+        subprocess.run([GEN, str(fa), str(n_reads), "150", str(genome), "--first", str(r * per), "--count", str(cnt)],
+                       check=True)
+        images.append(_image(str(fa)))
+    whole = tmp_path / "all.fasta"
+    with open(whole, "wb") as f:
+        for data, _ in images:
+            f.write(data)
+    cfg = ka.Config(k=k, mode=mode, bf_enable=True, est_unique=est_unique, fpr=0.01, min_abundance=2)
+    engines = [DeviceEngine(cfg) for _ in range(G)]
+    W = engines[0].W
+    stream = torch.cuda.current_stream().cuda_stream
+    plans = [ka.plan_chunks(data, k, ka.FMT_FASTA, chunk_size=128 * 1024) for data, _ in images]
+    for e, (data, img), ch in zip(engines, images, plans):
+        e.reset()
+        e.bloom(img.data_ptr(), ch, ka.FMT_FASTA, stream)
+    n, unit = engines[0].bloom_words()
+    sl = -(-n // (unit * G)) * unit
+    copies = [e.bloom_copy(sl * G, stream) for e in engines]
+    merged = [engines[d].bloom_merge(torch.cat([c[d * sl:(d + 1) * sl] for c in copies]), G, sl, stream)
+              for d in range(G)]
+    full = torch.cat(merged)
+    nis = [e.bloom_install(full, n, stream) for e in engines]
+    assert len(set(nis)) == 1 and nis[0] > 0
+    for e in engines:
+        e.bloom_finalize(owner_share(2 * nis[0], G))
+    routed = []
+    for e, (data, img), ch in zip(engines, images, plans):
+        e.count(img.data_ptr(), ch, ka.FMT_FASTA, stream)
+        recs, counts = e.route_table(G, stream)
+        torch.cuda.synchronize()
+        routed.append((recs[: sum(counts) * (W + 1)].clone(), counts))
+    for d in range(G):
+        recv = torch.cat([recs[sum(c[:d]) * (W + 1):(sum(c[:d]) + c[d]) * (W + 1)] for recs, c in routed])
+        engines[d].insert_counts(recv, recv.numel() // (W + 1), stream)
+        torch.cuda.synchronize()
+    return engines, whole, nis[0], full
+
+
+@pytest.mark.parametrize("layout", ["blocked", "reference"])
+@pytest.mark.parametrize("k,mode,G", [(31, 2, 2), (51, 0, 3), (95, 2, 4)])
+def test_sharded_bloom_emulated_ranks(tmp_path, monkeypatch, layout, k, mode, G):
+    """Sharded Bloom filter: the owners' union of T(c) >= 2 lines equals the
+    oracle's count of the whole input (the gate passes every k-mer seen twice, also when
+    its two sightings are on two ranks), and the combined filter's new_in_second estimate
+    is close to the number of distinct k-mers seen twice.  (The single-GPU direct pass's
+    own counter is below it at high coverage: concurrent insertions of one k-mer split its
+    filter-2 bits, so no thread counts it -- the reference's insertion_process has the same
+    race, double_bloomfilter.hpp:371-413.)"""
+    if layout == "reference":
+        monkeypatch.setenv("KC_BLOOM_LAYOUT", "reference")
+    engines, whole, nis, full = _emulated_bloom_job(tmp_path, k, mode, G, 12000, 20000, 400000)
+    lines = [set(e.owner_table().lines()) for e in engines]
+    for a in range(G):
+        for b in range(a + 1, G):
+            assert not ({l.rsplit(" ", 1)[0] for l in lines[a]} & {l.rsplit(" ", 1)[0] for l in lines[b]})
+    out = tmp_path / "oracle.txt"
+    oracle_count(str(whole), k, ["-m", str(mode), "-a", "2"], out)
+    assert sorted_digest_lines(set().union(*lines)) == sorted_digest_file(out)
+    # the combined filter's estimate against the true number of distinct k-mers seen twice
+    # (the oracle's T(c) >= 2 lines); above it by the false positives of the filter and the
+    # bit-level merge (filter-1 bits of different k-mers on two ranks)
+    n2 = sorted_digest_file(out)[1]
+    assert 0.9 * n2 <= nis <= 1.5 * n2, (nis, n2)
+
+
+class _OneRank:
+    """torch.distributed stand-in for a one-rank group (no collective is issued at world 1)."""
+
+    @staticmethod
+    def get_world_size(group=None):
+        return 1
+
+    @staticmethod
+    def get_rank(group=None):
+        return 0
+
+
+@pytest.mark.parametrize("k", [31, 63])
+def test_sharded_counter_bloom_one_rank(tmp_path, k):
+    """ShardedCounter's own Bloom path on the HIP engine (bloom_device -> bloom_finalize ->
+    count_device -> merge) at one rank: the oracle's T(c) >= 2 lines."""
+    from kaarme_amd.sharded import ShardedCounter
+
+    fa = tmp_path / "r.fasta"
+    subprocess.run([GEN, str(fa), "8000", "150", "20000"], check=True)
+    data, img = _image(str(fa))
+    cfg = ka.Config(k=k, mode=2, bf_enable=True, est_unique=300000, fpr=0.01, min_abundance=2)
+    sc = ShardedCounter(cfg, _OneRank())
+    stream = torch.cuda.current_stream().cuda_stream
+    ch = ka.plan_chunks(data, k, ka.FMT_FASTA)
+    sc.bloom_device(img.data_ptr(), ch, ka.FMT_FASTA, stream)
+    nis = sc.bloom_finalize()
+    sc.count_device(img.data_ptr(), ch, ka.FMT_FASTA, stream)
+    st = sc.finish()
+    assert st["new_in_second"] == nis > 0 and st["bf_windows"] == st["windows"]
+    out = tmp_path / "oracle.txt"
+    oracle_count(str(fa), k, ["-m", "2", "-a", "2"], out)
+    assert sorted_digest_lines(sc.lines()) == sorted_digest_file(out)

@@ -5,7 +5,10 @@ The pre-aggregated exchange of kaarme_amd.sharded (local counts -> owner-grouped
 owner) runs unchanged; the HIP engine is replaced by a NumPy engine that tokenizes
 PLAIN lines, canonicalises, splits keys into W words and owns keys by a hash of the key.
 The union of the owner tables must equal a single-process count and the owners must be
-disjoint.
+disjoint.  The sharded Bloom filter (ShardedCounter.bloom_finalize: all-to-all of filter
+slices, merge, all-gather) runs over gloo with a NumPy double Bloom filter of the blocked
+layout: every k-mer with count >= 2 must get its exact count, and a count-1 k-mer may pass
+the gate only as a true singleton.
 """
 import collections
 import json
@@ -74,21 +77,91 @@ class _Table:
         pass
 
 
+def bloom_positions(words, nblocks, nh):
+    """Blocked-layout model: one 16-word block per k-mer, position j = a 5-bit field of
+    its hash in word j mod 8 of each filter half (kc_common.h block_insert's shape)."""
+    h = 0
+    for w in words:
+        h = (h * 0xC2B2AE3D27D4EB4F + w + 7) & ((1 << 64) - 1)
+    h ^= h >> 29
+    h = (h * 0x9E3779B97F4A7C15) & ((1 << 64) - 1)
+    blk = (h >> 40) % nblocks
+    return [(blk * 16 + (j & 7), (h >> (5 * j)) & 31) for j in range(nh)]
+
+
+def merge_words(parts, nparts, n):
+    """kc_bloom_merge_device's rule on the blocked layout (the checker's restatement)."""
+    p = parts[: nparts * n].reshape(nparts, n // 16, 16)
+    once = np.zeros((n // 16, 8), dtype=np.uint32)
+    twice = np.zeros_like(once)
+    f2 = np.zeros_like(once)
+    for i in range(nparts):
+        x = p[i, :, :8]
+        twice |= once & x
+        once |= x
+        f2 |= p[i, :, 8:]
+    return np.concatenate([once, f2 | twice], axis=1).reshape(-1)
+
+
 class NumpyEngine:
     """Stand-in for sharded.DeviceEngine: same count / route_table / insert_counts contract
-    on CPU tensors (records: W key words + 1 count word)."""
+    on CPU tensors (records: W key words + 1 count word), and the Bloom pass contract
+    (bloom / bloom_words / bloom_copy / bloom_merge / bloom_install / bloom_finalize)."""
 
-    def __init__(self, k, lines):
+    NBLOCKS, NH, NH_GATE = 40, 7, 6
+
+    def __init__(self, k, lines, bf=False):
         self.k = k
         self.W = 2 * k // 64 + 1
         self.lines = lines
         self.kc = _Table()      # local
         self.owner = _Table()
+        self.bf = bf
+        self.filter = np.zeros(16 * self.NBLOCKS, dtype=np.uint32)
+        self.new_in_second = 0
+
+    def _has(self, pos, half):
+        return all((int(self.filter[w + half]) >> b) & 1 for w, b in pos)
+
+    def bloom(self, dev_ptr, chunks, fmt, stream=0):
+        for off, ln, _ in chunks:
+            for line in self.lines[off:off + ln]:
+                for km in canonical_windows(line, self.k):
+                    pos = bloom_positions(to_words(km, self.W), self.NBLOCKS, self.NH)
+                    half = 8 if self._has(pos, 0) else 0  # insertion_process: second sighting -> filter 2
+                    for w, b in pos:
+                        self.filter[w + half] |= np.uint32(1 << b)
+
+    def bloom_words(self):
+        return self.filter.size, 16
+
+    def bloom_copy(self, n_pad, stream=0):
+        out = np.zeros(n_pad, dtype=np.uint32)
+        out[: self.filter.size] = self.filter
+        return torch.from_numpy(out.view(np.int32))
+
+    def bloom_merge(self, parts, nparts, n, stream=0):
+        return torch.from_numpy(merge_words(parts.numpy().view(np.uint32), nparts, n).view(np.int32))
+
+    def bloom_install(self, full, n, stream=0):
+        self.filter = full[:n].numpy().view(np.uint32).copy()
+        x = sum(bin(int(v)).count("1") for i, v in enumerate(self.filter) if i % 16 >= 8)
+        m = 256 * self.NBLOCKS
+        self.new_in_second = round(-(m / self.NH) * np.log1p(-min(x, m - 1) / m))
+        return self.new_in_second
+
+    def bloom_finalize(self, owner_slots):
+        self.owner_slots = owner_slots
+        return self.new_in_second
 
     def count(self, dev_ptr, chunks, fmt, stream=0):
         for off, ln, _ in chunks:
             for line in self.lines[off:off + ln]:
-                self.kc.table.update(canonical_windows(line, self.k))
+                kms = canonical_windows(line, self.k)
+                if self.bf:  # the pass-2 gate: trunc(hf) filter-2 positions
+                    kms = [km for km in kms if self._has(bloom_positions(to_words(km, self.W), self.NBLOCKS,
+                                                                         self.NH)[: self.NH_GATE], 8)]
+                self.kc.table.update(kms)
 
     def route_table(self, parts, stream=0):
         groups = [[] for _ in range(parts)]
@@ -180,6 +253,51 @@ def test_sharded_union_equals_single(tmp_path, k):
     truth = collections.Counter(km for r in reads for km in canonical_windows(r, k))
     assert union == truth
     assert all(len(s) > 0 for s in shards)
+
+
+def _bloom_worker(rank, world, port, k, reads, outdir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        eng = NumpyEngine(k, reads, bf=True)
+        sc = ShardedCounter(Config(k=k, mode=2, bf_enable=True, est_unique=1000), dist, engine=eng)
+        per = (len(reads) + world - 1) // world
+        lo, hi = rank * per, min(len(reads), (rank + 1) * per)
+        sc.bloom_device(0, [(lo, hi - lo, 0)], 2)
+        nis = sc.bloom_finalize()
+        sc.count_device(0, [(lo, hi - lo, 0)], 2)
+        sc.sync()
+        with open(os.path.join(outdir, f"shard{rank}.json"), "w") as f:
+            json.dump({"owner": dict(eng.owner.table), "nis": nis, "filter": eng.filter.tolist()}, f)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("k,world", [(21, 2), (33, 3)])
+def test_sharded_bloom(tmp_path, k, world):
+    """Every rank's Bloom pass fills its own filter; the combined filter gates every rank's
+    counting pass: each k-mer seen twice anywhere (also once on each of two ranks) keeps its
+    exact count, and every rank installs the same filter and the same new_in_second."""
+    reads = make_reads(40, 70, seed=k)
+    mp.spawn(_bloom_worker, args=(world, _free_port(), k, reads, str(tmp_path)), nprocs=world, join=True)
+    shards = [json.load(open(tmp_path / f"shard{r}.json")) for r in range(world)]
+    assert all(s["filter"] == shards[0]["filter"] for s in shards)
+    assert all(s["nis"] == shards[0]["nis"] > 0 for s in shards)
+    union = collections.Counter()
+    for a in range(world):
+        for b in range(a + 1, world):
+            assert not (set(shards[a]["owner"]) & set(shards[b]["owner"]))
+        union.update(shards[a]["owner"])
+    truth = collections.Counter(km for r in reads for km in canonical_windows(r, k))
+    per = (len(reads) + world - 1) // world
+    ranks_of = collections.defaultdict(set)
+    for i, r in enumerate(reads):
+        for km in canonical_windows(r, k):
+            ranks_of[km].add(i // per)
+    assert any(truth[km] == 2 and len(ranks_of[km]) == 2 for km in truth), "no k-mer split over two ranks"
+    assert {km: c for km, c in union.items() if truth[km] >= 2} == {km: c for km, c in truth.items() if c >= 2}
+    assert all(truth[km] == 1 == c for km, c in union.items() if truth[km] < 2)
 
 
 def _exchange_worker(rank, world, port, outdir, chunk):
