@@ -42,61 +42,92 @@ from typing import List, Sequence, Tuple
 from . import Config, KmerCounter, words_for_k
 
 
-# Largest message per (peer, all-to-all) in int64 words.  RCCL 2.26 (the ROCm torch
-# wheel's) returned only part of a 1.4 GB single-peer all_to_all_single on MI355X, so big
-# exchanges go in rounds of at most this many words per peer.
+# Largest message per (peer, all-to-all) in int64 words (KC_EXCHANGE_CHUNK_MB overrides it;
+# 0 = one all-to-all).  An early multi-GPU run saw RCCL (the ROCm torch wheel's) return only
+# part of a 1.4 GB single-peer all_to_all_single.  No cause was found in the code: split sizes
+# are int64 in Python and size_t from c10d's computeLengthsAndOffsets through
+# all2all_single_unequal_split to ncclAllToAllv / ncclSend / ncclRecv (torch/csrc/cuda/nccl.h,
+# rccl.h), and 1.4 GB is below every 32-bit byte count; the run's record was not kept and one
+# GPU cannot host two RCCL ranks, so the observation is unconfirmed.  Big exchanges therefore
+# go in rounds of at most this many words per peer, and every exchange checks per-peer sums of
+# what arrived (`verify`) so that a short or corrupt delivery raises instead of miscounting.
 EXCHANGE_CHUNK_WORDS = 1 << 24
 
 
-def exchange(dist, keys, counts: Sequence[int], W: int, group=None, chunk_words: int = EXCHANGE_CHUNK_WORDS,
-             with_counts: bool = False):
+def chunk_words_default() -> int:
+    import os
+
+    mb = os.environ.get("KC_EXCHANGE_CHUNK_MB")
+    if mb is None:
+        return EXCHANGE_CHUNK_WORDS
+    return (int(mb) << 20) // 8 or (1 << 62)
+
+
+def exchange(dist, keys, counts: Sequence[int], W: int, group=None, chunk_words: int = 0,
+             with_counts: bool = False, verify: bool = True):
     """All-to-all of owner-grouped items of W int64 words each.  keys: int64 tensor
     holding sum(counts)*W words (group d = the items for rank d, in rank order).
     Returns (received items, n received[, items received from each rank]); the items
-    from rank s follow those of s-1."""
+    from rank s follow those of s-1.  verify: the senders' per-group word sums travel
+    beside the items and must equal the sums of the groups received (else RuntimeError)."""
     import torch
 
+    chunk_words = chunk_words or chunk_words_default()
     dev = keys.device
     world = len(counts)
     if world == 1:  # nothing leaves the rank
         return (keys, int(counts[0]), [int(counts[0])]) if with_counts else (keys, int(counts[0]))
-    send_counts = torch.tensor(list(counts), dtype=torch.int64, device=dev)
-    recv_counts = torch.empty_like(send_counts)
-    dist.all_to_all_single(recv_counts, send_counts, group=group)
-    recv = [int(x) for x in recv_counts.cpu().tolist()]
+    sw = [int(c) * W for c in counts]
+    so = [sum(sw[:d]) for d in range(world)]
+    head = [int(c) for c in counts]
+    if verify:  # wrapping int64 sums: the same on both sides for the same words
+        head += [int(keys[so[d]: so[d] + sw[d]].sum()) if sw[d] else 0 for d in range(world)]
+    send_head = torch.tensor(head, dtype=torch.int64, device=dev).view(-1 if not verify else 2, world)
+    send_head = send_head.t().contiguous().view(-1)  # [count_d, sum_d] per destination d
+    recv_head = torch.empty_like(send_head)
+    dist.all_to_all_single(recv_head, send_head, group=group)
+    rh = recv_head.view(world, -1).cpu().tolist()
+    recv = [int(r[0]) for r in rh]
     total = sum(recv)
     out = torch.empty(max(1, total * W), dtype=torch.int64, device=dev)
-    sw = [c * W for c in counts]
     rw = [r * W for r in recv]
+    ro = [sum(rw[:d]) for d in range(world)]
     big = torch.tensor([max(sw + rw + [0])], dtype=torch.int64, device=dev)
     dist.all_reduce(big, op=dist.ReduceOp.MAX, group=group)
     rounds = max(1, -(-int(big.item()) // chunk_words))
     if rounds == 1:
         dist.all_to_all_single(out[: total * W], keys[: sum(sw)], output_split_sizes=rw, input_split_sizes=sw,
                                group=group)
-        return (out, total, recv) if with_counts else (out, total)
-    so = [sum(sw[:d]) for d in range(world)]
-    ro = [sum(rw[:d]) for d in range(world)]
-    for r in range(rounds):
-        lo = r * chunk_words
-        sin = [min(max(sw[d] - lo, 0), chunk_words) for d in range(world)]
-        rin = [min(max(rw[d] - lo, 0), chunk_words) for d in range(world)]
-        send = torch.cat([keys[so[d] + lo: so[d] + lo + sin[d]] for d in range(world)])
-        got = torch.empty(max(1, sum(rin)), dtype=torch.int64, device=dev)
-        dist.all_to_all_single(got[: sum(rin)], send, output_split_sizes=rin, input_split_sizes=sin, group=group)
-        pos = 0
-        for d in range(world):
-            if rin[d]:
-                out[ro[d] + lo: ro[d] + lo + rin[d]].copy_(got[pos: pos + rin[d]])
-            pos += rin[d]
+    else:
+        for r in range(rounds):
+            lo = r * chunk_words
+            sin = [min(max(sw[d] - lo, 0), chunk_words) for d in range(world)]
+            rin = [min(max(rw[d] - lo, 0), chunk_words) for d in range(world)]
+            send = torch.cat([keys[so[d] + lo: so[d] + lo + sin[d]] for d in range(world)])
+            got = torch.empty(max(1, sum(rin)), dtype=torch.int64, device=dev)
+            dist.all_to_all_single(got[: sum(rin)], send, output_split_sizes=rin, input_split_sizes=sin,
+                                   group=group)
+            pos = 0
+            for d in range(world):
+                if rin[d]:
+                    out[ro[d] + lo: ro[d] + lo + rin[d]].copy_(got[pos: pos + rin[d]])
+                pos += rin[d]
+    if verify:
+        for s in range(world):
+            got_sum = int(out[ro[s]: ro[s] + rw[s]].sum()) if rw[s] else 0
+            if got_sum != int(rh[s][1]):
+                raise RuntimeError(f"all-to-all delivered corrupt data from rank {s}: {rw[s]} words, "
+                                   f"sum {got_sum} != the sender's {int(rh[s][1])} ({rounds} round(s) of "
+                                   f"<= {chunk_words} words per peer)")
     return (out, total, recv) if with_counts else (out, total)
 
 
-def all_gather_words(dist, mine, world: int, group=None, chunk_words: int = 2 * EXCHANGE_CHUNK_WORDS):
+def all_gather_words(dist, mine, world: int, group=None, chunk_words: int = 0):
     """[world x len(mine)] = every rank's `mine` (int32 words), in pieces of at most
-    chunk_words per rank (EXCHANGE_CHUNK_WORDS bytes, as the all-to-all's rounds)."""
+    chunk_words per rank (default: the all-to-all's round size in bytes)."""
     import torch
 
+    chunk_words = chunk_words or 2 * chunk_words_default()
     per = mine.numel()
     full = torch.empty(world * per, dtype=mine.dtype, device=mine.device)
     if world == 1:

@@ -300,6 +300,44 @@ def test_sharded_bloom(tmp_path, k, world):
     assert all(truth[km] == 1 == c for km, c in union.items() if truth[km] < 2)
 
 
+class _ShortDelivery:
+    """torch.distributed proxy whose item all-to-alls lose the last received word."""
+
+    def __getattr__(self, name):
+        return getattr(dist, name)
+
+    @staticmethod
+    def all_to_all_single(out, inp, output_split_sizes=None, input_split_sizes=None, group=None):
+        dist.all_to_all_single(out, inp, output_split_sizes=output_split_sizes, input_split_sizes=input_split_sizes,
+                               group=group)
+        if output_split_sizes is not None and out.numel():
+            out[-1] = 0
+
+
+def _corrupt_worker(rank, world, port, outdir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        keys = torch.arange(1, 1 + 2 * 6, dtype=torch.int64)
+        try:
+            exchange(_ShortDelivery(), keys, [3, 3], 2)
+            msg = "no error"
+        except RuntimeError as e:
+            msg = str(e)
+        with open(os.path.join(outdir, f"c{rank}.txt"), "w") as f:
+            f.write(msg)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_exchange_detects_short_delivery(tmp_path):
+    """A collective that delivers less than was sent raises on the receiving rank."""
+    mp.spawn(_corrupt_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        assert "corrupt data from rank 1" in open(tmp_path / f"c{r}.txt").read()
+
+
 def _exchange_worker(rank, world, port, outdir, chunk):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
