@@ -283,6 +283,18 @@ def run_workload(args, env, image=None):
     counter.profile(False)
     tm = counter.timing()
     st = counter.finish()  # raises on table overflow
+    compact = None
+    if not dist and args.compact:  # the Kaarme slot words built from this table
+        torch.cuda.synchronize()
+        c0 = time.perf_counter()
+        info = counter.compact()
+        c1 = time.perf_counter()
+        n = max(1, info["kmers"])
+        compact = {"build_ms": round((c1 - c0) * 1e3, 2), "kmers": info["kmers"],
+                   "chain_starts": info["chain_starts"], "bytes_per_kmer": round(info["bytes"] / n, 2),
+                   "table_bytes_per_kmer": round(info["table_bytes"] / n, 2),
+                   "note": "kc_compact after the timed steps (not in value): 8-byte slot words at load 0.8 + "
+                           "chain-start keys, vs the full-key table sized by -s"}
     counter.close()
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -358,6 +370,8 @@ def run_workload(args, env, image=None):
                        "batches_redone": st["part_fallbacks"]},
         "cpu_baseline": None,
     }
+    if compact:
+        out["compact"] = compact
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args)
     return out, image
@@ -381,6 +395,8 @@ def main():
     ap.add_argument("--cpu-sample-bases", type=int, default=150_000_000)
     ap.add_argument("--cpu-threads", type=int, default=0, help="-t of the reference (0 = core share + 2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-compact", dest="compact", action="store_false",
+                    help="skip the compact-representation figure (kc_compact after the timed steps)")
     ap.add_argument("--secondary", default="C3",
                     help="at N=1 with the default C2: also time this workload (the north star's k=51 Bloom "
                          "config) and attach it as a second record ('none' = skip)")
@@ -421,7 +437,8 @@ def main():
         rec, _ = run_workload(sec, env, image if same_image(primary, sec) else None)
         out[sec.config.lower()] = {key: rec[key] for key in ("value", "unit", "ms_per_step", "config", "roofline",
                                                             "kernel_ms", "windows_per_step_per_gpu",
-                                                            "distinct_per_gpu", "table_slots", "cpu_baseline")}
+                                                            "distinct_per_gpu", "table_slots", "cpu_baseline",
+                                                            "compact") if key in rec}
     del image
     if rank == 0:
         print(json.dumps(out), file=json_out, flush=True)

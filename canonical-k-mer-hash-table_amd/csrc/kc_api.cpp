@@ -130,6 +130,12 @@ struct kc_ctx {
     unsigned long long reuse_sum = 0; // checksum of the Bloom pass's chunk bytes
     uint64_t reuse_windows = 0;       // windows of that batch
     unsigned long long* d_sum = nullptr;  // CHECKSUM_SLOTS partial sums (+ CHECKSUM_SLOTS for kc_bloom_estimate)
+    // compact representation (kc_compact): slot words, chain-start keys, counters
+    uint64_t* d_cwords = nullptr;
+    uint64_t cslots = 0;
+    uint64_t* d_csecond = nullptr;
+    uint64_t cstarts = 0, ckmers = 0;
+    unsigned long long* d_cstat = nullptr;  // [0] chain starts / record cursor, [1] hops, [2] max hops, [3] bad walks
     uint32_t* d_keep_fill = nullptr;      // the kept partitions' segment fills: level 1 [F1][nblk1]
     uint32_t* d_keep_fill2 = nullptr;     // and level 2 [R_fine][B2]
     uint64_t keep_fill_cap = 0, keep_fill2_cap = 0;
@@ -881,6 +887,9 @@ void kc_destroy(kc_ctx* c) {
     hipFree(c->d_chunks);
     hipFree(c->d_ctr);
     hipFree(c->d_sum);
+    hipFree(c->d_cwords);
+    hipFree(c->d_csecond);
+    hipFree(c->d_cstat);
     hipFree(c->d_keep_fill);
     hipFree(c->d_keep_fill2);
     hipFree(c->d_table);
@@ -1310,6 +1319,14 @@ int kc_finish(kc_ctx* c, kc_stats* st) {
     return KC_OK;
 }
 
+// the compact representation is a snapshot of the table (kc_compact); kc_reset drops it
+static void drop_compact(kc_ctx* c) {
+    hipFree(c->d_cwords);
+    hipFree(c->d_csecond);
+    c->d_cwords = c->d_csecond = nullptr;
+    c->cslots = c->cstarts = c->ckmers = 0;
+}
+
 int kc_clear_table(kc_ctx* c) {
     if (!c) return KC_ERR_ARG;
     if (!c->nbuckets) return c->fail(KC_ERR_STATE, "no table");
@@ -1339,6 +1356,7 @@ int kc_reset(kc_ctx* c) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->n_chunks = c->n_bytes = 0;
     c->bloom_batches = 0;
+    drop_compact(c);
     c->reuse_kept = c->reuse_ok = false;
     c->reuse_level = 0;
     c->reuse_hits = 0;
@@ -1411,6 +1429,148 @@ int kc_dump(kc_ctx* c, uint64_t** records, uint64_t* n_records) {
     }
     *records = h;
     *n_records = n;
+    return KC_OK;
+}
+
+// ------------------------------------------------------------------------------
+// Kaarme's compact representation: kc_compact_impl.h
+// ------------------------------------------------------------------------------
+int kc_compact(kc_ctx* c, double load, kc_compact_info* info) {
+    if (!c) return KC_ERR_ARG;
+    if (load == 0) load = 0.8;
+    if (!(load > 0 && load <= 0.95)) return c->fail(KC_ERR_ARG, "load must be in (0, 0.95]");
+    if (!c->nbuckets) return c->fail(KC_ERR_STATE, "no table");
+    if (c->cfg.mode == 0)
+        return c->fail(KC_ERR_UNSUPPORTED, "the compact representation holds Kaarme counts (-m 1/2: 14 bits, "
+                                           "saturating at 16383)");
+    int rc = kc_sync(c);
+    if (rc) return rc;
+    rc = materialize_zero(c, c->stream);
+    if (rc) return rc;
+    drop_compact(c);
+    const TableView tv = table_view(c);
+    HIPCHK(c, hipMemsetAsync(&c->d_ctr->occupied, 0, 8, c->stream));
+    HIPCHK(c, launch_dump(tv, 1, ~0ULL, nullptr, c->d_ctr, c->stream));
+    unsigned long long occ = 0;
+    HIPCHK(c, hipMemcpyAsync(&occ, &c->d_ctr->occupied, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const uint64_t nslots = std::max<uint64_t>(64, (uint64_t)std::ceil((double)occ / load));
+    if (nslots >> 38) return c->fail(KC_ERR_ARG, "too many k-mers for 38-bit slot pointers");
+    uint64_t *src = nullptr, *second = nullptr;
+    if (!c->d_cstat && hipMalloc(&c->d_cstat, 4 * sizeof(unsigned long long)) != hipSuccess)
+        return c->fail(KC_ERR_NOMEM, "compact counters");
+    if (hipMalloc(&c->d_cwords, nslots * 8) != hipSuccess || hipMalloc(&src, nslots * 8) != hipSuccess ||
+        hipMalloc(&second, std::max<uint64_t>(1, occ) * c->W * 8) != hipSuccess) {
+        hipFree(src);
+        hipFree(second);
+        drop_compact(c);
+        return c->fail(KC_ERR_NOMEM, "compact representation allocation failed");
+    }
+    HIPCHK(c, hipMemsetAsync(c->d_cwords, 0, nslots * 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(src, 0xFF, nslots * 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->d_cstat, 0, 4 * sizeof(unsigned long long), c->stream));
+    CompactView cv{c->d_cwords, nslots, src, second, c->d_cstat};
+    HIPCHK(c, launch_compact_build(tv, cv, c->cfg.k, c->stream));
+    unsigned long long starts = 0;
+    HIPCHK(c, hipMemcpyAsync(&starts, c->d_cstat, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    hipFree(src);
+    // the secondary array at its size (the reference grows it as chains start, :2267-2278)
+    if (hipMalloc(&c->d_csecond, std::max<uint64_t>(1, starts) * c->W * 8) != hipSuccess) {
+        hipFree(second);
+        drop_compact(c);
+        return c->fail(KC_ERR_NOMEM, "secondary array allocation failed");
+    }
+    if (starts) HIPCHK(c, hipMemcpyAsync(c->d_csecond, second, starts * c->W * 8, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    hipFree(second);
+    c->cslots = nslots;
+    c->cstarts = starts;
+    c->ckmers = occ;
+    if (info) {
+        info->slots = nslots;
+        info->kmers = occ;
+        info->chain_starts = starts;
+        info->bytes = nslots * 8 + starts * c->W * 8;
+        info->table_bytes = c->nbuckets * BUCKET_WORDS * 8;
+    }
+    return KC_OK;
+}
+
+static CompactView compact_view(const kc_ctx* c) {
+    return CompactView{c->d_cwords, c->cslots, nullptr, c->d_csecond, c->d_cstat};
+}
+
+int kc_compact_dump(kc_ctx* c, uint64_t** records, uint64_t* n_records, uint64_t* max_hops, double* mean_hops) {
+    if (!c || !records || !n_records) return KC_ERR_ARG;
+    *records = nullptr;
+    *n_records = 0;
+    if (!c->d_cwords) return c->fail(KC_ERR_STATE, "no compact representation (kc_compact)");
+    int rc = kc_sync(c);
+    if (rc) return rc;
+    const CompactView cv = compact_view(c);
+    const uint64_t a = c->cfg.min_abundance;
+    unsigned long long st[4];
+    HIPCHK(c, hipMemsetAsync(c->d_cstat, 0, sizeof(st), c->stream));
+    HIPCHK(c, launch_compact_dump(c->W, cv, c->cfg.k, a, nullptr, c->d_cstat, c->d_cstat + 1, c->stream));
+    HIPCHK(c, hipMemcpyAsync(st, c->d_cstat, sizeof(st), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const uint64_t n = st[0];
+    if (st[3]) return c->fail(KC_ERR_STATE, std::to_string(st[3]) + " compact slots did not reconstruct");
+    const size_t rec = (size_t)(c->W + 1) * sizeof(uint64_t);
+    uint64_t* h = (uint64_t*)std::malloc(std::max<size_t>(1, n * rec));
+    if (!h) return c->fail(KC_ERR_NOMEM, "host allocation failed");
+    if (n) {
+        uint64_t* d = nullptr;
+        if (hipMalloc(&d, n * rec) != hipSuccess) {
+            std::free(h);
+            return c->fail(KC_ERR_NOMEM, "dump buffer allocation failed");
+        }
+        HIPCHK(c, hipMemsetAsync(c->d_cstat, 0, sizeof(st), c->stream));
+        HIPCHK(c, launch_compact_dump(c->W, cv, c->cfg.k, a, d, c->d_cstat, c->d_cstat + 1, c->stream));
+        HIPCHK(c, hipMemcpyAsync(h, d, n * rec, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(st, c->d_cstat, sizeof(st), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        hipFree(d);
+    }
+    if (max_hops) *max_hops = st[2];
+    if (mean_hops) *mean_hops = n ? (double)st[1] / (double)n : 0.0;
+    *records = h;
+    *n_records = n;
+    return KC_OK;
+}
+
+int kc_compact_lookup(kc_ctx* c, const uint64_t* keys, uint64_t n, uint32_t* counts) {
+    if (!c || (n && (!keys || !counts))) return KC_ERR_ARG;
+    if (!c->d_cwords) return c->fail(KC_ERR_STATE, "no compact representation (kc_compact)");
+    if (!n) return KC_OK;
+    int rc = kc_sync(c);
+    if (rc) return rc;
+    uint64_t* dk = nullptr;
+    uint32_t* dc = nullptr;
+    if (hipMalloc(&dk, n * c->W * 8) != hipSuccess || hipMalloc(&dc, n * 4) != hipSuccess) {
+        hipFree(dk);
+        return c->fail(KC_ERR_NOMEM, "lookup buffers");
+    }
+    HIPCHK(c, hipMemcpyAsync(dk, keys, n * c->W * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, launch_compact_lookup(c->W, compact_view(c), c->cfg.k, dk, n, dc, c->stream));
+    HIPCHK(c, hipMemcpyAsync(counts, dc, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    hipFree(dk);
+    hipFree(dc);
+    return KC_OK;
+}
+
+int kc_compact_read(kc_ctx* c, uint64_t* words, uint64_t n_words, uint64_t* second, uint64_t n_second_words) {
+    if (!c) return KC_ERR_ARG;
+    if (!c->d_cwords) return c->fail(KC_ERR_STATE, "no compact representation (kc_compact)");
+    if (n_words > c->cslots || n_second_words > c->cstarts * c->W || (n_words && !words) ||
+        (n_second_words && !second))
+        return c->fail(KC_ERR_ARG, "more words than the compact representation holds");
+    int rc = kc_sync(c);
+    if (rc) return rc;
+    if (n_words) HIPCHK(c, hipMemcpy(words, c->d_cwords, n_words * 8, hipMemcpyDeviceToHost));
+    if (n_second_words) HIPCHK(c, hipMemcpy(second, c->d_csecond, n_second_words * 8, hipMemcpyDeviceToHost));
     return KC_OK;
 }
 

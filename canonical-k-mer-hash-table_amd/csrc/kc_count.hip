@@ -65,6 +65,31 @@ hipError_t launch_insert_counts(const uint64_t* rec, uint64_t n, bool partitione
     KC_DISPATCH_W(t.W, insert_counts(rec, n, partitioned, t, ctr, pb, fresh, s));
 }
 
+#define KC_DISPATCH_CW(W_, CALL)               \
+    switch (W_) {                              \
+    case 1: return CompactOps<1>::CALL;        \
+    case 2: return CompactOps<2>::CALL;        \
+    case 3: return CompactOps<3>::CALL;        \
+    case 4: return CompactOps<4>::CALL;        \
+    case 5: return CompactOps<5>::CALL;        \
+    case 6: return CompactOps<6>::CALL;        \
+    case 7: return CompactOps<7>::CALL;        \
+    case 8: return CompactOps<8>::CALL;        \
+    default: return hipErrorInvalidValue;      \
+    }
+
+hipError_t launch_compact_build(TableView t, CompactView c, int k, hipStream_t s) {
+    KC_DISPATCH_CW(t.W, build(t, c, k, s));
+}
+hipError_t launch_compact_dump(int W, CompactView c, int k, uint64_t a, uint64_t* out, unsigned long long* cursor,
+                               unsigned long long* stats, hipStream_t s) {
+    KC_DISPATCH_CW(W, dump(c, k, a, out, cursor, stats, s));
+}
+hipError_t launch_compact_lookup(int W, CompactView c, int k, const uint64_t* keys, uint64_t n, uint32_t* counts,
+                                 hipStream_t s) {
+    KC_DISPATCH_CW(W, lookup(c, k, keys, n, counts, s));
+}
+
 hipError_t launch_dump(TableView t, int count_mode, uint64_t min_abundance, uint64_t* out, DevCounters* ctr,
                        hipStream_t s) {
     KC_DISPATCH_W(t.W, dump(t, count_mode, min_abundance, out, ctr, s));

@@ -262,6 +262,29 @@ struct WOps {
     static hipError_t text(TableView t, int count_mode, uint64_t a, int k, uint64_t blk0, uint64_t nblk,
                            const uint64_t* off, uint64_t base, uint8_t* out, size_t lds, hipStream_t s);
 };
+// Kaarme's compact representation, built after counting (kc_compact_impl.h)
+struct CompactView {
+    uint64_t* words;               // nslots 8-byte slot words (kmer.hpp:103-149 layout)
+    uint64_t nslots;
+    uint64_t* src;                 // build only: full-table slot (bucket * S + s) per compact slot, ~0 = empty
+    uint64_t* second;              // chain-start keys, W words each
+    unsigned long long* n_second;  // chain starts written
+};
+template <int W>
+struct CompactOps {
+    static hipError_t build(TableView t, CompactView c, int k, hipStream_t s);
+    static hipError_t dump(CompactView c, int k, uint64_t a, uint64_t* out, unsigned long long* cursor,
+                           unsigned long long* stats, hipStream_t s);
+    static hipError_t lookup(CompactView c, int k, const uint64_t* keys, uint64_t n, uint32_t* counts, hipStream_t s);
+};
+hipError_t launch_compact_build(TableView t, CompactView c, int k, hipStream_t s);
+// records {W key words, T(c)} of the slots with T(c) >= a (out == nullptr: count into cursor);
+// stats[0] += hops, stats[1] = max hops, stats[2] += walks that did not end
+hipError_t launch_compact_dump(int W, CompactView c, int k, uint64_t a, uint64_t* out, unsigned long long* cursor,
+                               unsigned long long* stats, hipStream_t s);
+hipError_t launch_compact_lookup(int W, CompactView c, int k, const uint64_t* keys, uint64_t n, uint32_t* counts,
+                                 hipStream_t s);
+
 extern template struct WOps<1>;
 extern template struct WOps<2>;
 extern template struct WOps<3>;
@@ -270,5 +293,13 @@ extern template struct WOps<5>;
 extern template struct WOps<6>;
 extern template struct WOps<7>;
 extern template struct WOps<8>;
+extern template struct CompactOps<1>;
+extern template struct CompactOps<2>;
+extern template struct CompactOps<3>;
+extern template struct CompactOps<4>;
+extern template struct CompactOps<5>;
+extern template struct CompactOps<6>;
+extern template struct CompactOps<7>;
+extern template struct CompactOps<8>;
 
 }  // namespace kc

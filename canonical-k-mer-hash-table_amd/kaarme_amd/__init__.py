@@ -48,7 +48,7 @@ EXPORTS = (
     "kc_route_table_device", "kc_insert_counts_device", "kc_clear_table", "kc_insert_counts_runs_device",
     "kc_xxh64", "kc_bloom_info", "kc_bloom_read", "kc_bloom_write", "kc_synth_skew_device",
     "kc_table_size_reference", "kc_bloom_get_device", "kc_bloom_merge_device", "kc_bloom_set_device",
-    "kc_bloom_estimate",
+    "kc_bloom_estimate", "kc_compact", "kc_compact_dump", "kc_compact_lookup", "kc_compact_read",
 )
 
 
@@ -79,6 +79,10 @@ class kc_timing(ctypes.Structure):
 class kc_synth_skew(ctypes.Structure):
     _fields_ = [("homo_frac", ctypes.c_double), ("dinuc_frac", ctypes.c_double),
                 ("repeat_len", ctypes.c_uint32), ("repeat_copies", ctypes.c_uint32)]
+
+
+class kc_compact_info(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in ("slots", "kmers", "chain_starts", "bytes", "table_bytes")]
 
 
 class kc_stats(ctypes.Structure):
@@ -156,6 +160,11 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "kc_bloom_merge_device": (I32, [P, P, ctypes.c_uint32, U64, P, P]),
         "kc_bloom_set_device": (I32, [P, P, U64, ctypes.POINTER(U64), P]),
         "kc_bloom_estimate": (I32, [P, ctypes.POINTER(U64), P]),
+        "kc_compact": (I32, [P, ctypes.c_double, ctypes.POINTER(kc_compact_info)]),
+        "kc_compact_dump": (I32, [P, ctypes.POINTER(ctypes.POINTER(U64)), ctypes.POINTER(U64), ctypes.POINTER(U64),
+                                  ctypes.POINTER(ctypes.c_double)]),
+        "kc_compact_lookup": (I32, [P, P, U64, P]),
+        "kc_compact_read": (I32, [P, P, U64, P, U64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -424,6 +433,44 @@ class KmerCounter:
         finally:
             self.lib.kc_free(p)
         return arr.reshape(-1, W + 1)
+
+    # -- Kaarme's compact representation (kc_compact*)
+    def compact(self, load: float = 0.0) -> dict:
+        """Build the compact slot words from the counted table; returns kc_compact_info."""
+        info = kc_compact_info()
+        self._chk(self.lib.kc_compact(self._ctx, load, ctypes.byref(info)), "kc_compact")
+        return {n: getattr(info, n) for n, _ in kc_compact_info._fields_}
+
+    def compact_dump(self):
+        """(records (n, W+1) as dump(), longest walk, mean walk) reconstructed from the compact words."""
+        p = ctypes.POINTER(ctypes.c_uint64)()
+        n, mx, mean = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_double()
+        self._chk(self.lib.kc_compact_dump(self._ctx, ctypes.byref(p), ctypes.byref(n), ctypes.byref(mx),
+                                           ctypes.byref(mean)), "kc_compact_dump")
+        W = self.lib.kc_key_words(self._ctx)
+        try:
+            arr = (np.ctypeslib.as_array(p, shape=(n.value * (W + 1),)).copy() if n.value
+                   else np.zeros(0, dtype=np.uint64))
+        finally:
+            self.lib.kc_free(p)
+        return arr.reshape(-1, W + 1), mx.value, mean.value
+
+    def compact_lookup(self, keys: np.ndarray) -> np.ndarray:
+        """T(c) of canonical keys (n, W) uint64 (dump's key layout) from the compact words; 0 = absent."""
+        k = np.ascontiguousarray(keys, dtype=np.uint64)
+        out = np.zeros(k.shape[0], dtype=np.uint32)
+        self._chk(self.lib.kc_compact_lookup(self._ctx, k.ctypes.data, k.shape[0], out.ctypes.data),
+                  "kc_compact_lookup")
+        return out
+
+    def compact_read(self, info: dict):
+        """(slot words, secondary-array words) as uint64 arrays."""
+        W = self.lib.kc_key_words(self._ctx)
+        words = np.zeros(info["slots"], dtype=np.uint64)
+        second = np.zeros(info["chain_starts"] * W, dtype=np.uint64)
+        self._chk(self.lib.kc_compact_read(self._ctx, words.ctypes.data, words.size, second.ctypes.data,
+                                           second.size), "kc_compact_read")
+        return words, second.reshape(-1, W)
 
     def lines(self) -> List[str]:
         """Sorted "<KMER> <count>" lines (what sort(kaarme output) yields)."""

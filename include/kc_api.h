@@ -185,6 +185,33 @@ int kc_bloom_set_device(kc_ctx* ctx, const uint32_t* dev_src, uint64_t n_words, 
                         void* hip_stream);
 int kc_bloom_estimate(kc_ctx* ctx, uint64_t* distinct_in_second, void* hip_stream);
 
+/* Kaarme's compact representation: PointerHashTableCanonicalAV's 8-byte
+ * slot words (OneCharacterAndPointerKMerAtomicVariable, kmer.hpp:103-149: occupied, predecessor
+ * exists, self / predecessor canonical during insertion, left and right character, 14-bit count,
+ * 38-bit predecessor slot) plus a secondary array of the chain starts' full keys, built from the
+ * counted table after the counting pass (the reference builds it while inserting,
+ * kmer_hash_table.cpp:2207-2567).  Every k-mer links to a k-mer of the table that precedes it on
+ * the strand its minimizer reads forward, so the reference's walk (reconstruct_kmer_in_slot,
+ * kmer_hash_table.cpp:3848-4058) rebuilds it in at most k - 2 hops.  -m 1 / -m 2 only (14-bit
+ * counts); a snapshot: later counting does not update it, kc_reset drops it.
+ *   kc_compact        builds it at the given load (slots = k-mers / load; 0 = 0.8);
+ *   kc_compact_dump   reconstructs every k-mer with T(c) >= a: records as kc_dump, plus the
+ *                     longest and the mean walk (hops);
+ *   kc_compact_lookup T(c) of canonical keys (host arrays, kc_key_words() words each, the
+ *                     kc_dump key layout) from the compact words alone, 0 if absent;
+ *   kc_compact_read   copies the slot words and the secondary array's words to the host. */
+typedef struct {
+    uint64_t slots;         /* slot words (8 bytes each) */
+    uint64_t kmers;         /* k-mers held (the table's distinct k-mers) */
+    uint64_t chain_starts;  /* k-mers without a predecessor: full keys in the secondary array */
+    uint64_t bytes;         /* slot words + secondary array */
+    uint64_t table_bytes;   /* the full-key table it was built from */
+} kc_compact_info;
+int kc_compact(kc_ctx* ctx, double load, kc_compact_info* info);
+int kc_compact_dump(kc_ctx* ctx, uint64_t** records, uint64_t* n_records, uint64_t* max_hops, double* mean_hops);
+int kc_compact_lookup(kc_ctx* ctx, const uint64_t* keys, uint64_t n, uint32_t* counts);
+int kc_compact_read(kc_ctx* ctx, uint64_t* words, uint64_t n_words, uint64_t* second, uint64_t n_second_words);
+
 /* Re-initialise the table, the Bloom filter and all counters (the table/filter
  * constructors again, without reallocating). */
 int kc_reset(kc_ctx* ctx);
