@@ -412,8 +412,26 @@ static hipStream_t pick_stream(kc_ctx* c, void* s) {
 // ------------------------------------------------------------------------------
 // src: the bytes the chunk descriptors' src_off point into (the host stage, or a
 // device-resident image read in place)
+// The tail of a segmented batch (the skew list, the batch's bookkeeping, the exact pipeline
+// behind the device overflow gate) does nothing unless the single-pass levels left a skew list
+// or overflowed.  For device images the host reads those two counters after the main phase
+// (the call waits for its batch) and launches the tail only when needed: ~20 idle kernel
+// launches and two region-grid passes less per batch (0.25 ms of C2's 15.9 ms step).  Host
+// chunks keep the device gate (their staging overlaps the previous batch).  KC_DEVICE_GATE=1
+// forces the device gate everywhere.
+static int tail_needed(kc_ctx* c, hipStream_t s, bool* need) {
+    unsigned long long f[2] = {0, 0};
+    HIPCHK(c, hipMemcpyAsync(&f[0], &c->d_ctr->part_overflow, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(&f[1], &c->d_ctr->spill_n, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    *need = f[0] != 0 || f[1] != 0;
+    return KC_OK;
+}
+
 static int run_batch(kc_ctx* c, const uint8_t* src, uint64_t used, uint64_t nchunks, int fmt, int pass, hipStream_t s,
-                     hipEvent_t ev_start = nullptr, hipEvent_t ev_gather = nullptr, bool keep = false) {
+                     hipEvent_t ev_start = nullptr, hipEvent_t ev_gather = nullptr, bool keep = false,
+                     bool host_gate = false) {
+    if (std::getenv("KC_DEVICE_GATE")) host_gate = false;
     const uint64_t ntiles = used / TILE;
     if (ntiles == 0) return KC_OK;
     std::array<hipEvent_t, 4> ev{ev_start, ev_gather, nullptr, nullptr};
@@ -468,15 +486,28 @@ static int run_batch(kc_ctx* c, const uint8_t* src, uint64_t used, uint64_t nchu
             c->pbf.keep_fill = c->d_keep_fill;
             c->pbf.keep_fill2 = c->d_keep_fill2;
         }
+        const bool split = host_gate && c->pbf.cap1 != 0;
         HIPCHK(c, launch_bloom_partitioned(sv, c->cfg.k, c->W, bv, c->bgeo, c->fgeo, c->d_ctr, c->pbf,
-                                           c->bloom_fresh, keep ? 1 : 0, s));
+                                           c->bloom_fresh, keep ? 1 : 0, s, split ? PH_MAIN : PH_ALL));
+        bool tail = false;
+        if (split && (rc = tail_needed(c, s, &tail))) return rc;
+        if (tail)
+            HIPCHK(c, launch_bloom_partitioned(sv, c->cfg.k, c->W, bv, c->bgeo, c->fgeo, c->d_ctr, c->pbf,
+                                               c->bloom_fresh, keep ? 1 : 0, s, PH_TAIL));
         c->bloom_fresh = false;
         c->reuse_kept = keep;
     } else if (mode != 1 && use_partitioned(c, syms)) {
         const char* env = std::getenv("KC_INSERT_PATH");
         int rc = ensure_part(c, syms, !(env && !std::strcmp(env, "exact")));
         if (rc) return rc;
-        HIPCHK(c, launch_count_partitioned(sv, syms, c->cfg.k, mode, tv, bv, c->d_ctr, c->pb, c->table_fresh, s));
+        const bool split = host_gate && c->pb.cap1 != 0;
+        HIPCHK(c, launch_count_partitioned(sv, syms, c->cfg.k, mode, tv, bv, c->d_ctr, c->pb, c->table_fresh, s,
+                                           split ? PH_MAIN : PH_ALL));
+        bool tail = false;
+        if (split && (rc = tail_needed(c, s, &tail))) return rc;
+        if (tail)
+            HIPCHK(c, launch_count_partitioned(sv, syms, c->cfg.k, mode, tv, bv, c->d_ctr, c->pb, c->table_fresh, s,
+                                               PH_TAIL));
         c->table_zero_pending = false;  // the fresh pass wrote every region
     } else {
         if (mode != 1) {
@@ -696,7 +727,7 @@ static int device_pass(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, si
         }
         // the image is tokenized in place (no gather into the stage): "gather" is ~0
         if (c->profiling) HIPCHK(c, hipEventRecord(e1, s));
-        int r = run_batch(c, img, used, batch.size(), fmt, pass, s, e0, e1, keep);
+        int r = run_batch(c, img, used, batch.size(), fmt, pass, s, e0, e1, keep, true);
         if (r) return r;
         if (keep && c->reuse_kept) {  // what a counting pass must present again, and its checksum
             c->reuse_img = img;

@@ -24,18 +24,18 @@ hipError_t launch_count(PackedView sym, uint64_t sym_bound, int k, int mode, Tab
 }
 
 hipError_t launch_count_partitioned(PackedView sym, uint64_t sym_bound, int k, int mode, TableView t, BloomView bf,
-                                    DevCounters* ctr, PartBufs pb, int fresh, hipStream_t s) {
+                                    DevCounters* ctr, PartBufs pb, int fresh, hipStream_t s, int phase) {
     (void)sym_bound;
-    KC_DISPATCH_W(t.W, count_partitioned(sym, k, mode, t, bf, ctr, pb, fresh, s));
+    KC_DISPATCH_W(t.W, count_partitioned(sym, k, mode, t, bf, ctr, pb, fresh, s, phase));
 }
 
 // the blocked layout's filter regions: R divides the block count, <= 1024 blocks each
 hipError_t launch_bloom_partitioned(PackedView sym, int k, int W, BloomView bf, TableView ft, TableView fg,
-                                    DevCounters* ctr, PartBufs pb, int fresh, int keep, hipStream_t s) {
+                                    DevCounters* ctr, PartBufs pb, int fresh, int keep, hipStream_t s, int phase) {
     if (!bf.blocked || ft.R == 0 || bf.nblocks % ft.R || bf.nblocks / ft.R > (uint64_t)BF_BLOCKS_PER_REGION) return hipErrorInvalidValue;
     // the fine bins refine the filter regions (both powers of two)
     if (keep && (fg.R < ft.R || fg.R % ft.R || (fg.R & (fg.R - 1)))) return hipErrorInvalidValue;
-    KC_DISPATCH_W(W, bloom_partitioned(sym, k, bf, ft, fg, ctr, pb, fresh, keep, s));
+    KC_DISPATCH_W(W, bloom_partitioned(sym, k, bf, ft, fg, ctr, pb, fresh, keep, s, phase));
 }
 
 hipError_t launch_count_reuse(int W, TableView t, BloomView bf, DevCounters* ctr, PartBufs pb, int fresh, int level,

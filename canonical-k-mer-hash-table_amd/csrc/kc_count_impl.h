@@ -2213,15 +2213,17 @@ static __global__ void k_batch_end(DevCounters* ctr) {
 // segment overflowed, in which case the segmented p3 left the table untouched).
 template <int W, int MODE>
 static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf, DevCounters* ctr, PartBufs pb,
-                                int fresh, hipStream_t s) {
+                                int fresh, hipStream_t s, int phase) {
     constexpr bool GATE3 = MODE == 4;
     if (pb.cap1 == 0) {
+        if (!(phase & PH_MAIN)) return hipSuccess;
         hipError_t e = part_level1<W, MODE>(sym, k, bf, ctr, pb, t.F1, coarse_bins(t), pb.keys1, s);
         if (e != hipSuccess) return e;
         return part_levels23<W, false, GATE3>(t, ctr, pb, s, nullptr, fresh, bf);
     }
     hipError_t e;
     const unsigned long long* gate = &ctr->part_overflow;
+    if (phase & PH_MAIN) {
     hipLaunchKernelGGL(k_batch_begin, dim3(1), dim3(1), 0, s, ctr);
     const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
     auto k1 = k_p1<W, MODE, true, BinRegion, OutSeg, scatter_threads<W>()>;
@@ -2240,6 +2242,8 @@ static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf
     hipLaunchKernelGGL((k_p2f<W, p2f_threads<W>()>), dim3(t.F1 * pb.B2), dim3(p2f_threads<W>()), sm2, s, t, pb, ctr,
                        1);
     if ((e = launch_p3<W, true, false, GATE3>(t, ctr, pb, nullptr, fresh, s, bf)) != hipSuccess) return e;
+    }
+    if (!(phase & PH_TAIL)) return hipGetLastError();
     // the skew lists (MODE 2 rolls its windows: no heavy records); the segmented level 3
     // wrote every region of a fresh table, so these read the table
     if ((e = insert_spill<W, GATE3>(t, bf, ctr, pb, s)) != hipSuccess) return e;
@@ -2255,10 +2259,10 @@ static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf
 // reference layout -> gate on the rolled root at level 1 (MODE 2)
 template <int W>
 static hipError_t count_part_w(PackedView sym, int k, int mode, TableView t, BloomView bf, DevCounters* ctr,
-                               PartBufs pb, int fresh, hipStream_t s) {
-    if (mode != 2) return launch_part_w<W, 0>(sym, k, t, bf, ctr, pb, fresh, s);
-    if (bf.blocked) return launch_part_w<W, 4>(sym, k, t, bf, ctr, pb, fresh, s);
-    return launch_part_w<W, 2>(sym, k, t, bf, ctr, pb, fresh, s);
+                               PartBufs pb, int fresh, hipStream_t s, int phase) {
+    if (mode != 2) return launch_part_w<W, 0>(sym, k, t, bf, ctr, pb, fresh, s, phase);
+    if (bf.blocked) return launch_part_w<W, 4>(sym, k, t, bf, ctr, pb, fresh, s, phase);
+    return launch_part_w<W, 2>(sym, k, t, bf, ctr, pb, fresh, s, phase);
 }
 // Bloom pass 1 on the blocked layout, partitioned: windows -> table key word 0 -> coarse
 // bins -> filter regions (ft: R = filter regions, F1 x F2) -> k_b3 (LDS-resident filter
@@ -2272,8 +2276,9 @@ static hipError_t count_part_w(PackedView sym, int k, int mode, TableView t, Blo
 // segment fills of both levels are copied aside (the skew-list pass reuses hist1 / hist2).
 template <int W, bool KEEP>
 static hipError_t bloom_part_w(PackedView sym, int k, BloomView bf, TableView ft, TableView fg, DevCounters* ctr,
-                               PartBufs pb, int fresh, hipStream_t s) {
+                               PartBufs pb, int fresh, hipStream_t s, int phase) {
     if (pb.cap1 == 0) {
+        if (!(phase & PH_MAIN)) return hipSuccess;
         hipError_t e = part_level1<W, 3>(sym, k, bf, ctr, pb, ft.F1, coarse_bins(ft), pb.keys1, s);
         if (e != hipSuccess) return e;
         if ((e = part_level2_exact<1>(ft, pb, s, nullptr)) != hipSuccess) return e;
@@ -2283,6 +2288,7 @@ static hipError_t bloom_part_w(PackedView sym, int k, BloomView bf, TableView ft
     const TableView& lg = KEEP ? fg : ft;  // the partition levels' geometry
     hipError_t e;
     const unsigned long long* gate = &ctr->part_overflow;
+    if (phase & PH_MAIN) {
     hipLaunchKernelGGL(k_batch_begin, dim3(1), dim3(1), 0, s, ctr);
     const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
     constexpr int NT = scatter_threads<W>(), NT2 = p2f_threads<OW>();
@@ -2308,6 +2314,8 @@ static hipError_t bloom_part_w(PackedView sym, int k, BloomView bf, TableView ft
         p3.B2 = (uint32_t)(fg.R / ft.R) * pb.B2;
     }
     if ((e = launch_b3<true>(bf, ft, ctr, p3, nullptr, fresh, s, OW)) != hipSuccess) return e;
+    }
+    if (!(phase & PH_TAIL)) return hipGetLastError();
     // spilled keys (table key word 0 of OW-word entries) through the exact levels into the
     // filter regions
     {
@@ -2437,15 +2445,15 @@ hipError_t WOps<W>::count(PackedView sym, uint64_t sym_bound, int k, int mode, T
 
 template <int W>
 hipError_t WOps<W>::count_partitioned(PackedView sym, int k, int mode, TableView t, BloomView bf, DevCounters* ctr,
-                                      PartBufs pb, int fresh, hipStream_t s) {
-    return count_part_w<W>(sym, k, mode, t, bf, ctr, pb, fresh, s);
+                                      PartBufs pb, int fresh, hipStream_t s, int phase) {
+    return count_part_w<W>(sym, k, mode, t, bf, ctr, pb, fresh, s, phase);
 }
 
 template <int W>
 hipError_t WOps<W>::bloom_partitioned(PackedView sym, int k, BloomView bf, TableView ft, TableView fg, DevCounters* ctr,
-                                      PartBufs pb, int fresh, int keep, hipStream_t s) {
-    if (keep) return bloom_part_w<W, true>(sym, k, bf, ft, fg, ctr, pb, fresh, s);
-    return bloom_part_w<W, false>(sym, k, bf, ft, fg, ctr, pb, fresh, s);
+                                      PartBufs pb, int fresh, int keep, hipStream_t s, int phase) {
+    if (keep) return bloom_part_w<W, true>(sym, k, bf, ft, fg, ctr, pb, fresh, s, phase);
+    return bloom_part_w<W, false>(sym, k, bf, ft, fg, ctr, pb, fresh, s, phase);
 }
 template <int W>
 hipError_t WOps<W>::count_reuse(TableView t, BloomView bf, DevCounters* ctr, PartBufs pb, int fresh, int level,

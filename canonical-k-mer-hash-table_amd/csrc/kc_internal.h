@@ -170,15 +170,22 @@ hipError_t launch_count(PackedView sv, uint64_t sym_bound, int k, int mode, Tabl
 // partitioned insert for modes 0 and 2 (same table, same result as launch_count; mode 2
 // gates at level 3 on the blocked Bloom layout, at level 1 on the reference layout)
 // fresh: the table is all zero (just allocated or reset): level 3 does not read it
+// phase (segmented layout): bit 0 = the single-pass levels (PH_MAIN), bit 1 = the batch's
+// tail: the skew list, the batch's bookkeeping and the exact pipeline behind the device
+// overflow gate (PH_TAIL).  The host may run the tail only when the main phase left a skew
+// list or an overflow (kc_api.cpp); with both empty every tail kernel is a no-op.
+constexpr int PH_MAIN = 1, PH_TAIL = 2, PH_ALL = 3;
 hipError_t launch_count_partitioned(PackedView sv, uint64_t sym_bound, int k, int mode, TableView t,
-                                    BloomView bf, DevCounters* ctr, PartBufs pb, int fresh, hipStream_t s);
+                                    BloomView bf, DevCounters* ctr, PartBufs pb, int fresh, hipStream_t s,
+                                    int phase = PH_ALL);
 // Bloom pass 1 on the blocked layout, partitioned: ft = the filter's region geometry
 // (R = filter regions of nblocks / R <= 1024 blocks, F1 x F2 as for the table; no buckets);
 // fresh: the filter is all zero (level 3 does not read it)
 // keep: levels 1 and 2 move whole table keys in the fine geometry fg (kept for the counting
 // pass, count_reuse); otherwise fg is unused
 hipError_t launch_bloom_partitioned(PackedView sv, int k, int W, BloomView bf, TableView ft, TableView fg,
-                                    DevCounters* ctr, PartBufs pb, int fresh, int keep, hipStream_t s);
+                                    DevCounters* ctr, PartBufs pb, int fresh, int keep, hipStream_t s,
+                                    int phase = PH_ALL);
 // the counting pass from the partitions kept by the Bloom pass (pb: their buffers), from
 // level 2 (level 2) or level 1 (level 1); gate: behind the Bloom gate (0: -m 1 -b, whose
 // filter is ignored); windows: the batch's windows (counted by the Bloom pass)
@@ -238,9 +245,9 @@ struct WOps {
     static hipError_t count(PackedView sym, uint64_t sym_bound, int k, int mode, TableView t, BloomView bf,
                             DevCounters* ctr, hipStream_t s);
     static hipError_t count_partitioned(PackedView sym, int k, int mode, TableView t, BloomView bf, DevCounters* ctr,
-                                        PartBufs pb, int fresh, hipStream_t s);
+                                        PartBufs pb, int fresh, hipStream_t s, int phase);
     static hipError_t bloom_partitioned(PackedView sym, int k, BloomView bf, TableView ft, TableView fg,
-                                        DevCounters* ctr, PartBufs pb, int fresh, int keep, hipStream_t s);
+                                        DevCounters* ctr, PartBufs pb, int fresh, int keep, hipStream_t s, int phase);
     static hipError_t count_reuse(TableView t, BloomView bf, DevCounters* ctr, PartBufs pb, int fresh, int level,
                                   int gate, uint64_t windows, hipStream_t s);
     static hipError_t route(PackedView sym, int k, DevCounters* ctr, PartBufs pb, uint32_t parts, uint64_t* out,
