@@ -78,6 +78,7 @@ struct kc_ctx {
     uint64_t R = 0;
     uint32_t F1 = 1, F2 = 1;
     int f2bits = 0;
+    bool seg_ok = true;  // the table's geometry fits the segmented single-pass levels (else exact layout)
 
     // partitioned insert buffers (pb: the table's levels; pbf: the Bloom pass's, same key
     // buffers, own histograms)
@@ -224,11 +225,39 @@ static int alloc_table(kc_ctx* c, uint64_t min_slots, uint32_t pow2_f1 = 0) {
         c->f2bits = std::max(0, rbits - f1);
         c->F2 = 1u << c->f2bits;
         c->F1 = pow2_f1;
+        c->seg_ok = true;
     } else {
-        const int f1bits = std::min(10, (rbits + 1) / 2);
+        // level 1 keeps F1 bins' arrays beside its tile in LDS (p1_lds_bytes), level 2 F2 bins'
+        // (p2f_lds_bytes): big tables (C4, C5 shares) take more regions per coarse bin until
+        // level 2 fits; for wide keys, if level 1 then does not fit, fewer, with level 2 at half
+        // its workgroup (launch_p2f)
+        auto f1_of = [&](int f2b) { return (uint32_t)((regions + (1ULL << f2b) - 1) >> f2b); };
+        auto l2_fits = [&](int f2b, int nt) {
+            const uint64_t b2 = std::max<uint64_t>(1, std::min<uint64_t>(64, 2048 / std::max<uint32_t>(1, f1_of(f2b))));
+            return p2f_lds_bytes(c->W, 1u << f2b, (uint32_t)((2048 + b2 - 1) / b2), nt) <= LDS_BYTES;
+        };
+        auto l1_fits = [&](int f2b) { return p1_lds_bytes(c->W, f1_of(f2b)) <= LDS_BYTES; };
+        int f1bits = std::min(10, (rbits + 1) / 2);
+        while (f1bits < rbits && !l2_fits(rbits - f1bits, 0)) f1bits++;
+        c->seg_ok = true;
+        if (!l1_fits(rbits - f1bits)) {
+            const int half = p2f_threads_w(c->W) / 2;
+            f1bits = std::min(10, (rbits + 1) / 2);
+            while (f1bits > 0 && !l1_fits(rbits - f1bits)) f1bits--;
+            if (c->W <= 2 || !l1_fits(rbits - f1bits) || !l2_fits(rbits - f1bits, half)) {
+                // beyond the segmented levels (wide keys in a multi-G-slot table, e.g. C5 on one
+                // GPU): the exact layout, whose 256-thread levels hold smaller tiles
+                const size_t tile = (size_t)COUNT_THREADS * run_width(c->W) * 8 * c->W + 16;
+                auto fits_x = [&](uint64_t bins) { return bins * 32 + tile <= LDS_BYTES; };
+                f1bits = 0;
+                while (f1bits <= rbits && !(fits_x(f1_of(rbits - f1bits)) && fits_x(1ULL << (rbits - f1bits)))) f1bits++;
+                if (f1bits > rbits) return c->fail(KC_ERR_ARG, "table too large for the partition levels");
+                c->seg_ok = false;
+            }
+        }
         c->f2bits = rbits - f1bits;
         c->F2 = 1u << c->f2bits;
-        c->F1 = (uint32_t)((regions + c->F2 - 1) / c->F2);
+        c->F1 = f1_of(c->f2bits);
     }
     c->R = (uint64_t)c->F1 * c->F2;
     if (c->R >= (1ULL << 32)) return c->fail(KC_ERR_ARG, "table too large");  // 32-bit region index (kc_common.h)
@@ -374,6 +403,7 @@ static int ensure_part_geo(kc_ctx* c, uint64_t syms, bool seg, const PartGeo& g,
 }
 // the table's levels
 static int ensure_part(kc_ctx* c, uint64_t syms, bool seg, uint32_t bins1 = 0) {
+    seg = seg && c->seg_ok;
     return ensure_part_geo(c, syms, seg, table_geo(c), c->pb, c->pb_cap, bins1);
 }
 

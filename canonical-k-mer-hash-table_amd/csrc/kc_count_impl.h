@@ -1202,7 +1202,7 @@ constexpr size_t p2f_smem(uint32_t F, uint32_t nseg_max) { return part_smem<W, N
 // IS: u64 words per level-1 item (W, or the whole table key of a kept level-1 output when
 // the Bloom pass reads only its word 0)
 template <int W, int NT, int IS = W>
-__global__ __launch_bounds__(NT, 2048 / NT) void k_p2f(TableView tv, PartBufs pb, DevCounters* __restrict__ ctr,
+__global__ __launch_bounds__(NT, (2048 / NT > 8 ? 8 : 2048 / NT)) void k_p2f(TableView tv, PartBufs pb, DevCounters* __restrict__ ctr,
                                                           int REC) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int RUNW = run_w<W>(), TW = NT * RUNW;
@@ -2195,6 +2195,26 @@ static hipError_t insert_spill(TableView t, BloomView bf, DevCounters* ctr, Part
     return part_levels23<W, true, GATE>(t, ctr, pb, s, nullptr, 0, bf);
 }
 
+// Segmented level 2 of the table's geometry t: the default workgroup, or half of it when the
+// F2 bins' arrays do not fit beside the full tile (wide keys in big tables, e.g. C5: k = 127,
+// a 1.25 G-slot share; kc_api.cpp alloc_table picks F2 for it)
+template <int W>
+static hipError_t launch_p2f(TableView t, PartBufs pb, DevCounters* ctr, int rec, hipStream_t s, uint32_t pad = 0) {
+    constexpr int NT = p2f_threads<W>(), NH = NT / 2;
+    const uint32_t nseg = std::max<uint32_t>(pad, (pb.nblk1 + pb.B2 - 1) / pb.B2);
+    hipError_t e;
+    const size_t sm = p2f_smem<W, NT>(t.F2, nseg);
+    if (sm <= LDS_BYTES || W <= 2) {
+        if ((e = set_smem(k_p2f<W, NT>, sm)) != hipSuccess) return e;
+        hipLaunchKernelGGL((k_p2f<W, NT>), dim3(t.F1 * pb.B2), dim3(NT), sm, s, t, pb, ctr, rec);
+    } else {
+        const size_t smh = p2f_smem<W, NH>(t.F2, nseg);
+        if ((e = set_smem(k_p2f<W, NH>, smh)) != hipSuccess) return e;
+        hipLaunchKernelGGL((k_p2f<W, NH>), dim3(t.F1 * pb.B2), dim3(NH), smh, s, t, pb, ctr, rec);
+    }
+    return hipGetLastError();
+}
+
 // batch bookkeeping of the skew lists: begin = clear the batch's flag and list counts,
 // end = add the lists' lengths to the job totals
 static __global__ void k_batch_begin(DevCounters* ctr) {
@@ -2231,16 +2251,13 @@ static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf
         const char* v = std::getenv("KC_P2F_SEGS");
         return v ? (uint32_t)std::atoi(v) : 0u;
     }();
-    const size_t sm1 = part_smem<W, scatter_threads<W>()>(t.F1) + heavy_smem<W>(),
-                 sm2 = p2f_smem<W, p2f_threads<W>()>(t.F2, std::max<uint32_t>(p2f_pad, (pb.nblk1 + pb.B2 - 1) / pb.B2));
+    const size_t sm1 = part_smem<W, scatter_threads<W>()>(t.F1) + heavy_smem<W>();
     if ((e = set_smem(k1, sm1)) != hipSuccess) return e;
-    if ((e = set_smem(k_p2f<W, p2f_threads<W>()>, sm2)) != hipSuccess) return e;
     const OutSeg o1{(uint64_t)pb.nblk1 * pb.cap1, 0, pb.cap1, pb.spill, pb.spill_cap, &ctr->spill_n,
                     &ctr->part_overflow, 1};
     hipLaunchKernelGGL(k1, dim3(pb.nblk1), dim3(scatter_threads<W>()), sm1, s, sym, k, bf, ctr, pb, t.F1, coarse_bins(t),
                        pb.keys1, pk, pkm1, o1, (const unsigned long long*)nullptr, 1);
-    hipLaunchKernelGGL((k_p2f<W, p2f_threads<W>()>), dim3(t.F1 * pb.B2), dim3(p2f_threads<W>()), sm2, s, t, pb, ctr,
-                       1);
+    if ((e = launch_p2f<W>(t, pb, ctr, 1, s, p2f_pad)) != hipSuccess) return e;
     if ((e = launch_p3<W, true, false, GATE3>(t, ctr, pb, nullptr, fresh, s, bf)) != hipSuccess) return e;
     }
     if (!(phase & PH_TAIL)) return hipGetLastError();
@@ -2357,10 +2374,7 @@ static hipError_t count_reuse_w(TableView t, BloomView bf, DevCounters* ctr, Par
     hipError_t e;
     hipLaunchKernelGGL(k_batch_begin, dim3(1), dim3(1), 0, s, ctr);
     if (level < 2) {
-        constexpr int NT = p2f_threads<W>();
-        const size_t sm2 = p2f_smem<W, NT>(t.F2, (pb.nblk1 + pb.B2 - 1) / pb.B2);
-        if ((e = set_smem(k_p2f<W, NT>, sm2)) != hipSuccess) return e;
-        hipLaunchKernelGGL((k_p2f<W, NT>), dim3(t.F1 * pb.B2), dim3(NT), sm2, s, t, pb, ctr, 1);
+        if ((e = launch_p2f<W>(t, pb, ctr, 1, s)) != hipSuccess) return e;
     }
     if ((e = launch_p3<W, true, false, GATE>(t, ctr, pb, nullptr, fresh, s, bf)) != hipSuccess) return e;
     // (from level 2 nothing can reach the skew list: no level of this pass scatters)

@@ -155,9 +155,12 @@ constexpr int p2f_threads_w(int W) { return KC_P2F_NT ? KC_P2F_NT : (W <= 2 ? 10
 constexpr size_t p1_lds_bytes(int W, uint32_t F1) {
     return (size_t)F1 * 32 + 16 + (size_t)scatter_threads_w(W) * run_width(W) * 8 * W + (size_t)64 * (W + 1) * 8;
 }
-constexpr size_t p2f_lds_bytes(int W, uint32_t F2, uint32_t nseg) {
-    return (size_t)F2 * 32 + 16 + (size_t)p2f_threads_w(W) * run_width(W) * 8 * W + ((size_t)nseg + 1) * 4;
+// nt: the level-2 workgroup (0 = p2f_threads_w; wide keys fall back to half of it when their
+// table's F2 does not fit beside the full tile, k_count_impl.h launch_p2f)
+constexpr size_t p2f_lds_bytes(int W, uint32_t F2, uint32_t nseg, int nt = 0) {
+    return (size_t)F2 * 32 + 16 + (size_t)(nt ? nt : p2f_threads_w(W)) * run_width(W) * 8 * W + ((size_t)nseg + 1) * 4;
 }
+constexpr size_t LDS_BYTES = 160 * 1024;  // per CU (one workgroup may take all of it)
 
 // ---- launchers (kc_tokenize.hip, kc_count.hip) -------------------------------------------------
 // src: bytes the chunk descriptors' src_off point into (host stage or device image)

@@ -542,3 +542,24 @@ def test_skewed_input_uses_the_skew_lists(case, seg, golden_input, tmp_path, mon
     assert st["heavy_records"] > 0 or st["part_fallbacks"] > 0  # the homopolymer reads (a redone batch: none)
     if seg == "tiny":
         assert st["spilled"] > 0
+
+
+@pytest.mark.parametrize("k", [51, 127])
+def test_big_table_geometry(tmp_path, k):
+    """Tables of the strong presets' size (-s 1.25e9 per GPU: the C4 / C5 shares) choose
+    partition geometries whose level-1 and level-2 LDS arrays fit (wide keys: more regions per
+    coarse bin, level 2 at half its workgroup); a small input through the device path gives
+    the oracle's counts."""
+    torch = pytest.importorskip("torch")
+    fa = tmp_path / "r.fasta"
+    subprocess.run([GEN, str(fa), "20000", "300", "100000"], check=True)
+    data = open(fa, "rb").read()
+    img = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+    with ka.KmerCounter(ka.Config(k=k, mode=2, min_abundance=1, table_slots=1_250_000_000)) as kc:
+        kc.count_device(img.data_ptr(), ka.plan_chunks(data, k, ka.FMT_FASTA), ka.FMT_FASTA)
+        st = kc.finish()
+        assert st["part_fallbacks"] == 0
+        lines = kc.lines()
+    out = tmp_path / "oracle.txt"
+    oracle_count(str(fa), k, ["-m", "2", "-a", "1"], out)
+    assert sorted_digest_lines(lines) == sorted_digest_file(out)
