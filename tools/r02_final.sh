@@ -1,11 +1,9 @@
 # round-2 final measurement call: GPU tests, smoke, the default bench line (C2 + c3 + CPU
-# baselines + compact), the skewed and strong-share presets, a kernel trace of the default bench
+# baselines + compact), the skewed preset, a kernel trace of the default bench
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > gpurun_out/f_tests.txt 2>&1 || exit 1
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/f_smoke.txt 2>&1 || exit 1
 timeout -k 10 600 python bench.py > gpurun_out/f_bench.json 2> gpurun_out/f_bench.err || exit 1
-for c in C2S C4 C5; do
-  timeout -k 10 300 python bench.py --config $c --no-cpu-baseline --no-compact > gpurun_out/f_bench_$c.json 2>> gpurun_out/f_bench.err || exit 1
-done
+timeout -k 10 300 python bench.py --config C2S --no-cpu-baseline --no-compact > gpurun_out/f_bench_C2S.json 2>> gpurun_out/f_bench.err || exit 1
 bash tools/gpu_prof.sh r02final --no-compact
