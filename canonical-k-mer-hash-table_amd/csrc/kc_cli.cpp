@@ -207,7 +207,12 @@ uint8_t* upload_image(int fd, const uint8_t* host, uint64_t size, int device, un
     if (hipMemGetInfo(&fr, &tot) != hipSuccess || size > fr / 4) return nullptr;  // room for the passes
     uint8_t* d = nullptr;
     if (hipMalloc(&d, size) != hipSuccess) return nullptr;
-    constexpr uint64_t SLICE = 32ull << 20;
+    // pinned staging per reader: two slices (KC_CLI_SLICE_MB, default 8 MiB).  Each reader's
+    // stream and page-locked slices cost more than its reads on a page-cached file: two readers
+    // of 8 MiB slices upload C2's 1 M-read sample in the least time (16 readers of 32 MiB took
+    // 2.5x as long; profiles/r02_v11_cli_upload.txt; KC_CLI_READERS overrides)
+    const char* sv = std::getenv("KC_CLI_SLICE_MB");
+    const uint64_t SLICE = (uint64_t)std::max(1, sv ? std::atoi(sv) : 8) << 20;
     const uint64_t nslices = (size + SLICE - 1) / SLICE;
     threads = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(threads, nslices));
     std::atomic<uint64_t> next{0};
@@ -386,7 +391,9 @@ int main(int argc, char** argv) {
     // (kc_api.h, partition reuse).  Its read is timed with the pass that needs it first,
     // as the reference's reader thread is.
     const bool host_path = std::getenv("KC_CLI_HOST") && std::atoi(std::getenv("KC_CLI_HOST")) != 0;
-    const unsigned readers = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const char* rv = std::getenv("KC_CLI_READERS");
+    const unsigned readers = rv ? (unsigned)std::max(1, std::atoi(rv))
+                                : std::max(1u, std::min(2u, std::thread::hardware_concurrency()));
     uint8_t* d_img = nullptr;
     auto load = [&]() {
         if (!host_path && !d_img) d_img = upload_image(gz ? -1 : fd, image, isize, a.device, readers);
