@@ -270,6 +270,8 @@ def run_workload(args, env, image=None):
     counter.profile(True)
     counter.timing()  # drop warmup events
     if dist:
+        counter.xstats = {key: 0 for key in counter.xstats}
+    if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -282,6 +284,16 @@ def run_workload(args, env, image=None):
     elapsed = t1 - t0
     counter.profile(False)
     tm = counter.timing()
+    xgmi = None
+    if dist and world > 1:  # the merge's exchange, per rank and step, beside the HBM figures
+        xs = counter.xstats
+        t = torch.tensor([xs["bytes_sent"], xs["exchange_s"]], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        sent, xsec = float(t[0].item()), float(t[1].item())
+        xgmi = {"sent_bytes_per_step_per_rank": int(sent / args.steps),
+                "exchange_ms_per_step": round(xsec / args.steps * 1e3, 3),
+                "gbs_per_rank": round(sent / max(xsec, 1e-9) / 1e9, 2), "peak_gbs_per_gpu": 7 * 153,
+                "note": "max over ranks; the all-to-all of {key, count} records incl. its count/sum headers"}
     st = counter.finish()  # raises on table overflow
     compact = None
     if not dist and args.compact:  # the Kaarme slot words built from this table
@@ -372,6 +384,8 @@ def run_workload(args, env, image=None):
     }
     if compact:
         out["compact"] = compact
+    if xgmi:
+        out["xgmi"] = xgmi
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args)
     return out, image

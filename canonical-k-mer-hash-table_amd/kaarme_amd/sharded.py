@@ -327,6 +327,8 @@ class ShardedCounter:
         self._pending = False
         self._stream = 0
         self._inflight = []
+        # exchange traffic of the merges (xGMI bytes reported beside HBM bytes)
+        self.xstats = {"bytes_sent": 0, "bytes_recv": 0, "exchange_s": 0.0, "merges": 0}
 
     # the counting pass over a device image (chunks from kaarme_amd.plan_chunks): local
     def count_device(self, dev_ptr: int, chunks: List[Tuple[int, int, int]], fmt: int, stream: int = 0):
@@ -341,7 +343,15 @@ class ShardedCounter:
         # the records hold the local counts now: a later merge must route only what is
         # counted after this one
         self.engine.clear_local()
+        import time
+
+        t0 = time.perf_counter()
         recv, n, per_rank = exchange(self.dist, recs, counts, self.W + 1, self.group, with_counts=True)
+        rec_bytes = (self.W + 1) * 8
+        self.xstats["bytes_sent"] += sum(c for d, c in enumerate(counts) if d != self.rank) * rec_bytes
+        self.xstats["bytes_recv"] += sum(c for d, c in enumerate(per_rank) if d != self.rank) * rec_bytes
+        self.xstats["exchange_s"] += time.perf_counter() - t0  # (route synced before, the sums check after)
+        self.xstats["merges"] += 1
         self.engine.insert_counts(recv, n, stream, group_counts=per_rank)
         self._inflight = [recv]  # the receive buffer must outlive the insert
         self._pending = False
