@@ -249,11 +249,14 @@ def test_counts_sum_to_windows_at_scale(insert_path):
                                          ("long.fasta", 127, ["-a", "1", "-s", "1000000"]),
                                          ("long.fasta", 200, ["-a", "1", "-s", "1000000"])])
 @pytest.mark.parametrize("spill", ["list", "full"])
-def test_segment_overflow_spills_or_falls_back(name, k, args, spill, golden_input, tmp_path, monkeypatch):
+@pytest.mark.parametrize("src", ["host", "device"])
+def test_segment_overflow_spills_or_falls_back(name, k, args, spill, src, golden_input, tmp_path, monkeypatch):
     """Tiny forced segment capacities overflow.  spill=list: the keys past a segment's end
     go to the spill list and are inserted through the exact levels after level 3;
     spill=full: the spill list is too small too, so the device redoes the whole batch on
-    the exact layout (behind the overflow gate).  Either way the result is the reference's."""
+    the exact layout (behind the overflow gate).  Either way the result is the reference's.
+    src=device: a device image, whose batch tail the host launches after reading the
+    overflow flag and the skew-list length (kc_api.cpp tail_needed)."""
     monkeypatch.setenv("KC_INSERT_PATH", "partitioned")
     monkeypatch.setenv("KC_SEG_CAP", "8")
     monkeypatch.setenv("KC_SPILL_CAP", "64" if spill == "full" else str(1 << 24))
@@ -263,8 +266,14 @@ def test_segment_overflow_spills_or_falls_back(name, k, args, spill, golden_inpu
                     batch_bytes=64 << 20)
     data = open(path, "rb").read()
     with ka.KmerCounter(cfg) as kc:
-        for off, ln, bh in ka.plan_chunks(data, k, ka.FMT_FASTA):
-            kc.count_chunk(data[off:off + ln], ka.FMT_FASTA, bool(bh))
+        chunks = ka.plan_chunks(data, k, ka.FMT_FASTA)
+        if src == "device":
+            import torch
+            img = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+            kc.count_device(img.data_ptr(), chunks, ka.FMT_FASTA)
+        else:
+            for off, ln, bh in chunks:
+                kc.count_chunk(data[off:off + ln], ka.FMT_FASTA, bool(bh))
         st = kc.finish()
         if spill == "full":
             assert st["part_fallbacks"] >= 1
@@ -461,16 +470,30 @@ def test_level1_reuse_declined_on_skewed_input(case, golden_input):
 
 
 @pytest.mark.parametrize("spill", ["list", "full"])
-def test_bloom_segment_overflow_spills_or_falls_back(spill, golden_input, tmp_path, monkeypatch):
+@pytest.mark.parametrize("src", ["host", "device"])
+def test_bloom_segment_overflow_spills_or_falls_back(spill, src, golden_input, tmp_path, monkeypatch):
     """Forced tiny segments in the partitioned Bloom pass and the gated count pass: spilled
     keys go through the exact levels (spill=list), or both passes are redone on the exact
-    layout (spill=full); the result is still the reference's."""
+    layout (spill=full); the result is still the reference's (src=device: host-launched
+    batch tails, and no partition reuse after a spill)."""
     monkeypatch.setenv("KC_INSERT_PATH", "partitioned")
     monkeypatch.setenv("KC_SEG_CAP", "8")
     monkeypatch.setenv("KC_SPILL_CAP", "64" if spill == "full" else str(1 << 24))
     path = golden_input("reads_w60.fasta")
     args = ["-b", "-u", "200000", "-a", "2"]
-    kc, st = ka.count_file(path, 31, min_abundance=2, bf_enable=True, est_unique=200000, fpr=0.01)
+    if src == "device":
+        import torch
+        data = open(path, "rb").read()
+        img = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+        chunks = ka.plan_chunks(data, 31, ka.FMT_FASTA)
+        kc = ka.KmerCounter(ka.Config(k=31, min_abundance=2, bf_enable=True, est_unique=200000, fpr=0.01))
+        kc.bloom_device(img.data_ptr(), chunks, ka.FMT_FASTA)
+        kc.bloom_finalize()
+        kc.count_device(img.data_ptr(), chunks, ka.FMT_FASTA)
+        st = kc.finish()
+        assert st["reused_passes"] == 0
+    else:
+        kc, st = ka.count_file(path, 31, min_abundance=2, bf_enable=True, est_unique=200000, fpr=0.01)
     with kc:
         if spill == "full":
             assert st["part_fallbacks"] >= 2
