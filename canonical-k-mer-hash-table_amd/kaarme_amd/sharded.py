@@ -79,11 +79,15 @@ def exchange(dist, keys, counts: Sequence[int], W: int, group=None, chunk_words:
         return (keys, int(counts[0]), [int(counts[0])]) if with_counts else (keys, int(counts[0]))
     sw = [int(c) * W for c in counts]
     so = [sum(sw[:d]) for d in range(world)]
-    head = [int(c) for c in counts]
-    if verify:  # wrapping int64 sums: the same on both sides for the same words
-        head += [int(keys[so[d]: so[d] + sw[d]].sum()) if sw[d] else 0 for d in range(world)]
-    send_head = torch.tensor(head, dtype=torch.int64, device=dev).view(-1 if not verify else 2, world)
-    send_head = send_head.t().contiguous().view(-1)  # [count_d, sum_d] per destination d
+
+    def group_sums(t, offs, lens):  # wrapping int64 sums: equal on both sides for equal words
+        return torch.stack([t[o: o + n].sum() if n else t.new_zeros(()) for o, n in zip(offs, lens)])
+
+    # the header per destination d: [count_d] or [count_d, sum of group d]
+    send_head = torch.tensor([int(c) for c in counts], dtype=torch.int64, device=dev).view(world, 1)
+    if verify:
+        send_head = torch.cat([send_head, group_sums(keys, so, sw).view(world, 1)], dim=1)
+    send_head = send_head.contiguous().view(-1)
     recv_head = torch.empty_like(send_head)
     dist.all_to_all_single(recv_head, send_head, group=group)
     rh = recv_head.view(world, -1).cpu().tolist()
@@ -113,11 +117,11 @@ def exchange(dist, keys, counts: Sequence[int], W: int, group=None, chunk_words:
                     out[ro[d] + lo: ro[d] + lo + rin[d]].copy_(got[pos: pos + rin[d]])
                 pos += rin[d]
     if verify:
+        got = group_sums(out, ro, rw).tolist()
         for s in range(world):
-            got_sum = int(out[ro[s]: ro[s] + rw[s]].sum()) if rw[s] else 0
-            if got_sum != int(rh[s][1]):
+            if got[s] != int(rh[s][1]):
                 raise RuntimeError(f"all-to-all delivered corrupt data from rank {s}: {rw[s]} words, "
-                                   f"sum {got_sum} != the sender's {int(rh[s][1])} ({rounds} round(s) of "
+                                   f"sum {got[s]} != the sender's {int(rh[s][1])} ({rounds} round(s) of "
                                    f"<= {chunk_words} words per peer)")
     return (out, total, recv) if with_counts else (out, total)
 
