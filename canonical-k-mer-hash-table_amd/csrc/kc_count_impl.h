@@ -494,11 +494,15 @@ struct BinRegion {  // level-1 bin (coarse: region >> f2bits) or level-2 bin (re
         return coarse ? r >> f2bits : r & mask;
     }
 };
+// level 1 always takes coarse bins: a copy with the mode known at compile time spares the
+// select between both bin formulas in every bin computation of k_p1 (three per key)
+DEV BinRegion level1_bins(const BinRegion& b) { return BinRegion{b.R, b.f2bits, b.mask, 1}; }
 struct BinOwner {
     static constexpr bool kOwner = true;
     uint32_t parts;
     DEV uint32_t operator()(uint64_t t0) const { return owner_of(t0, parts); }
 };
+DEV BinOwner level1_bins(const BinOwner& b) { return b; }
 
 // Where a scatter pass writes bin b.  Exact layout: one contiguous run per bin at offsets
 // from a histogram pass + scan.  Segmented layout (single pass, no histogram): a
@@ -874,10 +878,11 @@ constexpr int p1_out_words(int W, int MODE) { return MODE == 3 ? 1 : W; }
 // the histogram pass of a fallback, whose windows the segmented pass counted already).
 template <int W, int MODE, bool SCATTER, class Bin, class Out, int NT = COUNT_THREADS>
 __global__ __launch_bounds__(NT, 4) void k_p1(PackedView sv, int k, BloomView bf,
-                                                      DevCounters* __restrict__ ctr, PartBufs pb, uint32_t F, Bin bin,
+                                                      DevCounters* __restrict__ ctr, PartBufs pb, uint32_t F, Bin bin_arg,
                                                       uint64_t* __restrict__ out, uint64_t pow5_k, uint64_t pow5_km1,
                                                       Out o, const unsigned long long* gate, int count) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const Bin bin = level1_bins(bin_arg);
     constexpr int RUNW = run_w<W>(), TW = NT * RUNW;
     constexpr bool COUNTS = !SCATTER || Out::kSeg;
     constexpr bool ROLLED = MODE == 2;       // gate on the rolled root (reference layout)
