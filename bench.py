@@ -236,9 +236,20 @@ def run_workload(args, env, image=None):
     del host
     if args.batch_mib:
         cap = args.batch_mib << 20
-    else:  # as large as HBM allows (kc_api.cpp: ~28 W + 4 bytes of partition buffers per staged byte)
+    else:
+        # as large as HBM allows beside the table: kc_api.cpp ensure_part_geo keeps two level
+        # buffers of ~1.25 x 8W bytes per staged byte (segment slack) plus the skew list (an
+        # eighth of the windows as {W words, count} records), ~21 W + 3 bytes per staged byte.
+        # The table is 1.25 x -s slots in 128-byte buckets of 16 // (W + 1) slots (-b: sized
+        # from 2 x new_in_second, bounded here by 2 x -u).  The earlier table-blind rule
+        # (0.45 x free / (28 W + 4)) stays as a floor: every recorded configuration ran with it
+        # (C5 at full size takes the exact layout, whose buffers need less).  Batches stay
+        # within the 2 GiB measured on the device (C4 at full size: 2.06 GB).
         free, _ = torch.cuda.mem_get_info()
-        cap = int(0.45 * (free - nbytes)) // (28 * W + 4)
+        want = 1.25 * (slots if slots else 2 * (args.unique or 0))
+        table = int(want / (16 // (W + 1))) * 128
+        fit = int(0.85 * max(0, free - nbytes - table)) // (21 * W + 3)
+        cap = min(max(fit, int(0.45 * (free - nbytes)) // (28 * W + 4)), 1 << 31)
     batch = min((nbytes + len(chunks) * 4096 + (1 << 20)) // 4096 * 4096, cap // 4096 * 4096)
     windows_expected = N * (L - k + 1)
     tbl = " ".join(["-m", "2"] + table_args(slots, args.unique))

@@ -909,7 +909,10 @@ int kc_create(const kc_config* cfg, kc_ctx** out) {
                     while (f1 > 0 && p1_lds_bytes(c->W, 1u << f1) > p1_cap) f1--;
                     const uint32_t F2 = 1u << (fb - f1), F1 = 1u << f1;
                     const uint32_t B2 = std::max<uint32_t>(1, std::min<uint32_t>(64, 2048 / F1));
-                    if (p2f_lds_bytes(c->W, F2, 2048 / B2 + 1) <= 160 * 1024 &&
+                    // (budgeted at 32 bytes per level-2 bin, as before the scatter's bins
+                    // took 24: the finer bins that now fit, F2 = 1024 at C3's -u, measured
+                    // slower, 29.0 vs 31-32 G k-mers/s, profiles/r02_v15_bench.json)
+                    if (p2f_lds_bytes(c->W, F2, 2048 / B2 + 1) + (size_t)F2 * 8 <= 160 * 1024 &&
                         (1ULL << (fb - rbits)) * B2 <= MAX_SEG_GROUP)
                         break;
                 }

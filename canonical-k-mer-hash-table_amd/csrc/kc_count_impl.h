@@ -428,8 +428,8 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_count(PackedView sv, int k, T
 // --------------------------------------------------------------------------------
 // partitioned path
 // --------------------------------------------------------------------------------
-// LDS of a scatter pass: hist, start, lim, sp (u32 x F), gbase, dlt (u64 x F), then the keys
-constexpr size_t hist_smem(uint32_t F) { return (size_t)F * 32 + 16; }
+// LDS of a scatter pass: hist, start, lim, sp (u32 x F), gbase (u64 x F), then the keys
+constexpr size_t hist_smem(uint32_t F) { return bin_lds_bytes(F); }
 template <int W, int NT = COUNT_THREADS>
 constexpr size_t part_smem(uint32_t F) {
     return hist_smem(F) + (size_t)NT * run_w<W>() * 8 * W;
@@ -458,15 +458,16 @@ DEV void block_excl_scan_lds(const uint32_t* in, uint32_t* out, uint32_t n) {
 }
 
 // LDS of a scatter: per bin its tile count, its first tile slot, the tile slots that
-// fit its output (lim), the destination of its next key (gbase) and, for the write-out,
-// destination minus tile slot (dlt); then the tile's keys
+// fit its output (lim), the destination of its next key (gbase; during a tile's write-out
+// it holds destination minus tile slot, and the tile's end turns it back into the next
+// destination: 24 bytes per bin, which is what lets big tables keep wide bins at both
+// levels); then the tile's keys
 struct PartLds {
     uint32_t* hist;
     uint32_t* start;
     uint32_t* lim;
     uint32_t* sp;  // keys past the output's end: count, then offset in the tile's spill allocation
     uint64_t* gbase;
-    uint64_t* dlt;
     uint64_t* keys;
 };
 DEV PartLds part_lds(uint8_t* smem, uint32_t F) {
@@ -476,8 +477,7 @@ DEV PartLds part_lds(uint8_t* smem, uint32_t F) {
     l.lim = l.start + F;
     l.sp = l.lim + F;
     l.gbase = reinterpret_cast<uint64_t*>(l.sp + F);
-    l.dlt = l.gbase + F;
-    l.keys = l.dlt + F;
+    l.keys = l.gbase + F + (F & 1);  // 16-byte aligned
     return l;
 }
 
@@ -640,7 +640,7 @@ DEV bool scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const Out& o
         const uint32_t st = l.start[b], h = l.hist[b];
         const uint64_t g = l.gbase[b];
         const uint32_t fit = (uint32_t)min((uint64_t)h, o.room(b, g));
-        l.dlt[b] = g - st;
+        l.gbase[b] = g - st;  // destination minus tile slot (modulo 2^64) until the tile's end
         l.lim[b] = st + fit;
         l.sp[b] = h - fit;
         spills |= fit < h;
@@ -668,7 +668,7 @@ DEV bool scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const Out& o
         const uint32_t b = bin(key[0]);
         const uint32_t lim = l.lim[b];
         if (i < lim) {
-            const uint64_t dst = l.dlt[b] + i;
+            const uint64_t dst = l.gbase[b] + i;
 #pragma unroll
             for (int w = 0; w < W; w++) ks_store(out + dst * W + w, key[w]);
         } else if constexpr (Out::kSeg) {
@@ -686,7 +686,7 @@ DEV bool scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const Out& o
     if (KC_STAMP && stp) stp->mark(6);
     __syncthreads();
     for (uint32_t b = tid; b < F; b += NT) {
-        l.gbase[b] += l.lim[b] - l.start[b];  // the keys written (a segment's fill never passes its end)
+        l.gbase[b] += l.lim[b];  // past the keys written (a segment's fill never passes its end)
         l.hist[b] = 0;
     }
     __syncthreads();
@@ -2256,7 +2256,17 @@ static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf
         const char* v = std::getenv("KC_P2F_SEGS");
         return v ? (uint32_t)std::atoi(v) : 0u;
     }();
-    const size_t sm1 = part_smem<W, scatter_threads<W>()>(t.F1) + heavy_smem<W>();
+    // Short level-1 runs (fewer than 8 keys per bin and tile: big tables, C4 shares) leave
+    // partial 128-byte lines that L2 merges only while they stay resident: one workgroup per
+    // CU halves the open lines (C4 share: k_p1 writes 33 GB for 20 GB of keys; count
+    // 41.0 -> 40.15 ms; C2's 34-key runs lose 18 % that way, profiles/r02_v16_ab_p1_lds.txt)
+    static const long p1_lds_knob = [] {  // A/B knob: reserve at least this much LDS
+        const char* v = std::getenv("KC_P1_LDS_MIN");
+        return v ? std::atol(v) : -1L;
+    }();
+    const size_t p1_lds_min = p1_lds_knob >= 0 ? std::min(LDS_BYTES, (size_t)p1_lds_knob)
+                              : (size_t)p1_tile(W) < 8 * (size_t)t.F1 ? LDS_BYTES / 2 + 16 : 0;
+    const size_t sm1 = std::max(p1_lds_min, part_smem<W, scatter_threads<W>()>(t.F1) + heavy_smem<W>());
     if ((e = set_smem(k1, sm1)) != hipSuccess) return e;
     const OutSeg o1{(uint64_t)pb.nblk1 * pb.cap1, 0, pb.cap1, pb.spill, pb.spill_cap, &ctr->spill_n,
                     &ctr->part_overflow, 1};

@@ -150,15 +150,18 @@ constexpr int p1_tile(int W) { return scatter_threads_w(W) * run_width(W); }  //
 #ifndef KC_P2F_NT
 #define KC_P2F_NT 0  // 0: the default below
 #endif
+// a scatter's per-bin LDS arrays (k_count_impl.h PartLds: 4 x u32 + 1 x u64 per bin, the
+// tile's keys after them at a 16-byte boundary) and its static extras
+constexpr size_t bin_lds_bytes(uint32_t F) { return ((size_t)F * 24 + 15) / 16 * 16 + 16; }
 constexpr int p2f_threads_w(int W) { return KC_P2F_NT ? KC_P2F_NT : (W <= 2 ? 1024 : W <= 4 ? 512 : 256); }
 // segmented level 1 (k_p1, W-word output keys + the heavy table) for F1 coarse bins
 constexpr size_t p1_lds_bytes(int W, uint32_t F1) {
-    return (size_t)F1 * 32 + 16 + (size_t)scatter_threads_w(W) * run_width(W) * 8 * W + (size_t)64 * (W + 1) * 8;
+    return bin_lds_bytes(F1) + (size_t)scatter_threads_w(W) * run_width(W) * 8 * W + (size_t)64 * (W + 1) * 8;
 }
 // nt: the level-2 workgroup (0 = p2f_threads_w; wide keys fall back to half of it when their
 // table's F2 does not fit beside the full tile, k_count_impl.h launch_p2f)
 constexpr size_t p2f_lds_bytes(int W, uint32_t F2, uint32_t nseg, int nt = 0) {
-    return (size_t)F2 * 32 + 16 + (size_t)(nt ? nt : p2f_threads_w(W)) * run_width(W) * 8 * W + ((size_t)nseg + 1) * 4;
+    return bin_lds_bytes(F2) + (size_t)(nt ? nt : p2f_threads_w(W)) * run_width(W) * 8 * W + ((size_t)nseg + 1) * 4;
 }
 constexpr size_t LDS_BYTES = 160 * 1024;  // per CU (one workgroup may take all of it)
 
