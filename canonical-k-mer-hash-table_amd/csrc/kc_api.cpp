@@ -1520,25 +1520,28 @@ int kc_compact(kc_ctx* c, double load, kc_compact_info* info) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     const uint64_t nslots = std::max<uint64_t>(64, (uint64_t)std::ceil((double)occ / load));
     if (nslots >> 38) return c->fail(KC_ERR_ARG, "too many k-mers for 38-bit slot pointers");
-    uint64_t *src = nullptr, *second = nullptr;
+    uint64_t *src = nullptr, *second = nullptr, *inv = nullptr;
     if (!c->d_cstat && hipMalloc(&c->d_cstat, 4 * sizeof(unsigned long long)) != hipSuccess)
         return c->fail(KC_ERR_NOMEM, "compact counters");
     if (hipMalloc(&c->d_cwords, nslots * 8) != hipSuccess || hipMalloc(&src, nslots * 8) != hipSuccess ||
-        hipMalloc(&second, std::max<uint64_t>(1, occ) * c->W * 8) != hipSuccess) {
+        hipMalloc(&second, std::max<uint64_t>(1, occ) * c->W * 8) != hipSuccess ||
+        hipMalloc(&inv, c->nbuckets * c->S * 8) != hipSuccess) {
         hipFree(src);
         hipFree(second);
+        hipFree(inv);
         drop_compact(c);
         return c->fail(KC_ERR_NOMEM, "compact representation allocation failed");
     }
     HIPCHK(c, hipMemsetAsync(c->d_cwords, 0, nslots * 8, c->stream));
     HIPCHK(c, hipMemsetAsync(src, 0xFF, nslots * 8, c->stream));
     HIPCHK(c, hipMemsetAsync(c->d_cstat, 0, 4 * sizeof(unsigned long long), c->stream));
-    CompactView cv{c->d_cwords, nslots, src, second, c->d_cstat};
+    CompactView cv{c->d_cwords, nslots, src, second, c->d_cstat, inv};
     HIPCHK(c, launch_compact_build(tv, cv, c->cfg.k, c->stream));
     unsigned long long starts = 0;
     HIPCHK(c, hipMemcpyAsync(&starts, c->d_cstat, 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     hipFree(src);
+    hipFree(inv);
     // the secondary array at its size (the reference grows it as chains start, :2267-2278)
     if (hipMalloc(&c->d_csecond, std::max<uint64_t>(1, starts) * c->W * 8) != hipSuccess) {
         hipFree(second);

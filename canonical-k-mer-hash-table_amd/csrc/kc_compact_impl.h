@@ -120,23 +120,37 @@ __global__ __launch_bounds__(256) void k_cplace(TableView tv, CompactView cv) {
     while (atomicCAS(reinterpret_cast<unsigned long long*>(cv.words + p), 0ULL, (unsigned long long)word) != 0ULL)
         p = p + 1 == cv.nslots ? 0 : p + 1;
     cv.src[p] = g;
+    cv.inv[g] = p;
 }
 
-// compact slot holding table key tk, or CW_NONE (build: compares the full-table keys)
+// compact slot holding table key tk, or CW_NONE (build): the key is looked up in the
+// full-key table, whose probe sequence (the key's region, buckets from its start bucket,
+// kc_common.h) ends at the first bucket with a free slot, so a missing predecessor costs one
+// or two 128-byte bucket reads instead of a compact-array probe run at load 0.8 (each probe
+// comparing a random bucket's key); the found slot maps to its compact slot through inv.
 template <int W>
 DEV uint64_t cfind_built(const TableView& tv, const CompactView& cv, const uint64_t (&tk)[W]) {
     constexpr int S = BUCKET_WORDS / (W + 1);
-    uint64_t p = cslot_of(tk[0], cv.nslots);
-    while (true) {
-        const uint64_t g = cv.src[p];
-        if (g == CW_NONE) return CW_NONE;
-        const uint64_t* key = tv.buckets + (g / S) * BUCKET_WORDS + (g % S) * W;
-        bool eq = true;
+    const uint64_t region = region_of(tk[0], tv.R);
+    uint32_t b = bucket_in_region(tk[0], tv.R);
+    for (int probe = 0; probe < BPR; probe++) {
+        const uint64_t bucket = region * BPR + b;
+        const uint64_t* bk = tv.buckets + bucket * BUCKET_WORDS;
+        bool free = false;
 #pragma unroll
-        for (int i = 0; i < W; i++) eq &= key[i] == tk[i];
-        if (eq) return p;
-        p = p + 1 == cv.nslots ? 0 : p + 1;
+        for (int sl = 0; sl < S; sl++) {
+            const uint64_t w0 = bk[sl * W];
+            free |= w0 == EMPTY;
+            if (w0 != tk[0]) continue;
+            bool eq = true;
+#pragma unroll
+            for (int i = 1; i < W; i++) eq &= bk[sl * W + i] == tk[i];
+            if (eq) return cv.inv[bucket * S + sl];
+        }
+        if (free) return CW_NONE;
+        b = (b + 1) & (BPR - 1);
     }
+    return CW_NONE;
 }
 
 // k_clink: orientation, predecessor and flags of every compact slot; chain starts -> secondary

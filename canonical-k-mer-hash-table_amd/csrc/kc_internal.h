@@ -282,6 +282,7 @@ struct CompactView {
     uint64_t* src;                 // build only: full-table slot (bucket * S + s) per compact slot, ~0 = empty
     uint64_t* second;              // chain-start keys, W words each
     unsigned long long* n_second;  // chain starts written
+    uint64_t* inv;                 // build only: compact slot per full-table slot (written for occupied ones)
 };
 template <int W>
 struct CompactOps {
