@@ -101,6 +101,70 @@ DEV bool minimizer_forward(const uint64_t (&K)[W], int k, int m) {
     return ori;
 }
 inline int minimizer_len(int k) { return k >= 15 ? 15 : ((k & 1) ? k : k - 1); }
+// One scan of K's m-mers gives everything k_clink needs without rescanning each candidate
+// predecessor (k - m + 1 fmix64 per candidate: most of the link time at k = 127).
+// A candidate P = c + X[0..k-2] (X = K as its read shows it) has the m-mers of X at positions
+// 0..k-m-1 plus one new m-mer in front, so minimizer_forward(canonical(P)) follows from the
+// minimum over that range of X (and the orientation of its first and last occurrence: the
+// scan runs backwards on P's strand when P is not canonical) and the new m-mer's hash.  Hash
+// ~0 is never chosen and ties go to the first in scan order, exactly as minimizer_forward.
+struct MinRange {
+    uint64_t h = ~0ULL;  // smallest hash (~0: none)
+    bool first = true, last = true;  // forward flag of its first / last occurrence
+    DEV void add(uint64_t hh, bool f) {
+        if (hh < h) {
+            h = hh;
+            first = last = f;
+        } else if (hh == h && hh != ~0ULL) {
+            last = f;
+        }
+    }
+};
+struct MinScan {
+    bool ox;                // minimizer_forward(K)
+    MinRange lo, hi;        // K's m-mers at positions 0..k-m-1 and 1..k-m (K's strand)
+};
+template <int W>
+DEV MinScan minimizer_scan(const uint64_t (&K)[W], int k, int m) {
+    const uint64_t mask = (1ULL << (2 * m)) - 1;
+    uint64_t fw = 0, rv = 0, best = ~0ULL;
+    MinScan r;
+    r.ox = true;
+    for (int j = 0; j < k; j++) {
+        const uint32_t c = key_char<W>(K, k, j);
+        fw = ((fw << 2) | c) & mask;
+        rv = (rv >> 2) | ((uint64_t)(3 - c) << (2 * (m - 1)));
+        if (j >= m - 1) {
+            const int pos = j - (m - 1);
+            const bool f = fw < rv;
+            const uint64_t h = fmix64((f ? fw : rv) ^ 0x632BE59BD9B4E019ULL);
+            if (h < best) {
+                best = h;
+                r.ox = f;
+            }
+            if (pos < k - m) r.lo.add(h, f);
+            if (pos >= 1) r.hi.add(h, f);
+        }
+    }
+    return r;
+}
+// minimizer_forward(canonical(P)) == pc for P = c + X[0..k-2], pc = [P is canonical]:
+// xr = the m-mers of X at positions 0..k-m-1 on X's strand, X0 = X's first m - 1 characters
+DEV bool pred_reads_forward(const MinRange& xr, uint64_t x0, uint32_t c, int m, bool pc) {
+    const uint64_t mask = (1ULL << (2 * m)) - 1;
+    const uint64_t fw = (((uint64_t)c << (2 * (m - 1))) | x0) & mask;
+    uint64_t rv = 0;
+    for (int i = 0; i < m; i++) rv = (rv << 2) | (3 - ((fw >> (2 * i)) & 3));
+    const bool f0 = fw < rv;
+    const uint64_t h0 = fmix64((f0 ? fw : rv) ^ 0x632BE59BD9B4E019ULL);
+    bool ori;
+    if (pc) {  // scan on P's strand: the new m-mer comes first
+        ori = (h0 != ~0ULL && h0 <= xr.h) ? f0 : xr.h != ~0ULL ? xr.first : true;
+    } else {   // scan on the other strand: X's m-mers first (last occurrence first), flags flip
+        ori = (xr.h != ~0ULL && xr.h <= h0) ? !xr.last : h0 != ~0ULL ? !f0 : true;
+    }
+    return ori == pc;
+}
 
 DEV uint64_t cslot_of(uint64_t t0, uint64_t nslots) { return __umul64hi(t0, nslots); }
 
@@ -170,9 +234,21 @@ __global__ __launch_bounds__(256) void k_clink(TableView tv, CompactView cv, int
         from_tkey<W>(t, K);
         uint64_t rcK[W], X[W];
         revcomp<W>(K, rk, rcK);
-        const bool ox = minimizer_forward<W>(K, k, m);
+        const MinScan ms = minimizer_scan<W>(K, k, m);
+        const bool ox = ms.ox;
 #pragma unroll
         for (int i = 0; i < W; i++) X[i] = ox ? K[i] : rcK[i];  // X as its read shows it
+        // X's m-mers at positions 0..k-m-1 on X's strand: K's first k-m (ox) or, reversed and
+        // flipped, K's last k-m
+        MinRange xr = ms.lo;
+        if (!ox) {
+            xr = ms.hi;
+            const bool f = xr.first;
+            xr.first = !xr.last;
+            xr.last = !f;
+        }
+        uint64_t x0 = 0;  // X's first m - 1 characters
+        for (int j = 0; j < m - 1; j++) x0 = (x0 << 2) | key_char<W>(X, k, j);
         bool op = false;
         for (uint32_t c = 0; c < 4 && pred == CW_NONE; c++) {
             uint64_t P[W], rP[W], KP[W], tp[W];
@@ -180,7 +256,7 @@ __global__ __launch_bounds__(256) void k_clink(TableView tv, CompactView cv, int
             revcomp<W>(P, rk, rP);
             const bool pc = key_le<W>(P, rP);  // P as read is canonical
             canonical<W>(P, rP, KP);
-            if (minimizer_forward<W>(KP, k, m) != pc) continue;  // P reads the other way
+            if (!pred_reads_forward(xr, x0, c, m, pc)) continue;  // P reads the other way
             to_tkey<W>(KP, tp);
             pred = cfind_built<W>(tv, cv, tp);
             op = pc;
