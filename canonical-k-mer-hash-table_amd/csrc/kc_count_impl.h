@@ -1321,6 +1321,9 @@ constexpr int P3_THREADS = 1024;  // two 64 KiB regions per CU: 8 waves per SIMD
 #ifndef KC_P3_KB1
 #define KC_P3_KB1 4  // keys per thread per round, one-word keys
 #endif
+#ifndef KC_P3_KB2
+#define KC_P3_KB2 2  // two-word keys
+#endif
 template <int W, bool SEG, bool CNT, bool GATE = false>
 __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView tv, PartBufs pb,
                                                                   DevCounters* __restrict__ ctr,
@@ -1333,7 +1336,7 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
     constexpr int S = BUCKET_WORDS / (W + 1);
     // keys loaded per thread before inserting (memory-level parallelism); 1024-thread
     // groups already keep 8 waves per SIMD in flight
-    constexpr int KB = NT >= 1024 ? (W >= 2 || CNT ? 2 : KC_P3_KB1) : 8;  // (CNT items carry a count: 64 VGPRs)
+    constexpr int KB = NT >= 1024 ? (CNT || W > 2 ? 2 : W == 2 ? KC_P3_KB2 : KC_P3_KB1) : 8;  // (CNT items carry a count: 64 VGPRs)
     if constexpr (SEG) {
         if (ctr->part_overflow) return;
     } else {
