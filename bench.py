@@ -201,9 +201,35 @@ def same_image(a, b):
                                                                            pb.get("skew"))
 
 
-def run_workload(args, env, image=None):
-    """Times one workload (warmup + steps of a full counting job) and returns its JSON record
-    plus the device image (reusable by a workload with the same generator parameters)."""
+FIXTURES = os.path.join(REPO, "tests", "golden", "fullsize.json")
+
+
+def fixture_case(args):
+    """The tests/golden/fullsize.json case (reference output digest, tests/golden/make_fullsize.py)
+    whose input and options are this workload's at one GPU, or None."""
+    try:
+        with open(FIXTURES) as f:
+            doc = json.load(f)
+    except (OSError, ValueError):
+        return None
+    preset = PRESETS[args.config]
+    for name, c in doc.get("cases", {}).items():
+        inp = doc["inputs"][c["input"]]
+        skew = inp.get("skew")
+        same_in = ((inp["reads"], inp["read_len"], inp["genome"], inp["seed"], inp["err"]) ==
+                   (args.reads, args.read_len, args.genome, args.seed, args.err)
+                   and (list(skew) if skew else None) == (list(preset["skew"]) if preset.get("skew") else None))
+        a = c["args"]
+        opt = table_args(args.slots, args.unique)
+        if same_in and c["k"] == args.k and a[:2] == ["-m", "2"] and a[2:-2] == opt:
+            return dict(c, name=name, min_abundance=int(a[-1]), input_sha256=inp["sha256"])
+    return None
+
+
+def setup_job(args, env, image=None):
+    """The counting job one bench step runs: the device image (generated in HBM unless given),
+    the reference chunk table, the counter with the bench's table and staging geometry, and
+    step() = one full counting job.  tests/test_gpu_fullsize.py runs the same object."""
     torch, ka, lib, dist = env["torch"], env["ka"], env["lib"], env["dist"]
     rank, world, local = env["rank"], env["world"], env["local"]
     preset = PRESETS[args.config]
@@ -258,8 +284,11 @@ def run_workload(args, env, image=None):
     if sk:
         workload += (f", skew: {sk[0]:.0%} poly-A/T reads, {sk[1]:.0%} (CA)n reads, a {sk[2]}-bp repeat x "
                      f"{sk[3]} in the genome")
-    cfg = ka.Config(k=k, mode=2, table_slots=slots, min_abundance=2, batch_bytes=batch, device=local,
-                    bf_enable=bool(args.unique), est_unique=args.unique)
+    # -a only selects output lines (it does not change counting): the reference fixture's -a when
+    # this workload has one, so the parity digest covers the same lines
+    fx = fixture_case(args) if world == 1 and not dist else None
+    cfg = ka.Config(k=k, mode=2, table_slots=slots, min_abundance=fx["min_abundance"] if fx else 2, batch_bytes=batch,
+                    device=local, bf_enable=bool(args.unique), est_unique=args.unique)
     if dist:
         from kaarme_amd.sharded import ShardedCounter
         # strong presets: a rank's local table must hold its own input's distinct k-mers,
@@ -276,6 +305,37 @@ def run_workload(args, env, image=None):
         counter.count_device(image.data_ptr(), chunks, ka.FMT_FASTA, stream.cuda_stream)
         counter.sync()
 
+    return argparse.Namespace(counter=counter, image=image, chunks=chunks, step=step, N=N, first=first, nbytes=nbytes,
+                              slots=slots, strong=strong, windows_expected=windows_expected, tbl=tbl,
+                              workload=workload, fixture=fx, stream=stream)
+
+
+def parity_record(job, k):
+    """The timed job's output against the reference's (tests/golden/fullsize.json): SHA-256 of the
+    sorted output text from kc_dump, line count, sum of counts; after the timed steps."""
+    fx = job.fixture
+    if fx is None:
+        return None
+    from kaarme_amd.digest import sorted_text_digest
+    t0 = time.perf_counter()
+    got = sorted_text_digest(job.counter.dump(), k)
+    ok = (got["sorted_sha256"], got["lines"], got["count_sum"]) == (fx["sorted_sha256"], fx["lines"], fx["count_sum"])
+    return {"reference_case": f"tests/golden/fullsize.json {fx['name']}: oracle/_ref/kaarme "
+                              f"{' '.join(fx['args'])} on the same input", "match": ok,
+            "sorted_sha256": got["sorted_sha256"], "lines": got["lines"], "count_sum": got["count_sum"],
+            "digest_s": round(time.perf_counter() - t0, 2)}
+
+
+def run_workload(args, env, image=None):
+    """Times one workload (warmup + steps of a full counting job) and returns its JSON record
+    plus the device image (reusable by a workload with the same generator parameters)."""
+    torch, ka, dist = env["torch"], env["ka"], env["dist"]
+    rank, world = env["rank"], env["world"]
+    job = setup_job(args, env, image)
+    counter, image, chunks, step = job.counter, job.image, job.chunks, job.step
+    N, nbytes, strong, workload, tbl = job.N, job.nbytes, job.strong, job.workload, job.tbl
+    windows_expected = job.windows_expected
+    L, k = args.read_len, args.k
     for _ in range(args.warmup):
         step()
     counter.profile(True)
@@ -306,6 +366,7 @@ def run_workload(args, env, image=None):
                 "gbs_per_rank": round(sent / max(xsec, 1e-9) / 1e9, 2), "peak_gbs_per_gpu": 7 * 153,
                 "note": "max over ranks; the all-to-all of {key, count} records incl. its count/sum headers"}
     st = counter.finish()  # raises on table overflow
+    parity = parity_record(job, k) if args.verify else None
     compact = None
     if not dist and args.compact:  # the Kaarme slot words built from this table
         torch.cuda.synchronize()
@@ -393,6 +454,8 @@ def run_workload(args, env, image=None):
                        "batches_redone": st["part_fallbacks"]},
         "cpu_baseline": None,
     }
+    if parity:
+        out["parity"] = parity
     if compact:
         out["compact"] = compact
     if xgmi:
@@ -426,6 +489,8 @@ def main():
                     help="at N=1 with the default C2: also time this workload (the north star's k=51 Bloom "
                          "config) and attach it as a second record ('none' = skip)")
     ap.add_argument("--secondary-cpu-sample-bases", type=int, default=50_000_000)
+    ap.add_argument("--no-verify", dest="verify", action="store_false",
+                    help="skip the parity digest against the reference's output (tests/golden/fullsize.json)")
     ap.add_argument("--force-sharded", action="store_true",
                     help="use the sharded (RCCL) path even at one rank (testing)")
     args = ap.parse_args()
@@ -463,7 +528,7 @@ def main():
         out[sec.config.lower()] = {key: rec[key] for key in ("value", "unit", "ms_per_step", "config", "roofline",
                                                             "kernel_ms", "windows_per_step_per_gpu",
                                                             "distinct_per_gpu", "table_slots", "cpu_baseline",
-                                                            "compact") if key in rec}
+                                                            "parity", "compact") if key in rec}
     del image
     if rank == 0:
         print(json.dumps(out), file=json_out, flush=True)

@@ -143,6 +143,7 @@ struct kc_ctx {
     TableView fgeo{};                     // the kept partitions' fine geometry (powers of two)
     int reuse_level = 0;                  // kc_bloom_finalize: 2 = from level 2, 1 = from level 1
     uint64_t reuse_hits = 0;          // counting passes that reused (kc_stats.reused_passes)
+    int reuse_last_level = 0;         // the level the last reused pass started from (kc_stats.reuse_level)
 
     uint64_t n_chunks = 0, n_bytes = 0;
 
@@ -708,6 +709,7 @@ static int count_reused(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, s
     c->n_chunks += b.size();
     c->n_bytes += bytes;
     c->reuse_hits++;
+    c->reuse_last_level = c->reuse_level;
     if (c->profiling) {
         c->ev_pending.push_back(ev);
         c->pending_symbols_bound.push_back(syms);
@@ -1350,6 +1352,7 @@ int kc_finish(kc_ctx* c, kc_stats* st) {
         st->spilled = h.spilled;
         st->heavy_records = h.heavy;
         st->reused_passes = c->reuse_hits;
+        st->reuse_level = (uint64_t)c->reuse_last_level;
         st->bytes = c->n_bytes;
         // occupied slots
         if (c->nbuckets) {
@@ -1424,6 +1427,7 @@ int kc_reset(kc_ctx* c) {
     c->reuse_kept = c->reuse_ok = false;
     c->reuse_level = 0;
     c->reuse_hits = 0;
+    c->reuse_last_level = 0;
     return KC_OK;
 }
 

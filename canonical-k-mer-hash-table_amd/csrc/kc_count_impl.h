@@ -534,19 +534,9 @@ struct OutSeg {
     }
 };
 
-// Key-stream access policy (A/B knob, KC_NT: bit 0 = nontemporal loads of the level-1/2
-// key streams, which are read exactly once; bit 1 = nontemporal stores of the scatters)
-#ifndef KC_NT
-#define KC_NT 0
-#endif
-DEV uint64_t ks_load(const uint64_t* p) {
-    if constexpr (KC_NT & 1) return __builtin_nontemporal_load(p);
-    else return *p;
-}
-DEV void ks_store(uint64_t* p, uint64_t v) {
-    if constexpr (KC_NT & 2) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
+// key-stream loads and stores (nontemporal forms measured no faster: r01_v11_ab_nontemporal.txt)
+DEV uint64_t ks_load(const uint64_t* p) { return *p; }
+DEV void ks_store(uint64_t* p, uint64_t v) { *p = v; }
 
 // In-kernel phase stamps (measurement builds only, tools/probe: -DKC_STAMP=1): wave 0 of
 // each workgroup adds the cycles of every phase of the scatter into g_stamp[block][phase].
@@ -1318,12 +1308,6 @@ DEV uint32_t zero_byte_mask8(uint64_t x) {
 // contiguous slice of the filter (bloom_block and region_of share the hash prefix), so
 // the gate reads stay within a few KiB that L2 keeps.
 constexpr int P3_THREADS = 1024;  // two 64 KiB regions per CU: 8 waves per SIMD
-#ifndef KC_P3_KB1
-#define KC_P3_KB1 4  // keys per thread per round, one-word keys
-#endif
-#ifndef KC_P3_KB2
-#define KC_P3_KB2 2  // two-word keys
-#endif
 template <int W, bool SEG, bool CNT, bool GATE = false>
 __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView tv, PartBufs pb,
                                                                   DevCounters* __restrict__ ctr,
@@ -1336,7 +1320,8 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
     constexpr int S = BUCKET_WORDS / (W + 1);
     // keys loaded per thread before inserting (memory-level parallelism); 1024-thread
     // groups already keep 8 waves per SIMD in flight
-    constexpr int KB = NT >= 1024 ? (CNT || W > 2 ? 2 : W == 2 ? KC_P3_KB2 : KC_P3_KB1) : 8;  // (CNT items carry a count: 64 VGPRs)
+    // (8 one-word keys measured 1 % faster but spill; 3-4 two-word keys no faster: r02_v22/v23)
+    constexpr int KB = NT >= 1024 ? (CNT || W > 1 ? 2 : 4) : 8;  // (CNT items carry a count: 64 VGPRs)
     if constexpr (SEG) {
         if (ctr->part_overflow) return;
     } else {
@@ -1679,9 +1664,6 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
 // contiguous run [off2[r * B2], off2[(r + 1) * B2]).
 // keys per thread per round and workgroup size: 512 threads keep the insertion path within
 // its registers (72 VGPRs, no scratch spills; 1024-thread groups would be capped at 64)
-#ifndef KC_B3_KB
-#define KC_B3_KB 4
-#endif
 #ifndef KC_B3_NT
 #define KC_B3_NT 512
 #endif
@@ -1691,7 +1673,7 @@ __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView b
                                                                   DevCounters* __restrict__ ctr,
                                                                   const unsigned long long* gate, int fresh, int is) {
     // is: u64 words per item (word 0 is the table key word the filter uses)
-    constexpr int NT = B3_THREADS, KB = KC_B3_KB;
+    constexpr int NT = B3_THREADS, KB = 4;  // (8 or 2 keys per round: slower, r02_v21_ab_b3_kb.txt)
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ uint32_t s_pre[MAX_SEG_GROUP + 1];
     if constexpr (SEG) {

@@ -137,13 +137,10 @@ inline int slots_per_bucket(int W) { return BUCKET_WORDS / (W + 1); }
 // Windows rolled per thread in the partitioned kernels, and the workgroup size of the
 // segmented level 1 (tile = threads x windows), by key width: wide keys take fewer
 // windows per thread and smaller groups so that the registers and the LDS tile fit.
-#ifndef KC_RUNW_WIDE
-#define KC_RUNW_WIDE 8  // windows per thread for keys of three or four words (A/B knob)
-#endif
 #ifndef KC_SCATTER_NT12
 #define KC_SCATTER_NT12 512
 #endif
-constexpr int run_width(int W) { return W == 1 ? 16 : W == 2 ? 8 : W <= 4 ? KC_RUNW_WIDE : 4; }
+constexpr int run_width(int W) { return W == 1 ? 16 : W == 2 ? 8 : W <= 4 ? 8 : 4; }
 constexpr int scatter_threads_w(int W) { return W <= 2 ? KC_SCATTER_NT12 : W <= 4 ? 512 : 256; }
 constexpr int p1_tile(int W) { return scatter_threads_w(W) * run_width(W); }  // windows per segmented level-1 tile
 // level 2 (k_p2f): workgroup size by key width, and its LDS for F2 regions per coarse bin

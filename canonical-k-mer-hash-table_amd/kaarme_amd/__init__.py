@@ -89,7 +89,7 @@ class kc_stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in (
         "windows", "inserted", "distinct", "table_slots", "bf_windows", "bf_bits", "new_in_first",
         "new_in_second", "failed_in_first", "chunks", "bytes", "part_fallbacks", "spilled", "heavy_records",
-        "reused_passes")]
+        "reused_passes", "reuse_level")]
 
     def as_dict(self) -> dict:
         return {n: int(getattr(self, n)) for n, _ in self._fields_}

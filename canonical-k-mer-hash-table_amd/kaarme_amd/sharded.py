@@ -145,13 +145,32 @@ def all_gather_words(dist, mine, world: int, group=None, chunk_words: int = 0):
             tmp = full
         else:
             tmp = torch.empty(world * (hi - lo), dtype=mine.dtype, device=mine.device)
-        try:
+        # the API is chosen up front (gloo has no all_gather_into_tensor): a communication
+        # error propagates instead of sending this rank into a different collective
+        if _gather_into_tensor(dist, group):
             dist.all_gather_into_tensor(tmp, piece, group=group)
-        except (RuntimeError, AttributeError, NotImplementedError):  # backends without it
+        else:
             dist.all_gather(list(tmp.view(world, hi - lo).unbind(0)), piece, group=group)
         if tmp is not full:
             grid[:, lo:hi].copy_(tmp.view(world, hi - lo))
     return full
+
+
+def _gather_into_tensor(dist, group) -> bool:
+    return hasattr(dist, "all_gather_into_tensor") and dist.get_backend(group) != "gloo"
+
+
+def _on_stream(device: str, stream: int):
+    """Context that makes the caller's HIP stream torch's current stream, so the collectives
+    (which torch orders after its current stream) follow the kc_* work queued on `stream` and
+    the kc_* calls queued after them follow the collectives.  NULL stream / CPU: no-op."""
+    import contextlib
+
+    if device != "cuda" or not stream:
+        return contextlib.nullcontext()
+    import torch
+
+    return torch.cuda.stream(torch.cuda.ExternalStream(stream))
 
 
 def owner_share(slots: int, world: int) -> int:
@@ -331,6 +350,7 @@ class ShardedCounter:
         self._pending = False
         self._stream = 0
         self._inflight = []
+        self._warned = False
         # exchange traffic of the merges (xGMI bytes reported beside HBM bytes)
         self.xstats = {"bytes_sent": 0, "bytes_recv": 0, "exchange_s": 0.0, "merges": 0}
 
@@ -343,20 +363,21 @@ class ShardedCounter:
     def merge(self, stream: int = 0):
         """Route the local table's records to their owners (one all-to-all) and add them
         into the owner tables.  Collective: every rank calls it the same number of times."""
-        recs, counts = self.engine.route_table(self.world, stream)
-        # the records hold the local counts now: a later merge must route only what is
-        # counted after this one
-        self.engine.clear_local()
         import time
 
-        t0 = time.perf_counter()
-        recv, n, per_rank = exchange(self.dist, recs, counts, self.W + 1, self.group, with_counts=True)
-        rec_bytes = (self.W + 1) * 8
-        self.xstats["bytes_sent"] += sum(c for d, c in enumerate(counts) if d != self.rank) * rec_bytes
-        self.xstats["bytes_recv"] += sum(c for d, c in enumerate(per_rank) if d != self.rank) * rec_bytes
-        self.xstats["exchange_s"] += time.perf_counter() - t0  # (route synced before, the sums check after)
-        self.xstats["merges"] += 1
-        self.engine.insert_counts(recv, n, stream, group_counts=per_rank)
+        with _on_stream(self.device, stream):
+            recs, counts = self.engine.route_table(self.world, stream)
+            # the records hold the local counts now: a later merge must route only what is
+            # counted after this one
+            self.engine.clear_local()
+            t0 = time.perf_counter()
+            recv, n, per_rank = exchange(self.dist, recs, counts, self.W + 1, self.group, with_counts=True)
+            rec_bytes = (self.W + 1) * 8
+            self.xstats["bytes_sent"] += sum(c for d, c in enumerate(counts) if d != self.rank) * rec_bytes
+            self.xstats["bytes_recv"] += sum(c for d, c in enumerate(per_rank) if d != self.rank) * rec_bytes
+            self.xstats["exchange_s"] += time.perf_counter() - t0  # (route synced before, the sums check after)
+            self.xstats["merges"] += 1
+            self.engine.insert_counts(recv, n, stream, group_counts=per_rank)
         self._inflight = [recv]  # the receive buffer must outlive the insert
         self._pending = False
 
@@ -374,19 +395,31 @@ class ShardedCounter:
         import torch
 
         stream = self._stream if stream is None else stream
-        n, unit = self.engine.bloom_words()
-        world = self.world
-        per = -(-max(n, 1) // (unit * world)) * unit  # words of one rank's slice
-        send = self.engine.bloom_copy(per * world, stream)
-        if world > 1:  # rank d receives every rank's copy of slice d, in rank order
-            recv, got = exchange(self.dist, send.view(torch.int64), [per // 2] * world, 1, self.group)
-            parts = recv[:got].view(torch.int32)
-        else:
-            parts = send
-        mine = self.engine.bloom_merge(parts, world, per, stream)
-        full = all_gather_words(self.dist, mine, world, self.group)
-        nis = self.engine.bloom_install(full, n, stream)
-        self.engine.bloom_finalize(owner_share(2 * nis, world))
+        if self.world > 2 and not self._warned:
+            # the per-bit merge below passes a k-mer seen once on one rank when each of its
+            # filter-1 bits is also set on another rank by other k-mers (probability about
+            # (1 - (1 - rho)^(world - 1))^h at filter-1 fill rho): counts of k-mers seen at
+            # least twice stay exact, but more singletons reach the tables as world grows
+            # 
+            import warnings
+
+            warnings.warn(f"sharded Bloom filter over {self.world} ranks: singleton k-mers pass the combined "
+                          "gate more often than on one GPU (tables grow; counts >= 2 stay exact)")
+            self._warned = True
+        with _on_stream(self.device, stream):
+            n, unit = self.engine.bloom_words()
+            world = self.world
+            per = -(-max(n, 1) // (unit * world)) * unit  # words of one rank's slice
+            send = self.engine.bloom_copy(per * world, stream)
+            if world > 1:  # rank d receives every rank's copy of slice d, in rank order
+                recv, got = exchange(self.dist, send.view(torch.int64), [per // 2] * world, 1, self.group)
+                parts = recv[:got].view(torch.int32)
+            else:
+                parts = send
+            mine = self.engine.bloom_merge(parts, world, per, stream)
+            full = all_gather_words(self.dist, mine, world, self.group)
+            nis = self.engine.bloom_install(full, n, stream)
+            self.engine.bloom_finalize(owner_share(2 * nis, world))
         self._inflight = [send, parts, mine, full]
         return nis
 

@@ -86,7 +86,9 @@ typedef struct {
     uint64_t part_fallbacks;  /* partitioned batches redone on the exact layout (a full skew list) */
     uint64_t spilled;         /* keys past their segment's end, inserted through the exact levels */
     uint64_t heavy_records;   /* {k-mer, count} records of repeated windows (homopolymer runs) */
-    uint64_t reused_passes;   /* counting passes that started from the Bloom pass's level-1 output */
+    uint64_t reused_passes;   /* counting passes that started from the Bloom pass's kept partitions */
+    uint64_t reuse_level;     /* the partition level the last reused pass started from: 2 (level 3 only),
+                                 1 (levels 2-3), 0 = no reuse */
 } kc_stats;
 
 /* Creates the device table (PointerHashTableCanonicalAV ctor,

@@ -1,0 +1,119 @@
+"""Reference parity at the benchmarked configurations (BASELINE.md's
+parity rule): bench.py's own job -- the device image generated in HBM, one staging batch,
+the bench's table geometry, and for C3 the counting pass from the Bloom pass's kept level-2
+partitions -- against the reference CLI's output on the same input
+(tests/golden/fullsize.json, made by tests/golden/make_fullsize.py from oracle/_ref/kaarme).
+
+Compared: SHA-256 of the byte-sorted output text (kaarme_amd.digest from kc_dump records),
+its line count and the sum of its counts; the image's SHA-256 against the file kc_gen wrote
+for the reference.  The CPU test pins the digest helper against Python's own sort.
+"""
+import argparse
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, REPO
+
+sys.path.insert(0, REPO)
+
+FULLSIZE = os.path.join(GOLDEN, "fullsize.json")
+
+
+def _fixture():
+    with open(FULLSIZE) as f:
+        return json.load(f)
+
+
+def _bench_args(config):
+    import bench
+    base = argparse.Namespace(config=config, reads=None, read_len=None, genome=None, k=None, slots=None,
+                              unique=None, batch_mib=0, err=0.001, seed=42)
+    return bench, bench.resolve(base, config)
+
+
+@pytest.mark.parametrize("n", [0, 1, 7, 1000])
+@pytest.mark.parametrize("k", [5, 31, 51, 95])
+def test_digest_helper_matches_sorted_text(k, n):
+    from kaarme_amd import words_for_k
+    from kaarme_amd.digest import sorted_text_digest, _text_numpy
+    W = words_for_k(k)
+    rng = np.random.default_rng(k * 1000 + n)
+    keys = set()
+    while len(keys) < n:
+        keys.add(int(rng.integers(0, 1 << 62)) | (int(rng.integers(0, 1 << 62)) << 62))
+    recs = np.zeros((n, W + 1), dtype=np.uint64)
+    lines = []
+    for i, x in enumerate(sorted(keys)):
+        x &= (1 << (2 * k)) - 1
+        c = int(rng.choice([1, 2, 9, 10, 99, 100, 16383, 65535]))
+        for w in range(W):
+            recs[i, W - 1 - w] = (x >> (64 * w)) & ((1 << 64) - 1)
+        recs[i, W] = c
+        s = "".join("ACGT"[(x >> (2 * (k - 1 - j))) & 3] for j in range(k))
+        lines.append(f"{s} {c}\n".encode())
+    # de-duplicate keys that collided after the mask, as a counter's output would be
+    _, first = np.unique(recs[:, :W], axis=0, return_index=True)
+    recs = recs[np.sort(first)]
+    lines = [lines[i] for i in np.sort(first)]
+    rng.shuffle(recs)
+    want = b"".join(sorted(lines))
+    if len(recs):
+        assert _text_numpy(recs, k, W).tobytes() == want
+    d = sorted_text_digest(recs, k)
+    assert d["sorted_sha256"] == hashlib.sha256(want).hexdigest()
+    assert d["lines"] == len(lines)
+    assert d["count_sum"] == sum(int(l.split()[1]) for l in lines)
+
+
+def test_fixture_cases_match_bench_presets():
+    """Every full-size fixture is a bench workload (bench.fixture_case finds it)."""
+    doc = _fixture()
+    for name, c in doc["cases"].items():
+        bench, args = _bench_args(name)
+        fx = bench.fixture_case(args)
+        assert fx is not None and fx["name"] == name, name
+        assert fx["sorted_sha256"] == c["sorted_sha256"]
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("config", ["C2", "C3", "C2S"])
+def test_bench_job_equals_reference_output(config):
+    import torch
+    import kaarme_amd as ka
+    from kaarme_amd.digest import sorted_text_digest
+    doc = _fixture()
+    if config not in doc["cases"]:
+        pytest.skip(f"no {config} fixture")
+    bench, args = _bench_args(config)
+    env = {"torch": torch, "ka": ka, "lib": ka.load_library(), "dist": None, "rank": 0, "world": 1, "local": 0}
+    torch.cuda.set_device(0)
+    job = bench.setup_job(args, env)
+    fx = job.fixture
+    assert fx is not None and fx["name"] == config
+    try:
+        img = job.image.cpu().numpy()
+        assert hashlib.sha256(memoryview(img)).hexdigest() == fx["input_sha256"], "device image != kc_gen file"
+        del img
+        job.step()
+        st = job.counter.finish()
+        assert st["windows"] == job.windows_expected
+        assert st["chunks"] == len(job.chunks)
+        assert st["part_fallbacks"] == 0
+        if args.unique:  # the bench path: the counting pass from the kept level-2 partitions
+            assert st["reused_passes"] == 1 and st["reuse_level"] == 2, st
+        got = sorted_text_digest(job.counter.dump(), args.k)
+        assert got["lines"] == fx["lines"]
+        assert got["count_sum"] == fx["count_sum"]
+        assert got["sorted_sha256"] == fx["sorted_sha256"]
+        if fx["distinct"] is not None and not args.unique:
+            assert st["distinct"] == fx["distinct"]
+    finally:
+        job.counter.close()
+        del job
+        torch.cuda.empty_cache()
