@@ -343,6 +343,12 @@ constexpr int tile_win() { return COUNT_THREADS * run_w<W>(); }
 // the segmented (single-pass) level 1: kc_internal.h scatter_threads
 template <int W>
 constexpr int scatter_threads() { return scatter_threads_w(W); }
+// windows per thread of k_p1<W, ..., NT> (the segmented launch: p1_runw; the 256-thread exact
+// levels: run_w) and its LDS before the heavy table: the bins' arrays and the tile of OW-word keys
+template <int W, int NT>
+constexpr int k1_runw() { return NT == scatter_threads_w(W) ? p1_runw(W) : run_w<W>(); }
+template <int W, int OW, int NT>
+constexpr size_t p1_smem(uint32_t F) { return bin_lds_bytes(F) + (size_t)NT * k1_runw<W, NT>() * 8 * OW; }
 // Level 2 runs one 1024-thread workgroup per CU for keys of up to two words: twice the
 // tile of level 1 (16384 one-word keys, 128 KiB of LDS) halves the barriers per key and
 // doubles the runs each bin gets per tile (C2: k_p2f 5.6 -> 5.0 ms on one box); wider
@@ -363,9 +369,8 @@ DEV bool window_tkey(const PackedView& sv, uint64_t p, const RollConst& rk, uint
 
 // MODE 1/2: the Bloom root (RollingHasherDual mod 2^54) is a rolled quantity, so these
 // modes roll one contiguous run of run_w windows per thread.
-template <int W, class F>
+template <int W, int RUNW = run_w<W>(), class F>
 DEV void tile_rolled(const PackedView& sv, uint64_t t0, uint64_t t1, const RollConst& rk, F&& f) {
-    constexpr int RUNW = run_w<W>();
     const uint64_t r0 = t0 + (uint64_t)threadIdx.x * RUNW, r1 = min(r0 + RUNW, t1);
     if (r0 < r1) {
         const uint64_t ps = r0 >= (uint64_t)(rk.k - 1) ? r0 - (rk.k - 1) : 0;
@@ -684,6 +689,164 @@ DEV bool scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const Out& o
     return false;
 }
 
+// The segmented scatter of k_p1 and k_p2f, as a pipelined tile loop: three barriers per tile
+// instead of scatter_tile's six.  The write-out of tile t and the window arithmetic + rank
+// atomics of tile t+1 are not separated by a barrier (they touch disjoint LDS: keys / lim /
+// gbase / sp against registers / hist), so one wave's VALU work overlaps another's stores.
+// Per tile:
+//   rank atomics (hist was cleared by the previous tile's setup)              barrier 1
+//   wave 0: exclusive scan of hist -> start and the tile's key count           barrier 2
+//   placement into keys[]; per-bin setup (advances the previous tile's fill,
+//     clears hist); mid() (the caller may load its next tile into tk / ok)     barrier 3
+//   (a bin past its segment's end: one skew-list allocation for the tile)
+//   write-out
+// Before the first tile: hist = 0, lim = 0, gbase = each bin's first destination
+// (scatter_seg_init); after the last: a barrier, then a bin's next destination is
+// gbase + lim (scatter_seg_next).
+DEV void scatter_seg_init(const PartLds& l, uint32_t b, uint64_t first) {
+    l.hist[b] = 0;
+    l.lim[b] = 0;
+    l.gbase[b] = first;
+}
+DEV uint64_t scatter_seg_next(const PartLds& l, uint32_t b) { return l.gbase[b] + l.lim[b]; }
+
+// Where a scatter's write-out puts a key: W words at out[dst] (StoreWords), or a level-2
+// record of 6 bytes (StoreRec6: one-word keys in tables of >= 2^16 regions, k_p2f -> k_p3).
+struct StoreWords {
+    template <int W>
+    DEV void operator()(uint64_t* __restrict__ out, uint64_t dst, const uint64_t (&key)[W], uint32_t) const {
+#pragma unroll
+        for (int w = 0; w < W; w++) ks_store(out + dst * W + w, key[w]);
+    }
+};
+// Level-2 record of a one-word key (table key word 0 = x << 32 | lo): the region r holding it
+// fixes x to [xlo(r), xlo(r + 1)), xlo(r) = ceil(r 2^32 / R), a range of at most 2^16 values
+// when R >= 2^16, so a record is lo (32 bits) and d = x - xlo(r) (16 bits): 6 instead of 8
+// bytes per key for k_p2f to write and k_p3 to read.  Records go in pairs of three dwords
+// {lo_even, lo_odd, d_even | d_odd << 16} (one stream per segment; record p of the key array
+// at byte 6p, since segment starts are multiples of 8 records).
+DEV uint64_t region_xlo(uint64_t r, uint64_t R) { return ((r << 32) + R - 1) / R; }
+struct StoreRec6 {
+    const uint32_t* xlo;  // LDS: xlo of each bin's region
+    DEV void operator()(uint64_t* __restrict__ out, uint64_t dst, const uint64_t (&key)[1], uint32_t b) const {
+        uint32_t* q = reinterpret_cast<uint32_t*>(out) + (dst >> 1) * 3;
+        q[dst & 1] = (uint32_t)key[0];
+        reinterpret_cast<uint16_t*>(q + 2)[dst & 1] = (uint16_t)((uint32_t)(key[0] >> 32) - xlo[b]);
+    }
+};
+// the raw dwords of record p: lo | d-pair << 32 (decoded by rec6_key once the load is needed,
+// so a prefetch of the next items does not wait for its loads)
+DEV uint64_t rec6_raw(const uint64_t* __restrict__ keys, uint64_t p) {
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(keys) + (p >> 1) * 3;
+    return ((uint64_t)q[2] << 32) | q[p & 1];
+}
+DEV uint64_t rec6_key(uint64_t raw, bool odd, uint32_t xlo) {
+    const uint32_t dd = (uint32_t)(raw >> 32);
+    const uint32_t d = odd ? dd >> 16 : dd & 0xFFFFu;
+    return ((uint64_t)(xlo + d) << 32) | (uint32_t)raw;
+}
+
+template <int W, int RUNW, class Bin, class Out, int NT, class Mid = NoMid, class St = StoreWords>
+DEV void scatter_seg(const PartLds& l, uint32_t F, const Bin& bin, const Out& o, uint64_t (&tk)[RUNW][W],
+                     bool (&ok)[RUNW], uint64_t* __restrict__ out, Mid&& mid = Mid(), Stamps* stp = nullptr,
+                     const St& store = St()) {
+    static_assert(NT * RUNW <= 65536, "ranks ride in 16 bits");
+    __shared__ unsigned long long s_spbase;
+    __shared__ uint32_t s_spills, s_n;
+    const int tid = threadIdx.x, lane = tid & 63;
+    uint32_t pk[RUNW];  // bin << 16 | rank in the bin, ~0 = no key
+    if (KC_STAMP && stp) stp->mark(0);
+#pragma unroll
+    for (int j = 0; j < RUNW; j++) {
+        const uint32_t b = bin(tk[j][0]);
+        pk[j] = ok[j] ? (b << 16) | atomicAdd(&l.hist[b], 1u) : ~0u;
+    }
+    if (KC_STAMP && stp) stp->mark(1);
+    __syncthreads();  // 1
+    if (KC_STAMP && stp) stp->mark(2);
+    if (tid < 64) {
+        const uint32_t per = (F + 63) / 64, lo = min(F, lane * per), hi = min(F, lo + per);
+        uint32_t sum = 0;
+        for (uint32_t i = lo; i < hi; i++) sum += l.hist[i];
+        const uint32_t incl = wave_incl_sum(sum);
+        uint32_t run = incl - sum;
+        for (uint32_t i = lo; i < hi; i++) {
+            l.start[i] = run;
+            run += l.hist[i];
+        }
+        if (lane == 63) s_n = incl;
+        if (Out::kSeg && lane == 0) s_spills = 0;
+    }
+    __syncthreads();  // 2
+    if (KC_STAMP && stp) stp->mark(3);
+#pragma unroll
+    for (int j = 0; j < RUNW; j++)
+        if (pk[j] != ~0u) {
+            const uint32_t slot = l.start[pk[j] >> 16] + (pk[j] & 0xFFFFu);
+#pragma unroll
+            for (int w = 0; w < W; w++) l.keys[slot * W + w] = tk[j][w];
+        }
+    bool spills = false;
+    for (uint32_t b = tid; b < F; b += NT) {
+        const uint32_t st = l.start[b], h = l.hist[b];
+        const uint64_t g = l.gbase[b] + l.lim[b];  // the bin's next destination
+        const uint32_t fit = (uint32_t)min((uint64_t)h, o.room(b, g));
+        l.gbase[b] = g - st;  // destination minus tile slot (modulo 2^64) during the write-out
+        l.lim[b] = st + fit;
+        l.sp[b] = h - fit;
+        l.hist[b] = 0;
+        spills |= fit < h;
+    }
+    if (Out::kSeg && spills) s_spills = 1;
+    mid();
+    if (KC_STAMP && stp) stp->mark(4);
+    __syncthreads();  // 3
+    if constexpr (Out::kSeg) {
+        if (s_spills) {
+            // one allocation in the skew list for all the tile's spilled keys (a bin's spilled
+            // keys are the tail of its run in the tile)
+            const uint32_t last = l.sp[F - 1];
+            block_excl_scan_lds<NT>(l.sp, l.sp, F);
+            if (tid == 0) s_spbase = atomicAdd(o.spill_n, (unsigned long long)(l.sp[F - 1] + last));
+            __syncthreads();
+        }
+    }
+    if (KC_STAMP && stp) stp->mark(5);
+    const uint32_t n = s_n;
+    auto emit = [&](uint32_t i, const uint64_t (&key)[W], uint32_t b, uint32_t lim, uint64_t g) {
+        if (i < lim) {
+            store(out, g + i, key, b);
+        } else if constexpr (Out::kSeg) {
+            const uint64_t pos = s_spbase + l.sp[b] + (i - lim);
+            if (pos < o.spill_cap) {
+                uint64_t* r = o.spill + pos * (W + o.rec);
+#pragma unroll
+                for (int w = 0; w < W; w++) r[w] = key[w];
+                if (o.rec) r[W] = 1;
+            } else {
+                atomicOr(o.overflow, 1ULL);
+            }
+        }
+    };
+    // two keys per thread per round, their LDS reads issued together
+    for (uint32_t i0 = tid; i0 < n; i0 += 2 * NT) {
+        const uint32_t i1 = i0 + NT;
+        const bool has1 = i1 < n;
+        uint64_t k0[W], k1[W];
+#pragma unroll
+        for (int w = 0; w < W; w++) {
+            k0[w] = l.keys[i0 * W + w];
+            k1[w] = l.keys[(has1 ? i1 : i0) * W + w];
+        }
+        const uint32_t b0 = bin(k0[0]), b1 = bin(k1[0]);
+        const uint32_t lim0 = l.lim[b0], lim1 = l.lim[b1];
+        const uint64_t g0 = l.gbase[b0], g1 = l.gbase[b1];
+        emit(i0, k0, b0, lim0, g0);
+        if (has1) emit(i1, k1, b1, lim1, g1);
+    }
+    if (KC_STAMP && stp) stp->mark(6);
+}
+
 // MODE 3 and 5 are Bloom pass 1 (MODE 5 writes the whole table key: its level-1 output is
 // kept for the counting pass, kc_api.cpp "level-1 reuse")
 constexpr bool bloom_mode(int MODE) { return MODE == 3 || MODE == 5; }
@@ -789,9 +952,9 @@ DEV void skew_append(const PartBufs& pb, DevCounters* ctr, bool want, const uint
     }
 }
 
-template <int OW, int RUNW, int MODE, int NT>
-DEV void combine_repeats(uint64_t (&tk)[RUNW][OW], bool (&ok)[RUNW], const PartLds& l, const HeavyTab& h,
-                         const PartBufs& pb, DevCounters* ctr) {
+template <int OW, int RUNW, int MODE>
+DEV void combine_repeats(uint64_t (&tk)[RUNW][OW], bool (&ok)[RUNW], const HeavyTab& h, const PartBufs& pb,
+                         DevCounters* ctr) {
     // repeated windows (lane masks only in the common case): equal to the next window
     // (homopolymer) or to the one after ((CA)n)
     uint32_t rep = 0;
@@ -807,32 +970,26 @@ DEV void combine_repeats(uint64_t (&tk)[RUNW][OW], bool (&ok)[RUNW], const PartL
         if (e2) rep |= 5u << j;
     }
     if (__ballot(rep != 0) == 0) return;
-    // the wave's repeated windows, compacted into its share of the (idle) tile key area
-    const int lane = threadIdx.x & 63;
-    uint64_t* stage = l.keys + (size_t)(threadIdx.x >> 6) * 64 * RUNW * OW;
-    const uint32_t nrep = __builtin_popcount(rep);
-    const uint32_t incl = wave_incl_sum(nrep);
-    const uint32_t total = __shfl(incl, 63, 64);
-    uint32_t pos = incl - nrep;
-#pragma unroll
-    for (int j = 0; j < RUNW; j++)
-        if ((rep >> j) & 1) {
-#pragma unroll
-            for (int w = 0; w < OW; w++) stage[pos * OW + w] = tk[j][w];
-            pos++;
-            ok[j] = false;
-        }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    for (uint32_t i0 = 0; i0 < total; i0 += 64) {
-        const bool act = i0 + lane < total;
+    // window slot by window slot, the lanes holding a repeat there insert it (no LDS staging:
+    // the tile's key area may still be read by another wave's write-out, scatter_seg)
+#pragma unroll 1
+    for (int j = 0; j < RUNW; j++) {  // (not unrolled: one copy of the insertion code)
+        const bool act = (rep >> j) & 1;
+        if (__ballot(act) == 0) continue;
         uint64_t key[OW];
 #pragma unroll
-        for (int w = 0; w < OW; w++) key[w] = act ? stage[(i0 + lane) * OW + w] : 0;
+        for (int w = 0; w < OW; w++) key[w] = 0;
+#pragma unroll
+        for (int q = 0; q < RUNW; q++)
+            if (q == j)
+#pragma unroll
+                for (int w = 0; w < OW; w++) key[w] = tk[q][w];
         const bool full = heavy_insert<OW>(h, key, act, 1);
         skew_append<OW, MODE>(pb, ctr, full, key, 1);
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // stage reads done before the tile reuses it
+#pragma unroll
+    for (int j = 0; j < RUNW; j++)
+        if ((rep >> j) & 1) ok[j] = false;
 }
 // end of a workgroup's range: the heavy table's entries -> records of the skew list
 template <int OW, int MODE>
@@ -867,13 +1024,13 @@ constexpr int p1_out_words(int W, int MODE) { return MODE == 3 ? 1 : W; }
 // fill counts go to hist1).  `count`: add windows / inserted to the counters (off for
 // the histogram pass of a fallback, whose windows the segmented pass counted already).
 template <int W, int MODE, bool SCATTER, class Bin, class Out, int NT = COUNT_THREADS>
-__global__ __launch_bounds__(NT, 4) void k_p1(PackedView sv, int k, BloomView bf,
+__global__ __launch_bounds__(NT, NT >= 1024 ? 8 : 4) void k_p1(PackedView sv, int k, BloomView bf,
                                                       DevCounters* __restrict__ ctr, PartBufs pb, uint32_t F, Bin bin_arg,
                                                       uint64_t* __restrict__ out, uint64_t pow5_k, uint64_t pow5_km1,
                                                       Out o, const unsigned long long* gate, int count) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const Bin bin = level1_bins(bin_arg);
-    constexpr int RUNW = run_w<W>(), TW = NT * RUNW;
+    constexpr int RUNW = k1_runw<W, NT>(), TW = NT * RUNW;
     constexpr bool COUNTS = !SCATTER || Out::kSeg;
     constexpr bool ROLLED = MODE == 2;       // gate on the rolled root (reference layout)
     constexpr int OW = p1_out_words(W, MODE);  // words per output key
@@ -881,7 +1038,7 @@ __global__ __launch_bounds__(NT, 4) void k_p1(PackedView sv, int k, BloomView bf
     if (gate && !SCATTER && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&ctr->part_fallbacks, 1ULL);
     const PartLds l = part_lds(smem, F);
     constexpr bool HEAVY = Out::kSeg && !Bin::kOwner && !ROLLED;  // repeated windows -> heavy table
-    const HeavyTab ht = heavy_tab<OW>(smem + part_smem<OW, NT>(F));
+    const HeavyTab ht = heavy_tab<OW>(smem + p1_smem<W, OW, NT>(F));
     if constexpr (HEAVY) {
         heavy_clear(ht, OW);
         for (int i = threadIdx.x; i < HT; i += NT) ht.cnt[i] = 0;
@@ -893,10 +1050,11 @@ __global__ __launch_bounds__(NT, 4) void k_p1(PackedView sv, int k, BloomView bf
     Out ob = o;
     if constexpr (Out::kSeg) ob.base = (uint64_t)blockIdx.x * o.cap;  // segment (b, block) = b * nblk1 + block
     for (uint32_t b = tid; b < F; b += NT) {
-        l.hist[b] = 0;
-        if constexpr (SCATTER) {
-            if constexpr (Out::kSeg) l.gbase[b] = ob.start(b);
-            else l.gbase[b] = pb.off1[(uint64_t)b * pb.nblk1 + blockIdx.x];
+        if constexpr (Out::kSeg) {
+            scatter_seg_init(l, b, ob.start(b));
+        } else {
+            l.hist[b] = 0;
+            if constexpr (SCATTER) l.gbase[b] = pb.off1[(uint64_t)b * pb.nblk1 + blockIdx.x];
         }
     }
     __syncthreads();
@@ -929,12 +1087,12 @@ __global__ __launch_bounds__(NT, 4) void k_p1(PackedView sv, int k, BloomView bf
                     n_ins += MODE == 0 ? ok[j] : 0;  // MODE 4: level 3 counts the gated insertions
                 }
             }
-            if constexpr (HEAVY) combine_repeats<OW, RUNW, MODE, NT>(tk, ok, l, ht, pb, ctr);
+            if constexpr (HEAVY) combine_repeats<OW, RUNW, MODE>(tk, ok, ht, pb, ctr);
         } else {
             // rolled run: slot j <- the j-th symbol of the thread's run (static indices)
 #pragma unroll
             for (int j = 0; j < RUNW; j++) ok[j] = false;
-            tile_rolled<W>(sv, t0, t1, rk, [&](const uint64_t (&fwd)[W], const uint64_t (&rc)[W], uint64_t root) {
+            tile_rolled<W, RUNW>(sv, t0, t1, rk, [&](const uint64_t (&fwd)[W], const uint64_t (&rc)[W], uint64_t root) {
                 if constexpr (COUNTS) n_win++;
                 uint64_t key[W], t[W];
                 canonical<W>(fwd, rc, key);
@@ -953,7 +1111,9 @@ __global__ __launch_bounds__(NT, 4) void k_p1(PackedView sv, int k, BloomView bf
             });
         }
         if constexpr (SCATTER) {
-            scatter_tile<OW, RUNW, Bin, Out, NT>(l, F, bin, ob, tk, ok, out, NoMid(), &stp);
+            if constexpr (Out::kSeg)
+                scatter_seg<OW, RUNW, Bin, Out, NT>(l, F, bin, ob, tk, ok, out, NoMid(), &stp);
+            else scatter_tile<OW, RUNW, Bin, Out, NT>(l, F, bin, ob, tk, ok, out, NoMid(), &stp);
         } else {
 #pragma unroll
             for (int j = 0; j < RUNW; j++)
@@ -964,9 +1124,10 @@ __global__ __launch_bounds__(NT, 4) void k_p1(PackedView sv, int k, BloomView bf
         __syncthreads();
         for (uint32_t b = tid; b < F; b += NT) pb.hist1[(uint64_t)b * pb.nblk1 + blockIdx.x] = l.hist[b];
     }
-    if constexpr (Out::kSeg) {  // segment fills (the scatter's last barrier ordered gbase)
+    if constexpr (Out::kSeg) {  // segment fills, once the last write-out has read lim / gbase
+        __syncthreads();
         for (uint32_t b = tid; b < F; b += NT)
-            pb.hist1[(uint64_t)b * pb.nblk1 + blockIdx.x] = (uint32_t)(l.gbase[b] - ob.start(b));
+            pb.hist1[(uint64_t)b * pb.nblk1 + blockIdx.x] = (uint32_t)(scatter_seg_next(l, b) - ob.start(b));
     }
     if constexpr (SCATTER && Out::kSeg) stp.flush(0);
     if constexpr (HEAVY) heavy_flush<OW, MODE>(ht, pb, ctr);
@@ -1196,9 +1357,11 @@ constexpr size_t p2f_smem(uint32_t F, uint32_t nseg_max) { return part_smem<W, N
 #endif
 // IS: u64 words per level-1 item (W, or the whole table key of a kept level-1 output when
 // the Bloom pass reads only its word 0)
-template <int W, int NT, int IS = W>
+// REC6: write 6-byte level-2 records (StoreRec6) instead of whole keys (one-word keys)
+template <int W, int NT, int IS = W, bool REC6 = false>
 __global__ __launch_bounds__(NT, (2048 / NT > 8 ? 8 : 2048 / NT)) void k_p2f(TableView tv, PartBufs pb, DevCounters* __restrict__ ctr,
                                                           int REC) {
+    static_assert(!REC6 || W == 1, "6-byte records hold one-word keys");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int RUNW = run_w<W>(), TW = NT * RUNW;
     if (ctr->part_overflow) return;  // level 1 overflowed: the exact pipeline redoes the batch
@@ -1214,10 +1377,10 @@ __global__ __launch_bounds__(NT, (2048 / NT > 8 ? 8 : 2048 / NT)) void k_p2f(Tab
     const OutSeg o{(uint64_t)pb.B2 * pb.cap2, ((uint64_t)c * F * pb.B2 + j) * pb.cap2, pb.cap2,
                    pb.spill, pb.spill_cap, &ctr->spill_n, &ctr->part_overflow, REC};
     for (uint32_t i = tid; i <= nseg; i += NT) pre[i] = i < nseg ? pb.hist1[seg0 + i] : 0;
-    for (uint32_t b = tid; b < F; b += NT) {
-        l.hist[b] = 0;
-        l.gbase[b] = o.start(b);
-    }
+    uint32_t* xlo = pre + nseg + 1;  // REC6: xlo of the F regions of coarse bin c
+    if constexpr (REC6)
+        for (uint32_t b = tid; b < F; b += NT) xlo[b] = (uint32_t)region_xlo((uint64_t)c * F + b, tv.R);
+    for (uint32_t b = tid; b < F; b += NT) scatter_seg_init(l, b, o.start(b));
     __syncthreads();
     block_excl_scan_lds<NT>(pre, pre, nseg + 1);  // in place; pre[nseg] = total
     const uint32_t total = pre[nseg];
@@ -1253,23 +1416,25 @@ __global__ __launch_bounds__(NT, (2048 / NT > 8 ? 8 : 2048 / NT)) void k_p2f(Tab
     };
     uint64_t tk[RUNW][W];
     bool ok[RUNW];
-    Stamps stp;
-    stp.init();
     if (total) load_tile(0, tk, ok);
     for (uint32_t t0 = 0; t0 < total; t0 += TW) {
         // the next tile is loaded into the same registers as soon as this tile's keys sit
         // in LDS, so its loads overlap this tile's write-out (barriers wait for LDS only)
         const bool more = t0 + TW < total;
-        scatter_tile<W, RUNW, BinRegion, OutSeg, NT>(
-            l, F, bin, o, tk, ok, pb.keys2, [&]() {
-                if (KC_PREFETCH && more) load_tile(t0 + TW, tk, ok);
-            },
-            &stp);
+        auto mid = [&]() {
+            if (KC_PREFETCH && more) load_tile(t0 + TW, tk, ok);
+        };
+        if constexpr (REC6) {
+            scatter_seg<W, RUNW, BinRegion, OutSeg, NT>(l, F, bin, o, tk, ok, pb.keys2, mid, nullptr,
+                                                        StoreRec6{xlo});
+        } else {
+            scatter_seg<W, RUNW, BinRegion, OutSeg, NT>(l, F, bin, o, tk, ok, pb.keys2, mid);
+        }
         if (!KC_PREFETCH && more) load_tile(t0 + TW, tk, ok);
     }
-    stp.flush(1);
+    __syncthreads();  // the last write-out read lim / gbase
     for (uint32_t b = tid; b < F; b += NT)
-        pb.hist2[((uint64_t)c * F + b) * pb.B2 + j] = (uint32_t)(l.gbase[b] - o.start(b));
+        pb.hist2[((uint64_t)c * F + b) * pb.B2 + j] = (uint32_t)(scatter_seg_next(l, b) - o.start(b));
 }
 
 // LDS image of a region: the 16-byte chunks of each 128-byte bucket are XOR-swizzled
@@ -1308,7 +1473,8 @@ DEV uint32_t zero_byte_mask8(uint64_t x) {
 // contiguous slice of the filter (bloom_block and region_of share the hash prefix), so
 // the gate reads stay within a few KiB that L2 keeps.
 constexpr int P3_THREADS = 1024;  // two 64 KiB regions per CU: 8 waves per SIMD
-template <int W, bool SEG, bool CNT, bool GATE = false>
+// REC6: the segments hold 6-byte level-2 records (StoreRec6; one-word keys, SEG, not CNT)
+template <int W, bool SEG, bool CNT, bool GATE = false, bool REC6 = false>
 __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView tv, PartBufs pb,
                                                                   DevCounters* __restrict__ ctr,
                                                                   const unsigned long long* gate, int fresh,
@@ -1409,11 +1575,28 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
         pmask = (uint32_t)(vend - 1);
         psh = (m + 1) / 2;
     }
+    static_assert(!REC6 || (W == 1 && SEG && !CNT), "6-byte records: one-word keys in segments");
+    const uint32_t xlo_r = REC6 ? (uint32_t)region_xlo(r, tv.R) : 0;
     auto load_items = [&](uint64_t base, uint64_t (&kk)[KB][W], uint64_t (&add)[KB], uint32_t& ok) {
         ok = 0;
 #pragma unroll
         for (int q = 0; q < KB; q++) {
             const uint64_t i = base + threadIdx.x + (uint64_t)q * NT;
+            if constexpr (REC6) {
+                kk[q][0] = 0;
+                if (i < end) {
+                    while (nb <= i) {
+                        cs++;
+                        cb = nb;
+                        nb = s_pre[cs + 1];
+                    }
+                    const uint64_t p = (r * pb.B2 + cs) * pb.cap2 + (i - cb);
+                    kk[q][0] = rec6_raw(pb.keys2, p);
+                    ok |= (1u | (uint32_t)(p & 1) << 16) << q;  // valid, and (bit 16 + q) odd record
+                }
+                add[q] = 1;
+                continue;
+            }
             const uint64_t* src = nullptr;
             if (runs) {
                 uint32_t j = ((uint32_t)i * 0x9E3779B1u) & pmask;
@@ -1459,6 +1642,10 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
         const uint64_t nbase = base + (uint64_t)KB * NT;
         const bool more = KC_PREFETCH && W <= 2 && nbase < vend;  // W > 2: no spare registers
         if (more) load_items(nbase, nkk, nadd, nokm);
+        if constexpr (REC6) {
+#pragma unroll
+            for (int q = 0; q < KB; q++) kk[q][0] = rec6_key(kk[q][0], (okm >> (16 + q)) & 1, xlo_r);
+        }
         bool pass[KB];
 #pragma unroll
         for (int q = 0; q < KB; q++) {  // the gate reads of all KB items are issued together
@@ -2102,6 +2289,8 @@ static hipError_t launch_p3(TableView t, DevCounters* ctr, PartBufs pb, const un
         sm3 += (size_t)bf.slice_blocks * 32;
     }
     auto p3 = k_p3<W, SEG, CNT, GATE>;
+    if constexpr (W == 1 && SEG && !CNT)
+        if (pb.rec6) p3 = k_p3<1, true, false, GATE, true>;
     if (SEG && pb.B2 > MAX_SEG_GROUP) return hipErrorInvalidValue;
     hipError_t e = set_smem(p3, sm3);
     if (e != hipSuccess) return e;
@@ -2197,6 +2386,14 @@ static hipError_t launch_p2f(TableView t, PartBufs pb, DevCounters* ctr, int rec
     const uint32_t nseg = std::max<uint32_t>(pad, (pb.nblk1 + pb.B2 - 1) / pb.B2);
     hipError_t e;
     const size_t sm = p2f_smem<W, NT>(t.F2, nseg);
+    if constexpr (W == 1) {
+        if (pb.rec6) {  // 6-byte level-2 records, + the F2 regions' xlo in LDS
+            if ((e = set_smem(k_p2f<1, NT, 1, true>, sm + (size_t)t.F2 * 4)) != hipSuccess) return e;
+            hipLaunchKernelGGL((k_p2f<1, NT, 1, true>), dim3(t.F1 * pb.B2), dim3(NT), sm + (size_t)t.F2 * 4, s, t, pb,
+                               ctr, rec);
+            return hipGetLastError();
+        }
+    }
     if (sm <= LDS_BYTES || W <= 2) {
         if ((e = set_smem(k_p2f<W, NT>, sm)) != hipSuccess) return e;
         hipLaunchKernelGGL((k_p2f<W, NT>), dim3(t.F1 * pb.B2), dim3(NT), sm, s, t, pb, ctr, rec);
@@ -2236,6 +2433,8 @@ static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf
     }
     hipError_t e;
     const unsigned long long* gate = &ctr->part_overflow;
+    // one-word keys in a table of >= 2^16 regions: 6-byte level-2 records (StoreRec6)
+    pb.rec6 = W == 1 && t.R >= (1ULL << 16) && !std::getenv("KC_NO_REC6");
     if (phase & PH_MAIN) {
     hipLaunchKernelGGL(k_batch_begin, dim3(1), dim3(1), 0, s, ctr);
     const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
@@ -2254,7 +2453,7 @@ static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf
     }();
     const size_t p1_lds_min = p1_lds_knob >= 0 ? std::min(LDS_BYTES, (size_t)p1_lds_knob)
                               : (size_t)p1_tile(W) < 8 * (size_t)t.F1 ? LDS_BYTES / 2 + 16 : 0;
-    const size_t sm1 = std::max(p1_lds_min, part_smem<W, scatter_threads<W>()>(t.F1) + heavy_smem<W>());
+    const size_t sm1 = std::max(p1_lds_min, p1_smem<W, W, scatter_threads<W>()>(t.F1) + heavy_smem<W>());
     if ((e = set_smem(k1, sm1)) != hipSuccess) return e;
     const OutSeg o1{(uint64_t)pb.nblk1 * pb.cap1, 0, pb.cap1, pb.spill, pb.spill_cap, &ctr->spill_n,
                     &ctr->part_overflow, 1};
@@ -2314,7 +2513,7 @@ static hipError_t bloom_part_w(PackedView sym, int k, BloomView bf, TableView ft
     constexpr int NT = scatter_threads<W>(), NT2 = p2f_threads<OW>();
     auto k1 = k_p1<W, MODE, true, BinRegion, OutSeg, NT>;
     auto k2 = k_p2f<OW, NT2>;
-    const size_t sm1 = part_smem<OW, NT>(lg.F1) + heavy_smem<OW>(),
+    const size_t sm1 = p1_smem<W, OW, NT>(lg.F1) + heavy_smem<OW>(),
                  sm2 = p2f_smem<OW, NT2>(lg.F2, (pb.nblk1 + pb.B2 - 1) / pb.B2);
     if ((e = set_smem(k1, sm1)) != hipSuccess) return e;
     if ((e = set_smem(k2, sm2)) != hipSuccess) return e;

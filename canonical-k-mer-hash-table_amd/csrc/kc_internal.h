@@ -116,6 +116,8 @@ struct PartBufs {
     uint64_t spill_cap;     // a segment's end and of repeated windows; Bloom pass: keys), spill_cap entries
     uint32_t* keep_fill;    // Bloom pass keeping its partitions (partition reuse): copies of the
     uint32_t* keep_fill2;   // segment fills of levels 1 and 2 (the skew-list pass reuses hist1/2)
+    int rec6;               // segmented count pass, one-word keys, R >= 2^16: level 2 writes 6-byte
+                            // records (kc_count_impl.h StoreRec6) that its level 3 reads
 };
 
 struct BloomView {
@@ -137,12 +139,16 @@ inline int slots_per_bucket(int W) { return BUCKET_WORDS / (W + 1); }
 // Windows rolled per thread in the partitioned kernels, and the workgroup size of the
 // segmented level 1 (tile = threads x windows), by key width: wide keys take fewer
 // windows per thread and smaller groups so that the registers and the LDS tile fit.
-#ifndef KC_SCATTER_NT12
-#define KC_SCATTER_NT12 512
-#endif
 constexpr int run_width(int W) { return W == 1 ? 16 : W == 2 ? 8 : W <= 4 ? 8 : 4; }
-constexpr int scatter_threads_w(int W) { return W <= 2 ? KC_SCATTER_NT12 : W <= 4 ? 512 : 256; }
-constexpr int p1_tile(int W) { return scatter_threads_w(W) * run_width(W); }  // windows per segmented level-1 tile
+// The segmented level 1 (k_p1) of one- and two-word keys: 512-thread workgroups, two per CU.
+// (1024 threads with half the windows per thread -- 8 waves per SIMD within 64 VGPRs -- spill
+// and ran 30 % slower: profiles/r03_ab_p1_nt.txt)
+#ifndef KC_P1_NT12
+#define KC_P1_NT12 512
+#endif
+constexpr int scatter_threads_w(int W) { return W <= 2 ? KC_P1_NT12 : W <= 4 ? 512 : 256; }
+constexpr int p1_runw(int W) { return W <= 2 ? run_width(W) * 512 / KC_P1_NT12 : run_width(W); }
+constexpr int p1_tile(int W) { return scatter_threads_w(W) * p1_runw(W); }  // windows per segmented level-1 tile
 // level 2 (k_p2f): workgroup size by key width, and its LDS for F2 regions per coarse bin
 #ifndef KC_P2F_NT
 #define KC_P2F_NT 0  // 0: the default below
@@ -153,7 +159,7 @@ constexpr size_t bin_lds_bytes(uint32_t F) { return ((size_t)F * 24 + 15) / 16 *
 constexpr int p2f_threads_w(int W) { return KC_P2F_NT ? KC_P2F_NT : (W <= 2 ? 1024 : W <= 4 ? 512 : 256); }
 // segmented level 1 (k_p1, W-word output keys + the heavy table) for F1 coarse bins
 constexpr size_t p1_lds_bytes(int W, uint32_t F1) {
-    return bin_lds_bytes(F1) + (size_t)scatter_threads_w(W) * run_width(W) * 8 * W + (size_t)64 * (W + 1) * 8;
+    return bin_lds_bytes(F1) + (size_t)p1_tile(W) * 8 * W + (size_t)64 * (W + 1) * 8;
 }
 // nt: the level-2 workgroup (0 = p2f_threads_w; wide keys fall back to half of it when their
 // table's F2 does not fit beside the full tile, k_count_impl.h launch_p2f)

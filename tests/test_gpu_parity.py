@@ -586,3 +586,32 @@ def test_big_table_geometry(tmp_path, k):
     out = tmp_path / "oracle.txt"
     oracle_count(str(fa), k, ["-m", "2", "-a", "1"], out)
     assert sorted_digest_lines(lines) == sorted_digest_file(out)
+
+
+@pytest.mark.parametrize("slots", [200_000_000, 1_250_000_000])
+@pytest.mark.parametrize("k,seg", [(31, "default"), (25, "tiny"), (15, "default")])
+def test_six_byte_level2_records(tmp_path, k, seg, slots, monkeypatch):
+    """One-word keys in tables of >= 2^16 regions (C2's -s 2e8 rounds up to exactly 2^16; -s 1.25e9
+    gives 381 952, not a power of two) move 6-byte level-2 records (kc_count_impl.h StoreRec6:
+    32 low bits + the offset of the top half inside its region's range).  With tiny segments the
+    keys past their segment's end take the skew list beside them."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("KC_INSERT_PATH", "partitioned")
+    if seg == "tiny":
+        monkeypatch.setenv("KC_SEG_CAP", "64")
+        monkeypatch.setenv("KC_SPILL_CAP", str(1 << 24))
+    fa = tmp_path / "r.fasta"
+    subprocess.run([GEN, str(fa), "30000", "150", "200000", "-s", "5", "-n", "0.001"], check=True)
+    data = open(fa, "rb").read()
+    img = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+    with ka.KmerCounter(ka.Config(k=k, mode=2, min_abundance=1, table_slots=slots)) as kc:
+        kc.count_device(img.data_ptr(), ka.plan_chunks(data, k, ka.FMT_FASTA), ka.FMT_FASTA)
+        st = kc.finish()
+        assert st["part_fallbacks"] == 0
+        assert st["table_slots"] >= 65536 * 4096
+        if seg == "tiny":
+            assert st["spilled"] > 0
+        lines = kc.lines()
+    out = tmp_path / "oracle.txt"
+    oracle_count(str(fa), k, ["-m", "2", "-a", "1"], out)
+    assert sorted_digest_lines(lines) == sorted_digest_file(out)

@@ -212,6 +212,101 @@ static void bw(uint64_t bytes) {
     CK(hipFree(b));
 }
 
+
+// level 1 without the LDS sort: every key goes straight from its register to its bin's segment
+// at a position from a per-(workgroup, bin) LDS fill counter (no barriers, no tile in LDS);
+// the partial lines of neighbouring keys of a bin are merged in L2.  F bins (uniform hash),
+// tiles x 8192 keys per workgroup, 2048 workgroups of 512 threads.
+// MODE 0: direct scattered 8-byte stores; 1: wave-local counting sort through LDS first (runs
+// of a bin written by consecutive lanes), no workgroup barriers
+template <int MODE>
+__global__ __launch_bounds__(512, 4) void k_direct(uint64_t* out, int tiles, uint32_t F, uint64_t cap) {
+    extern __shared__ uint32_t sm[];
+    uint32_t* fill = sm;  // F counters
+    for (uint32_t b = threadIdx.x; b < F; b += 512) fill[b] = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t* wh = sm + F + wid * (2 * F + 2048 * 2);  // MODE 1: per wave: hist F, base F, keys 1024 x u64
+    uint64_t* wk = reinterpret_cast<uint64_t*>(wh + 2 * F);
+    uint64_t x = (blockIdx.x * 512ull + threadIdx.x) * 0x9E3779B97F4A7C15ULL;
+    for (int t = 0; t < tiles; t++) {
+        uint64_t v[16];
+        uint32_t b[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            x = x * 0xff51afd7ed558ccdULL + 0x632BE59BD9B4E019ULL;
+            v[j] = x;
+            b[j] = __umulhi((uint32_t)(x >> 32), F);
+        }
+        if constexpr (MODE == 0) {
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+                const uint32_t pos = atomicAdd(&fill[b[j]], 1u);
+                out[((uint64_t)b[j] * 2048 + blockIdx.x) * cap + pos] = v[j];
+            }
+        } else {
+            for (uint32_t i = lane; i < F; i += 64) wh[i] = 0;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            uint32_t rk[16];
+#pragma unroll
+            for (int j = 0; j < 16; j++) rk[j] = atomicAdd(&wh[b[j]], 1u);
+            // wave scan of the F counts (F / 64 per lane) + one fill atomic per (wave, bin)
+            uint32_t per = (F + 63) / 64, lo = lane * per, sum = 0;
+            for (uint32_t i = lo; i < lo + per && i < F; i++) sum += wh[i];
+            const uint32_t incl = wave_incl_sum(sum);
+            uint32_t run = incl - sum;
+            for (uint32_t i = lo; i < lo + per && i < F; i++) {
+                const uint32_t h = wh[i];
+                wh[F + i] = run;  // start of bin i in the wave's sorted block
+                wh[i] = h ? atomicAdd(&fill[i], h) : 0;  // destination of its first key
+                run += h;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+            for (int j = 0; j < 16; j++) wk[wh[F + b[j]] + rk[j]] = v[j] ^ ((uint64_t)b[j] << 48);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                const uint32_t i = q * 64 + lane;
+                const uint64_t key = wk[i];
+                const uint32_t bb = (uint32_t)(key >> 48) & 0xFFFF;  // (probe: the bin rides in the key)
+                const uint32_t pos = wh[bb] + (i - wh[F + bb]);
+                out[((uint64_t)bb * 2048 + blockIdx.x) * cap + pos] = key;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        }
+    }
+}
+static void direct() {
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (uint32_t F : {240u, 120u, 480u}) {
+        const int tiles = 72;
+        const uint64_t cap = ((uint64_t)tiles * 8192 / F * 5 / 4 + 15) / 16 * 16, n = (uint64_t)F * 2048 * cap;
+        uint64_t* o;
+        CK(hipMalloc(&o, n * 8));
+        for (int mode = 0; mode < 2; mode++) {
+            const size_t sm = mode ? (F + 8 * (2 * F + 4096)) * 4 : F * 4;
+            if (mode) CK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_direct<1>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm));
+            for (int rep = 0; rep < 2; rep++) {
+                CK(hipEventRecord(e0, 0));
+                if (mode == 0) k_direct<0><<<2048, 512, sm>>>(o, tiles, F, cap);
+                else k_direct<1><<<2048, 512, sm>>>(o, tiles, F, cap);
+                CK(hipEventRecord(e1, 0));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                const double bytes = 2048.0 * tiles * 8192 * 8;
+                printf("direct mode %d F %u: %.3f ms for %.2f GB = %.2f TB/s\n", mode, F, ms, bytes / 1e9,
+                       bytes / (ms * 1e-3) / 1e12);
+            }
+        }
+        CK(hipFree(o));
+    }
+}
+
 int main(int argc, char** argv) {
     if (argc > 1 && argv[1][0] == 'b') {
         bw(9600000000ULL);
@@ -219,6 +314,10 @@ int main(int argc, char** argv) {
     }
     if (argc > 1 && argv[1][0] == 't') {
         tilewr();
+        return 0;
+    }
+    if (argc > 1 && argv[1][0] == 'd') {
+        direct();
         return 0;
     }
     if (argc > 1 && argv[1][0] == 's') {
@@ -248,6 +347,7 @@ int main(int argc, char** argv) {
     t.f2bits = rbits - f1bits;
     t.F2 = 1u << t.f2bits;
     t.F1 = (uint32_t)((regions + t.F2 - 1) / t.F2);
+    if ((uint64_t)t.F1 * t.F2 >= 49152 && (uint64_t)t.F1 * t.F2 < 65536) t.F1 = (65536 + t.F2 - 1) / t.F2;  // alloc_table
     t.R = (uint64_t)t.F1 * t.F2;
     t.nbuckets = t.R * BPR;
     t.W = 1;
@@ -291,7 +391,7 @@ int main(int argc, char** argv) {
         h.stream_len = M;
         CK(hipMemcpy(ctr, &h, sizeof(h), hipMemcpyHostToDevice));
         CK(hipEventRecord(e0, 0));
-        CK(WOps<1>::count_partitioned(sv, k, 0, t, BloomView{}, ctr, pb, 1, 0));
+        CK(WOps<1>::count_partitioned(sv, k, 0, t, BloomView{}, ctr, pb, 1, 0, PH_ALL));
         CK(hipEventRecord(e1, 0));
         CK(hipEventSynchronize(e1));
         float ms = 0;
@@ -310,11 +410,11 @@ int main(int argc, char** argv) {
         DevCounters hc{};
         hc.stream_len = M;
         CK(hipMemcpy(ctr, &hc, sizeof(hc), hipMemcpyHostToDevice));
-        CK(WOps<1>::count_partitioned(sv, k, 0, t, BloomView{}, ctr, pb, 1, 0));
+        CK(WOps<1>::count_partitioned(sv, k, 0, t, BloomView{}, ctr, pb, 1, 0, PH_ALL));
         CK(hipDeviceSynchronize());
         CK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_stamp), sizeof(h)));
-        const char* ph[8] = {"before rank (extraction / prev)", "rank atomics", "barrier+scan", "placement",
-                             "setup", "mid+barrier", "write-out", "reset+barriers"};
+        const char* ph[8] = {"extraction+combine", "rank atomics", "barrier 1", "scan+barrier 2",
+                             "placement+setup", "barrier 3", "write-out", "-"};
         const int nb[3] = {(int)pb.nblk1, (int)(t.F1 * pb.B2), 2048};
         for (int part = 0; part < 3; part++) {
             if (part == 2) {  // level 3: 61440 workgroups folded onto 2048 slots; phases 0-3
