@@ -275,13 +275,30 @@ DEV void canonical(const uint64_t (&fwd)[W], const uint64_t (&rc)[W], uint64_t (
 }
 
 
+// Word sources of run_windows: the packed stream in HBM, or a workgroup's LDS stage of the
+// words [wb, wb + n) it covers (k_p1 loads the next tile's words while it scatters this one)
+struct PkGlobal {
+    const PackedView& sv;
+    DEV uint64_t pk(uint64_t w) const { return sv.pk[w]; }
+    DEV uint32_t bk(uint64_t w) const { return sv.bk[w]; }
+};
+struct PkStage {
+    const uint64_t* p;
+    const uint32_t* b;
+    int64_t wb;
+    DEV uint64_t pk(uint64_t w) const { return p[(int64_t)w - wb]; }
+    DEV uint32_t bk(uint64_t w) const { return b[(int64_t)w - wb]; }
+};
+
 // Table keys of the RUNW consecutive windows ending at r0 .. r0+RUNW-1: the state of
 // the window ending at r0-1 is extracted in O(1) (funnel shifts + the position of the
 // last break), then RUNW unrolled rolling steps (kmer_factory.cpp:172-239) produce the
 // rest, so every slot index is static.  ok[j] is false for windows that contain a
-// break or end at or beyond t1.
+// break or end at or beyond t1.  Reads words (r0 - k) / 32 - 1 .. r0 / 32 + 1 of sv.
 template <int W, int RUNW, class G>
-DEV void run_windows(const PackedView& sv, uint64_t r0, uint64_t t1, const RollConst& rk, G&& emit) {
+DEV void run_windows(const PackedView& sv, uint64_t r0, uint64_t t1, const RollConst& rk, G&& emit);
+template <int W, int RUNW, class Src, class G>
+DEV void run_windows_src(const Src& sv, uint64_t r0, uint64_t t1, const RollConst& rk, G&& emit) {
     static_assert(RUNW <= 32, "run must fit two packed words");
     const int k = rk.k;
     uint64_t fwd[W], rc[W];
@@ -296,10 +313,10 @@ DEV void run_windows(const PackedView& sv, uint64_t r0, uint64_t t1, const RollC
         } else {
             const uint64_t wl = (uint64_t)last >> 5;
             const int s = 2 * ((int)(last & 31) + 1);
-            uint64_t lo = sv.pk[wl];
+            uint64_t lo = sv.pk(wl);
 #pragma unroll
             for (int i = 0; i < W; i++) {
-                const uint64_t hi = wl >= (uint64_t)(i + 1) ? sv.pk[wl - i - 1] : 0;
+                const uint64_t hi = wl >= (uint64_t)(i + 1) ? sv.pk(wl - i - 1) : 0;
                 fwd[W - 1 - i] = s == 64 ? lo : ((hi << s) | (lo >> (64 - s)));
                 lo = hi;
             }
@@ -309,7 +326,7 @@ DEV void run_windows(const PackedView& sv, uint64_t r0, uint64_t t1, const RollC
             since = k;
             const int64_t wfirst = first < 0 ? 0 : (first >> 5);
             for (int64_t w = (int64_t)wl; w >= wfirst; w--) {
-                uint32_t m = sv.bk[w];
+                uint32_t m = sv.bk((uint64_t)w);
                 if (w == (int64_t)wl) m &= 0xFFFFFFFFu << (31 - (last & 31));
                 if (m) {
                     const int64_t q = (w << 5) + (31 - __builtin_ctz(m));  // highest-index break in word w
@@ -322,8 +339,8 @@ DEV void run_windows(const PackedView& sv, uint64_t r0, uint64_t t1, const RollC
         revcomp<W>(fwd, rk, rc);
     }
     const uint64_t wa = r0 >> 5;
-    const uint64_t pa = sv.pk[wa], pb = sv.pk[wa + 1];
-    const uint32_t ba = sv.bk[wa], bb = sv.bk[wa + 1];
+    const uint64_t pa = sv.pk(wa), pb = sv.pk(wa + 1);
+    const uint32_t ba = sv.bk(wa), bb = sv.bk(wa + 1);
     const int o0 = (int)(r0 & 31);
     if constexpr (W == 1) {
         // one-word keys: the run's RUNW incoming symbols and break bits are funnel-shifted
@@ -366,6 +383,11 @@ DEV void run_windows(const PackedView& sv, uint64_t r0, uint64_t t1, const RollC
             if (i == rk.rc_word) rc[i] |= (uint64_t)(3 - c) << rk.rc_bit;
         emit(j, r0 + j < t1 && since >= k, fwd, rc);
     }
+}
+
+template <int W, int RUNW, class G>
+DEV void run_windows(const PackedView& sv, uint64_t r0, uint64_t t1, const RollConst& rk, G&& emit) {
+    run_windows_src<W, RUNW>(PkGlobal{sv}, r0, t1, rk, emit);
 }
 
 }  // namespace kc

@@ -349,6 +349,15 @@ template <int W, int NT>
 constexpr int k1_runw() { return NT == scatter_threads_w(W) ? p1_runw(W) : run_w<W>(); }
 template <int W, int OW, int NT>
 constexpr size_t p1_smem(uint32_t F) { return bin_lds_bytes(F) + (size_t)NT * k1_runw<W, NT>() * 8 * OW; }
+// the segmented k_p1's LDS stage of the packed stream: two buffers of the words a tile reads
+// (kc_internal.h p1_stage_words), 8 + 4 bytes per word, after the heavy table
+#ifndef KC_P1_STAGE
+#define KC_P1_STAGE 1  // A/B: 0 = the windows read HBM directly
+#endif
+template <int W, int NT>
+constexpr int k1_stage_words() { return NT * k1_runw<W, NT>() / 32 + W + 3; }
+template <int W, int NT>
+constexpr size_t p1_stage_smem() { return (size_t)k1_stage_words<W, NT>() * 24; }
 // Level 2 runs one 1024-thread workgroup per CU for keys of up to two words: twice the
 // tile of level 1 (16384 one-word keys, 128 KiB of LDS) halves the barriers per key and
 // doubles the runs each bin gets per tile (C2: k_p2f 5.6 -> 5.0 ms on one box); wider
@@ -746,10 +755,11 @@ DEV uint64_t rec6_key(uint64_t raw, bool odd, uint32_t xlo) {
     return ((uint64_t)(xlo + d) << 32) | (uint32_t)raw;
 }
 
-template <int W, int RUNW, class Bin, class Out, int NT, class Mid = NoMid, class St = StoreWords>
+// pre(): called after the rank atomics (k_p1 issues the loads of its next tile's words there)
+template <int W, int RUNW, class Bin, class Out, int NT, class Mid = NoMid, class St = StoreWords, class Pre = NoMid>
 DEV void scatter_seg(const PartLds& l, uint32_t F, const Bin& bin, const Out& o, uint64_t (&tk)[RUNW][W],
                      bool (&ok)[RUNW], uint64_t* __restrict__ out, Mid&& mid = Mid(), Stamps* stp = nullptr,
-                     const St& store = St()) {
+                     const St& store = St(), Pre&& pre = Pre()) {
     static_assert(NT * RUNW <= 65536, "ranks ride in 16 bits");
     __shared__ unsigned long long s_spbase;
     __shared__ uint32_t s_spills, s_n;
@@ -761,20 +771,40 @@ DEV void scatter_seg(const PartLds& l, uint32_t F, const Bin& bin, const Out& o,
         const uint32_t b = bin(tk[j][0]);
         pk[j] = ok[j] ? (b << 16) | atomicAdd(&l.hist[b], 1u) : ~0u;
     }
+    pre();
     if (KC_STAMP && stp) stp->mark(1);
     __syncthreads();  // 1
     if (KC_STAMP && stp) stp->mark(2);
     if (tid < 64) {
-        const uint32_t per = (F + 63) / 64, lo = min(F, lane * per), hi = min(F, lo + per);
-        uint32_t sum = 0;
-        for (uint32_t i = lo; i < hi; i++) sum += l.hist[i];
-        const uint32_t incl = wave_incl_sum(sum);
-        uint32_t run = incl - sum;
-        for (uint32_t i = lo; i < hi; i++) {
-            l.start[i] = run;
-            run += l.hist[i];
+        if (F % 4 == 0) {  // (hist and start 16-byte aligned) four bins per 16-byte LDS access
+            const uint32_t per = (F / 4 + 63) / 64, lo = min(F / 4, lane * per), hi = min(F / 4, lo + per);
+            const uint4* h4 = reinterpret_cast<const uint4*>(l.hist);
+            uint4* s4 = reinterpret_cast<uint4*>(l.start);
+            uint32_t sum = 0;
+            for (uint32_t i = lo; i < hi; i++) {
+                const uint4 v = h4[i];
+                sum += v.x + v.y + v.z + v.w;
+            }
+            const uint32_t incl = wave_incl_sum(sum);
+            uint32_t run = incl - sum;
+            for (uint32_t i = lo; i < hi; i++) {
+                const uint4 v = h4[i];
+                s4[i] = make_uint4(run, run + v.x, run + v.x + v.y, run + v.x + v.y + v.z);
+                run += v.x + v.y + v.z + v.w;
+            }
+            if (lane == 63) s_n = incl;
+        } else {
+            const uint32_t per = (F + 63) / 64, lo = min(F, lane * per), hi = min(F, lo + per);
+            uint32_t sum = 0;
+            for (uint32_t i = lo; i < hi; i++) sum += l.hist[i];
+            const uint32_t incl = wave_incl_sum(sum);
+            uint32_t run = incl - sum;
+            for (uint32_t i = lo; i < hi; i++) {
+                l.start[i] = run;
+                run += l.hist[i];
+            }
+            if (lane == 63) s_n = incl;
         }
-        if (lane == 63) s_n = incl;
         if (Out::kSeg && lane == 0) s_spills = 0;
     }
     __syncthreads();  // 2
@@ -1047,6 +1077,25 @@ __global__ __launch_bounds__(NT, NT >= 1024 ? 8 : 4) void k_p1(PackedView sv, in
     const uint64_t M = ctr->stream_len;
     const uint64_t per = ((M + pb.nblk1 - 1) / pb.nblk1 + TW - 1) / TW * TW;
     const uint64_t lo = min(M, (uint64_t)blockIdx.x * per), hi = min(M, lo + per);
+    // Segmented count / Bloom passes read a tile's words from an LDS stage: the words of the
+    // next tile are loaded while this one is scattered (its rank atomics issue the loads, its
+    // placement stores them), so the windows of a tile start without waiting for HBM.  Tile
+    // t0 reads words (t0 >> 5) - W - 1 .. (t0 + TW) >> 5 (run_windows, t0 a multiple of 32).
+    constexpr bool STAGE = KC_P1_STAGE && Out::kSeg && !ROLLED;
+    constexpr int SW = k1_stage_words<W, NT>();
+    static_assert(!STAGE || SW <= NT, "one stage word per thread");
+    uint64_t* st_pk = reinterpret_cast<uint64_t*>(smem + p1_smem<W, OW, NT>(F) + heavy_smem<OW>());
+    uint32_t* st_bk = reinterpret_cast<uint32_t*>(st_pk + 2 * SW);
+    const uint64_t wlim = M ? ((M - 1) >> 5) + 1 : 0;  // the last word run_windows may read
+    auto stage_word = [&](uint64_t ts, int i, uint64_t& pw, uint32_t& bw) {
+        const int64_t w = (int64_t)(ts >> 5) - (W + 1) + i;
+        const bool in = w >= 0 && (uint64_t)w <= wlim;
+        pw = in ? sv.pk[w] : 0;
+        bw = in ? sv.bk[w] : 0;
+    };
+    if constexpr (STAGE)
+        if (lo < hi && tid < SW) stage_word(lo, tid, st_pk[tid], st_bk[tid]);
+    int par = 0;  // the stage buffer of the current tile
     Out ob = o;
     if constexpr (Out::kSeg) ob.base = (uint64_t)blockIdx.x * o.cap;  // segment (b, block) = b * nblk1 + block
     for (uint32_t b = tid; b < F; b += NT) {
@@ -1070,16 +1119,21 @@ __global__ __launch_bounds__(NT, NT >= 1024 ? 8 : 4) void k_p1(PackedView sv, in
             const uint64_t r0 = t0 + (uint64_t)tid * RUNW;
 #pragma unroll
             for (int j = 0; j < RUNW; j++) ok[j] = false;
-            if (r0 < t1)
-                run_windows<W, RUNW>(sv, r0, t1, rk,
-                                     [&](int j, bool valid, const uint64_t (&fwd)[W], const uint64_t (&rc)[W]) {
-                    uint64_t key[W], t[W];
-                    canonical<W>(fwd, rc, key);
-                    to_tkey<W>(key, t);
+            auto emit = [&](int j, bool valid, const uint64_t (&fwd)[W], const uint64_t (&rc)[W]) {
+                uint64_t key[W], t[W];
+                canonical<W>(fwd, rc, key);
+                to_tkey<W>(key, t);
 #pragma unroll
-                    for (int w = 0; w < OW; w++) tk[j][w] = t[w];
-                    ok[j] = valid;
-                });
+                for (int w = 0; w < OW; w++) tk[j][w] = t[w];
+                ok[j] = valid;
+            };
+            if (r0 < t1) {
+                if constexpr (STAGE)
+                    run_windows_src<W, RUNW>(PkStage{st_pk + par * SW, st_bk + par * SW, (int64_t)(t0 >> 5) - (W + 1)},
+                                             r0, t1, rk, emit);
+                else
+                    run_windows<W, RUNW>(sv, r0, t1, rk, emit);
+            }
             if constexpr (COUNTS) {
 #pragma unroll
                 for (int j = 0; j < RUNW; j++) {
@@ -1111,9 +1165,26 @@ __global__ __launch_bounds__(NT, NT >= 1024 ? 8 : 4) void k_p1(PackedView sv, in
             });
         }
         if constexpr (SCATTER) {
-            if constexpr (Out::kSeg)
-                scatter_seg<OW, RUNW, Bin, Out, NT>(l, F, bin, ob, tk, ok, out, NoMid(), &stp);
-            else scatter_tile<OW, RUNW, Bin, Out, NT>(l, F, bin, ob, tk, ok, out, NoMid(), &stp);
+            if constexpr (Out::kSeg) {
+                const bool nxt = STAGE && t0 + TW < hi && tid < SW;
+                uint64_t npk = 0;
+                uint32_t nbk = 0;
+                scatter_seg<OW, RUNW, Bin, Out, NT>(
+                    l, F, bin, ob, tk, ok, out,
+                    [&]() {  // placement phase: the next tile's words into the other buffer
+                        if (nxt) {
+                            st_pk[(par ^ 1) * SW + tid] = npk;
+                            st_bk[(par ^ 1) * SW + tid] = nbk;
+                        }
+                    },
+                    &stp, StoreWords(),
+                    [&]() {  // after the rank atomics: load them
+                        if (nxt) stage_word(t0 + TW, tid, npk, nbk);
+                    });
+                par ^= 1;
+            } else {
+                scatter_tile<OW, RUNW, Bin, Out, NT>(l, F, bin, ob, tk, ok, out, NoMid(), &stp);
+            }
         } else {
 #pragma unroll
             for (int j = 0; j < RUNW; j++)
@@ -2453,7 +2524,8 @@ static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf
     }();
     const size_t p1_lds_min = p1_lds_knob >= 0 ? std::min(LDS_BYTES, (size_t)p1_lds_knob)
                               : (size_t)p1_tile(W) < 8 * (size_t)t.F1 ? LDS_BYTES / 2 + 16 : 0;
-    const size_t sm1 = std::max(p1_lds_min, p1_smem<W, W, scatter_threads<W>()>(t.F1) + heavy_smem<W>());
+    const size_t sm1 = std::max(p1_lds_min, p1_smem<W, W, scatter_threads<W>()>(t.F1) + heavy_smem<W>() +
+                                                p1_stage_smem<W, scatter_threads<W>()>());
     if ((e = set_smem(k1, sm1)) != hipSuccess) return e;
     const OutSeg o1{(uint64_t)pb.nblk1 * pb.cap1, 0, pb.cap1, pb.spill, pb.spill_cap, &ctr->spill_n,
                     &ctr->part_overflow, 1};
@@ -2513,7 +2585,7 @@ static hipError_t bloom_part_w(PackedView sym, int k, BloomView bf, TableView ft
     constexpr int NT = scatter_threads<W>(), NT2 = p2f_threads<OW>();
     auto k1 = k_p1<W, MODE, true, BinRegion, OutSeg, NT>;
     auto k2 = k_p2f<OW, NT2>;
-    const size_t sm1 = p1_smem<W, OW, NT>(lg.F1) + heavy_smem<OW>(),
+    const size_t sm1 = p1_smem<W, OW, NT>(lg.F1) + heavy_smem<OW>() + p1_stage_smem<W, NT>(),
                  sm2 = p2f_smem<OW, NT2>(lg.F2, (pb.nblk1 + pb.B2 - 1) / pb.B2);
     if ((e = set_smem(k1, sm1)) != hipSuccess) return e;
     if ((e = set_smem(k2, sm2)) != hipSuccess) return e;

@@ -157,9 +157,11 @@ constexpr int p1_tile(int W) { return scatter_threads_w(W) * p1_runw(W); }  // w
 // tile's keys after them at a 16-byte boundary) and its static extras
 constexpr size_t bin_lds_bytes(uint32_t F) { return ((size_t)F * 24 + 15) / 16 * 16 + 16; }
 constexpr int p2f_threads_w(int W) { return KC_P2F_NT ? KC_P2F_NT : (W <= 2 ? 1024 : W <= 4 ? 512 : 256); }
-// segmented level 1 (k_p1, W-word output keys + the heavy table) for F1 coarse bins
+// k_p1's LDS stage of the packed stream: two buffers of the words one tile reads, 12 bytes each
+constexpr size_t p1_stage_bytes(int W) { return (size_t)(p1_tile(W) / 32 + W + 3) * 24; }
+// segmented level 1 (k_p1, W-word output keys + the heavy table + the stage) for F1 coarse bins
 constexpr size_t p1_lds_bytes(int W, uint32_t F1) {
-    return bin_lds_bytes(F1) + (size_t)p1_tile(W) * 8 * W + (size_t)64 * (W + 1) * 8;
+    return bin_lds_bytes(F1) + (size_t)p1_tile(W) * 8 * W + (size_t)64 * (W + 1) * 8 + p1_stage_bytes(W);
 }
 // nt: the level-2 workgroup (0 = p2f_threads_w; wide keys fall back to half of it when their
 // table's F2 does not fit beside the full tile, k_count_impl.h launch_p2f)
