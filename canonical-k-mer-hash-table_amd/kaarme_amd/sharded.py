@@ -77,6 +77,12 @@ def exchange(dist, keys, counts: Sequence[int], W: int, group=None, chunk_words:
     world = len(counts)
     if world == 1:  # nothing leaves the rank
         return (keys, int(counts[0]), [int(counts[0])]) if with_counts else (keys, int(counts[0]))
+    if _host_staged(dist, group, keys):
+        # gloo moves host tensors only: the items cross through host memory (tests with several
+        # ranks on one GPU; RCCL moves device memory directly)
+        res = exchange(dist, keys.cpu(), counts, W, group, chunk_words, True, verify)
+        out = res[0].to(dev)
+        return (out, res[1], res[2]) if with_counts else (out, res[1])
     sw = [int(c) * W for c in counts]
     so = [sum(sw[:d]) for d in range(world)]
 
@@ -132,6 +138,8 @@ def all_gather_words(dist, mine, world: int, group=None, chunk_words: int = 0):
     import torch
 
     chunk_words = chunk_words or 2 * chunk_words_default()
+    if world > 1 and _host_staged(dist, group, mine):
+        return all_gather_words(dist, mine.cpu(), world, group, chunk_words).to(mine.device)
     per = mine.numel()
     full = torch.empty(world * per, dtype=mine.dtype, device=mine.device)
     if world == 1:
@@ -158,6 +166,11 @@ def all_gather_words(dist, mine, world: int, group=None, chunk_words: int = 0):
 
 def _gather_into_tensor(dist, group) -> bool:
     return hasattr(dist, "all_gather_into_tensor") and dist.get_backend(group) != "gloo"
+
+
+def _host_staged(dist, group, t) -> bool:
+    """Device tensors over gloo (which collects host tensors only) go through host memory."""
+    return t.is_cuda and dist.get_backend(group) == "gloo"
 
 
 def _on_stream(device: str, stream: int):

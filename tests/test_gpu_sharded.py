@@ -6,12 +6,13 @@ The per-rank outputs must be disjoint and their union must equal the oracle's co
 the whole input (bit-exact sorted output).  The same ranks over RCCL are what bench.py
 runs at N > 1; tests/test_sharded.py covers the collective itself over gloo.
 """
+import os
 import subprocess
 
 import pytest
 import torch
 
-from conftest import GEN, oracle_count, sorted_digest_file, sorted_digest_lines
+from conftest import GEN, REPO, oracle_count, sorted_digest_file, sorted_digest_lines
 import kaarme_amd as ka
 from kaarme_amd.sharded import DeviceEngine
 
@@ -352,3 +353,36 @@ def test_sharded_counter_bloom_one_rank(tmp_path, k):
     out = tmp_path / "oracle.txt"
     oracle_count(str(fa), k, ["-m", "2", "-a", "2"], out)
     assert sorted_digest_lines(sc.lines()) == sorted_digest_file(out)
+
+
+@pytest.mark.parametrize("G", [2, 4, 8])
+def test_sharded_bloom_excess_at_design_load(tmp_path, G):
+    """the combined filter decides 'seen twice' bit by bit, so a k-mer seen once passes
+    the gate when each of its filter-1 positions is also set on another rank by other k-mers --
+    about (1 - (1 - rho)^(G - 1))^h at filter-1 fill rho.  With -u equal to the true distinct
+    count (rho ~ 1/2, the filter's design load) the counts of k-mers seen at least twice stay
+    exact; the singletons that reach the owner tables are measured here
+    and written to gpurun_out/bloom_excess_G<G>.json."""
+    import json
+
+    out = tmp_path / "oracle.txt"
+    # the whole input's distinct k-mers (the estimate a user would pass as -u)
+    n_reads, genome = 16000, 40000
+    fa = tmp_path / "whole.fasta"
+    subprocess.run([GEN, str(fa), str(n_reads), "150", str(genome)], check=True)
+    oracle_count(str(fa), 31, ["-m", "2", "-a", "1"], out)
+    distinct = sorted_digest_file(out)[1]
+    engines, whole, nis, full = _emulated_bloom_job(tmp_path, 31, 2, G, n_reads, genome, distinct)
+    lines = set().union(*[set(e.owner_table().lines()) for e in engines])
+    owner_distinct = sum(e.owner_table().finish()["distinct"] for e in engines)
+    oracle_count(str(whole), 31, ["-m", "2", "-a", "2"], out)
+    solid = sorted_digest_file(out)
+    assert sorted_digest_lines(lines) == solid
+    singletons = distinct - solid[1]
+    excess = (owner_distinct - solid[1]) / max(1, singletons)
+    os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(REPO, "gpurun_out", f"bloom_excess_G{G}.json"), "w") as f:
+        json.dump({"G": G, "distinct": distinct, "solid": solid[1], "owner_distinct": owner_distinct,
+                   "singletons_passed_frac": excess, "nis": nis}, f)
+    for e in engines:
+        e.close()
