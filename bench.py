@@ -75,10 +75,14 @@ def cpu_baseline(args):
     kind = "reference" if os.path.exists(ref) else ("port" if os.path.exists(orc) else None)
     if kind is None:
         return None
-    # about 150 M bases (10-30 s of reference work on a 16-core share)
+    # about 150 M bases (10-30 s of reference work on a 16-core share), from a genome scaled with
+    # the sample so that its coverage is the workload's (a 1 M-read sample of the
+    # 50 Mbp genome is a 3x-coverage input, a different workload for the reference's chains)
     n = max(1, args.cpu_sample_bases // args.read_len)
     if kind == "port":
         n = max(1, n // 20)
+    n = min(n, args.reads)
+    genome = max(10 * args.read_len, round(args.genome * n / args.reads))
     # The box gives one GPU's job a 16-core share of a larger host (OMP_NUM_THREADS is set to
     # it; the affinity mask still lists every CPU).  -t = share + 2: share hashing workers plus
     # the IO thread (main.cpp:383).
@@ -88,8 +92,8 @@ def cpu_baseline(args):
         fa = os.path.join(td, "sample.fasta")
         sk = PRESETS[args.config].get("skew")
         skew_args = (["--homo", str(sk[0]), "--dinuc", str(sk[1]), "--repeat", str(sk[2]), str(sk[3])] if sk else [])
-        subprocess.run([gen, fa, str(args.reads), str(args.read_len), str(args.genome), "-s", str(args.seed),
-                        "-e", str(args.err), "--first", "0", "--count", str(n)] + skew_args, check=True)
+        subprocess.run([gen, fa, str(n), str(args.read_len), str(genome), "-s", str(args.seed),
+                        "-e", str(args.err)] + skew_args, check=True)
         with open(fa, "rb") as f:  # pre-warm the page cache
             while f.read(1 << 24):
                 pass
@@ -130,9 +134,11 @@ def cpu_baseline(args):
     return {"value": windows / secs, "unit": "k-mers/s", "cores": cores, "kind": kind, "e2e": e2e,
             "attempts": 1 + len(failures), "failed_exit_codes": failures, "cpu_model": cpu_model(),
             "nproc": os.cpu_count(), "core_share": share,
-            "sample": f"first {n} reads of the same generator ({windows} windows, k={args.k}, "
-                      f"-m 2 {' '.join(targs)} -t {threads}, {secs:.2f} s counting time"
-                      f"{' incl. the Bloom pass' if args.unique else ''})"}
+            "coverage": round(n * args.read_len / genome, 2),
+            "workload_coverage": round(args.reads * args.read_len / args.genome, 2),
+            "sample": f"{n} reads of the same generator on a {genome}-base genome (the workload's coverage; "
+                      f"{windows} windows, k={args.k}, -m 2 {' '.join(targs)} -t {threads}, {secs:.2f} s counting "
+                      f"time{' incl. the Bloom pass' if args.unique else ''})"}
 
 
 def cli_e2e(fasta, cli_args, windows):
@@ -168,18 +174,30 @@ def cpu_model():
     return None
 
 
+def kernel_source_digest():
+    """SHA-256 (16 hex) of the engine's kernel and host sources: what a PMC summary was measured with."""
+    import hashlib
+    h = hashlib.sha256()
+    src = os.path.join(PKG, "csrc")
+    for name in sorted(os.listdir(src)):
+        with open(os.path.join(src, name), "rb") as f:
+            h.update(name.encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
+
+
 def load_traffic(workload):
-    """HBM bytes per roofline launch of this workload from the committed rocprofv3 PMC summary, if any."""
+    """(HBM bytes per roofline launch, entry) of this workload from the committed rocprofv3 PMC
+    summary profiles/pmc_traffic.json, if any."""
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        if d.get("workload") == workload:  # single-workload layout
-            return d.get("bytes_per_launch")
-        return d.get("workloads", {}).get(workload, {}).get("bytes_per_launch")
+        e = d.get("workloads", {}).get(workload)
+        if e:
+            return e.get("bytes_per_launch"), e
     except (OSError, ValueError):
         pass
-    return None
+    return None, None
 
 
 def resolve(args, name):
@@ -419,7 +437,8 @@ def run_workload(args, env, image=None):
         count_ms = tm["count_ms"] / pairs
         units_per_step = pairs / args.steps
     achieved = bytes_per_launch / (count_ms * 1e-3) / 1e9
-    traffic = load_traffic(workload)
+    traffic, tentry = load_traffic(workload)
+    traffic_stale = bool(tentry) and tentry.get("source_sha") != kernel_source_digest()
     if dist:
         kname = "local count pass + merge insert of the received {key, count} records"
     elif args.unique:
@@ -432,9 +451,12 @@ def run_workload(args, env, image=None):
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": kname,
                 "kernel_ms": round(count_ms, 4), "algorithmic_bytes_per_launch": int(bytes_per_launch)}
     if traffic:
-        # the bytes this design moves (rocprofv3 PMC, profiles/pmc_traffic.json) over the same time
+        # the bytes this design moves (rocprofv3 PMC, profiles/pmc_traffic.json) over the same time;
+        # stale = measured with other kernel sources than these (the entry's source_sha)
         roofline["traffic_gbs"] = round(traffic / (count_ms * 1e-3) / 1e9, 2)
         roofline["traffic_frac"] = round(traffic / (count_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+        roofline["traffic_source"] = {"stale": traffic_stale, "source_sha": tentry.get("source_sha"),
+                                      "commit": tentry.get("commit")}
     step_ms = elapsed / args.steps * 1e3
     out = {
         "metric": METRIC, "value": value, "unit": "k-mers/s", "n_gpus": world, "steps": args.steps,

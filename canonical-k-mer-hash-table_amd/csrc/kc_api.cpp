@@ -455,9 +455,9 @@ static hipStream_t pick_stream(kc_ctx* c, void* s) {
 // behind the device overflow gate) does nothing unless the single-pass levels left a skew list
 // or overflowed.  For device images the host reads those two counters after the main phase
 // (the call waits for its batch) and launches the tail only when needed: ~20 idle kernel
-// launches and two region-grid passes less per batch (0.25 ms of C2's 15.9 ms step).  Host
-// chunks keep the device gate (their staging overlaps the previous batch).  KC_DEVICE_GATE=1
-// forces the device gate everywhere.
+// launches and two region-grid passes less per batch (0.25 ms of C2's 15.9 ms step).  Images
+// of several batches and host chunks keep the device gate (their batches queue behind each
+// other).  KC_DEVICE_GATE=1 forces the device gate everywhere.
 static int tail_needed(kc_ctx* c, hipStream_t s, bool* need) {
     unsigned long long f[2] = {0, 0};
     HIPCHK(c, hipMemcpyAsync(&f[0], &c->d_ctr->part_overflow, 8, hipMemcpyDeviceToHost, s));
@@ -741,17 +741,19 @@ static int device_pass(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, si
     }
     std::vector<ChunkDesc> batch;
     uint64_t used = 0;
-    // level-1 reuse: the Bloom pass keeps its level-1 output if it is the job's only batch
-    bool keep = false;
-    if (pass == 1 && c->bloom_batches == 0 && reuse_enabled()) {
+    // one staging batch holds the whole image?
+    bool single = false;
+    {
         uint64_t tot = 0, cnt = 0;
         for (size_t i = 0; i < n; i++)
             if (chunks[i].len) {
                 tot += round_up(chunks[i].len, TILE);
                 cnt++;
             }
-        keep = cnt > 0 && tot <= c->batch_bytes && cnt <= c->max_chunks;
+        single = cnt > 0 && tot <= c->batch_bytes && cnt <= c->max_chunks;
     }
+    // level-1 reuse: the Bloom pass keeps its level-1 output if it is the job's only batch
+    const bool keep = pass == 1 && c->bloom_batches == 0 && reuse_enabled() && single;
     auto launch = [&]() -> int {
         if (batch.empty()) return KC_OK;
         // descriptors go through the (idle) pinned desc buffer of the current slot
@@ -767,7 +769,9 @@ static int device_pass(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, si
         }
         // the image is tokenized in place (no gather into the stage): "gather" is ~0
         if (c->profiling) HIPCHK(c, hipEventRecord(e1, s));
-        int r = run_batch(c, img, used, batch.size(), fmt, pass, s, e0, e1, keep, true);
+        // the host gate of the batch's tail (the call waits for the batch) only for a one-batch
+        // image; the batches of a larger image keep the device gate (kc_api.h: kc_count_device)
+        int r = run_batch(c, img, used, batch.size(), fmt, pass, s, e0, e1, keep, single);
         if (r) return r;
         if (keep && c->reuse_kept) {  // what a counting pass must present again, and its checksum
             c->reuse_img = img;

@@ -116,6 +116,14 @@ int kc_count_chunk(kc_ctx* ctx, const uint8_t* buf, size_t len, int fmt, int bro
  * stream) after the work already queued there, so a buffer produced on that stream
  * (e.g. by PyTorch on its current stream) is safe to pass.  The image must stay valid
  * until the work completes (kc_sync).  Every *_device entry point follows this rule.
+ * Host waits inside these two calls (the work is still ordered on hip_stream):
+ *   - an image that fits one staging batch (kc_config.batch_bytes): the call returns once
+ *     the batch's single-pass levels have run -- it reads two device counters (skew list,
+ *     segment overflow) to launch the batch's fallback work only when it is needed;
+ *   - an image of several batches: before batch i+1 is queued, the call waits until batch i's
+ *     chunk descriptors have reached the device (queued after the work before it), so at most
+ *     one batch is queued ahead; the fallback work stays behind a device-side gate;
+ *   - the counting pass that reuses the Bloom pass's partitions waits for its work (below).
  * Level-1 reuse: when the Bloom pass is one staging batch, it keeps its window
  * partition, and a counting pass given the same image pointer, chunk table and format
  * -- and the same bytes, checked by a checksum of the chunks -- starts from that

@@ -23,6 +23,9 @@ COUNT_PASS = ("k_p1<", "k_p2<", "k_p2f<", "k_p3<", "k_b3<", "k_scanA", "k_scanB"
 # reads device images in place), i.e. the counters are in KiB.
 KIB_CALIBRATED = 1024.0
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import kernel_source_digest  # noqa: E402
+
 
 def short(name):
     n = name.split("(")[0].replace("void ", "").replace("kc::", "")
@@ -95,6 +98,9 @@ def main():
             book.setdefault(old["workload"], {c: v for c, v in old.items() if c != "workload"})
         book[bench["config"]["workload"]] = {
             "bytes_per_launch": int(total), "unit_bytes": unit,
+            # the kernel sources this was measured with (bench.py marks the entry stale when
+            # the sources differ) and the commit, when the caller passes it (KC_COMMIT)
+            "source_sha": kernel_source_digest(), "commit": os.environ.get("KC_COMMIT"),
             "method": "2*FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md HBM), unit calibrated on k_gather 16-B "
                       "stores; count-pass kernels (with -b: Bloom pass + counting pass) summed per launch",
             "per_kernel": per_kernel}

@@ -179,5 +179,6 @@ def test_committed_traffic_book_covers_the_bench_workloads():
     spec.loader.exec_module(bench)
     for name in ("c2", "c3", "c4s", "c5s"):
         line = json.load(open(os.path.join(root, "profiles", f"r01_v11_bench_{name}.json")))
-        got = bench.load_traffic(line["config"]["workload"])
+        got, entry = bench.load_traffic(line["config"]["workload"])
         assert got and got > line["roofline"]["algorithmic_bytes_per_launch"] * 0.5, name
+        assert entry["bytes_per_launch"] == got
