@@ -436,6 +436,7 @@ def run_workload(args, env, image=None):
                             + windows_step * p_gate * ((1 + u) * K + 8)) * args.steps / pairs
         count_ms = tm["count_ms"] / pairs
         units_per_step = pairs / args.steps
+        filter_rmw = windows_step * (8 * nh + 4 * nh_gate) * args.steps / pairs
     achieved = bytes_per_launch / (count_ms * 1e-3) / 1e9
     traffic, tentry = load_traffic(workload)
     traffic_stale = bool(tentry) and tentry.get("source_sha") != kernel_source_digest()
@@ -450,6 +451,14 @@ def run_workload(args, env, image=None):
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": kname,
                 "kernel_ms": round(count_ms, 4), "algorithmic_bytes_per_launch": int(bytes_per_launch)}
+    if args.unique:
+        # the same without SURVEY 8d's per-window filter-word RMWs (ceil(hf) 8-byte
+        # pass-1 RMWs and trunc(hf) 4-byte pass-2 tests), which the blocked filter never performs
+        # (k_b3 sweeps each 64 KiB filter region once per pass instead)
+        b2 = bytes_per_launch - filter_rmw
+        roofline["without_filter_rmw"] = {"achieved": round(b2 / (count_ms * 1e-3) / 1e9, 2),
+                                          "frac": round(b2 / (count_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+                                          "algorithmic_bytes_per_launch": int(b2)}
     if traffic:
         # the bytes this design moves (rocprofv3 PMC, profiles/pmc_traffic.json) over the same time;
         # stale = measured with other kernel sources than these (the entry's source_sha)

@@ -525,6 +525,24 @@ static int run_batch(kc_ctx* c, const uint8_t* src, uint64_t used, uint64_t nchu
             c->pbf.keep_fill = c->d_keep_fill;
             c->pbf.keep_fill2 = c->d_keep_fill2;
         }
+        // two-word keys: the kept levels as 12-byte records (kc_count_impl.h Rec12) when a record
+        // holds the table key's bits below its bin: hb + 1 + xb <= 32 at both levels
+        c->pbf.rec12 = 0;
+        if (keep && c->W == 2 && !std::getenv("KC_NO_REC12")) {
+            int f1 = 0, rb = 0;
+            while ((1u << f1) < c->fgeo.F1) f1++;
+            while ((1ULL << rb) < c->fgeo.R) rb++;
+            const int hb = std::max(0, 2 * c->cfg.k - 96);
+            int b2s = 0;
+            while ((1u << b2s) < c->pbf.B2) b2s++;
+            if (hb + 1 + (32 - f1) <= 32 && hb + 1 + (32 - rb) <= 32 && f1 >= 1 && (1u << b2s) == c->pbf.B2) {
+                c->pbf.rec12 = R12_P1 | R12_IN | R12_OUT | R12_L2;
+                c->pbf.r12_hb = hb;
+                c->pbf.r12_xb1 = 32 - f1;
+                c->pbf.r12_xb2 = 32 - rb;
+                c->pbf.r12_b2s = b2s;
+            }
+        }
         const bool split = host_gate && c->pbf.cap1 != 0;
         HIPCHK(c, launch_bloom_partitioned(sv, c->cfg.k, c->W, bv, c->bgeo, c->fgeo, c->d_ctr, c->pbf,
                                            c->bloom_fresh, keep ? 1 : 0, s, split ? PH_MAIN : PH_ALL));
@@ -693,6 +711,13 @@ static int count_reused(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, s
         return KC_OK;
     }
     pr.hist1 = c->d_keep_fill;
+    // the kept records' format: level 2 read by level 3, or level 1 read by level 2 (which then
+    // writes whole keys in the table's own geometry)
+    pr.rec12 = c->pbf.rec12 ? (c->reuse_level == 2 ? R12_L2 : R12_IN) : 0;
+    pr.r12_hb = c->pbf.r12_hb;
+    pr.r12_xb1 = c->pbf.r12_xb1;
+    pr.r12_xb2 = c->pbf.r12_xb2;
+    pr.r12_b2s = c->pbf.r12_b2s;
     if (c->reuse_level == 2) {  // a table region = fgeo.R / R consecutive fine bins
         pr.hist2 = c->d_keep_fill2;
         pr.cap2 = c->pbf.cap2;

@@ -28,18 +28,26 @@ DEV uint64_t fmix64(uint64_t k) {
 }
 
 // ---- table keys -------------------------------------------------------------------
-// The table stores the canonical key through a bijection ("tkey"): word 0 becomes
-// tmix(key0 ^ MIX_C ^ (g & M62)), g = a hash of the other words; words 1.. are kept.
-// tmix(x) = y ^ (y >> 32) with y = x * TMUL (odd, so both steps are bijections): one
-// 64-bit multiply per window.  The top bits of y (regions, buckets, coarse bins) depend
-// on every bit of x; the low half (shard owner) is folded with the high half.  The hash
-// is computed once per window, every later level is a bit field of tkey word 0, and
-// k_dump inverts the mix.  key0 < 2^62 and MIX_C has bit 63 set, so the tmix argument
-// is never 0 and neither is tkey word 0 (tmix(x) = 0 only for x = 0): 0 marks an empty slot.
+// The table stores the canonical key through a bijection ("tkey"), word 0 a strong mix of the
+// whole key and never 0 (0 marks an empty slot):
+//   W = 1:  t0 = tmix(key0 ^ MIX_C)
+//   W >= 2: t0 = tmix(x), x = key[W-1] ^ g(key[0..W-2]); t1 = key0; t[i] = key[i-1] (i >= 2)
+//           (x = 0 is stored as tmix(TK_ZERO) with TK_FLAG set in t1)
+// tmix(x) = y ^ (y >> 32) with y = x * TMUL (odd, so both steps are bijections): one 64-bit
+// multiply per window.  The top bits of y (regions, buckets, coarse bins) depend on every bit
+// of x; the low half (shard owner) is folded with the high half.  For W >= 2 the last key word
+// (the newest 32 characters) goes through the mix and word 1 keeps key word 0, which holds only
+// the 2k - 64(W-1) <= 62 oldest-character bits: a level record of a two-word key needs t0's
+// bits below its bin plus those bits (kc_count_impl.h Rec12).  The hash is computed once per
+// window, every later level is a bit field of tkey word 0, and k_dump inverts the mix.
+// W = 1: key0 < 2^62 and MIX_C has bit 63 set, so the tmix argument is never 0 and neither is
+// t0 (tmix(x) = 0 only for x = 0).
 constexpr uint64_t MIX_C = 0x9E3779B97F4A7C15ULL;  // bit 63 set
 constexpr uint64_t M62 = (1ULL << 62) - 1;
 constexpr uint64_t TMUL = 0x9E3779B97F4A7C15ULL;      // odd
 constexpr uint64_t TMUL_INV = 0xF1DE83E19937733DULL;  // TMUL * TMUL_INV = 1 (mod 2^64)
+constexpr uint64_t TK_ZERO = 0x6A09E667F3BCC909ULL;   // the stand-in of a zero mix argument
+constexpr uint64_t TK_FLAG = 1ULL << 62;              // t1: the mix argument was 0
 
 DEV uint64_t tmix(uint64_t x) {
     const uint64_t y = x * TMUL;
@@ -48,24 +56,36 @@ DEV uint64_t tmix(uint64_t x) {
 DEV uint64_t tmix_inv(uint64_t t) {
     return (t ^ (t >> 32)) * TMUL_INV;  // y ^ (y >> 32) is an involution
 }
+// hash of key words 0 .. W-2 (W >= 2)
 template <int W>
 DEV uint64_t side_hash(const uint64_t (&w)[W]) {
     uint64_t g = 0;
 #pragma unroll
-    for (int i = 1; i < W; i++) g = fmix64(g ^ w[i] ^ (0x243f6a8885a308d3ULL * i));
-    return g & M62;
+    for (int i = 0; i + 1 < W; i++) g = fmix64(g ^ w[i] ^ (0x243f6a8885a308d3ULL * (i + 1)));
+    return g;
 }
 template <int W>
 DEV void to_tkey(const uint64_t (&key)[W], uint64_t (&t)[W]) {
-    t[0] = tmix(key[0] ^ MIX_C ^ side_hash<W>(key));
+    if constexpr (W == 1) {
+        t[0] = tmix(key[0] ^ MIX_C);
+    } else {
+        const uint64_t x = key[W - 1] ^ side_hash<W>(key);
+        t[0] = tmix(x ? x : TK_ZERO);
+        t[1] = key[0] | (x ? 0 : TK_FLAG);
 #pragma unroll
-    for (int i = 1; i < W; i++) t[i] = key[i];
+        for (int i = 2; i < W; i++) t[i] = key[i - 1];
+    }
 }
 template <int W>
 DEV void from_tkey(const uint64_t (&t)[W], uint64_t (&key)[W]) {
+    if constexpr (W == 1) {
+        key[0] = tmix_inv(t[0]) ^ MIX_C;
+    } else {
+        key[0] = t[1] & ~TK_FLAG;
 #pragma unroll
-    for (int i = 1; i < W; i++) key[i] = t[i];
-    key[0] = tmix_inv(t[0]) ^ MIX_C ^ side_hash<W>(t);
+        for (int i = 2; i < W; i++) key[i - 1] = t[i];
+        key[W - 1] = ((t[1] & TK_FLAG) ? 0 : tmix_inv(t[0])) ^ side_hash<W>(key);
+    }
 }
 
 // ---- table geometry -------------------------------------------------------------

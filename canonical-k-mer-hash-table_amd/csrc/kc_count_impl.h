@@ -756,6 +756,31 @@ DEV uint64_t rec6_key(uint64_t raw, bool odd, uint32_t xlo) {
 }
 
 // pre(): called after the rank atomics (k_p1 issues the loads of its next tile's words there)
+// Level record of a two-word key in a power-of-two bin geometry (kc_internal.h PartBufs.rec12):
+// table key (t0, t1) with t0 = x << 32 | lo and the bin = the top bits of x above xb; t1 = key
+// word 0 (2k - 64 bits) | TK_FLAG.  Three dwords {lo, t1 low, t1 bits 32.. (hb = 2k - 96, or 0) |
+// flag << hb | (x mod 2^xb) << (hb + 1)}: 12 instead of 16 bytes when hb + 1 + xb <= 32 (the host
+// checks it: k <= 55 at level 2 of a 2^16-bin geometry, k = 51 at level 1 of >= 2^7 bins).
+struct Rec12 {
+    int hb, xb;
+    DEV uint3 enc(uint64_t t0, uint64_t t1) const {
+        const uint32_t x = (uint32_t)(t0 >> 32), d = x & ((1u << xb) - 1);
+        const uint32_t hi = ((uint32_t)(t1 >> 32) & ((1u << hb) - 1)) | (uint32_t)((t1 >> 62) & 1) << hb;
+        return make_uint3((uint32_t)t0, (uint32_t)t1, hi | d << (hb + 1));
+    }
+    DEV void dec(uint3 r, uint32_t bin, uint64_t& t0, uint64_t& t1) const {
+        const uint32_t x = (bin << xb) | (r.z >> (hb + 1));
+        t0 = ((uint64_t)x << 32) | r.x;
+        t1 = ((uint64_t)(r.z & ((1u << hb) - 1)) << 32) | r.y | ((uint64_t)((r.z >> hb) & 1) << 62);
+    }
+};
+struct StoreRec12 {
+    Rec12 rc;
+    DEV void operator()(uint64_t* __restrict__ out, uint64_t dst, const uint64_t (&key)[2], uint32_t) const {
+        reinterpret_cast<uint3*>(out)[dst] = rc.enc(key[0], key[1]);
+    }
+};
+
 template <int W, int RUNW, class Bin, class Out, int NT, class Mid = NoMid, class St = StoreWords, class Pre = NoMid>
 DEV void scatter_seg(const PartLds& l, uint32_t F, const Bin& bin, const Out& o, uint64_t (&tk)[RUNW][W],
                      bool (&ok)[RUNW], uint64_t* __restrict__ out, Mid&& mid = Mid(), Stamps* stp = nullptr,
@@ -1169,18 +1194,24 @@ __global__ __launch_bounds__(NT, NT >= 1024 ? 8 : 4) void k_p1(PackedView sv, in
                 const bool nxt = STAGE && t0 + TW < hi && tid < SW;
                 uint64_t npk = 0;
                 uint32_t nbk = 0;
-                scatter_seg<OW, RUNW, Bin, Out, NT>(
-                    l, F, bin, ob, tk, ok, out,
-                    [&]() {  // placement phase: the next tile's words into the other buffer
-                        if (nxt) {
-                            st_pk[(par ^ 1) * SW + tid] = npk;
-                            st_bk[(par ^ 1) * SW + tid] = nbk;
-                        }
-                    },
-                    &stp, StoreWords(),
-                    [&]() {  // after the rank atomics: load them
-                        if (nxt) stage_word(t0 + TW, tid, npk, nbk);
-                    });
+                auto mid = [&]() {  // placement phase: the next tile's words into the other buffer
+                    if (nxt) {
+                        st_pk[(par ^ 1) * SW + tid] = npk;
+                        st_bk[(par ^ 1) * SW + tid] = nbk;
+                    }
+                };
+                auto pre = [&]() {  // after the rank atomics: load them
+                    if (nxt) stage_word(t0 + TW, tid, npk, nbk);
+                };
+                if constexpr (OW == 2 && MODE == 5) {  // the kept level 1 as 12-byte records
+                    if (pb.rec12 & R12_P1) {
+                        scatter_seg<OW, RUNW, Bin, Out, NT>(l, F, bin, ob, tk, ok, out, mid, &stp,
+                                                            StoreRec12{Rec12{pb.r12_hb, pb.r12_xb1}}, pre);
+                        par ^= 1;
+                        continue;
+                    }
+                }
+                scatter_seg<OW, RUNW, Bin, Out, NT>(l, F, bin, ob, tk, ok, out, mid, &stp, StoreWords(), pre);
                 par ^= 1;
             } else {
                 scatter_tile<OW, RUNW, Bin, Out, NT>(l, F, bin, ob, tk, ok, out, NoMid(), &stp);
@@ -1458,6 +1489,8 @@ __global__ __launch_bounds__(NT, (2048 / NT > 8 ? 8 : 2048 / NT)) void k_p2f(Tab
     // segment cursor of this thread (its indices grow monotonically): segment cs holds
     // [cb, nb) of the virtual run, both bounds kept in registers
     uint32_t cs = 0, cb = 0, nb = nseg ? pre[1] : 0;
+    // two-word keys: level 1 read as / level 2 written as 12-byte records (PartBufs.rec12)
+    const bool rin = W == 2 && (pb.rec12 & R12_IN), rout = W == 2 && (pb.rec12 & R12_OUT);
     const uint64_t* sp = pb.keys1 + seg0 * pb.cap1 * IS;  // segment cs
     // a wave takes 64 * RUNW consecutive positions of the tile (the cursor rarely moves)
     const uint32_t wpos = (uint32_t)(tid >> 6) * (64 * RUNW) + (tid & 63);
@@ -1470,6 +1503,7 @@ __global__ __launch_bounds__(NT, (2048 / NT > 8 ? 8 : 2048 / NT)) void k_p2f(Tab
             const uint32_t i = t0 + wpos + q * 64;
             ok[q] = i < total;
             const uint64_t* src = pb.keys1;
+            uint64_t item = 0;
             if (ok[q]) {
                 if (nb <= i) {
                     do {
@@ -1480,6 +1514,15 @@ __global__ __launch_bounds__(NT, (2048 / NT > 8 ? 8 : 2048 / NT)) void k_p2f(Tab
                     sp = pb.keys1 + (seg0 + cs) * pb.cap1 * IS;
                 }
                 src = sp + (uint64_t)(i - cb) * IS;
+                item = (seg0 + cs) * pb.cap1 + (i - cb);
+            }
+            if constexpr (W == 2) {
+                if (rin) {  // a 12-byte record, kept raw (decoded when the tile is scattered)
+                    const uint3 v = reinterpret_cast<const uint3*>(pb.keys1)[item];
+                    tk[q][0] = v.x | (uint64_t)v.y << 32;
+                    tk[q][1] = v.z;
+                    continue;
+                }
             }
 #pragma unroll
             for (int w = 0; w < W; w++) tk[q][w] = ks_load(src + w);
@@ -1487,6 +1530,8 @@ __global__ __launch_bounds__(NT, (2048 / NT > 8 ? 8 : 2048 / NT)) void k_p2f(Tab
     };
     uint64_t tk[RUNW][W];
     bool ok[RUNW];
+    Stamps stp;
+    stp.init();
     if (total) load_tile(0, tk, ok);
     for (uint32_t t0 = 0; t0 < total; t0 += TW) {
         // the next tile is loaded into the same registers as soon as this tile's keys sit
@@ -1495,15 +1540,32 @@ __global__ __launch_bounds__(NT, (2048 / NT > 8 ? 8 : 2048 / NT)) void k_p2f(Tab
         auto mid = [&]() {
             if (KC_PREFETCH && more) load_tile(t0 + TW, tk, ok);
         };
+        if constexpr (W == 2) {
+            if (rin) {  // the level-1 records of coarse bin c
+                const Rec12 r1{pb.r12_hb, pb.r12_xb1};
+#pragma unroll
+                for (int q = 0; q < RUNW; q++) {
+                    const uint3 v = make_uint3((uint32_t)tk[q][0], (uint32_t)(tk[q][0] >> 32), (uint32_t)tk[q][1]);
+                    r1.dec(v, c, tk[q][0], tk[q][1]);
+                }
+            }
+        }
         if constexpr (REC6) {
-            scatter_seg<W, RUNW, BinRegion, OutSeg, NT>(l, F, bin, o, tk, ok, pb.keys2, mid, nullptr,
+            scatter_seg<W, RUNW, BinRegion, OutSeg, NT>(l, F, bin, o, tk, ok, pb.keys2, mid, &stp,
                                                         StoreRec6{xlo});
+        } else if constexpr (W == 2) {
+            if (rout)
+                scatter_seg<W, RUNW, BinRegion, OutSeg, NT>(l, F, bin, o, tk, ok, pb.keys2, mid, &stp,
+                                                            StoreRec12{Rec12{pb.r12_hb, pb.r12_xb2}});
+            else
+                scatter_seg<W, RUNW, BinRegion, OutSeg, NT>(l, F, bin, o, tk, ok, pb.keys2, mid, &stp);
         } else {
-            scatter_seg<W, RUNW, BinRegion, OutSeg, NT>(l, F, bin, o, tk, ok, pb.keys2, mid);
+            scatter_seg<W, RUNW, BinRegion, OutSeg, NT>(l, F, bin, o, tk, ok, pb.keys2, mid, &stp);
         }
         if (!KC_PREFETCH && more) load_tile(t0 + TW, tk, ok);
     }
     __syncthreads();  // the last write-out read lim / gbase
+    stp.flush(1);
     for (uint32_t b = tid; b < F; b += NT)
         pb.hist2[((uint64_t)c * F + b) * pb.B2 + j] = (uint32_t)(scatter_seg_next(l, b) - o.start(b));
 }
@@ -1648,11 +1710,31 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
     }
     static_assert(!REC6 || (W == 1 && SEG && !CNT), "6-byte records: one-word keys in segments");
     const uint32_t xlo_r = REC6 ? (uint32_t)region_xlo(r, tv.R) : 0;
+    const bool r12 = W == 2 && SEG && !CNT && (pb.rec12 & R12_L2);  // Rec12 level-2 records
     auto load_items = [&](uint64_t base, uint64_t (&kk)[KB][W], uint64_t (&add)[KB], uint32_t& ok) {
         ok = 0;
 #pragma unroll
         for (int q = 0; q < KB; q++) {
             const uint64_t i = base + threadIdx.x + (uint64_t)q * NT;
+            if constexpr (W == 2 && SEG && !CNT) {
+                if (r12) {  // a 12-byte record, kept raw with its fine bin (decoded when used)
+                    kk[q][0] = kk[q][1] = 0;
+                    if (i < end) {
+                        while (nb <= i) {
+                            cs++;
+                            cb = nb;
+                            nb = s_pre[cs + 1];
+                        }
+                        const uint64_t seg = r * pb.B2 + cs;
+                        const uint3 v = reinterpret_cast<const uint3*>(pb.keys2)[seg * pb.cap2 + (i - cb)];
+                        kk[q][0] = v.x | (uint64_t)v.y << 32;
+                        kk[q][1] = v.z | (uint64_t)(seg >> pb.r12_b2s) << 32;
+                        ok |= 1u << q;
+                    }
+                    add[q] = 1;
+                    continue;
+                }
+            }
             if constexpr (REC6) {
                 kk[q][0] = 0;
                 if (i < end) {
@@ -1716,6 +1798,16 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
         if constexpr (REC6) {
 #pragma unroll
             for (int q = 0; q < KB; q++) kk[q][0] = rec6_key(kk[q][0], (okm >> (16 + q)) & 1, xlo_r);
+        }
+        if constexpr (W == 2) {
+            if (r12) {
+                const Rec12 rc{pb.r12_hb, pb.r12_xb2};
+#pragma unroll
+                for (int q = 0; q < KB; q++) {
+                    const uint3 v = make_uint3((uint32_t)kk[q][0], (uint32_t)(kk[q][0] >> 32), (uint32_t)kk[q][1]);
+                    rc.dec(v, (uint32_t)(kk[q][1] >> 32), kk[q][0], kk[q][1]);
+                }
+            }
         }
         bool pass[KB];
 #pragma unroll
@@ -1983,7 +2075,14 @@ __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView b
                         cb = nb;
                         nb = s_pre[cs + 1];
                     }
-                    t0[q] = pb.keys2[((r * pb.B2 + cs) * pb.cap2 + (i - cb)) * is];
+                    const uint64_t seg = r * pb.B2 + cs, item = seg * pb.cap2 + (i - cb);
+                    if (pb.rec12 & R12_L2) {  // 12-byte records of fine bin seg >> r12_b2s (Rec12)
+                        const uint3 v = reinterpret_cast<const uint3*>(pb.keys2)[item];
+                        const uint32_t x = (uint32_t)(seg >> pb.r12_b2s) << pb.r12_xb2 | v.z >> (pb.r12_hb + 1);
+                        t0[q] = (uint64_t)x << 32 | v.x;
+                    } else {
+                        t0[q] = pb.keys2[item * is];
+                    }
                 } else {
                     t0[q] = pb.keys2[i * is];
                 }

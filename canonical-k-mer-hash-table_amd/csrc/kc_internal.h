@@ -118,7 +118,16 @@ struct PartBufs {
     uint32_t* keep_fill2;   // segment fills of levels 1 and 2 (the skew-list pass reuses hist1/2)
     int rec6;               // segmented count pass, one-word keys, R >= 2^16: level 2 writes 6-byte
                             // records (kc_count_impl.h StoreRec6) that its level 3 reads
+    // two-word keys in power-of-two bin geometries (the Bloom pass that keeps its partitions, and
+    // the counting pass from them): 12-byte level records (kc_count_impl.h Rec12).  rec12 bits:
+    // R12_P1 k_p1 writes them at level 1, R12_IN k_p2f reads level 1 as them, R12_OUT k_p2f
+    // writes them at level 2, R12_L2 k_b3 / k_p3 read level 2 as them
+    int rec12;
+    int r12_hb;             // bits of table-key word 1 above 32 (2k - 96, or 0)
+    int r12_xb1, r12_xb2;   // bits of t0's top half below the level-1 / level-2 bin
+    int r12_b2s;            // log2 of the level-2 segments per bin (fine bin of a segment = segment >> r12_b2s)
 };
+constexpr int R12_P1 = 1, R12_IN = 2, R12_OUT = 4, R12_L2 = 8;
 
 struct BloomView {
     uint32_t* bits;         // 2 * nbits filter bits, interleaved: bit 2h = filter 1, 2h+1 = filter 2

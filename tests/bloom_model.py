@@ -80,11 +80,16 @@ def fmix64(k):
 
 
 def table_key0(kmer):
+    """Word 0 of the table key (kc_common.h to_tkey): W = 1: tmix(key0 ^ MIX_C); W >= 2:
+    tmix(last word ^ g(the other words)), a zero argument standing as TK_ZERO."""
     w = canonical_words(kmer)
-    g = 0
-    for i in range(1, len(w)):
-        g = fmix64(g ^ w[i] ^ ((0x243F6A8885A308D3 * i) & M64))
-    x = w[0] ^ 0x9E3779B97F4A7C15 ^ (g & ((1 << 62) - 1))
+    if len(w) == 1:
+        x = w[0] ^ 0x9E3779B97F4A7C15
+    else:
+        g = 0
+        for i in range(len(w) - 1):
+            g = fmix64(g ^ w[i] ^ ((0x243F6A8885A308D3 * (i + 1)) & M64))
+        x = (w[-1] ^ g) or 0x6A09E667F3BCC909
     y = (x * 0x9E3779B97F4A7C15) & M64
     return y ^ (y >> 32)
 
