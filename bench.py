@@ -254,10 +254,14 @@ def setup_job(args, env, image=None):
     L, k = args.read_len, args.k
     W = ka.words_for_k(k)
     strong = preset["scale"] == "strong"
+    # --share G (one GPU, strong presets): rank 0's share of a G-rank job -- its reads and its
+    # local table -- counted without the exchange (the per-rank half of a sharded step)
+    share = args.share if strong and world == 1 and not dist and args.share > 1 else 0
+    ranks = share or world
     if strong:  # this rank's share of the reads and of the table capacity
-        first = args.reads * rank // world
-        N = args.reads * (rank + 1) // world - first
-        slots = -(-args.slots // world) if args.slots else 0
+        first = args.reads * rank // ranks
+        N = args.reads * (rank + 1) // ranks - first
+        slots = -(-args.slots // ranks) if args.slots else 0
     else:
         first, N, slots = rank * args.reads, args.reads, args.slots
     stream = torch.cuda.current_stream()
@@ -296,22 +300,41 @@ def setup_job(args, env, image=None):
         cap = min(max(fit, int(0.45 * (free - nbytes)) // (28 * W + 4)), 1 << 31)
     batch = min((nbytes + len(chunks) * 4096 + (1 << 20)) // 4096 * 4096, cap // 4096 * 4096)
     windows_expected = N * (L - k + 1)
+    estimate = None
+    if strong and (share or (dist and world > 1)):
+        # a rank's local table holds its own input's distinct k-mers, which its 1/G share of -s
+        # does not bound: sized from a HyperLogLog estimate of them (kc_estimate_distinct_device,
+        # once per job before the timed steps), 1.1 x the estimate (x 1.25 buckets: load <= 0.73)
+        torch.cuda.synchronize()
+        e0 = time.perf_counter()
+        probe = ka.KmerCounter(ka.Config(k=k, mode=2, table_slots=1 << 16, batch_bytes=batch, device=local))
+        est = probe.estimate_distinct_device(image.data_ptr(), chunks, ka.FMT_FASTA, stream.cuda_stream)
+        probe.close()
+        local_slots = min(windows_expected, int(1.1 * est) + (1 << 20))
+        estimate = {"distinct_estimate": int(est), "local_slots": local_slots,
+                    "ms": round((time.perf_counter() - e0) * 1e3, 1),
+                    "method": "HyperLogLog, 2^14 registers (~0.8 % std. error); local table = 1.1 x estimate"}
     tbl = " ".join(["-m", "2"] + table_args(slots, args.unique))
     workload = (f"{args.config}: synthetic {N} x {L} bp reads/GPU, k={k}, {tbl}" if not strong else
                 f"{args.config}: synthetic {args.reads} x {L} bp reads over {world} GPU(s), k={k}, {tbl} per GPU")
+    if share:
+        workload = (f"{args.config} share 1/{share}: synthetic {N} x {L} bp reads (rank 0 of {args.reads} over "
+                    f"{share} GPUs), k={k}, -m 2, local table from the distinct estimate, no exchange")
     if sk:
         workload += (f", skew: {sk[0]:.0%} poly-A/T reads, {sk[1]:.0%} (CA)n reads, a {sk[2]}-bp repeat x "
                      f"{sk[3]} in the genome")
     # -a only selects output lines (it does not change counting): the reference fixture's -a when
     # this workload has one, so the parity digest covers the same lines
     fx = fixture_case(args) if world == 1 and not dist else None
-    cfg = ka.Config(k=k, mode=2, table_slots=slots, min_abundance=fx["min_abundance"] if fx else 2, batch_bytes=batch,
+    cfg = ka.Config(k=k, mode=2, table_slots=estimate["local_slots"] if share else slots,
+                    min_abundance=fx["min_abundance"] if fx else 2, batch_bytes=batch,
                     device=local, bf_enable=bool(args.unique), est_unique=args.unique)
     if dist:
         from kaarme_amd.sharded import ShardedCounter
-        # strong presets: a rank's local table must hold its own input's distinct k-mers,
-        # which its 1/world share of -s does not bound
-        counter = ShardedCounter(cfg, dist, local_slots=min(args.slots or 0, windows_expected) if strong else 0)
+        local_slots = 0
+        if strong:
+            local_slots = estimate["local_slots"] if estimate else min(args.slots or 0, windows_expected)
+        counter = ShardedCounter(cfg, dist, local_slots=local_slots)
     else:
         counter = ka.KmerCounter(cfg)
 
@@ -325,7 +348,7 @@ def setup_job(args, env, image=None):
 
     return argparse.Namespace(counter=counter, image=image, chunks=chunks, step=step, N=N, first=first, nbytes=nbytes,
                               slots=slots, strong=strong, windows_expected=windows_expected, tbl=tbl,
-                              workload=workload, fixture=fx, stream=stream)
+                              workload=workload, fixture=fx, stream=stream, estimate=estimate, share=share)
 
 
 def parity_record(job, k):
@@ -491,7 +514,11 @@ def run_workload(args, env, image=None):
         out["compact"] = compact
     if xgmi:
         out["xgmi"] = xgmi
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if job.estimate:
+        out["local_table"] = job.estimate
+    if job.share:
+        out["config"]["parallelism"] = f"one rank's share of hash-prefix shard x{job.share} (no exchange)"
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not job.share:
         out["cpu_baseline"] = cpu_baseline(args)
     return out, image
 
@@ -522,6 +549,9 @@ def main():
     ap.add_argument("--secondary-cpu-sample-bases", type=int, default=50_000_000)
     ap.add_argument("--no-verify", dest="verify", action="store_false",
                     help="skip the parity digest against the reference's output (tests/golden/fullsize.json)")
+    ap.add_argument("--share", type=int, default=0,
+                    help="strong presets on one GPU: time rank 0's share of a G-rank job (its reads, its local "
+                         "table sized from the distinct estimate; no exchange)")
     ap.add_argument("--force-sharded", action="store_true",
                     help="use the sharded (RCCL) path even at one rank (testing)")
     args = ap.parse_args()

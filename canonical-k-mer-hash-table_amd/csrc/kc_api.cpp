@@ -131,6 +131,7 @@ struct kc_ctx {
     unsigned long long reuse_sum = 0; // checksum of the Bloom pass's chunk bytes
     uint64_t reuse_windows = 0;       // windows of that batch
     unsigned long long* d_sum = nullptr;  // CHECKSUM_SLOTS partial sums (+ CHECKSUM_SLOTS for kc_bloom_estimate)
+    uint32_t* d_hll = nullptr;            // HLL_M registers of kc_estimate_distinct_device
     // compact representation (kc_compact): slot words, chain-start keys, counters
     uint64_t* d_cwords = nullptr;
     uint64_t cslots = 0;
@@ -473,6 +474,12 @@ static int run_batch(kc_ctx* c, const uint8_t* src, uint64_t used, uint64_t nchu
     if (std::getenv("KC_DEVICE_GATE")) host_gate = false;
     const uint64_t ntiles = used / TILE;
     if (ntiles == 0) return KC_OK;
+    if (pass == 3) {  // the distinct-count sketch (kc_estimate_distinct_device): tokenize + k_hll
+        HIPCHK(c, launch_tokenize(src, ntiles, c->d_chunks, (int)nchunks, fmt, c->d_tiles, c->d_touts, c->d_tblk,
+                                  PackedView{c->d_pk, c->d_bk}, used + nchunks, c->d_ctr, s));
+        HIPCHK(c, launch_hll(PackedView{c->d_pk, c->d_bk}, c->cfg.k, c->W, c->d_ctr, c->d_hll, s));
+        return KC_OK;
+    }
     std::array<hipEvent_t, 4> ev{ev_start, ev_gather, nullptr, nullptr};
     if (c->profiling) {
         if (!ev[0]) {
@@ -990,6 +997,7 @@ void kc_destroy(kc_ctx* c) {
     hipFree(c->d_chunks);
     hipFree(c->d_ctr);
     hipFree(c->d_sum);
+    hipFree(c->d_hll);
     hipFree(c->d_cwords);
     hipFree(c->d_csecond);
     hipFree(c->d_cstat);
@@ -1102,6 +1110,33 @@ int kc_count_device(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, size_
         if (rc || done) return rc;
     }
     return device_pass(c, img, chunks, n, fmt, 0, pick_stream(c, s));
+}
+
+int kc_estimate_distinct_device(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, size_t n, int fmt, void* sp,
+                                double* estimate) {
+    if (!c || !estimate || (!img && n) || (!chunks && n)) return KC_ERR_ARG;
+    hipStream_t s = pick_stream(c, sp);
+    if (!c->d_hll && hipMalloc(&c->d_hll, HLL_M * 4) != hipSuccess)
+        return c->fail(KC_ERR_NOMEM, "sketch allocation failed");
+    HIPCHK(c, hipMemsetAsync(c->d_hll, 0, HLL_M * 4, s));
+    int rc = device_pass(c, img, chunks, n, fmt, 3, s);
+    if (rc) return rc;
+    std::vector<uint32_t> reg(HLL_M);
+    HIPCHK(c, hipMemcpyAsync(reg.data(), c->d_hll, HLL_M * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    // Flajolet et al. 2007: E = alpha_m m^2 / sum 2^-M[j]; linear counting m ln(m / V) below
+    // 2.5 m when V registers are empty (a 64-bit hash needs no large-range correction)
+    double sum = 0;
+    uint32_t zeros = 0;
+    for (uint32_t v : reg) {
+        sum += std::ldexp(1.0, -(int)v);
+        zeros += v == 0;
+    }
+    const double m = HLL_M, alpha = 0.7213 / (1.0 + 1.079 / m);
+    double e = alpha * m * m / sum;
+    if (e <= 2.5 * m && zeros) e = m * std::log(m / zeros);
+    *estimate = e;
+    return KC_OK;
 }
 
 int kc_route_device(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, size_t n, int fmt, uint32_t nshards,

@@ -90,6 +90,10 @@ hipError_t launch_compact_lookup(int W, CompactView c, int k, const uint64_t* ke
     KC_DISPATCH_CW(W, lookup(c, k, keys, n, counts, s));
 }
 
+hipError_t launch_hll(PackedView sym, int k, int W, DevCounters* ctr, uint32_t* regs, hipStream_t s) {
+    KC_DISPATCH_W(W, hll(sym, k, ctr, regs, s));
+}
+
 hipError_t launch_dump(TableView t, int count_mode, uint64_t min_abundance, uint64_t* out, DevCounters* ctr,
                        hipStream_t s) {
     KC_DISPATCH_W(t.W, dump(t, count_mode, min_abundance, out, ctr, s));

@@ -756,11 +756,14 @@ DEV uint64_t rec6_key(uint64_t raw, bool odd, uint32_t xlo) {
 }
 
 // pre(): called after the rank atomics (k_p1 issues the loads of its next tile's words there)
-// Level record of a two-word key in a power-of-two bin geometry (kc_internal.h PartBufs.rec12):
-// table key (t0, t1) with t0 = x << 32 | lo and the bin = the top bits of x above xb; t1 = key
-// word 0 (2k - 64 bits) | TK_FLAG.  Three dwords {lo, t1 low, t1 bits 32.. (hb = 2k - 96, or 0) |
-// flag << hb | (x mod 2^xb) << (hb + 1)}: 12 instead of 16 bytes when hb + 1 + xb <= 32 (the host
-// checks it: k <= 55 at level 2 of a 2^16-bin geometry, k = 51 at level 1 of >= 2^7 bins).
+// Level record of a two-word key (kc_internal.h PartBufs.rec12): table key (t0, t1) with
+// t0 = x << 32 | lo, t1 = key word 0 (2k - 64 bits) | TK_FLAG.  Three dwords {lo, t1 low, t1 bits
+// 32.. (hb = 2k - 96, or 0) | flag << hb | (x mod 2^xb) << (hb + 1)}: 12 instead of 16 bytes when
+// hb + 1 + xb <= 32.  The record's bin spans fewer than 2^xb values of x from its lowest, x0, so
+// x = x0 + ((x - x0) mod 2^xb) is recovered from x mod 2^xb: x0 = bin << xb in a power-of-two
+// geometry (the Bloom pass's fine bins), region_xlo of the bin's first region in the table's
+// (R12_REG).  The host checks the spans (k <= 51 at level 1 of >= 2^7 bins; k <= 55 at level 2
+// of >= 2^16 regions).
 struct Rec12 {
     int hb, xb;
     DEV uint3 enc(uint64_t t0, uint64_t t1) const {
@@ -768,8 +771,8 @@ struct Rec12 {
         const uint32_t hi = ((uint32_t)(t1 >> 32) & ((1u << hb) - 1)) | (uint32_t)((t1 >> 62) & 1) << hb;
         return make_uint3((uint32_t)t0, (uint32_t)t1, hi | d << (hb + 1));
     }
-    DEV void dec(uint3 r, uint32_t bin, uint64_t& t0, uint64_t& t1) const {
-        const uint32_t x = (bin << xb) | (r.z >> (hb + 1));
+    DEV void dec(uint3 r, uint32_t x0, uint64_t& t0, uint64_t& t1) const {
+        const uint32_t x = x0 + (((r.z >> (hb + 1)) - x0) & ((1u << xb) - 1));
         t0 = ((uint64_t)x << 32) | r.x;
         t1 = ((uint64_t)(r.z & ((1u << hb) - 1)) << 32) | r.y | ((uint64_t)((r.z >> hb) & 1) << 62);
     }
@@ -1203,7 +1206,7 @@ __global__ __launch_bounds__(NT, NT >= 1024 ? 8 : 4) void k_p1(PackedView sv, in
                 auto pre = [&]() {  // after the rank atomics: load them
                     if (nxt) stage_word(t0 + TW, tid, npk, nbk);
                 };
-                if constexpr (OW == 2 && MODE == 5) {  // the kept level 1 as 12-byte records
+                if constexpr (OW == 2) {  // level 1 as 12-byte records (the kept Bloom levels, the table's)
                     if (pb.rec12 & R12_P1) {
                         scatter_seg<OW, RUNW, Bin, Out, NT>(l, F, bin, ob, tk, ok, out, mid, &stp,
                                                             StoreRec12{Rec12{pb.r12_hb, pb.r12_xb1}}, pre);
@@ -1491,6 +1494,7 @@ __global__ __launch_bounds__(NT, (2048 / NT > 8 ? 8 : 2048 / NT)) void k_p2f(Tab
     uint32_t cs = 0, cb = 0, nb = nseg ? pre[1] : 0;
     // two-word keys: level 1 read as / level 2 written as 12-byte records (PartBufs.rec12)
     const bool rin = W == 2 && (pb.rec12 & R12_IN), rout = W == 2 && (pb.rec12 & R12_OUT);
+    const uint32_t x0c = rin ? (uint32_t)region_xlo((uint64_t)c * F, tv.R) : 0;  // coarse bin c's lowest x
     const uint64_t* sp = pb.keys1 + seg0 * pb.cap1 * IS;  // segment cs
     // a wave takes 64 * RUNW consecutive positions of the tile (the cursor rarely moves)
     const uint32_t wpos = (uint32_t)(tid >> 6) * (64 * RUNW) + (tid & 63);
@@ -1546,7 +1550,7 @@ __global__ __launch_bounds__(NT, (2048 / NT > 8 ? 8 : 2048 / NT)) void k_p2f(Tab
 #pragma unroll
                 for (int q = 0; q < RUNW; q++) {
                     const uint3 v = make_uint3((uint32_t)tk[q][0], (uint32_t)(tk[q][0] >> 32), (uint32_t)tk[q][1]);
-                    r1.dec(v, c, tk[q][0], tk[q][1]);
+                    r1.dec(v, x0c, tk[q][0], tk[q][1]);
                 }
             }
         }
@@ -1709,8 +1713,11 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
         psh = (m + 1) / 2;
     }
     static_assert(!REC6 || (W == 1 && SEG && !CNT), "6-byte records: one-word keys in segments");
-    const uint32_t xlo_r = REC6 ? (uint32_t)region_xlo(r, tv.R) : 0;
     const bool r12 = W == 2 && SEG && !CNT && (pb.rec12 & R12_L2);  // Rec12 level-2 records
+    // (in the table's geometry, R12_REG: decoded against region r's lowest x; from the Bloom
+    // pass's fine bins: against the fine bin's)
+    const bool r12_reg = r12 && (pb.rec12 & R12_REG);
+    const uint32_t xlo_r = REC6 || r12_reg ? (uint32_t)region_xlo(r, tv.R) : 0;
     auto load_items = [&](uint64_t base, uint64_t (&kk)[KB][W], uint64_t (&add)[KB], uint32_t& ok) {
         ok = 0;
 #pragma unroll
@@ -1805,7 +1812,7 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
 #pragma unroll
                 for (int q = 0; q < KB; q++) {
                     const uint3 v = make_uint3((uint32_t)kk[q][0], (uint32_t)(kk[q][0] >> 32), (uint32_t)kk[q][1]);
-                    rc.dec(v, (uint32_t)(kk[q][1] >> 32), kk[q][0], kk[q][1]);
+                    rc.dec(v, r12_reg ? xlo_r : (uint32_t)(kk[q][1] >> 32) << pb.r12_xb2, kk[q][0], kk[q][1]);
                 }
             }
         }
@@ -2588,6 +2595,33 @@ static __global__ void k_batch_end(DevCounters* ctr) {
     ctr->heavy += ctr->heavy_n;
 }
 
+// Rec12 in the table's geometry (R12_REG): a coarse bin spans at most ceil(F2 * 2^32 / R) values
+// of x, a region ceil(2^32 / R); level 1 (k_p1 -> k_p2f) and level 2 (k_p2f -> k_p3) take the
+// 12-byte records independently, each when hb + 1 + xb <= 32 (KC_NO_REC12: 16-byte records)
+static inline void set_rec12_table(PartBufs& pb, const TableView& t, int k) {
+    pb.rec12 = 0;
+    if (std::getenv("KC_NO_REC12") || t.R == 0) return;
+    const int hb = std::max(0, 2 * k - 96);
+    auto span_bits = [](uint64_t span) {
+        int b = 0;
+        while (b < 32 && (1ULL << b) < span) b++;
+        return b;
+    };
+    const uint64_t f2 = 1ULL << t.f2bits;
+    const int xb1 = span_bits(((f2 << 32) + t.R - 1) / t.R), xb2 = span_bits(((1ULL << 32) + t.R - 1) / t.R);
+    if (hb + 1 + xb1 <= 32) {
+        pb.rec12 |= R12_P1 | R12_IN;
+        pb.r12_xb1 = xb1;
+    }
+    if (hb + 1 + xb2 <= 32) {
+        pb.rec12 |= R12_OUT | R12_L2;
+        pb.r12_xb2 = xb2;
+    }
+    if (pb.rec12) pb.rec12 |= R12_REG;
+    pb.r12_hb = hb;
+    pb.r12_b2s = 0;
+}
+
 // Segmented pipeline (pb.cap1 != 0): p1 -> p2f -> p3<SEG>, each a single pass; then
 // the exact pipeline behind the overflow gate (its kernels return at once unless a
 // segment overflowed, in which case the segmented p3 left the table untouched).
@@ -2605,6 +2639,8 @@ static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf
     const unsigned long long* gate = &ctr->part_overflow;
     // one-word keys in a table of >= 2^16 regions: 6-byte level-2 records (StoreRec6)
     pb.rec6 = W == 1 && t.R >= (1ULL << 16) && !std::getenv("KC_NO_REC6");
+    // two-word keys: 12-byte records at each level whose bins span few enough values of x
+    if constexpr (W == 2) set_rec12_table(pb, t, k);
     if (phase & PH_MAIN) {
     hipLaunchKernelGGL(k_batch_begin, dim3(1), dim3(1), 0, s, ctr);
     const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
@@ -2919,6 +2955,54 @@ template <int W>
 hipError_t WOps<W>::text(TableView t, int count_mode, uint64_t a, int k, uint64_t blk0, uint64_t nblk,
                          const uint64_t* off, uint64_t base, uint8_t* out, size_t lds, hipStream_t s) {
     return text_w<W>(t, count_mode, a, k, blk0, nblk, off, base, out, lds, s);
+}
+
+// --------------------------------------------------------------------------------
+// k_hll<W>: HyperLogLog registers of a batch's distinct canonical k-mers, the estimate the
+// host sizes tables from (kc_estimate_distinct_device; the reference takes -s from its user,
+// main.cpp:134-154).  2^HLL_P registers in LDS: register = the top HLL_P bits of the table
+// key's word 0 (a bijective mix of the key; for W >= 2 of its last word and a hash of the
+// others), value = 1 + the leading zeros of its other bits; merged into the context's
+// registers with atomicMax.  Grid-stride over the batch's tiles, one tile per round.
+// --------------------------------------------------------------------------------
+template <int W>
+__global__ __launch_bounds__(COUNT_THREADS) void k_hll(PackedView sv, int k, const DevCounters* __restrict__ ctr,
+                                                       uint32_t* __restrict__ regs, uint64_t pow5_k,
+                                                       uint64_t pow5_km1) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint32_t* r = reinterpret_cast<uint32_t*>(smem);
+    for (uint32_t i = threadIdx.x; i < HLL_M; i += COUNT_THREADS) r[i] = 0;
+    __syncthreads();
+    constexpr int TW = tile_win<W>(), RUNW = run_w<W>();
+    const uint64_t M = ctr->stream_len;
+    const RollConst rk = make_roll<W>(k, pow5_k, pow5_km1);
+    for (uint64_t t0 = (uint64_t)blockIdx.x * TW; t0 < M; t0 += (uint64_t)gridDim.x * TW) {
+        const uint64_t t1 = min(t0 + TW, M), r0 = t0 + (uint64_t)threadIdx.x * RUNW;
+        if (r0 < t1)
+            run_windows<W, RUNW>(sv, r0, t1, rk,
+                                 [&](int, bool valid, const uint64_t (&fwd)[W], const uint64_t (&rc)[W]) {
+                if (!valid) return;
+                uint64_t key[W], tk[W];
+                canonical<W>(fwd, rc, key);
+                to_tkey<W>(key, tk);
+                const uint32_t j = (uint32_t)(tk[0] >> (64 - HLL_P));
+                const uint64_t rest = (tk[0] << HLL_P) | (1ULL << (HLL_P - 1));  // (<= 64 - HLL_P zeros)
+                atomicMax(&r[j], (uint32_t)__builtin_clzll(rest) + 1);
+            });
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < HLL_M; i += COUNT_THREADS)
+        if (r[i]) atomicMax(&regs[i], r[i]);
+}
+
+template <int W>
+hipError_t WOps<W>::hll(PackedView sym, int k, DevCounters* ctr, uint32_t* regs, hipStream_t s) {
+    const size_t sm = (size_t)HLL_M * 4;
+    hipError_t e = set_smem(k_hll<W>, sm);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_hll<W>, dim3(512), dim3(COUNT_THREADS), sm, s, sym, k, ctr, regs, pow5_mod54(k),
+                       pow5_mod54(k - 1));
+    return hipGetLastError();
 }
 
 }  // namespace kc

@@ -128,6 +128,9 @@ struct PartBufs {
     int r12_b2s;            // log2 of the level-2 segments per bin (fine bin of a segment = segment >> r12_b2s)
 };
 constexpr int R12_P1 = 1, R12_IN = 2, R12_OUT = 4, R12_L2 = 8;
+// R12_REG: the records are in the table's own geometry (the counting pass's levels): a bin's
+// lowest x is region_xlo of its first region, not bin << xb
+constexpr int R12_REG = 16;
 
 struct BloomView {
     uint32_t* bits;         // 2 * nbits filter bits, interleaved: bit 2h = filter 1, 2h+1 = filter 2
@@ -244,6 +247,10 @@ hipError_t launch_check_runs(const uint64_t* rec, const uint64_t* gstart, uint32
                              unsigned long long* flag, hipStream_t s);
 hipError_t launch_insert_counts_runs(const uint64_t* rec, const uint64_t* gstart, uint32_t G, TableView t,
                                      DevCounters* ctr, uint32_t* m_len, uint64_t* m_start, int fresh, hipStream_t s);
+// HyperLogLog registers of the distinct-count estimate (kc_count_impl.h k_hll)
+constexpr int HLL_P = 14;
+constexpr uint32_t HLL_M = 1u << HLL_P;
+hipError_t launch_hll(PackedView sym, int k, int W, DevCounters* ctr, uint32_t* regs, hipStream_t s);
 hipError_t launch_dump(TableView t, int count_mode, uint64_t min_abundance, uint64_t* out, DevCounters* ctr,
                        hipStream_t s);
 // GPU text formatting (kc_write): bytes of each TEXT_T-bucket block into block_bytes and
@@ -284,6 +291,7 @@ struct WOps {
                                          DevCounters* ctr, uint32_t* m_len, uint64_t* m_start, int fresh, hipStream_t s);
     static hipError_t dump(TableView t, int count_mode, uint64_t min_abundance, uint64_t* out, DevCounters* ctr,
                            hipStream_t s);
+    static hipError_t hll(PackedView sym, int k, DevCounters* ctr, uint32_t* regs, hipStream_t s);
     static hipError_t text_bytes(TableView t, int count_mode, uint64_t a, int k, uint32_t* block_bytes, uint64_t* off,
                                  uint64_t* bsum, hipStream_t s);
     static hipError_t text(TableView t, int count_mode, uint64_t a, int k, uint64_t blk0, uint64_t nblk,

@@ -134,6 +134,15 @@ int kc_bloom_device(kc_ctx* ctx, const uint8_t* dev_image, const kc_chunk* chunk
                     void* hip_stream);
 int kc_count_device(kc_ctx* ctx, const uint8_t* dev_image, const kc_chunk* chunks, size_t n_chunks, int fmt,
                     void* hip_stream);
+/* Distinct-count estimate of a device image (no reference counterpart: Kaarme takes the
+ * table size from its user, -s, main.cpp:134-154, or from the Bloom pass, main.cpp:454): the
+ * canonical k-mers of the image's windows into a HyperLogLog sketch of 2^14 registers
+ * (~0.8 % standard error), so a caller can size a table (kc_config.table_slots) before
+ * counting, e.g. a rank's local table in a sharded job.  Counts nothing and leaves the
+ * table alone; the call waits for its work (the estimate is a host value).  Any context of
+ * the same k can run it (its table size does not matter). */
+int kc_estimate_distinct_device(kc_ctx* ctx, const uint8_t* dev_image, const kc_chunk* chunks, size_t n_chunks,
+                                int fmt, void* hip_stream, double* estimate);
 /* Wait for all work enqueued on the context. */
 int kc_sync(kc_ctx* ctx);
 

@@ -32,7 +32,7 @@ def _fixture():
 def _bench_args(config):
     import bench
     base = argparse.Namespace(config=config, reads=None, read_len=None, genome=None, k=None, slots=None,
-                              unique=None, batch_mib=0, err=0.001, seed=42)
+                              unique=None, batch_mib=0, err=0.001, seed=42, share=0)
     return bench, bench.resolve(base, config)
 
 

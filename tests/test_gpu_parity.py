@@ -615,3 +615,61 @@ def test_six_byte_level2_records(tmp_path, k, seg, slots, monkeypatch):
     out = tmp_path / "oracle.txt"
     oracle_count(str(fa), k, ["-m", "2", "-a", "1"], out)
     assert sorted_digest_lines(lines) == sorted_digest_file(out)
+
+
+@pytest.mark.parametrize("slots", [2_000_000, 300_000_000])
+@pytest.mark.parametrize("k,seg", [(33, "default"), (51, "default"), (51, "tiny"), (55, "default")])
+def test_twelve_byte_table_records(tmp_path, k, seg, slots, monkeypatch):
+    """Two-word keys in the counting pass's own geometry (not a power of two: -s 2e6 gives 977
+    regions, -s 3e8 146 485) move 12-byte level records (kc_count_impl.h Rec12, R12_REG: x
+    recovered from x mod 2^xb and the bin's lowest x) where the bins are narrow enough: k = 33 at
+    both levels; k = 51 at level 2 (and level 1 of the big table); k = 55 at level 2 of the big
+    table only.  Compared with the oracle and with the 16-byte records (KC_NO_REC12)."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("KC_INSERT_PATH", "partitioned")
+    if seg == "tiny":
+        monkeypatch.setenv("KC_SEG_CAP", "64")
+        monkeypatch.setenv("KC_SPILL_CAP", str(1 << 24))
+    fa = tmp_path / "r.fasta"
+    subprocess.run([GEN, str(fa), "30000", "150", "200000", "-s", "7", "-n", "0.001"], check=True)
+    data = open(fa, "rb").read()
+    img = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+    got = {}
+    for rec in ("12", "16"):
+        if rec == "16":
+            monkeypatch.setenv("KC_NO_REC12", "1")
+        with ka.KmerCounter(ka.Config(k=k, mode=2, min_abundance=1, table_slots=slots)) as kc:
+            kc.count_device(img.data_ptr(), ka.plan_chunks(data, k, ka.FMT_FASTA), ka.FMT_FASTA)
+            st = kc.finish()
+            assert st["part_fallbacks"] == 0
+            if seg == "tiny" and slots < 10 ** 8:  # (146 485 regions leave every segment short)
+                assert st["spilled"] > 0
+            got[rec] = sorted_digest_lines(kc.lines())
+    out = tmp_path / "oracle.txt"
+    oracle_count(str(fa), k, ["-m", "2", "-a", "1"], out)
+    assert got["12"] == sorted_digest_file(out)
+    assert got["16"] == got["12"]
+
+
+@pytest.mark.parametrize("k", [15, 31, 51, 127])
+def test_distinct_estimate(tmp_path, k):
+    """kc_estimate_distinct_device (HyperLogLog, 2^14 registers, ~0.8 % standard error) against
+    the exact distinct count of the same image; it counts nothing (the table stays empty)."""
+    torch = pytest.importorskip("torch")
+    fa = tmp_path / "r.fasta"
+    subprocess.run([GEN, str(fa), "60000", "150", "2000000", "-s", "11", "-n", "0.002"], check=True)
+    data = open(fa, "rb").read()
+    img = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+    chunks = ka.plan_chunks(data, k, ka.FMT_FASTA)
+    with ka.KmerCounter(ka.Config(k=k, mode=2, min_abundance=1, table_slots=1 << 24)) as kc:
+        est = kc.estimate_distinct_device(img.data_ptr(), chunks, ka.FMT_FASTA)
+        est_small = kc.estimate_distinct_device(img.data_ptr(), chunks[:1], ka.FMT_FASTA)
+        kc.count_device(img.data_ptr(), chunks, ka.FMT_FASTA)
+        st = kc.finish()
+        assert st["windows"] > 0
+        exact = st["distinct"]
+    assert abs(est - exact) / exact < 0.04, (est, exact)
+    with ka.KmerCounter(ka.Config(k=k, mode=2, min_abundance=1, table_slots=1 << 24)) as kc:
+        kc.count_device(img.data_ptr(), chunks[:1], ka.FMT_FASTA)
+        exact_small = kc.finish()["distinct"]
+    assert abs(est_small - exact_small) / exact_small < 0.04, (est_small, exact_small)
