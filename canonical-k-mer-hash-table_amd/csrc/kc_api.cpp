@@ -282,7 +282,10 @@ static int alloc_table(kc_ctx* c, uint64_t min_slots, uint32_t pow2_f1 = 0) {
             return c->fail(KC_ERR_NOMEM, "table allocation failed (" + std::to_string(bytes) + " bytes)");
         c->table_cap_bytes = bytes;
     }
-    HIPCHK(c, hipMemsetAsync(c->d_table, 0, bytes, c->stream));
+    // zeroed lazily: a fresh partitioned pass writes every region from zero-filled LDS (C3's
+    // counting pass: 0.66 ms of its 31 ms step was this memset), anything else that reads the
+    // table first runs materialize_zero
+    c->table_zero_pending = true;
     c->table_fresh = true;
     return KC_OK;
 }
