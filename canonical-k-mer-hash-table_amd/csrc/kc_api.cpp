@@ -243,6 +243,12 @@ static int alloc_table(kc_ctx* c, uint64_t min_slots, uint32_t pow2_f1 = 0) {
         auto l1_fits = [&](int f2b) { return p1_lds_bytes(c->W, f1_of(f2b)) <= LDS_BYTES; };
         int f1bits = std::min(10, (rbits + 1) / 2);
         while (f1bits < rbits && !l2_fits(rbits - f1bits, 0)) f1bits++;
+        // level-1 runs of fewer than 8 keys per tile cost level 1 its second workgroup per CU
+        // (launch_part_w): fewer, wider coarse bins while level 2 still fits (C4 share: 542 x 512
+        // -> 271 x 1024 bins, k_p1 14.9 -> 9.9 ms, k_p2f 11.0 -> 12.3 ms, r03_ab_c4s_coarse_bins.txt)
+        while (f1bits > 1 && (uint64_t)p1_tile(c->W) < 8ULL * f1_of(rbits - f1bits) &&
+               l2_fits(rbits - f1bits + 1, 0))
+            f1bits--;
         c->seg_ok = true;
         if (!l1_fits(rbits - f1bits)) {
             const int half = p2f_threads_w(c->W) / 2;
