@@ -567,18 +567,20 @@ def test_skewed_input_uses_the_skew_lists(case, seg, golden_input, tmp_path, mon
         assert st["spilled"] > 0
 
 
-@pytest.mark.parametrize("k", [51, 127])
-def test_big_table_geometry(tmp_path, k):
-    """Tables of the strong presets' size (-s 1.25e9 per GPU: the C4 / C5 shares) choose
-    partition geometries whose level-1 and level-2 LDS arrays fit (wide keys: more regions per
-    coarse bin, level 2 at half its workgroup); a small input through the device path gives
-    the oracle's counts."""
+@pytest.mark.parametrize("k,slots", [(51, 1_250_000_000), (127, 1_250_000_000), (51, 567_000_000),
+                                     (33, 567_000_000)])
+def test_big_table_geometry(tmp_path, k, slots):
+    """Tables of the strong presets' size (-s 1.25e9 per GPU; 5.67e8 = the C4 share's
+    estimate-sized local table) choose partition geometries whose level-1 and level-2 LDS
+    arrays fit (wide keys: more regions per coarse bin, level 2 at half its workgroup; level-1
+    runs under 8 keys per tile: fewer, wider coarse bins, 271 x 1024 for 5.67e8); a small input
+    through the device path gives the oracle's counts."""
     torch = pytest.importorskip("torch")
     fa = tmp_path / "r.fasta"
     subprocess.run([GEN, str(fa), "20000", "300", "100000"], check=True)
     data = open(fa, "rb").read()
     img = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
-    with ka.KmerCounter(ka.Config(k=k, mode=2, min_abundance=1, table_slots=1_250_000_000)) as kc:
+    with ka.KmerCounter(ka.Config(k=k, mode=2, min_abundance=1, table_slots=slots)) as kc:
         kc.count_device(img.data_ptr(), ka.plan_chunks(data, k, ka.FMT_FASTA), ka.FMT_FASTA)
         st = kc.finish()
         assert st["part_fallbacks"] == 0
