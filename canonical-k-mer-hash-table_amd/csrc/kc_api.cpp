@@ -1421,8 +1421,9 @@ int kc_insert_keys_device(kc_ctx* c, const uint64_t* keys, uint64_t n, void* sp)
     return KC_OK;
 }
 
-int kc_sync(kc_ctx* c) {
-    if (!c) return KC_ERR_ARG;
+// the readers of the table (finish, dump, write, compact, ...): the staged work done and a
+// deferred reset carried out first
+static int sync_for_read(kc_ctx* c) {
     int rc = flush_host(c);
     if (rc) return rc;
     rc = materialize_zero(c, c->stream);  // a deferred reset is due before anyone reads the table
@@ -1431,8 +1432,18 @@ int kc_sync(kc_ctx* c) {
     return KC_OK;
 }
 
+// (a deferred reset stays deferred: the next fresh pass writes every region anyway -- the
+// sharded merge empties the local table and syncs every step)
+int kc_sync(kc_ctx* c) {
+    if (!c) return KC_ERR_ARG;
+    int rc = flush_host(c);
+    if (rc) return rc;
+    HIPCHK(c, hipDeviceSynchronize());
+    return KC_OK;
+}
+
 int kc_finish(kc_ctx* c, kc_stats* st) {
-    int rc = kc_sync(c);
+    int rc = sync_for_read(c);
     if (rc) return rc;
     DevCounters h;
     HIPCHK(c, hipMemcpy(&h, c->d_ctr, sizeof(h), hipMemcpyDeviceToHost));
@@ -1570,7 +1581,7 @@ int kc_dump(kc_ctx* c, uint64_t** records, uint64_t* n_records) {
     if (!c || !records || !n_records) return KC_ERR_ARG;
     *records = nullptr;
     *n_records = 0;
-    int rc = kc_sync(c);
+    int rc = sync_for_read(c);
     if (rc) return rc;
     if (!c->nbuckets) return c->fail(KC_ERR_STATE, "no table");
     TableView tv = table_view(c);
@@ -1610,7 +1621,7 @@ int kc_compact(kc_ctx* c, double load, kc_compact_info* info) {
     if (c->cfg.mode == 0)
         return c->fail(KC_ERR_UNSUPPORTED, "the compact representation holds Kaarme counts (-m 1/2: 14 bits, "
                                            "saturating at 16383)");
-    int rc = kc_sync(c);
+    int rc = sync_for_read(c);
     if (rc) return rc;
     rc = materialize_zero(c, c->stream);
     if (rc) return rc;
@@ -1676,7 +1687,7 @@ int kc_compact_dump(kc_ctx* c, uint64_t** records, uint64_t* n_records, uint64_t
     *records = nullptr;
     *n_records = 0;
     if (!c->d_cwords) return c->fail(KC_ERR_STATE, "no compact representation (kc_compact)");
-    int rc = kc_sync(c);
+    int rc = sync_for_read(c);
     if (rc) return rc;
     const CompactView cv = compact_view(c);
     const uint64_t a = c->cfg.min_abundance;
@@ -1714,7 +1725,7 @@ int kc_compact_lookup(kc_ctx* c, const uint64_t* keys, uint64_t n, uint32_t* cou
     if (!c || (n && (!keys || !counts))) return KC_ERR_ARG;
     if (!c->d_cwords) return c->fail(KC_ERR_STATE, "no compact representation (kc_compact)");
     if (!n) return KC_OK;
-    int rc = kc_sync(c);
+    int rc = sync_for_read(c);
     if (rc) return rc;
     uint64_t* dk = nullptr;
     uint32_t* dc = nullptr;
@@ -1737,7 +1748,7 @@ int kc_compact_read(kc_ctx* c, uint64_t* words, uint64_t n_words, uint64_t* seco
     if (n_words > c->cslots || n_second_words > c->cstarts * c->W || (n_words && !words) ||
         (n_second_words && !second))
         return c->fail(KC_ERR_ARG, "more words than the compact representation holds");
-    int rc = kc_sync(c);
+    int rc = sync_for_read(c);
     if (rc) return rc;
     if (n_words) HIPCHK(c, hipMemcpy(words, c->d_cwords, n_words * 8, hipMemcpyDeviceToHost));
     if (n_second_words) HIPCHK(c, hipMemcpy(second, c->d_csecond, n_second_words * 8, hipMemcpyDeviceToHost));
@@ -1759,7 +1770,7 @@ static uint64_t text_piece_bytes() {
 int kc_write(kc_ctx* c, const char* path) {
     if (!c || !path) return KC_ERR_ARG;
     if (c->cfg.min_abundance == 0) return KC_OK;  // parallel_parser.hpp:1536 / 858
-    int rc = kc_sync(c);
+    int rc = sync_for_read(c);
     if (rc) return rc;
     if (!c->nbuckets) return c->fail(KC_ERR_STATE, "no table");
     const TableView tv = table_view(c);
