@@ -144,6 +144,8 @@ struct kc_ctx {
     uint32_t* d_keep_fill2 = nullptr;     // and level 2 [R_fine][B2]
     uint64_t keep_fill_cap = 0, keep_fill2_cap = 0;
     TableView fgeo{};                     // the kept partitions' fine geometry (powers of two)
+    uint64_t fgeo_max_R = 0;              // the create-time fine regions (the most the LDS fits)
+    uint64_t fgeo_next_R = 0;             // fine regions learned from the last finalize (0 = keep)
     int reuse_level = 0;                  // kc_bloom_finalize: 2 = from level 2, 1 = from level 1
     uint64_t reuse_hits = 0;          // counting passes that reused (kc_stats.reused_passes)
     int reuse_last_level = 0;         // the level the last reused pass started from (kc_stats.reuse_level)
@@ -992,6 +994,7 @@ int kc_create(const kc_config* cfg, kc_ctx** out) {
                     c->fgeo.F2 = 1u << c->fgeo.f2bits;
                     c->fgeo.F1 = 1u << f1;
                     c->fgeo.W = c->W;
+                    c->fgeo_max_R = c->fgeo.R;
                 }
             }
         }
@@ -1102,6 +1105,16 @@ int kc_bloom_finalize(kc_ctx* c, uint64_t* new_in_second) {
         else if (p2f_lds_bytes(c->W, (uint32_t)(rt / c->fgeo.F1), nseg) <= 160 * 1024 && rt < (1ULL << 32))
             c->reuse_level = 1;
         reuse = c->reuse_level != 0;
+        // adaptive fine geometry for the context's next job (kc_reset applies it): fine
+        // bins as coarse as the table regions just sized, so that a level-2 region is one
+        // fine bin (one segment group per k_p3 workgroup, fewer and fuller level-2 bins:
+        // C3 31.3 -> 29.4 ms, profiles/r03_ab_fb16.txt); back to the create-time geometry
+        // when this job's table outgrew the learned one.  The first job keeps the default.
+        const uint64_t floor_r = std::max<uint64_t>(c->bgeo.R, c->fgeo.F1);
+        if (c->reuse_level == 2)
+            c->fgeo_next_R = std::max(rt, floor_r);
+        else if (rt > c->fgeo.R && c->fgeo.R < c->fgeo_max_R)
+            c->fgeo_next_R = c->fgeo_max_R;
     }
     if (reuse) {
         unsigned long long part[CHECKSUM_SLOTS];
@@ -1536,6 +1549,15 @@ int kc_reset(kc_ctx* c) {
     drop_compact(c);
     c->reuse_kept = c->reuse_ok = false;
     c->reuse_level = 0;
+    if (c->fgeo_next_R && c->fgeo_next_R != c->fgeo.R && c->fgeo_next_R <= c->fgeo_max_R) {
+        int fb = 0, f1 = 0;
+        while ((1ULL << fb) < c->fgeo_next_R) fb++;
+        while ((1u << f1) < c->fgeo.F1) f1++;
+        c->fgeo.R = 1ULL << fb;
+        c->fgeo.f2bits = fb - f1;
+        c->fgeo.F2 = 1u << c->fgeo.f2bits;
+    }
+    c->fgeo_next_R = 0;
     c->reuse_hits = 0;
     c->reuse_last_level = 0;
     return KC_OK;
