@@ -347,7 +347,7 @@ int main(int argc, char** argv) {
     std::cout << "  output file:              " << a.output << std::endl;
     std::cout << "  device:                   MI355X (HIP device " << a.device << ")" << std::endl;
 
-    if (a.k > KC_MAX_K) {  // eight 64-bit key words (include/kc_api.h); INTEGRATION.md "Differences"
+    if (a.k > KC_MAX_K) {  // fifteen 64-bit key words (include/kc_api.h); INTEGRATION.md "Differences"
         std::cerr << "k-mer length above " << KC_MAX_K << " is not supported by this build" << std::endl;
         return 1;
     }

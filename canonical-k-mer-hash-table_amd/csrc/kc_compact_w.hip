@@ -1,5 +1,5 @@
 // kc_compact_w.hip -- the compact-representation kernels (kc_compact_impl.h) for ONE key
-// width: compiled once per W with -DKC_W=1..8, like kc_count_w.hip.
+// width: compiled once per W with -DKC_W=1..15, like kc_count_w.hip.
 #ifndef KC_W
 #error "compile with -DKC_W=<key words>"
 #endif

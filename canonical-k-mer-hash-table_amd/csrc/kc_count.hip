@@ -1,5 +1,5 @@
 // kc_count.hip -- W-dispatch of the counting entry points (kc_internal.h launch_*): the
-// kernels of every key width W = 1..8 live in their own translation unit
+// kernels of every key width W = 1..15 live in their own translation unit
 // (kc_count_w.hip -DKC_W=W, kernels in kc_count_impl.h).
 #include "kc_internal.h"
 
@@ -15,6 +15,13 @@ namespace kc {
     case 6: return WOps<6>::CALL;              \
     case 7: return WOps<7>::CALL;              \
     case 8: return WOps<8>::CALL;              \
+    case 9: return WOps<9>::CALL;              \
+    case 10: return WOps<10>::CALL;            \
+    case 11: return WOps<11>::CALL;            \
+    case 12: return WOps<12>::CALL;            \
+    case 13: return WOps<13>::CALL;            \
+    case 14: return WOps<14>::CALL;            \
+    case 15: return WOps<15>::CALL;            \
     default: return hipErrorInvalidValue;      \
     }
 
@@ -75,6 +82,13 @@ hipError_t launch_insert_counts(const uint64_t* rec, uint64_t n, bool partitione
     case 6: return CompactOps<6>::CALL;        \
     case 7: return CompactOps<7>::CALL;        \
     case 8: return CompactOps<8>::CALL;        \
+    case 9: return CompactOps<9>::CALL;        \
+    case 10: return CompactOps<10>::CALL;      \
+    case 11: return CompactOps<11>::CALL;      \
+    case 12: return CompactOps<12>::CALL;      \
+    case 13: return CompactOps<13>::CALL;      \
+    case 14: return CompactOps<14>::CALL;      \
+    case 15: return CompactOps<15>::CALL;      \
     default: return hipErrorInvalidValue;      \
     }
 

@@ -1,5 +1,5 @@
 // kc_count_impl.h -- canonical k-mer insertion, Bloom passes and the table dump.
-// Included by kc_count_w.hip, which is compiled once per key width W (-DKC_W=1..8).
+// Included by kc_count_w.hip, which is compiled once per key width W (-DKC_W=1..15).
 //
 // The reference inserts every window with process_kmer_MT (kmer_hash_table.cpp:
 // 2207-2567): a CAS-probed table shared by all threads.  Two MI355X paths produce the

@@ -143,8 +143,8 @@ struct BloomView {
                             // (blocks; 0 = the gate reads HBM)
 };
 
-constexpr int MAX_K = 255;     // largest k: eight key words (KCO_MAXW of the oracle)
-constexpr int MAX_W = 8;
+constexpr int MAX_K = 479;     // largest k: fifteen key words + the count fill one 128-byte bucket
+constexpr int MAX_W = 15;      // (KCO_MAXW of the oracle)
 inline int words_for_k(int k) { return k / 32 + 1; }          // spare top bit for EMPTY
 inline int slots_per_bucket(int W) { return BUCKET_WORDS / (W + 1); }
 

@@ -177,7 +177,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     return lib
 
 
-MAX_K = 255  # include/kc_api.h KC_MAX_K
+MAX_K = 479  # include/kc_api.h KC_MAX_K
 
 
 def words_for_k(k: int) -> int:

@@ -27,10 +27,11 @@
 extern "C" {
 #endif
 
-/* Largest k-mer length: keys of up to eight 64-bit words (the reference sizes its blocks
-   dynamically, kmer_factory.cpp:33, and accepts any k > 0, main.cpp:135; INTEGRATION.md
-   "Differences" states this bound). */
-#define KC_MAX_K 255
+/* Largest k-mer length: keys of up to fifteen 64-bit words, which with their count fill
+   one 128-byte table bucket (the reference sizes its blocks dynamically,
+   kmer_factory.cpp:33, and accepts any k > 0, main.cpp:135; INTEGRATION.md "Differences"
+   states this bound). */
+#define KC_MAX_K 479
 
 #define KC_OK 0
 #define KC_ERR_ARG (-1)         /* invalid argument */

@@ -2,7 +2,8 @@
 
 Run in the build container (needs /root/reference):
     make -C oracle ref oracle && make -C canonical-k-mer-hash-table_amd
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py [--append]
+(--append: keep the cases already in cases.json and run the reference only for new ones)
 
 What it writes (all data, no reference source):
   * small inputs (*.fasta / *.txt, committed) made by our generators
@@ -39,6 +40,8 @@ INPUTS = {
     "reads.txt": {"gen": ["1000", "150", "30000", "-s", "7", "-n", "0.002", "--plain"], "commit": True},
     "long.fasta": {"gen": ["40", "5000", "20000", "-s", "5", "-e", "0.01"], "commit": True},
     "edge.fasta": {"edge": [11, 300, 300, 800, 0.02, False], "commit": True},
+    # long reads with few errors: k-mers of k >= 256 seen twice or more
+    "long_lo.fasta": {"gen": ["60", "6000", "20000", "-s", "6", "-e", "0.0005"], "commit": False},
     "edge.txt": {"edge": [3, 200, 0, 800, 0.02, True], "commit": True},
     "big_edge.fasta": {"edge": [7, 16000, 2000, 400, 0.002, False], "commit": False},
     "big_reads.fasta": {"gen": ["150000", "150", "2000000", "-s", "9", "-e", "0.002", "-w", "60"],
@@ -90,6 +93,16 @@ CASES = [
     ("long.fasta", 255, ["-m", "0", "-a", "1", "-s", "1000000"]),
     ("long.fasta", 255, ["-b", "-u", "300000", "-f", "0.05", "-a", "2"]),
     ("edge.fasta", 140, ["-a", "1", "-s", "1000000"]),
+    # k = 256..479: keys of nine to fifteen words (one slot per 128-byte bucket)
+    ("long.fasta", 257, ["-a", "1", "-s", "1000000"]),
+    ("long.fasta", 300, ["-a", "1", "-s", "1000000"]),
+    ("long.fasta", 300, ["-m", "0", "-a", "1", "-s", "1000000"]),
+    ("long.fasta", 421, ["-m", "1", "-a", "1", "-s", "1000000"]),
+    ("long_lo.fasta", 289, ["-a", "2", "-s", "1000000"]),
+    ("long_lo.fasta", 383, ["-b", "-u", "300000", "-a", "2"]),
+    ("long_lo.fasta", 479, ["-a", "2", "-s", "1000000"]),
+    ("long_lo.fasta", 479, ["-m", "0", "-a", "3", "-s", "1000000"]),
+    ("long_lo.fasta", 479, ["-m", "0", "-b", "-u", "300000", "-a", "1"]),
     ("big_edge.fasta", 161, ["-a", "1", "-s", "8000000"]),
     # skew (hot keys: homopolymers, dinucleotide repeats, a high-copy repeat)
     ("skew.fasta", 31, ["-a", "1", "-s", "4000000"]),
@@ -140,8 +153,18 @@ def main():
         path = build_input(name, HERE if r["commit"] else work)
         inputs[name] = {"sha256": sha256_file(path), "bytes": os.path.getsize(path), "commit": r["commit"]}
         inputs[name].update({k: v for k, v in r.items() if k in ("gen", "edge")})
+    old = {}
+    if "--append" in sys.argv[1:]:
+        with open(os.path.join(HERE, "cases.json")) as f:
+            prev = json.load(f)
+        for c in prev["cases"]:
+            if prev["inputs"][c["input"]]["sha256"] == inputs[c["input"]]["sha256"]:
+                old[(c["input"], c["k"], tuple(c["args"]))] = c
     cases = []
     for name, k, args in CASES:
+        if (name, k, tuple(args)) in old:
+            cases.append(old[(name, k, tuple(args))])
+            continue
         src = os.path.join(HERE if INPUTS[name]["commit"] else work, name)
         out = os.path.join(work, "ref.out")
         if os.path.exists(out):

@@ -43,7 +43,7 @@ def test_compact_golden(case, golden_input):
         assert max_hops <= max(0, case["k"] - 2)
 
 
-@pytest.mark.parametrize("k", [5, 15, 21, 31, 32, 33, 51, 63, 64, 95, 127, 200, 255])
+@pytest.mark.parametrize("k", [5, 15, 21, 31, 32, 33, 51, 63, 64, 95, 127, 200, 255, 300, 479])
 def test_compact_reference_walk_and_lookup(tmp_path, k):
     """Synthetic reads (errors, both strands): the slot words walked by the reference's
     algorithm (Python restatement) give the dumped k-mers; lookups by key give the counts,

@@ -107,9 +107,9 @@ def test_cli_option_semantics(golden_input, tmp_path):
     assert run_cli(tmp_path / "missing.fa", 31, "-s", 1000).returncode == 105
     assert run_cli(fa).returncode == 106
     assert run_cli("-h").returncode == 0
-    # k above KC_MAX_K (eight key words) is refused with a message (INTEGRATION.md Differences)
-    r = run_cli(fa, 256, "-s", 1000, "-o", tmp_path / "big_k.txt")
-    assert r.returncode == 1 and "above 255" in r.stderr and not (tmp_path / "big_k.txt").exists()
+    # k above KC_MAX_K (fifteen key words) is refused with a message (INTEGRATION.md Differences)
+    r = run_cli(fa, 480, "-s", 1000, "-o", tmp_path / "big_k.txt")
+    assert r.returncode == 1 and "above 479" in r.stderr and not (tmp_path / "big_k.txt").exists()
 
 
 def test_cli_format_checks(tmp_path):
