@@ -332,10 +332,12 @@ class _OneRank:
         return 0
 
 
-@pytest.mark.parametrize("k", [31, 63])
-def test_sharded_counter_bloom_one_rank(tmp_path, k):
+@pytest.mark.parametrize("k,side", [(31, False), (63, False), (31, True)])
+def test_sharded_counter_bloom_one_rank(tmp_path, k, side):
     """ShardedCounter's own Bloom path on the HIP engine (bloom_device -> bloom_finalize ->
-    count_device -> merge) at one rank: the oracle's T(c) >= 2 lines."""
+    count_device -> merge) at one rank: the oracle's T(c) >= 2 lines.  side: the caller's
+    stream is not torch's current stream (bloom_finalize and merge order their collectives
+    and kc_* calls on it, sharded.py _on_stream)."""
     from kaarme_amd.sharded import ShardedCounter
 
     fa = tmp_path / "r.fasta"
@@ -343,7 +345,12 @@ def test_sharded_counter_bloom_one_rank(tmp_path, k):
     data, img = _image(str(fa))
     cfg = ka.Config(k=k, mode=2, bf_enable=True, est_unique=300000, fpr=0.01, min_abundance=2)
     sc = ShardedCounter(cfg, _OneRank())
-    stream = torch.cuda.current_stream().cuda_stream
+    if side:
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        stream = s.cuda_stream
+    else:
+        stream = torch.cuda.current_stream().cuda_stream
     ch = ka.plan_chunks(data, k, ka.FMT_FASTA)
     sc.bloom_device(img.data_ptr(), ch, ka.FMT_FASTA, stream)
     nis = sc.bloom_finalize()
