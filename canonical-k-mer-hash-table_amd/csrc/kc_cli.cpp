@@ -47,6 +47,7 @@ struct Args {
     bool have_s = false, have_u = false;
     unsigned long long slots = 0, unique = 0;
     int device = 0;
+    std::string gunzip_to;  // test hook: write the decompressed input there and exit (no GPU)
 };
 
 void usage(const char* prog) {
@@ -95,6 +96,66 @@ bool parse_double(const std::string& s, double* v) {
     char* end = nullptr;
     *v = std::strtod(s.c_str(), &end);
     return end && *end == 0;
+}
+
+// BGZF input (blocked gzip, bgzip / htslib: every member carries its compressed size in a
+// 'BC' extra subfield and is at most 64 KiB uncompressed): the members are inflated by up to
+// `nt` threads straight into their slots of one buffer (each member's ISIZE gives its slot).
+// Returns false when the file is not BGZF (the caller reads it as one stream); *bad is set
+// when a member does not inflate to its ISIZE (corrupt input).
+static bool gunzip_bgzf(const uint8_t* z, uint64_t n, int nt, std::vector<uint8_t>* out, bool* bad) {
+    std::vector<uint64_t> off, len, dst;
+    std::vector<uint32_t> usz;
+    uint64_t p = 0, total = 0;
+    while (p < n) {
+        if (n - p < 28 || z[p] != 0x1f || z[p + 1] != 0x8b || z[p + 2] != 8 || !(z[p + 3] & 4)) return false;
+        const uint32_t xlen = z[p + 10] | (uint32_t)z[p + 11] << 8;
+        if (12 + (uint64_t)xlen > n - p) return false;
+        uint64_t bsize = 0;
+        for (uint32_t q = 0; q + 4 <= xlen;) {
+            const uint8_t* f = z + p + 12 + q;
+            const uint32_t sl = f[2] | (uint32_t)f[3] << 8;
+            if (f[0] == 'B' && f[1] == 'C' && sl == 2 && q + 6 <= xlen) {
+                bsize = (f[4] | (uint32_t)f[5] << 8) + 1ULL;
+                break;
+            }
+            q += 4 + sl;
+        }
+        if (bsize < 20 + (uint64_t)xlen || bsize > n - p) return false;
+        const uint8_t* t = z + p + bsize - 4;
+        const uint32_t isz = t[0] | (uint32_t)t[1] << 8 | (uint32_t)t[2] << 16 | (uint32_t)t[3] << 24;
+        off.push_back(p);
+        len.push_back(bsize);
+        usz.push_back(isz);
+        dst.push_back(total);
+        total += isz;
+        p += bsize;
+    }
+    if (off.size() < 2) return false;  // one member: nothing to split
+    out->resize(total);
+    std::atomic<uint64_t> next{0};
+    std::atomic<bool> fail{false};
+    auto work = [&]() {
+        uint8_t dummy = 0;
+        for (uint64_t i; (i = next.fetch_add(1)) < off.size() && !fail.load();) {
+            z_stream st{};
+            if (inflateInit2(&st, 16 + MAX_WBITS) != Z_OK) { fail = true; break; }
+            st.next_in = const_cast<Bytef*>(z + off[i]);
+            st.avail_in = (uInt)len[i];
+            st.next_out = usz[i] ? out->data() + dst[i] : &dummy;
+            st.avail_out = usz[i] ? usz[i] : 1;
+            const int r = inflate(&st, Z_FINISH);
+            if (r != Z_STREAM_END || st.total_out != usz[i] || st.avail_in != 0) fail = true;
+            inflateEnd(&st);
+        }
+    };
+    const int T = std::max(1, std::min<int>(nt, (int)std::min<uint64_t>(off.size(), 64)));
+    std::vector<std::thread> th;
+    for (int i = 1; i < T; i++) th.emplace_back(work);
+    work();
+    for (auto& x : th) x.join();
+    *bad = fail.load();
+    return true;
 }
 
 // returns -1 on success, else exit code
@@ -151,6 +212,8 @@ int parse(int argc, char** argv, Args* a) {
                 if (!parse_uint(v, &u)) return cli_error(kConversion, "Could not convert: " + o + " = " + v);
                 a->unique = u;
                 a->have_u = true;
+            } else if (o == "--gunzip-to") {
+                a->gunzip_to = v;
             } else if (o == "--device") {
                 if (!parse_int(v, &si) || si < 0) return cli_error(kConversion, "Could not convert: " + o + " = " + v);
                 a->device = (int)si;
@@ -291,7 +354,22 @@ int main(int argc, char** argv) {
     uint64_t isize = 0;
     std::vector<uint8_t> gzbuf;
     void* map = nullptr;
-    if (gz) {
+    bool bgzf = false;
+    if (gz) {  // BGZF: members inflated in parallel
+        void* zm = mmap(nullptr, fsize, PROT_READ, MAP_PRIVATE, fd, 0);
+        if (zm != MAP_FAILED) {
+            const unsigned hw = std::thread::hardware_concurrency();
+            bool bad = false;
+            bgzf = gunzip_bgzf((const uint8_t*)zm, fsize, (int)std::min(16u, hw ? hw : 1u), &gzbuf, &bad);
+            munmap(zm, fsize);
+            if (bgzf && bad) {
+                std::cerr << "gzip input " << a.input << " is corrupt or truncated: a BGZF member does not inflate"
+                          << std::endl;
+                return 1;
+            }
+        }
+    }
+    if (gz && !bgzf) {
         gzFile g = gzdopen(dup(fd), "r");
         if (!g) { std::cerr << "cannot open " << a.input << " as gzip\n"; return 1; }
         gzbuffer(g, 1 << 20);
@@ -308,6 +386,8 @@ int main(int argc, char** argv) {
             return 1;
         }
         gzclose(g);
+    }
+    if (gz) {
         image = gzbuf.data();
         isize = gzbuf.size();
     } else if (fsize) {
@@ -316,6 +396,13 @@ int main(int argc, char** argv) {
         madvise(map, fsize, MADV_SEQUENTIAL);
         image = (const uint8_t*)map;
         isize = fsize;
+    }
+    if (!a.gunzip_to.empty()) {  // test hook (tests/test_host.py): the decompressed bytes, no GPU work
+        FILE* f = std::fopen(a.gunzip_to.c_str(), "wb");
+        if (!f || (isize && std::fwrite(image, 1, isize, f) != isize)) { std::cerr << "cannot write " << a.gunzip_to << "\n"; return 1; }
+        std::fclose(f);
+        std::cout << "gunzip: " << isize << " bytes" << (bgzf ? " (BGZF, parallel)" : "") << std::endl;
+        return 0;
     }
     const unsigned char sym = isize ? image[0] : 0;
     int fmt;

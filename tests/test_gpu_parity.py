@@ -176,7 +176,7 @@ def test_cli_end_to_end(case, cli_path, golden_input, tmp_path):
 @pytest.mark.parametrize("name,k,args", [("reads_w60.fasta", 31, ["-m", "2", "-a", "1", "-s", "1000000"]),
                                          ("reads.txt", 31, ["-a", "1", "-s", "1000000"]),
                                          ("big_reads.fasta", 31, ["-a", "2", "-s", "8000000"])])
-@pytest.mark.parametrize("members", [1, 3])
+@pytest.mark.parametrize("members", [1, 3, "bgzf"])
 def test_cli_gzip_input_is_counted_whole(name, k, args, members, golden_input, tmp_path):
     """gzip input (an extension): the reference reads only part of a
     compressed file; the drop-in CLI decompresses every member of the
@@ -187,10 +187,15 @@ def test_cli_gzip_input_is_counted_whole(name, k, args, members, golden_input, t
     case = next(c for c in CASES if c["input"] == name and c["k"] == k and c["args"] == args)
     raw = open(golden_input(name), "rb").read()
     gz = tmp_path / (name + ".gz")
-    cuts = [len(raw) * i // members for i in range(members + 1)]
-    with open(gz, "wb") as f:  # concatenated members split at arbitrary bytes
-        for a, b in zip(cuts, cuts[1:]):
-            f.write(gzip.compress(raw[a:b], compresslevel=1))
+    if members == "bgzf":  # blocked gzip: members inflated in parallel (kc_cli.cpp gunzip_bgzf)
+        from test_host import _bgzf
+
+        gz.write_bytes(_bgzf(raw))
+    else:
+        cuts = [len(raw) * i // members for i in range(members + 1)]
+        with open(gz, "wb") as f:  # concatenated members split at arbitrary bytes
+            for a, b in zip(cuts, cuts[1:]):
+                f.write(gzip.compress(raw[a:b], compresslevel=1))
     out = tmp_path / "out.kaarme_counts"
     r = subprocess.run([CLI, str(gz), str(k), "-t", "3", "-o", str(out)] + args, capture_output=True, text=True)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]

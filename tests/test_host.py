@@ -182,3 +182,48 @@ def test_committed_traffic_book_covers_the_bench_workloads():
         got, entry = bench.load_traffic(line["config"]["workload"])
         assert got and got > line["roofline"]["algorithmic_bytes_per_launch"] * 0.5, name
         assert entry["bytes_per_launch"] == got
+
+
+def _bgzf(data, block=60000):
+    """BGZF (bgzip's blocked gzip): members of <= 64 KiB with their size in a 'BC' extra field,
+    ending with the empty EOF member."""
+    import struct
+    import zlib
+
+    out = bytearray()
+    for chunk in [data[i:i + block] for i in range(0, len(data), block)] + [b""]:
+        c = zlib.compressobj(6, zlib.DEFLATED, -15)
+        cd = c.compress(chunk) + c.flush()
+        bsize = 18 + len(cd) + 8
+        out += bytes([0x1F, 0x8B, 8, 4, 0, 0, 0, 0, 0, 0xFF]) + struct.pack("<H", 6) + b"BC"
+        out += struct.pack("<HH", 2, bsize - 1) + cd + struct.pack("<II", zlib.crc32(chunk) & 0xFFFFFFFF, len(chunk))
+    return bytes(out)
+
+
+def test_cli_gunzip_bgzf_parallel_and_streams(golden_input, tmp_path):
+    """gzip input (an extension, DESIGN §6): BGZF members inflate in parallel into their slots;
+    other gzip files (one or several members) go through one zlib stream; a corrupt member fails."""
+    import gzip
+
+    data = open(golden_input("reads_w60.fasta"), "rb").read() * 3
+    bz = _bgzf(data)
+    assert gzip.decompress(bz) == data  # the writer above makes valid gzip
+    src = tmp_path / "r.fasta.gz"
+    src.write_bytes(bz)
+    out = tmp_path / "out.bin"
+    r = run_cli(src, 31, "-s", 1000, "--gunzip-to", out)
+    assert r.returncode == 0 and "BGZF, parallel" in r.stdout, r.stderr
+    assert out.read_bytes() == data
+    # plain multi-member gzip: one stream
+    mm = tmp_path / "m.fasta.gz"
+    mm.write_bytes(gzip.compress(data[:100000]) + gzip.compress(data[100000:]))
+    r = run_cli(mm, 31, "-s", 1000, "--gunzip-to", out)
+    assert r.returncode == 0 and "BGZF" not in r.stdout and out.read_bytes() == data
+    # a corrupt BGZF member (a byte of the second member's deflate data flipped)
+    bad = bytearray(bz)
+    second = bz.index(b"\x1f\x8b\x08\x04", 1)
+    bad[second + 40] ^= 0xFF
+    badp = tmp_path / "bad.fasta.gz"
+    badp.write_bytes(bytes(bad))
+    r = run_cli(badp, 31, "-s", 1000, "--gunzip-to", out)
+    assert r.returncode == 1 and "corrupt" in r.stderr
