@@ -175,11 +175,14 @@ def cpu_model():
 
 
 def kernel_source_digest():
-    """SHA-256 (16 hex) of the engine's kernel and host sources: what a PMC summary was measured with."""
+    """SHA-256 (16 hex) of the engine's kernel and host sources: what a PMC summary was measured with
+    (the drop-in CLI's kc_cli.cpp is not part of the library bench.py runs)."""
     import hashlib
     h = hashlib.sha256()
     src = os.path.join(PKG, "csrc")
     for name in sorted(os.listdir(src)):
+        if name == "kc_cli.cpp":
+            continue
         with open(os.path.join(src, name), "rb") as f:
             h.update(name.encode() + b"\0" + f.read())
     return h.hexdigest()[:16]
