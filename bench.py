@@ -526,6 +526,64 @@ def run_workload(args, env, image=None):
     return out, image
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n, cpu_only):
+    """Starts `n` rank processes of this same command line (RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_ADDR=127.0.0.1 / MASTER_PORT in their environment, as torch.distributed.run would set
+    them) and waits for them.  The launcher itself never touches the GPU: the ranks are children,
+    not an exec.  Rank 0 prints the JSON line on the inherited stdout.  Returns the exit code
+    (the first nonzero rank's; a failed rank stops the others)."""
+    if not cpu_only:
+        import torch  # counting devices does not initialise the GPU on this image
+        have = torch.cuda.device_count()
+        if have < n:
+            log(f"error: --gpus {n} but {have} GPU(s) visible")
+            return 2
+    port = str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 1
+                log(f"rank {procs.index(p)} exited with {c}: stopping the other ranks")
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def launch_check(args):
+    """--launch-only: join the process group (gloo on CPU) and report how many ranks joined."""
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group(args.backend)
+    t = torch.ones(1)
+    dist.all_reduce(t)
+    rank, world = dist.get_rank(), dist.get_world_size()
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "k-mers/s", "n_gpus": world,
+                          "ranks_joined": int(t.item()), "launch_only": True, "backend": args.backend}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -557,7 +615,22 @@ def main():
                          "table sized from the distinct estimate; no exchange)")
     ap.add_argument("--force-sharded", action="store_true",
                     help="use the sharded (RCCL) path even at one rank (testing)")
+    ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
+                    help="torch.distributed backend of the ranks (nccl = RCCL; gloo only with --launch-only)")
+    ap.add_argument("--launch-only", action="store_true",
+                    help="start the ranks, join the process group and print the line without any GPU work "
+                         "(tests the N-rank launch on CPU)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `bench.py --gpus N` without a launcher starts its own N rank processes
+        # (before anything here touches the GPU) instead of timing one GPU
+        sys.exit(launch_ranks(args.gpus, args.launch_only))
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and world_env != args.gpus:
+        log(f"error: --gpus {args.gpus} but WORLD_SIZE={world_env}")
+        sys.exit(2)
+    if args.launch_only:
+        sys.exit(launch_check(args))
     # stdout carries exactly one JSON line: libraries (RCCL prints a version banner at
     # communicator init) write to fd 1 too, so fd 1 becomes stderr and the JSON goes to a
     # private copy of the original stdout
