@@ -146,7 +146,15 @@ struct kc_ctx {
     TableView fgeo{};                     // the kept partitions' fine geometry (powers of two)
     uint64_t fgeo_max_R = 0;              // the create-time fine regions (the most the LDS fits)
     uint64_t fgeo_next_R = 0;             // fine regions learned from the last finalize (0 = keep)
-    int reuse_level = 0;                  // kc_bloom_finalize: 2 = from level 2, 1 = from level 1
+    int reuse_level = 0;                  // kc_bloom_finalize: 3 = counted by the fused pass, 2 = from level 2,
+                                          // 1 = from level 1
+    // Fused Bloom + counting pass (run_batch): the kept batch's table counted during the Bloom
+    // pass itself (launch_bloom_count_fused), "speculatively": it stands only if the counting
+    // pass presents the same input (count_reused, level 3); any other use of the table first
+    // drops it (settle_spec).  The table's size comes from a sample of the kept fine bins
+    // (launch_bloom_probe); the reference's 2 * new_in_second stays the job's min_slots.
+    bool spec_table = false;
+    uint32_t* d_probe = nullptr;          // PROBE_BINS sample counts
     uint64_t reuse_hits = 0;          // counting passes that reused (kc_stats.reused_passes)
     int reuse_last_level = 0;         // the level the last reused pass started from (kc_stats.reuse_level)
 
@@ -209,6 +217,8 @@ static uint64_t bloom_words(const kc_ctx* c) {
     const uint64_t w = std::max<uint64_t>(1, (2 * c->bf_bits + 31) / 32);
     return c->bloom_blocked ? std::max<uint64_t>(w, 16 * bloom_blocks(c->bf_bits)) : w;
 }
+
+static int alloc_regions(kc_ctx* c);
 
 // pow2_f1 != 0: R = F1 x F2 with F1 = pow2_f1 (the Bloom filter's coarse bins) and F2 a power
 // of two, so the table's coarse bins are the filter's hash-prefix bins (level-1 reuse)
@@ -280,6 +290,11 @@ static int alloc_table(kc_ctx* c, uint64_t min_slots, uint32_t pow2_f1 = 0) {
         }
     }
     c->R = (uint64_t)c->F1 * c->F2;
+    return alloc_regions(c);
+}
+
+// the table's memory for c->R regions (the geometry set by the caller)
+static int alloc_regions(kc_ctx* c) {
     if (c->R >= (1ULL << 32)) return c->fail(KC_ERR_ARG, "table too large");  // 32-bit region index (kc_common.h)
     c->nbuckets = c->R * BPR;
     const size_t bytes = c->nbuckets * BUCKET_WORDS * sizeof(uint64_t);
@@ -300,6 +315,34 @@ static int alloc_table(kc_ctx* c, uint64_t min_slots, uint32_t pow2_f1 = 0) {
     return KC_OK;
 }
 
+// the fused pass's table: exactly R regions (a power of two), coarse bins = min(f1, R) of them
+static int alloc_table_pow2(kc_ctx* c, uint64_t R, uint32_t f1) {
+    int rb = 0, fb = 0;
+    while ((1ULL << rb) < R) rb++;
+    while ((1u << fb) < f1) fb++;
+    fb = std::min(fb, rb);
+    c->f2bits = rb - fb;
+    c->F2 = 1u << c->f2bits;
+    c->F1 = 1u << fb;
+    c->R = R;
+    c->seg_ok = true;
+    return alloc_regions(c);
+}
+
+// Drop the fused pass's speculative table before anything but the confirming counting pass
+// uses the table: before kc_bloom_finalize there is no table yet; after it, the table the
+// reference would have (2 * new_in_second slots), fresh.
+static int settle_spec(kc_ctx* c) {
+    if (!c->spec_table) return KC_OK;
+    c->spec_table = false;
+    c->reuse_ok = false;
+    if (!c->bloom_final) {
+        c->nbuckets = 0;
+        return KC_OK;
+    }
+    return alloc_table(c, c->min_slots);
+}
+
 static TableView table_view(const kc_ctx* c) {
     TableView tv;
     tv.buckets = c->d_table;
@@ -316,6 +359,8 @@ static TableView table_view(const kc_ctx* c) {
 // Perform a deferred table reset before the table is read or updated by anything but a
 // fresh level-3 pass.
 static int materialize_zero(kc_ctx* c, hipStream_t s) {
+    const int rc = settle_spec(c);
+    if (rc) return rc;
     if (!c->table_zero_pending || !c->d_table) return KC_OK;
     HIPCHK(c, hipMemsetAsync(c->d_table, 0, c->nbuckets * BUCKET_WORDS * sizeof(uint64_t), s));
     c->table_zero_pending = false;
@@ -481,6 +526,48 @@ static int tail_needed(kc_ctx* c, hipStream_t s, bool* need) {
     return KC_OK;
 }
 
+static bool fuse_enabled() {
+    const char* v = std::getenv("KC_FUSE");
+    return !(v && *v == '0');
+}
+
+// The fused pass's table regions from the probe's sample of the kept fine bins: the distinct
+// keys passing the gate, scaled to all fine bins, at a mean load of KC_FUSE_LOAD (0.7) of a
+// region's slots, as a power of two between the bounds the fused kernel needs (regions =
+// unions of fine bins, of whole filter blocks, <= 1024 blocks and MAX_SEG_GROUP segments
+// each).  0 = no fused pass (a sampled bin outgrew the probe, or the bounds cross).
+// KC_FUSE_R forces the region count (tests, A/B).
+static uint64_t fused_regions(const kc_ctx* c, const uint32_t* probe, uint32_t ns) {
+    uint64_t sum = 0;
+    for (uint32_t i = 0; i < ns; i++) {
+        if (probe[i] == ~0u) return 0;
+        sum += probe[i];
+    }
+    static const double load = [] {
+        const char* v = std::getenv("KC_FUSE_LOAD");
+        const double x = v ? std::atof(v) : 0.7;
+        return x > 0.05 && x <= 1.0 ? x : 0.7;
+    }();
+    const uint64_t nblocks = bloom_blocks(c->bf_bits), fine = c->fgeo.R;
+    const double est = (double)sum * (double)(fine / ns);
+    const uint64_t need = (uint64_t)std::ceil(est / (load * c->S * BPR));
+    uint64_t lo = std::max<uint64_t>(nblocks / BF_BLOCKS_PER_REGION,
+                                     fine * c->pbf.B2 / MAX_SEG_GROUP + (fine * c->pbf.B2 % MAX_SEG_GROUP != 0));
+    uint64_t rt = 1;
+    while (rt < std::max<uint64_t>(need, lo)) rt <<= 1;
+    // regions no finer than the fine bins: a fuller table (mean load up to 0.9; a region that
+    // overflows still only costs the fallback) rather than no fused pass
+    if (rt > fine && est <= 0.9 * (double)fine * c->S * BPR) rt = fine;
+    if (const char* v = std::getenv("KC_FUSE_R")) rt = std::strtoull(v, 0, 10);
+    if (std::getenv("KC_REUSE_DEBUG"))
+        std::fprintf(stderr, "fused sizing: probe sum %llu of %u bins, est %.0f, need %llu, lo %llu, rt %llu, fine %llu, "
+                     "nblocks %llu, B2 %u\n", (unsigned long long)sum, ns, est, (unsigned long long)need,
+                     (unsigned long long)lo, (unsigned long long)rt, (unsigned long long)fine,
+                     (unsigned long long)nblocks, c->pbf.B2);
+    if (rt == 0 || (rt & (rt - 1)) || rt > fine || rt > nblocks || rt < lo) return 0;
+    return rt;
+}
+
 static int run_batch(kc_ctx* c, const uint8_t* src, uint64_t used, uint64_t nchunks, int fmt, int pass, hipStream_t s,
                      hipEvent_t ev_start = nullptr, hipEvent_t ev_gather = nullptr, bool keep = false,
                      bool host_gate = false) {
@@ -518,6 +605,10 @@ static int run_batch(kc_ctx* c, const uint8_t* src, uint64_t used, uint64_t nchu
     if (mode == 1) {
         c->bloom_batches++;
         c->reuse_kept = false;
+    }
+    {
+        const int rc = settle_spec(c);  // a second Bloom batch or a counting batch: not the fused pass's
+        if (rc) return rc;
     }
     if (mode == 1 && c->bloom_blocked && use_partitioned_bloom(c, syms)) {
         const char* env = std::getenv("KC_INSERT_PATH");
@@ -564,10 +655,39 @@ static int run_batch(kc_ctx* c, const uint8_t* src, uint64_t used, uint64_t nchu
             }
         }
         const bool split = host_gate && c->pbf.cap1 != 0;
-        HIPCHK(c, launch_bloom_partitioned(sv, c->cfg.k, c->W, bv, c->bgeo, c->fgeo, c->d_ctr, c->pbf,
-                                           c->bloom_fresh, keep ? 1 : 0, s, split ? PH_MAIN : PH_ALL));
+        // the fused Bloom + counting pass (k_bf3): the kept levels, a sizing probe, then one
+        // workgroup per table region does both passes -- unless the levels left a skew list
+        const bool fuse = split && keep && fuse_enabled() && c->cfg.mode != 1 && c->fgeo.R <= bv.nblocks;
+        if (std::getenv("KC_REUSE_DEBUG"))
+            std::fprintf(stderr, "bloom batch: split %d keep %d fine %llu nblocks %llu -> fuse %d\n", (int)split,
+                         (int)keep, (unsigned long long)c->fgeo.R, (unsigned long long)bv.nblocks, (int)fuse);
         bool tail = false;
-        if (split && (rc = tail_needed(c, s, &tail))) return rc;
+        if (fuse) {
+            HIPCHK(c, launch_bloom_partitioned(sv, c->cfg.k, c->W, bv, c->bgeo, c->fgeo, c->d_ctr, c->pbf,
+                                               c->bloom_fresh, 1, s, PH_LEVELS));
+            PartBufs pk = c->pbf;
+            pk.hist2 = c->d_keep_fill2;  // the kept fills (hist2 itself is the skew pass's scratch)
+            const uint32_t ns = (uint32_t)std::min<uint64_t>(PROBE_BINS, c->fgeo.R);
+            HIPCHK(c, launch_bloom_probe(c->W, bv, c->fgeo, pk, ns, c->bloom_fresh, c->d_probe, s));
+            uint32_t probe[PROBE_BINS];
+            HIPCHK(c, hipMemcpyAsync(probe, c->d_probe, ns * 4, hipMemcpyDeviceToHost, s));
+            if ((rc = tail_needed(c, s, &tail))) return rc;  // (its sync covers the probe's copy)
+            const uint64_t rt = tail ? 0 : fused_regions(c, probe, ns);
+            if (rt) {
+                if ((rc = alloc_table_pow2(c, rt, c->fgeo.F1))) return rc;
+                pk.B2 = (uint32_t)(c->fgeo.R / rt) * c->pbf.B2;
+                HIPCHK(c, launch_bloom_count_fused(c->W, bv, table_view(c), c->fgeo, pk, c->d_ctr, c->bloom_fresh, s));
+                c->spec_table = true;
+                c->table_fresh = c->table_zero_pending = false;  // every region written
+            } else {
+                HIPCHK(c, launch_bloom_partitioned(sv, c->cfg.k, c->W, bv, c->bgeo, c->fgeo, c->d_ctr, c->pbf,
+                                                   c->bloom_fresh, 1, s, PH_B3));
+            }
+        } else {
+            HIPCHK(c, launch_bloom_partitioned(sv, c->cfg.k, c->W, bv, c->bgeo, c->fgeo, c->d_ctr, c->pbf,
+                                               c->bloom_fresh, keep ? 1 : 0, s, split ? PH_MAIN : PH_ALL));
+            if (split && (rc = tail_needed(c, s, &tail))) return rc;
+        }
         if (tail)
             HIPCHK(c, launch_bloom_partitioned(sv, c->cfg.k, c->W, bv, c->bgeo, c->fgeo, c->d_ctr, c->pbf,
                                                c->bloom_fresh, keep ? 1 : 0, s, PH_TAIL));
@@ -719,9 +839,30 @@ static int count_reused(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, s
         release();
         return KC_OK;
     }
+    const uint64_t syms = used + b.size();
+    if (c->reuse_level == 3) {  // the fused pass counted these bytes: its table stands
+        HIPCHK(c, launch_spec_commit(c->d_ctr, c->reuse_windows, s));
+        if (ev[3]) HIPCHK(c, hipEventRecord(ev[3], s));
+        c->spec_table = false;
+        c->table_fresh = false;
+        c->table_zero_pending = false;
+        c->n_chunks += b.size();
+        c->n_bytes += bytes;
+        c->reuse_hits++;
+        c->reuse_last_level = 3;
+        if (c->profiling) {
+            c->ev_pending.push_back(ev);
+            c->pending_symbols_bound.push_back(syms);
+        }
+        if (s != c->stream) {
+            HIPCHK(c, hipEventRecord(c->xev, s));
+            HIPCHK(c, hipStreamWaitEvent(c->stream, c->xev, 0));
+        }
+        *done = true;
+        return KC_OK;
+    }
     // the table's partition buffers for this batch, with the Bloom pass's partitions as its
     // level 1 (and level 2); the kept buffers must not have moved
-    const uint64_t syms = used + b.size();
     if ((rc = ensure_part(c, syms, true))) return rc;
     PartBufs pr = c->pb;
     if (pr.keys1 != c->pbf.keys1 || (c->reuse_level == 2 && pr.keys2 != c->pbf.keys2) || pr.nblk1 != c->pbf.nblk1 ||
@@ -807,13 +948,14 @@ static int device_pass(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, si
                                  hipMemcpyHostToDevice, s));
         HIPCHK(c, hipEventRecord(c->h_free[c->cur], s));
         hipEvent_t e0 = nullptr, e1 = nullptr;
-        if (c->profiling) {
+        const bool timed = c->profiling && pass != 3;  // (the sketch pass is not a timed batch)
+        if (timed) {
             e0 = c->get_event();
             e1 = c->get_event();
             HIPCHK(c, hipEventRecord(e0, s));
         }
         // the image is tokenized in place (no gather into the stage): "gather" is ~0
-        if (c->profiling) HIPCHK(c, hipEventRecord(e1, s));
+        if (timed) HIPCHK(c, hipEventRecord(e1, s));
         // the checksum of a batch the Bloom pass may keep (what a counting pass must present
         // again) runs on a second stream beside the pass's levels: both only read the image
         // (C3: 0.31 ms of streaming hidden under the latency-bound level 1)
@@ -950,6 +1092,7 @@ int kc_create(const kc_config* cfg, kc_ctx** out) {
         if (hipMalloc(&c->d_bloom, words * 4) != hipSuccess)
             return bail(KC_ERR_NOMEM, "Bloom filter allocation failed");
         if (hipMemsetAsync(c->d_bloom, 0, words * 4, c->stream) != hipSuccess) return bail(KC_ERR_HIP, "memset");
+        if (hipMalloc(&c->d_probe, PROBE_BINS * 4) != hipSuccess) return bail(KC_ERR_NOMEM, "probe allocation failed");
         c->bloom_fresh = true;
         if (c->bloom_blocked) {
             // filter regions of up to BF_BLOCKS_PER_REGION (1024) blocks = 64 KiB, F1 x F2 as
@@ -989,12 +1132,21 @@ int kc_create(const kc_config* cfg, kc_ctx** out) {
                         break;
                 }
                 if (fb >= rbits) {
+                    c->fgeo_max_R = 1ULL << fb;
+                    // the job starts at no more than 2^16 fine bins (KC_FGEO_R): -u usually
+                    // overstates the k-mers that pass the gate (C3: -u 4e8 for 50 M), and
+                    // level 2's 256-bin scatter of C2's table is the fastest shape; the fused
+                    // pass sizes its table from the data and takes these bins whole
+                    const char* v = std::getenv("KC_FGEO_R");
+                    const uint64_t cap = v ? std::max<uint64_t>(1, std::strtoull(v, 0, 10)) : (1ULL << 16);
+                    while (fb > rbits && (1ULL << fb) > cap) fb--;
+                    f1 = std::min(fb, std::min(8, (fb + 1) / 2 + 1));
+                    while (f1 > 0 && p1_lds_bytes(c->W, 1u << f1) > p1_cap) f1--;
                     c->fgeo.R = 1ULL << fb;
                     c->fgeo.f2bits = fb - f1;
                     c->fgeo.F2 = 1u << c->fgeo.f2bits;
                     c->fgeo.F1 = 1u << f1;
                     c->fgeo.W = c->W;
-                    c->fgeo_max_R = c->fgeo.R;
                 }
             }
         }
@@ -1025,6 +1177,7 @@ void kc_destroy(kc_ctx* c) {
     hipFree(c->d_ctr);
     hipFree(c->d_sum);
     hipFree(c->d_hll);
+    hipFree(c->d_probe);
     hipFree(c->d_cwords);
     hipFree(c->d_csecond);
     hipFree(c->d_cstat);
@@ -1093,6 +1246,27 @@ int kc_bloom_finalize(kc_ctx* c, uint64_t* new_in_second) {
     bool reuse = c->reuse_kept && c->bloom_batches == 1 && h.part_fallbacks == 0 && h.spilled == 0 && h.heavy == 0;
     const uint64_t slots = 2 * h.new_in_second;  // main.cpp:454
     c->reuse_level = 0;
+    if (c->spec_table && (!reuse || h.spec_overflow)) {
+        // a region of the fused pass's table overflowed (the probe underestimated it): the
+        // counting pass runs from the kept level 2 into the reference-sized table instead
+        c->spec_table = false;
+        if (std::getenv("KC_REUSE_DEBUG"))
+            std::fprintf(stderr, "fused pass dropped: %llu keys did not fit\n", (unsigned long long)h.spec_overflow);
+    }
+    if (c->spec_table) {
+        // the fused pass counted the batch: the table stands if the counting pass presents the
+        // same input (count_reused); min_slots stays the reference's 2 * new_in_second
+        unsigned long long part[CHECKSUM_SLOTS];
+        HIPCHK(c, hipMemcpy(part, c->d_sum, sizeof(part), hipMemcpyDeviceToHost));
+        c->reuse_sum = 0;
+        for (auto v : part) c->reuse_sum += v;
+        c->reuse_windows = h.bf_windows;
+        c->reuse_level = 3;
+        c->reuse_ok = true;
+        c->min_slots = slots;
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        return KC_OK;
+    }
     if (reuse) {
         uint64_t want = std::max<uint64_t>(slots, 64);
         want += want / 4;
@@ -1137,6 +1311,8 @@ int kc_bloom_finalize(kc_ctx* c, uint64_t* new_in_second) {
 int kc_count_chunk(kc_ctx* c, const uint8_t* buf, size_t len, int fmt, int bh) {
     if (!c) return KC_ERR_ARG;
     if (!c->nbuckets) return c->fail(KC_ERR_STATE, "kc_bloom_finalize must precede the counting pass");
+    const int rc = settle_spec(c);
+    if (rc) return rc;
     return add_host_chunk(c, buf, len, fmt, bh, 0);
 }
 
@@ -1149,6 +1325,8 @@ int kc_count_device(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, size_
         const int rc = count_reused(c, img, chunks, n, fmt, pick_stream(c, s), &done);
         if (rc || done) return rc;
     }
+    const int rc = settle_spec(c);  // (another input than the fused pass's)
+    if (rc) return rc;
     return device_pass(c, img, chunks, n, fmt, 0, pick_stream(c, s));
 }
 
@@ -1293,6 +1471,10 @@ int kc_route_table_device(kc_ctx* c, uint32_t nshards, uint64_t* dev_out, uint64
 
 int kc_insert_counts_device(kc_ctx* c, const uint64_t* recs, uint64_t n, void* sp) {
     if (!c || (!recs && n)) return KC_ERR_ARG;
+    {
+        const int r0 = settle_spec(c);
+        if (r0) return r0;
+    }
     if (!c->nbuckets) return c->fail(KC_ERR_STATE, "no table");
     hipStream_t s = pick_stream(c, sp);
     int rc = flush_host(c);
@@ -1333,6 +1515,10 @@ int kc_insert_counts_device(kc_ctx* c, const uint64_t* recs, uint64_t n, void* s
 int kc_insert_counts_runs_device(kc_ctx* c, const uint64_t* recs, const uint64_t* group_counts, uint32_t ngroups,
                                  void* sp) {
     if (!c || !group_counts || ngroups == 0 || ngroups > 64) return KC_ERR_ARG;
+    {
+        const int r0 = settle_spec(c);
+        if (r0) return r0;
+    }
     if (!c->nbuckets) return c->fail(KC_ERR_STATE, "no table");
     std::vector<uint64_t> gs(ngroups + 1, 0);
     uint64_t maxn = 0;
@@ -1397,6 +1583,10 @@ int kc_insert_counts_runs_device(kc_ctx* c, const uint64_t* recs, const uint64_t
 
 int kc_insert_keys_device(kc_ctx* c, const uint64_t* keys, uint64_t n, void* sp) {
     if (!c || (!keys && n)) return KC_ERR_ARG;
+    {
+        const int r0 = settle_spec(c);
+        if (r0) return r0;
+    }
     if (!c->nbuckets) return c->fail(KC_ERR_STATE, "no table");
     hipStream_t s = pick_stream(c, sp);
     int rc = flush_host(c);
@@ -1519,6 +1709,8 @@ static void drop_compact(kc_ctx* c) {
 
 int kc_clear_table(kc_ctx* c) {
     if (!c) return KC_ERR_ARG;
+    const int rc = settle_spec(c);
+    if (rc) return rc;
     if (!c->nbuckets) return c->fail(KC_ERR_STATE, "no table");
     c->table_zero_pending = true;  // deferred: see materialize_zero
     c->table_fresh = true;
@@ -1549,6 +1741,10 @@ int kc_reset(kc_ctx* c) {
     drop_compact(c);
     c->reuse_kept = c->reuse_ok = false;
     c->reuse_level = 0;
+    if (c->spec_table) {  // (a job's table is sized again after its Bloom pass)
+        c->spec_table = false;
+        if (!c->bloom_final) c->nbuckets = 0;
+    }
     if (c->fgeo_next_R && c->fgeo_next_R != c->fgeo.R && c->fgeo_next_R <= c->fgeo_max_R) {
         int fb = 0, f1 = 0;
         while ((1ULL << fb) < c->fgeo_next_R) fb++;
@@ -2010,6 +2206,7 @@ int kc_bloom_write(kc_ctx* c, const uint32_t* words, uint64_t n) {
     if (n > bloom_words(c)) return c->fail(KC_ERR_ARG, "more words than the filter holds");
     int rc = kc_sync(c);
     if (rc) return rc;
+    if ((rc = settle_spec(c))) return rc;  // the fused pass gated by the filter being replaced
     HIPCHK(c, hipMemcpy(c->d_bloom, words, n * 4, hipMemcpyHostToDevice));
     c->bloom_fresh = false;
     return KC_OK;
@@ -2070,6 +2267,7 @@ int kc_bloom_set_device(kc_ctx* c, const uint32_t* dev_src, uint64_t n_words, ui
     hipStream_t s = pick_stream(c, sp);
     int rc = after_host_work(c, s);
     if (rc) return rc;
+    if ((rc = settle_spec(c))) return rc;  // the fused pass gated by the local filter
     HIPCHK(c, hipMemcpyAsync(c->d_bloom, dev_src, n_words * 4, hipMemcpyDeviceToDevice, s));
     c->bloom_fresh = false;
     uint64_t est = 0;

@@ -124,6 +124,10 @@ static bool gunzip_bgzf(const uint8_t* z, uint64_t n, int nt, std::vector<uint8_
         if (bsize < 20 + (uint64_t)xlen || bsize > n - p) return false;
         const uint8_t* t = z + p + bsize - 4;
         const uint32_t isz = t[0] | (uint32_t)t[1] << 8 | (uint32_t)t[2] << 16 | (uint32_t)t[3] << 24;
+        if (isz > 65536) {  // a BGZF member holds at most 64 KiB: a forged or corrupt ISIZE
+            *bad = true;
+            return true;
+        }
         off.push_back(p);
         len.push_back(bsize);
         usz.push_back(isz);
@@ -132,7 +136,12 @@ static bool gunzip_bgzf(const uint8_t* z, uint64_t n, int nt, std::vector<uint8_
         p += bsize;
     }
     if (off.size() < 2) return false;  // one member: nothing to split
-    out->resize(total);
+    try {
+        out->resize(total);
+    } catch (const std::bad_alloc&) {
+        *bad = true;
+        return true;
+    }
     std::atomic<uint64_t> next{0};
     std::atomic<bool> fail{false};
     auto work = [&]() {

@@ -33,6 +33,7 @@
 #pragma once
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 
 #include "kc_common.h"
 
@@ -2131,6 +2132,372 @@ __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView b
 }
 
 // --------------------------------------------------------------------------------
+// Fused Bloom pass 1 + gated counting pass (kc_api.cpp run_batch: a one-batch Bloom pass
+// over a device image whose kept level-2 partitions are clean, with the table sized from a
+// sample of them before the Bloom pass ends).  The reference runs pass 1 over the whole input
+// and then a second pass that counts the k-mers whose filter-2 bits are all set
+// (parallel_parser.hpp:2680-2974, the gate at 2436-2453).  A k-mer's filter block and its
+// table region are the same hash prefix (bloom_block, region_of): once every key of one table
+// region has been through insertion_process, that region's blocks are final, so the same
+// workgroup gates the same keys and counts them into the region.  The keys are read twice,
+// the second time right after the first (a workgroup's ~0.2-0.4 MB stays in the Infinity
+// Cache), instead of by two launches 12 GB of records apart (k_b3 in the Bloom pass, then
+// k_p3<GATE> in the counting pass).
+// --------------------------------------------------------------------------------
+// a kept level-2 item (segment seg of the fine bins, entry j): word 0 of its table key, or
+// the whole key (Rec12 records decoded against their fine bin's lowest x)
+template <int W>
+DEV uint64_t kept_t0(const PartBufs& pb, uint64_t seg, uint64_t j) {
+    if constexpr (W == 2) {
+        if (pb.rec12 & R12_L2) {
+            const uint3 v = reinterpret_cast<const uint3*>(pb.keys2)[seg * pb.cap2 + j];
+            const uint32_t x = (uint32_t)(seg >> pb.r12_b2s) << pb.r12_xb2 | v.z >> (pb.r12_hb + 1);
+            return (uint64_t)x << 32 | v.x;
+        }
+    }
+    return pb.keys2[(seg * pb.cap2 + j) * W];
+}
+template <int W>
+DEV void kept_key(const PartBufs& pb, uint64_t seg, uint64_t j, uint64_t (&t)[W]) {
+    if constexpr (W == 2) {
+        if (pb.rec12 & R12_L2) {
+            const uint3 v = reinterpret_cast<const uint3*>(pb.keys2)[seg * pb.cap2 + j];
+            const Rec12 rc{pb.r12_hb, pb.r12_xb2};
+            rc.dec(v, (uint32_t)(seg >> pb.r12_b2s) << pb.r12_xb2, t[0], t[1]);
+            return;
+        }
+    }
+    const uint64_t* src = pb.keys2 + (seg * pb.cap2 + j) * W;
+#pragma unroll
+    for (int w = 0; w < W; w++) t[w] = src[w];
+}
+
+// insert one table key with count `add` into an LDS region with slot tags (k_p3's tagged
+// probe): false when the region is full
+template <int W>
+DEV bool lds_insert_tagged(uint64_t* lt, uint64_t* tg, uint64_t R, const uint64_t (&kk)[W], uint64_t add) {
+    constexpr int S = BUCKET_WORDS / (W + 1);
+    constexpr uint32_t SMASK = (1u << S) - 1;
+    const uint64_t k0 = kk[0];
+    uint32_t b = bucket_in_region(k0, R);
+    const uint32_t tag = slot_tag(k0);
+    const uint64_t bc = 0x0101010101010101ULL * tag;
+    for (int probe = 0; probe < 4 * BPR;) {
+        const uint64_t tw = tg[b];
+        uint32_t m = zero_byte_mask8(tw ^ bc) & SMASK;
+        int slot = -1;
+        while (m) {
+            const int sl = __builtin_ctz(m);
+            m &= m - 1;
+            bool eq = *lds_word(lt, b, sl * W) == k0;
+#pragma unroll
+            for (int w = 1; w < W; w++) eq &= *lds_word(lt, b, sl * W + w) == kk[w];
+            if (eq) {
+                slot = sl;
+                break;
+            }
+        }
+        uint64_t a = add;
+        if (slot < 0) {
+            const uint32_t em = zero_byte_mask8(tw) & SMASK;
+            if (!em) {
+                b = (b + 1) & (BPR - 1);
+                probe++;
+                continue;
+            }
+            const int e = __builtin_ctz(em);
+            const uint64_t old =
+                atomicCAS(reinterpret_cast<unsigned long long*>(lds_word(lt, b, e * W)), 0ULL, (unsigned long long)k0);
+            if (old == EMPTY) {
+#pragma unroll
+                for (int w = 1; w < W; w++)
+                    __hip_atomic_store(lds_word(lt, b, e * W + w), kk[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __hip_atomic_store(reinterpret_cast<uint8_t*>(tg + b) + e, (uint8_t)tag, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+                if constexpr (W > 1) a += READY;
+                slot = e;
+            } else if (W == 1 && old == k0) {
+                slot = e;
+            } else {
+                probe++;
+                continue;
+            }
+        }
+        atomicAdd(reinterpret_cast<unsigned long long*>(lds_word(lt, b, S * W + slot)), (unsigned long long)a);
+        return true;
+    }
+    return false;
+}
+
+// One workgroup per table region r (tv.R a power of two): segments [r * B2, (r + 1) * B2) of
+// the kept fine bins (pb.B2 = fine bins per region x their segments, fills in pb.hist2), filter
+// blocks [r * bpr, (r + 1) * bpr), bpr = nblocks / R.  Phase 1 = k_b3 on the region's blocks;
+// the blocks go back to HBM; phase 2 = k_p3<GATE> on the region (the table is fresh: zero-filled,
+// every region written).  LGATE: the blocks' filter-2 halves stay in LDS for the gate
+// (bpr * 32 bytes beside the 68 KiB table image); otherwise the gate reads the blocks just
+// written (L2).  Region overflow -> ctr->spec_overflow (the host then drops the table).
+#ifndef KC_BF3_NT
+#define KC_BF3_NT 1024
+#endif
+constexpr int BF3_THREADS = KC_BF3_NT;  // two per CU: 8 waves per SIMD for the count phase's latency
+template <int W, bool LGATE>
+__global__ __launch_bounds__(BF3_THREADS, BF3_THREADS / 128) void k_bf3(BloomView bf, TableView tv, PartBufs pb,
+                                                                    DevCounters* __restrict__ ctr, int fresh_filter) {
+    constexpr int NT = BF3_THREADS, KB1 = NT >= 1024 ? 2 : 4, KB2 = W > 2 ? 1 : NT >= 1024 ? 2 : 4;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ uint32_t s_pre[MAX_SEG_GROUP + 1];
+    const uint64_t r = blockIdx.x;
+    const uint32_t bpr = (uint32_t)(bf.nblocks / tv.R);
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (uint32_t j = 0; j < pb.B2; j++) {
+            s_pre[j] = acc;
+            acc += pb.hist2[r * pb.B2 + j];
+        }
+        s_pre[pb.B2] = acc;
+    }
+    __syncthreads();
+    const uint32_t end = s_pre[pb.B2];
+    const uint64_t seg0 = r * pb.B2;
+    // ---- phase 1: insertion_process for every key of the region (k_b3)
+    uint32_t* lf = reinterpret_cast<uint32_t*>(smem);
+    uint4* l4 = reinterpret_cast<uint4*>(smem);
+    const uint32_t n4f = bpr * BF_BLOCK_WORDS / 4;
+    uint4* g4f = reinterpret_cast<uint4*>(bf.bits + r * bpr * BF_BLOCK_WORDS);
+    for (uint32_t i = threadIdx.x; i < n4f; i += NT) l4[i] = fresh_filter ? make_uint4(0, 0, 0, 0) : g4f[i];
+    __syncthreads();
+    const uint64_t blk0 = r * bpr;
+    const int lane = threadIdx.x & 63;
+    BloomLocal bl = {0, 0, 0};
+    {
+        uint64_t* wq = reinterpret_cast<uint64_t*>(smem + (size_t)bpr * BF_BLOCK_WORDS * 4) + (threadIdx.x >> 6) * 64;
+        uint32_t cs = 0, cb = 0, nb = s_pre[1];
+        for (uint32_t base = 0; base < end; base += KB1 * NT) {
+            uint64_t t0[KB1];
+#pragma unroll
+            for (int q = 0; q < KB1; q++) {
+                const uint32_t i = base + threadIdx.x + q * NT;
+                t0[q] = EMPTY;
+                if (i < end) {
+                    while (nb <= i) {
+                        cs++;
+                        cb = nb;
+                        nb = s_pre[cs + 1];
+                    }
+                    t0[q] = kept_t0<W>(pb, seg0 + cs, i - cb);
+                }
+            }
+            bool slow[KB1];
+            uint32_t pre[KB1], rank[KB1], total = 0;
+#pragma unroll
+            for (int q = 0; q < KB1; q++) {
+                slow[q] = base + threadIdx.x + q * NT < end &&
+                          !block_gate(lf + (uint32_t)(bloom_block(t0[q], bf.nblocks) - blk0) * BF_BLOCK_WORDS + 8, t0[q],
+                                      bf.nh);
+                const uint64_t bal = __ballot(slow[q]);
+                pre[q] = total;
+                rank[q] = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                total += (uint32_t)__popcll(bal);
+            }
+            for (uint32_t r0 = 0; r0 < total; r0 += 64) {
+#pragma unroll
+                for (int q = 0; q < KB1; q++)
+                    if (slow[q] && pre[q] + rank[q] - r0 < 64) wq[pre[q] + rank[q] - r0] = t0[q];
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                if (lane < total - r0) {
+                    const uint64_t t = wq[lane];
+                    block_insert(lf + (uint32_t)(bloom_block(t, bf.nblocks) - blk0) * BF_BLOCK_WORDS, t, bf.nh, bl);
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n4f; i += NT) g4f[i] = l4[i];  // the final blocks
+    if constexpr (LGATE) {  // block b's filter-2 words to gs + 8 b (host: 2 * bpr <= 2 * NT)
+        const uint32_t i0 = threadIdx.x, i1 = threadIdx.x + NT;
+        const uint4 v0 = i0 < 2 * bpr ? l4[(i0 >> 1) * 4 + 2 + (i0 & 1)] : make_uint4(0, 0, 0, 0);
+        const uint4 v1 = i1 < 2 * bpr ? l4[(i1 >> 1) * 4 + 2 + (i1 & 1)] : make_uint4(0, 0, 0, 0);
+        __syncthreads();
+        if (i0 < 2 * bpr) l4[i0] = v0;
+        if (i1 < 2 * bpr) l4[i1] = v1;
+    } else {
+        __syncthreads();  // the write-back's LDS reads before the table image overwrites them
+    }
+    // ---- phase 2: the same keys behind the gate into the region's LDS table (k_p3<GATE>)
+    const uint32_t* gs = reinterpret_cast<const uint32_t*>(smem);
+    uint64_t* lt = reinterpret_cast<uint64_t*>(smem + (LGATE ? (size_t)bpr * 32 : 0));
+    uint64_t* tg = lt + BPR * BUCKET_WORDS;
+    uint4* t4 = reinterpret_cast<uint4*>(lt);
+    constexpr int N4 = BPR * BUCKET_WORDS / 2, NT4 = BPR / 2;
+    for (int i = threadIdx.x; i < N4 + NT4; i += NT) t4[i] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    uint32_t n_fail = 0, n_ins = 0;
+    uint32_t cs = 0, cb = 0, nb = s_pre[1];
+    auto load = [&](uint32_t base, uint64_t (&kk)[KB2][W], uint32_t& ok) {
+        ok = 0;
+#pragma unroll
+        for (int q = 0; q < KB2; q++) {
+            const uint32_t i = base + threadIdx.x + q * NT;
+#pragma unroll
+            for (int w = 0; w < W; w++) kk[q][w] = 0;
+            if (i < end) {
+                while (nb <= i) {
+                    cs++;
+                    cb = nb;
+                    nb = s_pre[cs + 1];
+                }
+                kept_key<W>(pb, seg0 + cs, i - cb, kk[q]);
+                ok |= 1u << q;
+            }
+        }
+    };
+    uint64_t kk[KB2][W];
+    uint32_t okm = 0;
+    if (end) load(0, kk, okm);
+    for (uint32_t base = 0; base < end; base += KB2 * NT) {
+        uint64_t nkk[KB2][W];
+        uint32_t nokm = 0;
+        const uint32_t nbase = base + KB2 * NT;
+        const bool more = W <= 2 && nbase < end;  // the next round's loads in flight during this one's inserts
+        if (more) load(nbase, nkk, nokm);
+        bool pass[KB2];
+#pragma unroll
+        for (int q = 0; q < KB2; q++) {
+            const uint64_t t0 = kk[q][0];
+            pass[q] = (okm >> q) & 1;
+            if (LGATE)
+                pass[q] = pass[q] && block_gate(gs + (uint32_t)(bloom_block(t0, bf.nblocks) - blk0) * 8, t0, bf.nh_gate);
+            else
+                pass[q] = pass[q] && block_gate(bloom_block_ptr(bf, t0) + 8, t0, bf.nh_gate);
+            n_ins += pass[q];
+        }
+#pragma unroll
+        for (int q = 0; q < KB2; q++)
+            if (pass[q] && !lds_insert_tagged<W>(lt, tg, tv.R, kk[q], 1)) n_fail++;
+        if (more) {
+            okm = nokm;
+#pragma unroll
+            for (int q = 0; q < KB2; q++)
+#pragma unroll
+                for (int w = 0; w < W; w++) kk[q][w] = nkk[q][w];
+        } else if (nbase < end) {
+            load(nbase, kk, okm);
+        }
+    }
+    __syncthreads();
+    uint4* g4 = reinterpret_cast<uint4*>(tv.buckets + r * BPR * BUCKET_WORDS);
+    for (int i = threadIdx.x; i < N4; i += NT) g4[i] = t4[lds_chunk(i >> 3, i & 7)];
+    block_add4(bl.new_first, bl.new_second, bl.failed, n_ins, &ctr->new_in_first, &ctr->new_in_second,
+               &ctr->failed_in_first, &ctr->spec_inserted);
+    if (n_fail) atomicAdd(&ctr->spec_overflow, (unsigned long long)n_fail);
+}
+
+// The fused pass's sizing probe: one workgroup per sampled fine bin fb = blockIdx.x * stride
+// (segments [fb * B2, (fb + 1) * B2) of the kept level 2): the bin's Bloom pass on its own
+// blocks in LDS (insertion_process per key), then the distinct word-0 table keys that pass
+// the gate, counted in an LDS set.  out[blockIdx.x] = that count, ~0u past 3/4 of the set.
+constexpr int PROBE_THREADS = 512;
+constexpr uint32_t PROBE_SET = 4096;
+template <int W>
+__global__ __launch_bounds__(PROBE_THREADS) void k_bprobe(BloomView bf, uint64_t fineR, uint32_t stride, PartBufs pb,
+                                                       int fresh_filter, uint32_t* __restrict__ out) {
+    constexpr int NT = PROBE_THREADS;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ uint32_t s_pre[MAX_SEG_GROUP + 1];
+    __shared__ uint32_t s_cnt, s_sat;
+    const uint64_t fb = (uint64_t)blockIdx.x * stride;
+    const uint32_t bpf = (uint32_t)(bf.nblocks / fineR);
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (uint32_t j = 0; j < pb.B2; j++) {
+            s_pre[j] = acc;
+            acc += pb.hist2[fb * pb.B2 + j];
+        }
+        s_pre[pb.B2] = acc;
+        s_cnt = 0;
+        s_sat = 0;
+    }
+    uint32_t* lf = reinterpret_cast<uint32_t*>(smem);
+    uint64_t* set = reinterpret_cast<uint64_t*>(smem + (size_t)bpf * BF_BLOCK_WORDS * 4);
+    const uint32_t* g = bf.bits + fb * bpf * BF_BLOCK_WORDS;
+    for (uint32_t i = threadIdx.x; i < bpf * BF_BLOCK_WORDS; i += NT) lf[i] = fresh_filter ? 0u : g[i];
+    for (uint32_t i = threadIdx.x; i < PROBE_SET; i += NT) set[i] = EMPTY;
+    __syncthreads();
+    const uint32_t end = s_pre[pb.B2];
+    const uint64_t blk0 = fb * bpf, seg0 = fb * pb.B2;
+    BloomLocal bl = {0, 0, 0};
+    auto item = [&](uint32_t i) {
+        uint32_t lo = 0, hi = pb.B2;  // the segment holding item i
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_pre[mid] <= i) lo = mid;
+            else hi = mid;
+        }
+        return kept_t0<W>(pb, seg0 + lo, i - s_pre[lo]);
+    };
+    for (uint32_t i = threadIdx.x; i < end; i += NT) {
+        const uint64_t t = item(i);
+        block_insert(lf + (uint32_t)(bloom_block(t, bf.nblocks) - blk0) * BF_BLOCK_WORDS, t, bf.nh, bl);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < end && !*(volatile uint32_t*)&s_sat; i += NT) {
+        const uint64_t t = item(i);
+        if (!block_gate(lf + (uint32_t)(bloom_block(t, bf.nblocks) - blk0) * BF_BLOCK_WORDS + 8, t, bf.nh_gate))
+            continue;
+        uint32_t h = (uint32_t)((t * 0x9E3779B97F4A7C15ULL) >> 52);  // 12 bits: PROBE_SET slots
+        bool done = false;
+        for (uint32_t p = 0; p < PROBE_SET && !done; p++, h = (h + 1) & (PROBE_SET - 1)) {
+            const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long*>(set + h), 0ULL, (unsigned long long)t);
+            if (old == EMPTY) {
+                if (atomicAdd(&s_cnt, 1u) + 1 > PROBE_SET / 4 * 3) s_sat = 1;
+                done = true;
+            } else if (old == t) {
+                done = true;
+            }
+        }
+        if (!done) s_sat = 1;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) out[blockIdx.x] = s_sat ? ~0u : s_cnt;
+}
+
+template <int W>
+static hipError_t bloom_count_fused_w(BloomView bf, TableView t, TableView fg, PartBufs pb, DevCounters* ctr,
+                                      int fresh_filter, hipStream_t s) {
+    (void)fg;
+    const uint64_t bpr = bf.nblocks / t.R;
+    const size_t tbl = (size_t)BPR * BUCKET_WORDS * 8 + (size_t)BPR * 8;
+    const size_t ph1 = (size_t)bpr * BF_BLOCK_WORDS * 4 + (size_t)(BF3_THREADS / 64) * 64 * 8;
+    // the filter-2 slice beside the table image if two workgroups still fit a CU (KC_FUSE_GATE:
+    // lds / global forces one)
+    const size_t lg = (size_t)bpr * 32 + tbl;
+    static const int knob = [] {
+        const char* v = std::getenv("KC_FUSE_GATE");
+        return v ? (!std::strcmp(v, "lds") ? 1 : !std::strcmp(v, "global") ? 0 : -1) : -1;
+    }();
+    const bool lgate = bpr <= BF3_THREADS && (knob == 1 || (knob < 0 && std::max(lg, ph1) + 2048 <= 80 * 1024));
+    const size_t sm = std::max(ph1, lgate ? lg : tbl);
+    auto kern = lgate ? k_bf3<W, true> : k_bf3<W, false>;
+    hipError_t e = set_smem(kern, sm);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3((unsigned)t.R), dim3(BF3_THREADS), sm, s, bf, t, pb, ctr, fresh_filter);
+    return hipGetLastError();
+}
+
+template <int W>
+static hipError_t bloom_probe_w(BloomView bf, TableView fg, PartBufs pb, uint32_t nsample, int fresh_filter,
+                                uint32_t* out, hipStream_t s) {
+    const size_t sm = (size_t)(bf.nblocks / fg.R) * BF_BLOCK_WORDS * 4 + (size_t)PROBE_SET * 8;
+    hipError_t e = set_smem(k_bprobe<W>, sm);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_bprobe<W>, dim3(nsample), dim3(PROBE_THREADS), sm, s, bf, fg.R, (uint32_t)(fg.R / nsample), pb,
+                       fresh_filter, out);
+    return hipGetLastError();
+}
+
+// --------------------------------------------------------------------------------
 // shard merge over region-sorted groups (kc_insert_counts_runs_device): the records a
 // rank receives are G groups (one per sender), each in the sender's table order, i.e.
 // sorted by region when the sender's table has this table's geometry.  Region run bounds
@@ -2714,7 +3081,7 @@ static hipError_t bloom_part_w(PackedView sym, int k, BloomView bf, TableView ft
     const TableView& lg = KEEP ? fg : ft;  // the partition levels' geometry
     hipError_t e;
     const unsigned long long* gate = &ctr->part_overflow;
-    if (phase & PH_MAIN) {
+    if (phase & (PH_MAIN | PH_LEVELS)) {
     hipLaunchKernelGGL(k_batch_begin, dim3(1), dim3(1), 0, s, ctr);
     const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
     constexpr int NT = scatter_threads<W>(), NT2 = p2f_threads<OW>();
@@ -2729,7 +3096,6 @@ static hipError_t bloom_part_w(PackedView sym, int k, BloomView bf, TableView ft
     hipLaunchKernelGGL(k1, dim3(pb.nblk1), dim3(NT), sm1, s, sym, k, bf, ctr, pb, lg.F1, coarse_bins(lg), pb.keys1, pk,
                        pkm1, o1, (const unsigned long long*)nullptr, 1);
     hipLaunchKernelGGL(k2, dim3(lg.F1 * pb.B2), dim3(NT2), sm2, s, lg, pb, ctr, 0);
-    PartBufs p3 = pb;  // k_b3's view: a filter region = R_fine / R_f consecutive fine bins
     if constexpr (KEEP) {
         if (pb.keep_fill &&
             ((e = hipMemcpyAsync(pb.keep_fill, pb.hist1, (size_t)fg.F1 * pb.nblk1 * 4, hipMemcpyDeviceToDevice, s)) !=
@@ -2737,9 +3103,12 @@ static hipError_t bloom_part_w(PackedView sym, int k, BloomView bf, TableView ft
              (e = hipMemcpyAsync(pb.keep_fill2, pb.hist2, (size_t)fg.R * pb.B2 * 4, hipMemcpyDeviceToDevice, s)) !=
                  hipSuccess))
             return e;
-        p3.B2 = (uint32_t)(fg.R / ft.R) * pb.B2;
     }
-    if ((e = launch_b3<true>(bf, ft, ctr, p3, nullptr, fresh, s, OW)) != hipSuccess) return e;
+    }
+    if (phase & (PH_MAIN | PH_B3)) {  // (PH_B3 alone: after PH_LEVELS, hist2 untouched in between)
+        PartBufs p3 = pb;  // k_b3's view: a filter region = R_fine / R_f consecutive fine bins
+        if constexpr (KEEP) p3.B2 = (uint32_t)(fg.R / ft.R) * pb.B2;
+        if ((e = launch_b3<true>(bf, ft, ctr, p3, nullptr, fresh, s, OW)) != hipSuccess) return e;
     }
     if (!(phase & PH_TAIL)) return hipGetLastError();
     // spilled keys (table key word 0 of OW-word entries) through the exact levels into the
@@ -2883,6 +3252,17 @@ hipError_t WOps<W>::count_reuse(TableView t, BloomView bf, DevCounters* ctr, Par
                                 int gate, uint64_t windows, hipStream_t s) {
     if (gate) return count_reuse_w<W, true>(t, bf, ctr, pb, fresh, level, windows, s);
     return count_reuse_w<W, false>(t, bf, ctr, pb, fresh, level, windows, s);
+}
+
+template <int W>
+hipError_t WOps<W>::bloom_count_fused(BloomView bf, TableView t, TableView fg, PartBufs pb, DevCounters* ctr,
+                                      int fresh_filter, hipStream_t s) {
+    return bloom_count_fused_w<W>(bf, t, fg, pb, ctr, fresh_filter, s);
+}
+template <int W>
+hipError_t WOps<W>::bloom_probe(BloomView bf, TableView fg, PartBufs pb, uint32_t nsample, int fresh_filter,
+                                uint32_t* out, hipStream_t s) {
+    return bloom_probe_w<W>(bf, fg, pb, nsample, fresh_filter, out, s);
 }
 
 template <int W>

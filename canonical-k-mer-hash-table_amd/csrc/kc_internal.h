@@ -78,6 +78,10 @@ struct DevCounters {
     unsigned long long heavy_n;         uint64_t _p14[15];
     unsigned long long spilled;         uint64_t _p15[15];
     unsigned long long heavy;           uint64_t _p16[15];
+    // fused Bloom + counting pass (k_bf3): the gated insertions it made into the speculative
+    // table, added to `inserted` when the counting pass confirms the same input (kc_api.cpp)
+    unsigned long long spec_inserted;   uint64_t _p17[15];
+    unsigned long long spec_overflow;   uint64_t _p18[15];  // keys the fused pass could not place
 };
 
 // The symbol stream: 32 symbols per word, symbol j of word w at bits 62-2j of pk[w]
@@ -198,6 +202,9 @@ hipError_t launch_count(PackedView sv, uint64_t sym_bound, int k, int mode, Tabl
 // overflow gate (PH_TAIL).  The host may run the tail only when the main phase left a skew
 // list or an overflow (kc_api.cpp); with both empty every tail kernel is a no-op.
 constexpr int PH_MAIN = 1, PH_TAIL = 2, PH_ALL = 3;
+// Bloom pass only: the main phase's partition levels without its level 3 (k_b3), and k_b3 alone
+// (the host runs the fused pass, launch_bloom_count_fused, or k_b3 in between)
+constexpr int PH_LEVELS = 4, PH_B3 = 8;
 hipError_t launch_count_partitioned(PackedView sv, uint64_t sym_bound, int k, int mode, TableView t,
                                     BloomView bf, DevCounters* ctr, PartBufs pb, int fresh, hipStream_t s,
                                     int phase = PH_ALL);
@@ -214,6 +221,22 @@ hipError_t launch_bloom_partitioned(PackedView sv, int k, int W, BloomView bf, T
 // filter is ignored); windows: the batch's windows (counted by the Bloom pass)
 hipError_t launch_count_reuse(int W, TableView t, BloomView bf, DevCounters* ctr, PartBufs pb, int fresh, int level,
                               int gate, uint64_t windows, hipStream_t s);
+// Fused Bloom pass 1 + gated counting pass over the kept level-2 fine bins (partition reuse with
+// the table sized before the Bloom pass ends): one workgroup per table region r of t (R a power
+// of two <= fg.R, <= nblocks): the region's filter blocks in LDS take insertion_process for every
+// key of its fine bins, then the same keys behind the gate go into the region's LDS table.
+// pb: the kept partitions (keys2 / hist2 = fills / cap2 / B2 = segments per fine bin / rec12).
+// The table must be fresh (every region is written); inserted counts go to ctr->spec_inserted.
+hipError_t launch_bloom_count_fused(int W, BloomView bf, TableView t, TableView fg, PartBufs pb, DevCounters* ctr,
+                                    int fresh_filter, hipStream_t s);
+// The fused pass's table size from a sample of the kept fine bins: for nsample fine bins spread
+// over fg (fresh filter), the distinct table-key words that pass the gate after the bin's own
+// Bloom pass; out[i] = that count, or ~0u when the bin's keys outgrew the probe's set
+constexpr uint32_t PROBE_BINS = 64;
+hipError_t launch_bloom_probe(int W, BloomView bf, TableView fg, PartBufs pb, uint32_t nsample, int fresh_filter,
+                              uint32_t* out, hipStream_t s);
+// ctr->inserted += ctr->spec_inserted (the counting pass confirmed the fused pass's input)
+hipError_t launch_spec_commit(DevCounters* ctr, uint64_t windows, hipStream_t s);
 // 64-bit checksum of the chunks' bytes (a promise check between two passes over one image):
 // CHECKSUM_SLOTS partial sums in out (their sum is the checksum)
 constexpr int CHECKSUM_SLOTS = 64;
@@ -277,6 +300,10 @@ struct WOps {
                                         DevCounters* ctr, PartBufs pb, int fresh, int keep, hipStream_t s, int phase);
     static hipError_t count_reuse(TableView t, BloomView bf, DevCounters* ctr, PartBufs pb, int fresh, int level,
                                   int gate, uint64_t windows, hipStream_t s);
+    static hipError_t bloom_count_fused(BloomView bf, TableView t, TableView fg, PartBufs pb, DevCounters* ctr,
+                                        int fresh_filter, hipStream_t s);
+    static hipError_t bloom_probe(BloomView bf, TableView fg, PartBufs pb, uint32_t nsample, int fresh_filter,
+                                  uint32_t* out, hipStream_t s);
     static hipError_t route(PackedView sym, int k, DevCounters* ctr, PartBufs pb, uint32_t parts, uint64_t* out,
                             hipStream_t s);
     static hipError_t insert_keys(const uint64_t* keys, uint64_t n, bool partitioned, TableView t, DevCounters* ctr,

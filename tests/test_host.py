@@ -227,3 +227,12 @@ def test_cli_gunzip_bgzf_parallel_and_streams(golden_input, tmp_path):
     badp.write_bytes(bytes(bad))
     r = run_cli(badp, 31, "-s", 1000, "--gunzip-to", out)
     assert r.returncode == 1 and "corrupt" in r.stderr
+    # a forged ISIZE: the first member claims 4 GiB -- rejected as corrupt, not
+    # allocated (BGZF members hold at most 64 KiB)
+    forged = bytearray(bz)
+    first_end = bz.index(b"\x1f\x8b\x08\x04", 1)
+    forged[first_end - 4:first_end] = (0xFFFFFFF0).to_bytes(4, "little")
+    fp = tmp_path / "forged.fasta.gz"
+    fp.write_bytes(bytes(forged))
+    r = run_cli(fp, 31, "-s", 1000, "--gunzip-to", out)
+    assert r.returncode == 1 and "corrupt" in r.stderr, (r.returncode, r.stderr[-500:])
