@@ -103,8 +103,13 @@ def cpu_baseline(args):
         # -b -u: the estimate scaled to the sample (the filter is sized for the reads counted)
         unique = max(1000, args.unique * n // max(1, args.reads)) if args.unique else 0
         targs = table_args(slots, unique)
+        # -a: the workload's output threshold (the reference fixture's: C2 1, C3 2), so both the
+        # reference and the drop-in CLI write their output and time it
+        amin = str(fixture_case(args)["min_abundance"]) if fixture_case(args) else "2"
+        out_txt = os.path.join(td, "ref_out.txt")
+        write_s = None
         if kind == "reference":
-            cmd = [ref, fa, str(args.k), "-m", "2", "-t", str(threads), "-a", "0"] + targs
+            cmd = [ref, fa, str(args.k), "-m", "2", "-t", str(threads), "-a", amin, "-o", out_txt] + targs
             # the reference's worker threads occasionally crash it (seen once in ~10 runs
             # on the box: killed before its timers); one more attempt, a CPU-only rerun,
             # reported as `attempts` with the failed runs' exit codes
@@ -121,8 +126,11 @@ def cpu_baseline(args):
             else:
                 return None
             secs = (int(m.group(1)) + (int(mb.group(1)) if mb else 0)) / 1e6
+            mw = re.search(r"Time used to write k-mers in a file: (\d+) microseconds", p.stdout)
+            write_s = int(mw.group(1)) / 1e6 if mw else None
+            out_bytes = os.path.getsize(out_txt) if os.path.exists(out_txt) else None
             cores = threads - 2  # t-2 hashing workers (+ 1 mostly idle IO thread, main.cpp:383)
-            e2e = cli_e2e(fa, [str(args.k), "-m", "2", "-t", str(threads), "-a", "0"] + targs, windows)
+            e2e = cli_e2e(fa, [str(args.k), "-m", "2", "-t", str(threads), "-a", amin] + targs, windows)
         else:
             t0 = time.perf_counter()
             subprocess.run([orc, "count", fa, str(args.k), "-a", "0"] + targs, check=True, capture_output=True)
@@ -131,14 +139,17 @@ def cpu_baseline(args):
     if kind != "reference":
         failures = []
         e2e = None
+        out_bytes = None
     return {"value": windows / secs, "unit": "k-mers/s", "cores": cores, "kind": kind, "e2e": e2e,
+            "write_s": write_s, "output_bytes": out_bytes,
             "attempts": 1 + len(failures), "failed_exit_codes": failures, "cpu_model": cpu_model(),
             "nproc": os.cpu_count(), "core_share": share,
             "coverage": round(n * args.read_len / genome, 2),
             "workload_coverage": round(args.reads * args.read_len / args.genome, 2),
             "sample": f"{n} reads of the same generator on a {genome}-base genome (the workload's coverage; "
-                      f"{windows} windows, k={args.k}, -m 2 {' '.join(targs)} -t {threads}, {secs:.2f} s counting "
-                      f"time{' incl. the Bloom pass' if args.unique else ''})"}
+                      f"{windows} windows, k={args.k}, -m 2 {' '.join(targs)} -t {threads} -a {amin if kind == 'reference' else 0}, "
+                      f"{secs:.2f} s counting time{' incl. the Bloom pass' if args.unique else ''}; write_s = its "
+                      f"'Time used to write k-mers in a file')"}
 
 
 def cli_e2e(fasta, cli_args, windows):
@@ -158,7 +169,9 @@ def cli_e2e(fasta, cli_args, windows):
         log("drop-in CLI e2e run failed:", p.stdout[-300:], p.stderr[-300:])
         return None
     secs = (int(m.group(1)) + (int(mb.group(1)) if mb else 0)) / 1e6
+    mw = re.search(r"Time used to write k-mers in a file: (\d+) microseconds", p.stdout)
     return {"value": windows / secs, "unit": "k-mers/s", "build_s": round(secs, 4), "process_wall_s": round(wall, 3),
+            "write_s": int(mw.group(1)) / 1e6 if mw else None,
             "path": "drop-in CLI bin/kaarme on the same sample file: page-cached file -> HBM (parallel pread, "
                     "pinned slices) -> passes; the reference's own timer lines",
             "input_path": "device image" if "Input path: device image" in p.stdout else "host chunks"}
@@ -370,6 +383,47 @@ def parity_record(job, k):
             "digest_s": round(time.perf_counter() - t0, 2)}
 
 
+def writer_record(job, verify):
+    """The output writer at full size (kmer_hash_table.cpp:4318-4524): kc_write of
+    the timed job's table (device formatting, double-buffered copy-out, file writes) timed to a
+    file in TMPDIR; with verify, the SHA-256 of the byte-sorted file against the reference's output
+    digest (tests/golden/fullsize.json) -- the bytes the writer produced, not the records."""
+    import hashlib
+    fx = job.fixture
+    with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
+        path = os.path.join(td, "out.txt")
+        t0 = time.perf_counter()
+        job.counter.write(path)
+        secs = time.perf_counter() - t0
+        size = os.path.getsize(path)
+        rec = {"seconds": round(secs, 3), "bytes": size, "gbs": round(size / secs / 1e9, 2),
+               "path": "kc_write: k_text_bytes + k_text on the device, pinned double-buffered copy-out, fwrite "
+                       "to TMPDIR (page cache)"}
+        if fx is not None:
+            # the reference CLI writing the same job's output on the GPU box's 16-core share (its own
+            # "Time used to write k-mers in a file", profiles/r03_ref_fullsize_box.txt)
+            ref_w = {"C2": 59.446, "C3": 31.586}.get(fx["name"])
+            if ref_w:
+                rec["reference_write_s"] = ref_w
+                rec["reference_write_source"] = "profiles/r03_ref_fullsize_box.txt (oracle/_ref/kaarme -t 18)"
+        if verify and fx is not None:
+            t1 = time.perf_counter()
+            env = dict(os.environ, LC_ALL="C")
+            p = subprocess.Popen(["sort", "-S", "12G", "--parallel=16", "-T", td, path], stdout=subprocess.PIPE,
+                                 env=env)
+            h = hashlib.sha256()
+            lines = 0
+            for b in iter(lambda: p.stdout.read(1 << 24), b""):
+                h.update(b)
+                lines += b.count(b"\n")
+            ok = p.wait() == 0
+            rec["parity"] = {"match": ok and h.hexdigest() == fx["sorted_sha256"] and lines == fx["lines"],
+                             "sorted_sha256": h.hexdigest(), "lines": lines,
+                             "reference_case": f"tests/golden/fullsize.json {fx['name']}",
+                             "digest_s": round(time.perf_counter() - t1, 2)}
+    return rec
+
+
 def run_workload(args, env, image=None):
     """Times one workload (warmup + steps of a full counting job) and returns its JSON record
     plus the device image (reusable by a workload with the same generator parameters)."""
@@ -411,6 +465,7 @@ def run_workload(args, env, image=None):
                 "note": "max over ranks; the all-to-all of {key, count} records incl. its count/sum headers"}
     st = counter.finish()  # raises on table overflow
     parity = parity_record(job, k) if args.verify else None
+    writer = writer_record(job, args.verify) if (args.writer and not dist and job.fixture is not None) else None
     compact = None
     if not dist and args.compact:  # the Kaarme slot words built from this table
         torch.cuda.synchronize()
@@ -515,6 +570,8 @@ def run_workload(args, env, image=None):
         out["parity"] = parity
     if compact:
         out["compact"] = compact
+    if writer:
+        out["writer"] = writer
     if xgmi:
         out["xgmi"] = xgmi
     if job.estimate:
@@ -610,6 +667,8 @@ def main():
     ap.add_argument("--secondary-cpu-sample-bases", type=int, default=50_000_000)
     ap.add_argument("--no-verify", dest="verify", action="store_false",
                     help="skip the parity digest against the reference's output (tests/golden/fullsize.json)")
+    ap.add_argument("--no-writer", dest="writer", action="store_false",
+                    help="skip writing the timed job's output with kc_write (timed, and digested with --verify)")
     ap.add_argument("--share", type=int, default=0,
                     help="strong presets on one GPU: time rank 0's share of a G-rank job (its reads, its local "
                          "table sized from the distinct estimate; no exchange)")
@@ -665,7 +724,7 @@ def main():
         out[sec.config.lower()] = {key: rec[key] for key in ("value", "unit", "ms_per_step", "config", "roofline",
                                                             "kernel_ms", "windows_per_step_per_gpu",
                                                             "distinct_per_gpu", "table_slots", "cpu_baseline",
-                                                            "parity", "compact") if key in rec}
+                                                            "parity", "compact", "writer") if key in rec}
     del image
     if rank == 0:
         print(json.dumps(out), file=json_out, flush=True)

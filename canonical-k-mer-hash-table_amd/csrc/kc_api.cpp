@@ -222,12 +222,14 @@ static int alloc_regions(kc_ctx* c);
 
 // pow2_f1 != 0: R = F1 x F2 with F1 = pow2_f1 (the Bloom filter's coarse bins) and F2 a power
 // of two, so the table's coarse bins are the filter's hash-prefix bins (level-1 reuse)
-static int alloc_table(kc_ctx* c, uint64_t min_slots, uint32_t pow2_f1 = 0) {
+// phys_slots != 0: size the device table for that many k-mers instead of min_slots (the
+// reference's capacity stays min_slots: kc_stats, KC_STRICT_CAPACITY)
+static int alloc_table(kc_ctx* c, uint64_t min_slots, uint32_t pow2_f1 = 0, uint64_t phys_slots = 0) {
     c->min_slots = min_slots;
     // Kaarme's table holds exactly next_prime3mod4(min_slots) slots and dies when
     // full; open addressing on the GPU keeps 25 % headroom over that.  The table is
     // R = F1 * F2 regions of BPR 128-byte buckets (a region = one LDS-resident table).
-    uint64_t want = std::max<uint64_t>(min_slots, 64);
+    uint64_t want = std::max<uint64_t>(phys_slots ? phys_slots : min_slots, 64);
     want = want + want / 4;
     const uint64_t buckets = (want + c->S - 1) / c->S;
     const uint64_t regions = std::max<uint64_t>(1, (buckets + BPR - 1) / BPR);
@@ -886,17 +888,34 @@ static int count_reused(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, s
     }
     const BloomView bv{c->d_bloom, c->bf_bits ? c->bf_bits - 1 : 0, c->nh, c->nh_gate, c->bloom_blocked,
                        bloom_blocks(c->bf_bits)};
+    // the counters a redo must restore (windows, inserted, overflow: one 128-byte line each)
+    unsigned long long before[3];
+    HIPCHK(c, hipMemcpyAsync(&before[0], &c->d_ctr->windows, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(&before[1], &c->d_ctr->inserted, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(&before[2], &c->d_ctr->overflow, 8, hipMemcpyDeviceToHost, s));
     // -m 1 -b counts every window (the reference ignores its filter, main.cpp:482-489)
     HIPCHK(c, launch_count_reuse(c->W, table_view(c), bv, c->d_ctr, pr, c->table_fresh, c->reuse_level,
                                  c->cfg.mode != 1, c->reuse_windows, s));
     if (ev[3]) HIPCHK(c, hipEventRecord(ev[3], s));
-    unsigned long long ovf = 0;
+    unsigned long long ovf = 0, full = 0;
     HIPCHK(c, hipMemcpyAsync(&ovf, &c->d_ctr->part_overflow, sizeof(ovf), hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(&full, &c->d_ctr->overflow, sizeof(full), hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
     if (ovf) {  // a full skew list: nothing was inserted, the ordinary pass redoes the batch
         if (std::getenv("KC_REUSE_DEBUG")) std::fprintf(stderr, "reuse: level 2 overflowed\n");
         release();
         return KC_OK;
+    }
+    if (full != before[2]) {
+        // a region of the table sized for the gated k-mers overflowed: the ordinary counting pass
+        // redoes the batch into the reference-sized table (2 * new_in_second), counters restored
+        if (std::getenv("KC_REUSE_DEBUG")) std::fprintf(stderr, "reuse: table region overflowed, redo\n");
+        HIPCHK(c, hipMemcpyAsync(&c->d_ctr->windows, &before[0], 8, hipMemcpyHostToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(&c->d_ctr->inserted, &before[1], 8, hipMemcpyHostToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(&c->d_ctr->overflow, &before[2], 8, hipMemcpyHostToDevice, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        release();
+        return alloc_table(c, c->min_slots);
     }
     c->table_fresh = false;
     c->table_zero_pending = false;  // the fresh level 3 wrote every region
@@ -1267,8 +1286,20 @@ int kc_bloom_finalize(kc_ctx* c, uint64_t* new_in_second) {
         HIPCHK(c, hipStreamSynchronize(c->stream));
         return KC_OK;
     }
+    // The counting pass from the kept partitions can redo itself into the reference-sized
+    // table (count_reused: a region that overflowed), so its table is sized for the k-mers the
+    // gate passes -- new_in_second (~ the k-mers seen twice) plus 30 % for the singletons the
+    // filter lets through -- instead of the reference's 2 * new_in_second (C3: 2^15 instead of
+    // 2^16 regions, 2.1 GB less to write).  KC_BF_TABLE=reference keeps 2 * new_in_second.
+    uint64_t phys = 0;
+    {
+        const char* v = std::getenv("KC_BF_TABLE");
+        if (reuse && !(v && !std::strcmp(v, "reference")))
+            phys = std::min<uint64_t>(slots, h.new_in_second + h.new_in_second * 3 / 10);
+        if (reuse && v && !std::strcmp(v, "tiny")) phys = std::max<uint64_t>(64, h.new_in_second / 8);  // (tests)
+    }
     if (reuse) {
-        uint64_t want = std::max<uint64_t>(slots, 64);
+        uint64_t want = std::max<uint64_t>(phys ? phys : slots, 64);
         want += want / 4;
         const uint64_t regions = std::max<uint64_t>(1, ((want + c->S - 1) / c->S + BPR - 1) / BPR);
         uint64_t rt = c->fgeo.F1;
@@ -1302,7 +1333,7 @@ int kc_bloom_finalize(kc_ctx* c, uint64_t* new_in_second) {
         std::fprintf(stderr, "reuse finalize: kept %d batches %d fallbacks %llu spilled %llu heavy %llu -> level %d\n",
                      (int)c->reuse_kept, c->bloom_batches, (unsigned long long)h.part_fallbacks,
                      (unsigned long long)h.spilled, (unsigned long long)h.heavy, c->reuse_level);
-    rc = alloc_table(c, slots, reuse ? c->fgeo.F1 : 0);
+    rc = alloc_table(c, slots, reuse ? c->fgeo.F1 : 0, reuse ? phys : 0);
     if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return KC_OK;

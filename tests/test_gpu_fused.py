@@ -178,3 +178,26 @@ def test_fused_two_steps_one_context(partitioned):
         st2, b = _bloom_job(kc, img, chunks)
     assert st1["reuse_level"] == st2["reuse_level"] == 3
     assert np.array_equal(a, b)
+
+
+def test_gated_table_overflow_redoes_the_count(partitioned, monkeypatch):
+    """The counting pass from the kept partitions fills a table sized for the gated k-mers
+    (new_in_second + 30 %); when a region overflows (forced: KC_BF_TABLE=tiny, an eighth of
+    new_in_second) the ordinary counting pass redoes the batch into the reference-sized table,
+    with the windows / inserted counters restored."""
+    torch = pytest.importorskip("torch")
+    k = 51
+    img = _image(torch, 300_000, 150, 3_000_000, 14)
+    chunks = ka.plan_chunks(bytes(img.cpu().numpy()), k, ka.FMT_FASTA)
+    want = _exact_solid(img, chunks, k)
+    cfg = ka.Config(k=k, min_abundance=2, bf_enable=True, est_unique=8_000_000, fpr=0.01)
+    monkeypatch.setenv("KC_FUSE", "0")
+    with ka.KmerCounter(cfg) as kc:
+        st_ok, got_ok = _bloom_job(kc, img, chunks)
+    monkeypatch.setenv("KC_BF_TABLE", "tiny")
+    with ka.KmerCounter(cfg) as kc:
+        st, got = _bloom_job(kc, img, chunks)
+    assert st_ok["reused_passes"] == 1 and st["reused_passes"] == 0
+    assert st["windows"] == st_ok["windows"] == 300_000 * (150 - k + 1)
+    assert st["table_slots"] > st_ok["table_slots"]
+    assert np.array_equal(got, want) and np.array_equal(got_ok, want)
