@@ -317,7 +317,8 @@ def setup_job(args, env, image=None):
     batch = min((nbytes + len(chunks) * 4096 + (1 << 20)) // 4096 * 4096, cap // 4096 * 4096)
     windows_expected = N * (L - k + 1)
     estimate = None
-    if strong and (share or (dist and world > 1)):
+    if (strong and (share or (dist and world > 1))) or (dist and args.unique):
+        # (sharded Bloom jobs too: the rank's ungated local count holds all its distinct k-mers)
         # a rank's local table holds its own input's distinct k-mers, which its 1/G share of -s
         # does not bound: sized from a HyperLogLog estimate of them (kc_estimate_distinct_device,
         # once per job before the timed steps), 1.1 x the estimate (x 1.25 buckets: load <= 0.73)
@@ -348,7 +349,7 @@ def setup_job(args, env, image=None):
     if dist:
         from kaarme_amd.sharded import ShardedCounter
         local_slots = 0
-        if strong:
+        if strong or args.unique:
             local_slots = estimate["local_slots"] if estimate else min(args.slots or 0, windows_expected)
         counter = ShardedCounter(cfg, dist, local_slots=local_slots)
     else:

@@ -1612,6 +1612,84 @@ int kc_insert_counts_runs_device(kc_ctx* c, const uint64_t* recs, const uint64_t
     return KC_OK;
 }
 
+int kc_bloom_records_device(kc_ctx* c, const uint64_t* recs, uint64_t n, void* sp) {
+    if (!c || (!recs && n)) return KC_ERR_ARG;
+    if (!c->cfg.bf_enable || c->bloom_final) return c->fail(KC_ERR_STATE, "bloom pass not active");
+    if (!c->bloom_blocked) return c->fail(KC_ERR_ARG, "records need the blocked Bloom layout");
+    hipStream_t s = pick_stream(c, sp);
+    int rc = flush_host(c);
+    if (rc) return rc;
+    if ((rc = settle_spec(c))) return rc;
+    c->bloom_batches++;  // (a Bloom pass of records keeps no partitions)
+    c->reuse_kept = false;
+    if (n == 0) return KC_OK;
+    if (s != c->stream) {
+        HIPCHK(c, hipEventRecord(c->xev, c->stream));
+        HIPCHK(c, hipStreamWaitEvent(s, c->xev, 0));
+    }
+    // exact-layout levels for items of W + 1 words in the filter's region geometry
+    const PartGeo g{c->bgeo.F1, c->bgeo.F2, c->bgeo.R, c->W + 1};
+    if ((rc = ensure_part_geo(c, n, false, g, c->pbf, c->pbf_cap))) return rc;
+    const BloomView bv{c->d_bloom, c->bf_bits ? c->bf_bits - 1 : 0, c->nh, c->nh_gate, c->bloom_blocked,
+                       bloom_blocks(c->bf_bits)};
+    std::array<hipEvent_t, 4> ev{};
+    if (c->profiling) {
+        ev[2] = c->get_event();
+        ev[3] = c->get_event();
+        HIPCHK(c, hipEventRecord(ev[2], s));
+    }
+    HIPCHK(c, launch_bloom_records(c->W, recs, n, bv, c->bgeo, c->d_ctr, c->pbf, c->bloom_fresh, s));
+    c->bloom_fresh = false;
+    if (c->profiling) {
+        HIPCHK(c, hipEventRecord(ev[3], s));
+        c->ev_pending.push_back(ev);
+    }
+    if (s != c->stream) {
+        HIPCHK(c, hipEventRecord(c->xev, s));
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->xev, 0));
+    }
+    return KC_OK;
+}
+
+int kc_count_records_device(kc_ctx* c, const uint64_t* recs, uint64_t n, void* sp) {
+    if (!c || (!recs && n)) return KC_ERR_ARG;
+    {
+        const int r0 = settle_spec(c);
+        if (r0) return r0;
+    }
+    if (!c->nbuckets) return c->fail(KC_ERR_STATE, "no table (kc_bloom_finalize must precede the counting pass)");
+    const bool gate = c->cfg.bf_enable && c->cfg.mode != 1;  // -m 1 -b ignores the filter (main.cpp:482-489)
+    if (gate && !c->bloom_blocked) return c->fail(KC_ERR_ARG, "records need the blocked Bloom layout");
+    hipStream_t s = pick_stream(c, sp);
+    int rc = flush_host(c);
+    if (rc) return rc;
+    if (n == 0) return KC_OK;
+    if (s != c->stream) {
+        HIPCHK(c, hipEventRecord(c->xev, c->stream));
+        HIPCHK(c, hipStreamWaitEvent(s, c->xev, 0));
+    }
+    if ((rc = ensure_part(c, (n * (c->W + 1) + c->W - 1) / c->W, false))) return rc;  // records: W + 1 words
+    const BloomView bv{c->d_bloom, c->bf_bits ? c->bf_bits - 1 : 0, c->nh, c->nh_gate, c->bloom_blocked,
+                       bloom_blocks(c->bf_bits)};
+    std::array<hipEvent_t, 4> ev{};
+    if (c->profiling) {
+        ev[2] = c->get_event();
+        ev[3] = c->get_event();
+        HIPCHK(c, hipEventRecord(ev[2], s));
+    }
+    HIPCHK(c, launch_count_records(c->W, recs, n, table_view(c), bv, c->d_ctr, c->pb, c->table_fresh, gate ? 1 : 0, s));
+    c->table_fresh = c->table_zero_pending = false;
+    if (c->profiling) {
+        HIPCHK(c, hipEventRecord(ev[3], s));
+        c->ev_pending.push_back(ev);
+    }
+    if (s != c->stream) {
+        HIPCHK(c, hipEventRecord(c->xev, s));
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->xev, 0));
+    }
+    return KC_OK;
+}
+
 int kc_insert_keys_device(kc_ctx* c, const uint64_t* keys, uint64_t n, void* sp) {
     if (!c || (!keys && n)) return KC_ERR_ARG;
     {

@@ -68,6 +68,19 @@ hipError_t launch_bloom_probe(int W, BloomView bf, TableView fg, PartBufs pb, ui
     KC_DISPATCH_W(W, bloom_probe(bf, fg, pb, nsample, fresh_filter, out, s));
 }
 
+hipError_t launch_bloom_records(int W, const uint64_t* rec, uint64_t n, BloomView bf, TableView ft, DevCounters* ctr,
+                                PartBufs pb, int fresh, hipStream_t s) {
+    if (!bf.blocked || ft.R == 0 || bf.nblocks % ft.R || bf.nblocks / ft.R > (uint64_t)BF_BLOCKS_PER_REGION)
+        return hipErrorInvalidValue;
+    KC_DISPATCH_W(W, bloom_records(rec, n, bf, ft, ctr, pb, fresh, s));
+}
+
+hipError_t launch_count_records(int W, const uint64_t* rec, uint64_t n, TableView t, BloomView bf, DevCounters* ctr,
+                                PartBufs pb, int fresh, int gate, hipStream_t s) {
+    if (gate && !bf.blocked) return hipErrorInvalidValue;
+    KC_DISPATCH_W(W, count_records(rec, n, t, bf, ctr, pb, fresh, gate, s));
+}
+
 hipError_t launch_route(PackedView sym, int k, int W, DevCounters* ctr, PartBufs pb, uint32_t parts, uint64_t* out,
                         hipStream_t s) {
     KC_DISPATCH_W(W, route(sym, k, ctr, pb, parts, out, s));

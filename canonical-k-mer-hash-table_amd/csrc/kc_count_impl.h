@@ -1307,7 +1307,7 @@ __global__ __launch_bounds__(COUNT_THREADS, 4) void k_p1k(const uint64_t* __rest
     if constexpr (!SCATTER) {
         __syncthreads();
         for (uint32_t b = tid; b < F; b += COUNT_THREADS) pb.hist1[(uint64_t)b * pb.nblk1 + blockIdx.x] = l.hist[b];
-        if (cnt_word < 0) added = blockIdx.x == 0 && tid == 0 ? n : 0;
+        if (cnt_word < 0) added = cnt_word == -1 && blockIdx.x == 0 && tid == 0 ? n : 0;  // (-2: counted later)
         if (dn.dn) added = 0;  // spilled windows: counted by level 1 (or at level 3 behind the gate)
         block_add4(added, n_inv, 0, 0, &ctr->inserted, &ctr->invalid, nullptr, nullptr);
     }
@@ -2040,8 +2040,12 @@ constexpr int B3_THREADS = KC_B3_NT;  // two 64 KiB regions per CU
 template <bool SEG>
 __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView bf, uint32_t bpr, PartBufs pb,
                                                                   DevCounters* __restrict__ ctr,
-                                                                  const unsigned long long* gate, int fresh, int is) {
-    // is: u64 words per item (word 0 is the table key word the filter uses)
+                                                                  const unsigned long long* gate, int fresh, int is,
+                                                                  int cntw) {
+    // is: u64 words per item (word 0 is the table key word the filter uses); cntw >= 0: items
+    // are pre-aggregated {key, count} records (kc_bloom_records_device) with the count in word
+    // cntw, and a record of count >= 2 takes insertion_process twice -- the filter updates of a
+    // k-mer seen twice, as the reference makes them (double_bloomfilter.hpp:371-413)
     constexpr int NT = B3_THREADS, KB = 4;  // (8 or 2 keys per round: slower, r02_v21_ab_b3_kb.txt)
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ uint32_t s_pre[MAX_SEG_GROUP + 1];
@@ -2071,6 +2075,8 @@ __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView b
     const uint64_t blk0 = r * bpr;
     const int lane = threadIdx.x & 63;
     uint64_t* wq = reinterpret_cast<uint64_t*>(smem + (size_t)bpr * BF_BLOCK_WORDS * 4) + (threadIdx.x >> 6) * 64;
+    uint32_t* wf = reinterpret_cast<uint32_t*>(smem + (size_t)bpr * BF_BLOCK_WORDS * 4 + (size_t)(NT / 64) * 64 * 8) +
+                   (threadIdx.x >> 6) * 64;  // (cntw >= 0: the queue entries' counts >= 2)
     BloomLocal bl = {0, 0, 0};
     uint32_t cs = 0, cb = 0, nb = 0;  // SEG: segment cursor (indices grow monotonically)
     if constexpr (SEG) nb = s_pre[1];
@@ -2080,8 +2086,10 @@ __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView b
     struct Raw {
         uint3 v[KB];
         uint32_t xhi[KB];
+        uint32_t two;  // bit q: item q is a record of count >= 2
     };
     auto fetch = [&](uint64_t base, Raw& w) {
+        w.two = 0;
 #pragma unroll
         for (int q = 0; q < KB; q++) {
             const uint64_t i = base + threadIdx.x + (uint64_t)q * NT;
@@ -2105,6 +2113,7 @@ __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView b
                 } else {
                     const uint64_t t = pb.keys2[i * is];
                     w.v[q] = make_uint3((uint32_t)t, (uint32_t)(t >> 32), 0);
+                    if (cntw >= 0) w.two |= (uint32_t)((pb.keys2[i * is + cntw] & CNT_MASK) >= 2) << q;
                 }
             }
         }
@@ -2137,12 +2146,16 @@ __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView b
         for (uint32_t r0 = 0; r0 < total; r0 += 64) {
 #pragma unroll
             for (int q = 0; q < KB; q++)
-                if (slow[q] && pre[q] + rank[q] - r0 < 64) wq[pre[q] + rank[q] - r0] = t0[q];
+                if (slow[q] && pre[q] + rank[q] - r0 < 64) {
+                    wq[pre[q] + rank[q] - r0] = t0[q];
+                    if (cntw >= 0) wf[pre[q] + rank[q] - r0] = (cur.two >> q) & 1;
+                }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's queue writes land
             if (lane < total - r0) {
                 const uint64_t t = wq[lane];
                 const uint32_t lb = (uint32_t)(bloom_block(t, bf.nblocks) - blk0);
                 block_insert(lf + lb * BF_BLOCK_WORDS, t, bf.nh, bl);
+                if (cntw >= 0 && wf[lane]) block_insert(lf + lb * BF_BLOCK_WORDS, t, bf.nh, bl);  // its second sighting
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // queue reads done before reuse
         }
@@ -2886,13 +2899,15 @@ static hipError_t part_levels23(TableView t, DevCounters* ctr, PartBufs pb, hipS
 
 template <bool SEG>
 static hipError_t launch_b3(BloomView bf, TableView ft, DevCounters* ctr, PartBufs pb, const unsigned long long* gate,
-                            int fresh, hipStream_t s, int is = 1) {
+                            int fresh, hipStream_t s, int is = 1, int cntw = -1) {
     const uint32_t bpr = (uint32_t)(bf.nblocks / ft.R);
-    const size_t sm = (size_t)bpr * BF_BLOCK_WORDS * 4 + (size_t)(B3_THREADS / 64) * 64 * 8;  // + wave queues
+    // + wave queues (+ their count flags for records)
+    const size_t sm = (size_t)bpr * BF_BLOCK_WORDS * 4 + (size_t)(B3_THREADS / 64) * 64 * (cntw >= 0 ? 12 : 8);
     if (SEG && pb.B2 > MAX_SEG_GROUP) return hipErrorInvalidValue;
     hipError_t e = set_smem(k_b3<SEG>, sm);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_b3<SEG>, dim3((unsigned)ft.R), dim3(B3_THREADS), sm, s, bf, bpr, pb, ctr, gate, fresh, is);
+    hipLaunchKernelGGL(k_b3<SEG>, dim3((unsigned)ft.R), dim3(B3_THREADS), sm, s, bf, bpr, pb, ctr, gate, fresh, is,
+                       cntw);
     return hipGetLastError();
 }
 
@@ -3210,6 +3225,51 @@ static hipError_t insert_items_part(const uint64_t* items, uint64_t n, TableView
 }
 
 
+// Bloom pass 1 over pre-aggregated {key, count} records (kc_bloom_records_device, the owner
+// side of the sharded Bloom filter): the exact levels move whole records into the filter's
+// regions (ft), k_b3 inserts each record once, twice when its count is >= 2
+template <int W>
+static hipError_t bloom_records_w(const uint64_t* rec, uint64_t n, BloomView bf, TableView ft, DevCounters* ctr,
+                                  PartBufs pb, int fresh, hipStream_t s) {
+    constexpr int IW = W + 1;
+    if (n == 0) return hipSuccess;
+    const BinRegion bin = coarse_bins(ft);
+    const size_t sm1 = part_smem<IW>(ft.F1), sm1h = hist_smem(ft.F1);
+    hipError_t e;
+    if ((e = set_smem(k_p1k<IW, false>, sm1h)) != hipSuccess) return e;
+    if ((e = set_smem(k_p1k<IW, true>, sm1)) != hipSuccess) return e;
+    hipLaunchKernelGGL((k_p1k<IW, false>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1h, s, rec, n, pb, ft.F1, bin, ctr, -2,
+                       DevN{}, IW);
+    launch_scan(pb.hist1, (uint64_t)ft.F1 * pb.nblk1, pb.off1, pb.bsum, s);
+    hipLaunchKernelGGL((k_p1k<IW, true>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1, s, rec, n, pb, ft.F1, bin, ctr, -2,
+                       DevN{}, IW);
+    if ((e = part_level2_exact<IW>(ft, pb, s, nullptr)) != hipSuccess) return e;
+    return launch_b3<false>(bf, ft, ctr, pb, nullptr, fresh, s, IW, W);
+}
+
+// the counting pass over {key, count} records behind the gate (kc_count_records_device): the
+// exact levels into the table's regions, k_p3<CNT, GATE> adds the counts of the records whose
+// filter-2 bits are set (inserted += those counts); gate = 0: every record
+template <int W>
+static hipError_t count_records_w(const uint64_t* rec, uint64_t n, TableView t, BloomView bf, DevCounters* ctr,
+                                  PartBufs pb, int fresh, int gate, hipStream_t s) {
+    constexpr int IW = W + 1;
+    if (n == 0) return hipSuccess;
+    const BinRegion bin = coarse_bins(t);
+    const size_t sm1 = part_smem<IW>(t.F1), sm1h = hist_smem(t.F1);
+    hipError_t e;
+    if ((e = set_smem(k_p1k<IW, false>, sm1h)) != hipSuccess) return e;
+    if ((e = set_smem(k_p1k<IW, true>, sm1)) != hipSuccess) return e;
+    const int cw = gate ? -2 : W;  // gated: level 3 counts what passes
+    hipLaunchKernelGGL((k_p1k<IW, false>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1h, s, rec, n, pb, t.F1, bin, ctr, cw,
+                       DevN{}, IW);
+    launch_scan(pb.hist1, (uint64_t)t.F1 * pb.nblk1, pb.off1, pb.bsum, s);
+    hipLaunchKernelGGL((k_p1k<IW, true>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1, s, rec, n, pb, t.F1, bin, ctr, cw,
+                       DevN{}, IW);
+    if (gate) return part_levels23<W, true, true>(t, ctr, pb, s, nullptr, fresh, bf);
+    return part_levels23<W, true>(t, ctr, pb, s, nullptr, fresh);
+}
+
 template <int W>
 static hipError_t insert_keys_w(const uint64_t* keys, uint64_t n, bool partitioned, TableView t, DevCounters* ctr,
                                 PartBufs pb, int fresh, hipStream_t s) {
@@ -3281,6 +3341,17 @@ template <int W>
 hipError_t WOps<W>::bloom_probe(BloomView bf, TableView fg, PartBufs pb, uint32_t nsample, int fresh_filter,
                                 uint32_t* out, hipStream_t s) {
     return bloom_probe_w<W>(bf, fg, pb, nsample, fresh_filter, out, s);
+}
+
+template <int W>
+hipError_t WOps<W>::bloom_records(const uint64_t* rec, uint64_t n, BloomView bf, TableView ft, DevCounters* ctr,
+                                  PartBufs pb, int fresh, hipStream_t s) {
+    return bloom_records_w<W>(rec, n, bf, ft, ctr, pb, fresh, s);
+}
+template <int W>
+hipError_t WOps<W>::count_records(const uint64_t* rec, uint64_t n, TableView t, BloomView bf, DevCounters* ctr,
+                                  PartBufs pb, int fresh, int gate, hipStream_t s) {
+    return count_records_w<W>(rec, n, t, bf, ctr, pb, fresh, gate, s);
 }
 
 template <int W>

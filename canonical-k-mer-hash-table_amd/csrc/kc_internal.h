@@ -235,6 +235,14 @@ hipError_t launch_bloom_count_fused(int W, BloomView bf, TableView t, TableView 
 constexpr uint32_t PROBE_BINS = 64;
 hipError_t launch_bloom_probe(int W, BloomView bf, TableView fg, PartBufs pb, uint32_t nsample, int fresh_filter,
                               uint32_t* out, hipStream_t s);
+// The two passes over pre-aggregated {W key words, count} records (the owner side of the sharded
+// Bloom filter, kaarme_amd/sharded.py): Bloom pass 1 (a record of count >= 2 inserted twice) into
+// the filter's regions ft, and the gated (gate = 1) or plain counting pass into the table t.
+// pb: exact-layout buffers for items of W + 1 words (kc_api.cpp ensure_part_geo)
+hipError_t launch_bloom_records(int W, const uint64_t* rec, uint64_t n, BloomView bf, TableView ft, DevCounters* ctr,
+                                PartBufs pb, int fresh, hipStream_t s);
+hipError_t launch_count_records(int W, const uint64_t* rec, uint64_t n, TableView t, BloomView bf, DevCounters* ctr,
+                                PartBufs pb, int fresh, int gate, hipStream_t s);
 // ctr->inserted += ctr->spec_inserted (the counting pass confirmed the fused pass's input)
 hipError_t launch_spec_commit(DevCounters* ctr, uint64_t windows, hipStream_t s);
 // 64-bit checksum of the chunks' bytes (a promise check between two passes over one image):
@@ -304,6 +312,10 @@ struct WOps {
                                         int fresh_filter, hipStream_t s);
     static hipError_t bloom_probe(BloomView bf, TableView fg, PartBufs pb, uint32_t nsample, int fresh_filter,
                                   uint32_t* out, hipStream_t s);
+    static hipError_t bloom_records(const uint64_t* rec, uint64_t n, BloomView bf, TableView ft, DevCounters* ctr,
+                                    PartBufs pb, int fresh, hipStream_t s);
+    static hipError_t count_records(const uint64_t* rec, uint64_t n, TableView t, BloomView bf, DevCounters* ctr,
+                                    PartBufs pb, int fresh, int gate, hipStream_t s);
     static hipError_t route(PackedView sym, int k, DevCounters* ctr, PartBufs pb, uint32_t parts, uint64_t* out,
                             hipStream_t s);
     static hipError_t insert_keys(const uint64_t* keys, uint64_t n, bool partitioned, TableView t, DevCounters* ctr,

@@ -49,7 +49,7 @@ EXPORTS = (
     "kc_xxh64", "kc_bloom_info", "kc_bloom_read", "kc_bloom_write", "kc_synth_skew_device",
     "kc_table_size_reference", "kc_bloom_get_device", "kc_bloom_merge_device", "kc_bloom_set_device",
     "kc_bloom_estimate", "kc_compact", "kc_compact_dump", "kc_compact_lookup", "kc_compact_read",
-    "kc_estimate_distinct_device",
+    "kc_estimate_distinct_device", "kc_bloom_records_device", "kc_count_records_device",
 )
 
 
@@ -147,6 +147,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "kc_insert_keys_device": (I32, [P, P, U64, P]),
         "kc_route_table_device": (I32, [P, ctypes.c_uint32, P, U64, P, P]),
         "kc_insert_counts_device": (I32, [P, P, U64, P]),
+        "kc_bloom_records_device": (I32, [P, P, U64, P]),
+        "kc_count_records_device": (I32, [P, P, U64, P]),
         "kc_profile": (I32, [P, I32]),
         "kc_get_timing": (I32, [P, ctypes.POINTER(kc_timing)]),
         "kc_synth_device": (I32, [P, U64, U64, U64, U64, ctypes.c_uint32, ctypes.c_uint32,
@@ -352,6 +354,16 @@ class KmerCounter:
         self._chk(self.lib.kc_route_table_device(self._ctx, nshards, ctypes.c_void_p(out_ptr or None), out_capacity,
                                                  counts, ctypes.c_void_p(stream or None)), "kc_route_table_device")
         return [int(x) for x in counts]
+
+    def bloom_records_device(self, rec_ptr: int, n_records: int, stream: int = 0):
+        """Bloom pass 1 over {key, count} records (include/kc_api.h kc_bloom_records_device)."""
+        self._chk(self.lib.kc_bloom_records_device(self._ctx, ctypes.c_void_p(rec_ptr), n_records,
+                                                   ctypes.c_void_p(stream or None)), "kc_bloom_records_device")
+
+    def count_records_device(self, rec_ptr: int, n_records: int, stream: int = 0):
+        """The counting pass over {key, count} records behind the gate (kc_count_records_device)."""
+        self._chk(self.lib.kc_count_records_device(self._ctx, ctypes.c_void_p(rec_ptr), n_records,
+                                                   ctypes.c_void_p(stream or None)), "kc_count_records_device")
 
     def insert_counts_device(self, rec_ptr: int, n_records: int, stream: int = 0):
         self._chk(self.lib.kc_insert_counts_device(self._ctx, ctypes.c_void_p(rec_ptr), n_records,

@@ -20,17 +20,20 @@ The per-window alternative (kc_route_device + kc_insert_keys_device: route every
 window's key to its owner, no local table) stays in the C ABI and is exercised by
 tests/test_gpu_sharded.py.
 
-Bloom prefilter (-b, main.cpp:395-461 / parallel_parser.hpp:2680-2974), sharded:
-  1. every rank runs the Bloom pass over its own input into its own filter;
-  2. `bloom_finalize` combines the filters: the filter's words are cut into one slice per
-     rank, an all-to-all hands every rank the ranks' copies of its slice, the rank merges
-     them (kc_bloom_merge_device: filter 1 = OR, filter 2 = OR | filter-1 bits set in two
-     copies, so a k-mer seen twice anywhere passes the gate) and an all-gather gives every
-     rank the combined filter; kc_bloom_set_device installs it and sets new_in_second to
-     its filter-2 estimate, the same on every rank, which sizes the tables (2 x, main.cpp:454:
-     the local table whole, the owner table its 1/world share);
-  3. the counting pass is gated by the combined filter on every rank, then merged as above.
-For every k-mer with count >= 2 the owners hold the single-GPU (and reference) count.
+Bloom prefilter (-b, main.cpp:395-461 / parallel_parser.hpp:2680-2974), sharded by the same
+owner as the table: each rank holds the filter of the k-mers it owns, sized for
+its 1/world share of -u, so one filter's worth of bits is spread over the ranks.
+  1. `bloom_device`: every rank counts its own input, ungated, into its local table;
+  2. `bloom_finalize` (collective): the local tables' {key, count} records go to their owners
+     in one all-to-all; each owner runs Bloom pass 1 over what it received
+     (kc_bloom_records_device: insertion_process once per record, twice for a record of
+     count >= 2), sizes its table from its new_in_second (2 x, main.cpp:454), and counts the
+     same records behind its gate (kc_count_records_device).  A k-mer seen twice in the whole
+     input -- twice on one rank, or once on each of two -- sets its filter-2 bits at its owner,
+     and a k-mer seen once meets one filter holding exactly the insertions one GPU's filter
+     would hold for it, so the owners gate as the reference's single filter does;
+  3. `count_device` over the same input then only confirms it (the owners counted it).
+new_in_second is the sum of the owners' counters (all-reduce).
 
 The exchange logic (:func:`exchange`) is backend-agnostic torch code: the CPU tests run
 it over ``gloo`` with a NumPy engine, the GPU path over RCCL with the HIP engine.
@@ -132,38 +135,6 @@ def exchange(dist, keys, counts: Sequence[int], W: int, group=None, chunk_words:
     return (out, total, recv) if with_counts else (out, total)
 
 
-def all_gather_words(dist, mine, world: int, group=None, chunk_words: int = 0):
-    """[world x len(mine)] = every rank's `mine` (int32 words), in pieces of at most
-    chunk_words per rank (default: the all-to-all's round size in bytes)."""
-    import torch
-
-    chunk_words = chunk_words or 2 * chunk_words_default()
-    if world > 1 and _host_staged(dist, group, mine):
-        return all_gather_words(dist, mine.cpu(), world, group, chunk_words).to(mine.device)
-    per = mine.numel()
-    full = torch.empty(world * per, dtype=mine.dtype, device=mine.device)
-    if world == 1:
-        full.copy_(mine)
-        return full
-    grid = full.view(world, per)
-    for lo in range(0, per, chunk_words):
-        hi = min(per, lo + chunk_words)
-        piece = mine[lo:hi].contiguous()
-        if hi - lo == per:
-            tmp = full
-        else:
-            tmp = torch.empty(world * (hi - lo), dtype=mine.dtype, device=mine.device)
-        # the API is chosen up front (gloo has no all_gather_into_tensor): a communication
-        # error propagates instead of sending this rank into a different collective
-        if _gather_into_tensor(dist, group):
-            dist.all_gather_into_tensor(tmp, piece, group=group)
-        else:
-            dist.all_gather(list(tmp.view(world, hi - lo).unbind(0)), piece, group=group)
-        if tmp is not full:
-            grid[:, lo:hi].copy_(tmp.view(world, hi - lo))
-    return full
-
-
 def _gather_into_tensor(dist, group) -> bool:
     return hasattr(dist, "all_gather_into_tensor") and dist.get_backend(group) != "gloo"
 
@@ -222,14 +193,21 @@ class DeviceEngine:
     """The HIP engine of one rank: a local table counting the rank's input and an owner
     table holding the merged counts of the k-mers this rank owns."""
 
-    def __init__(self, cfg: Config, local_slots: int = 0):
+    def __init__(self, cfg: Config, local_slots: int = 0, world: int = 1):
         import dataclasses
 
         self.cfg = cfg  # the owner table: this rank's share of -s
+        self.world = world
         # the local table must hold every distinct k-mer of this rank's input, which the
         # owner share does not bound (a rank sees ~all k-mers of the genome at low
-        # per-rank coverage): local_slots, e.g. min(-s total, this rank's windows)
-        local = dataclasses.replace(cfg, table_slots=max(cfg.table_slots, local_slots))
+        # per-rank coverage): local_slots, e.g. min(-s total, this rank's windows).  With the
+        # Bloom filter the local count is ungated (the owners gate): it holds every distinct
+        # k-mer of the rank's input, -u unless local_slots is given
+        if cfg.bf_enable:
+            local = dataclasses.replace(cfg, bf_enable=False,
+                                        table_slots=max(local_slots, cfg.est_unique, cfg.table_slots))
+        else:
+            local = dataclasses.replace(cfg, table_slots=max(cfg.table_slots, local_slots))
         self.kc = KmerCounter(local)    # local table (also used by the per-window route path)
         # every rank's local table has the owner table's geometry: the records a rank
         # receives are region-sorted groups, merged in one pass (kc_insert_counts_runs_device)
@@ -280,7 +258,12 @@ class DeviceEngine:
 
     def owner_table(self) -> KmerCounter:
         if self.owner is None:
-            self.owner = KmerCounter(self.cfg)
+            import dataclasses
+
+            cfg = self.cfg
+            if cfg.bf_enable:  # the owner's filter: its 1/world share of -u
+                cfg = dataclasses.replace(cfg, est_unique=max(1, -(-cfg.est_unique // self.world)))
+            self.owner = KmerCounter(cfg)
         return self.owner
 
     def insert_counts(self, recs, n: int, stream: int = 0, group_counts=None):
@@ -289,47 +272,19 @@ class DeviceEngine:
         else:
             self.owner_table().insert_counts_device(recs.data_ptr(), n, stream)
 
-    # -- sharded Bloom filter
+    # -- owner-sharded Bloom filter: the rank's ungated local count, then the owner's two
+    # passes over the {key, count} records it receives
     def bloom(self, dev_ptr: int, chunks, fmt: int, stream: int = 0):
-        self.kc.bloom_device(dev_ptr, chunks, fmt, stream)
+        self.kc.count_device(dev_ptr, chunks, fmt, stream)
 
-    def bloom_words(self):
-        """(filter words, merge unit in words): whole 16-word blocks, or int64 pairs."""
-        info = self.kc.bloom_info()
-        return info["words"], 16 if info["layout"] == "blocked" else 2
+    def bloom_records(self, recs, n: int, stream: int = 0):
+        self.owner_table().bloom_records_device(recs.data_ptr(), n, stream)
 
-    def bloom_copy(self, n_pad: int, stream: int = 0):
-        import torch
+    def owner_bloom_finalize(self) -> int:
+        return self.owner_table().bloom_finalize()
 
-        n = self.kc.bloom_info()["words"]
-        out = torch.zeros(n_pad, dtype=torch.int32, device="cuda")
-        self.kc.bloom_get_device(out.data_ptr(), 0, n, stream)
-        return out
-
-    def bloom_merge(self, parts, nparts: int, n: int, stream: int = 0):
-        import torch
-
-        out = torch.empty(n, dtype=torch.int32, device="cuda")
-        self.kc.bloom_merge_device(parts.data_ptr(), nparts, n, out.data_ptr(), stream)
-        return out
-
-    def bloom_install(self, full, n: int, stream: int = 0) -> int:
-        return self.kc.bloom_set_device(full.data_ptr(), n, stream)
-
-    def bloom_finalize(self, owner_slots: int) -> int:
-        """Size the local table (2 x new_in_second) and the owner table (owner_slots)."""
-        import dataclasses
-
-        nis = self.kc.bloom_finalize()
-        ocfg = dataclasses.replace(self.cfg, bf_enable=False, table_slots=owner_slots)
-        if self.owner is not None and self.owner.cfg == ocfg:
-            self.owner.reset()
-        else:
-            if self.owner is not None:
-                self.owner.close()
-            self.owner = KmerCounter(ocfg)
-        self.same_geometry = False
-        return nis
+    def count_records(self, recs, n: int, stream: int = 0):
+        self.owner_table().count_records_device(recs.data_ptr(), n, stream)
 
     def reset(self):
         self.kc.reset()
@@ -357,18 +312,27 @@ class ShardedCounter:
         self.rank = dist.get_rank(group)
         self.W = words_for_k(cfg.k)
         if engine is None:
-            engine = DeviceEngine(cfg, local_slots)
+            engine = DeviceEngine(cfg, local_slots, self.world)
         self.engine = engine
         self.device = getattr(self.engine, "device", "cpu")
         self._pending = False
         self._stream = 0
         self._inflight = []
-        self._warned = False
+        self._bloom_input = None  # the Bloom pass's (image, chunks, format): the owners count it
+        self._counted = False
         # exchange traffic of the merges (xGMI bytes reported beside HBM bytes)
         self.xstats = {"bytes_sent": 0, "bytes_recv": 0, "exchange_s": 0.0, "merges": 0}
 
     # the counting pass over a device image (chunks from kaarme_amd.plan_chunks): local
     def count_device(self, dev_ptr: int, chunks: List[Tuple[int, int, int]], fmt: int, stream: int = 0):
+        if self.cfg.bf_enable:
+            # the owners counted the Bloom pass's input behind their gates (bloom_finalize): the
+            # counting pass must present that input again (the reference reads the file twice)
+            if not self._counted or self._bloom_input != (dev_ptr, tuple(map(tuple, chunks)), fmt):
+                raise ValueError("a sharded Bloom job counts the input of its Bloom pass (bloom_device, "
+                                 "bloom_finalize, count_device over the same image and chunks)")
+            self._counted = False
+            return
         self.engine.count(dev_ptr, chunks, fmt, stream)
         self._pending = True
         self._stream = stream
@@ -394,47 +358,43 @@ class ShardedCounter:
         self._inflight = [recv]  # the receive buffer must outlive the insert
         self._pending = False
 
-    # the Bloom pass over a device image: into this rank's own filter
+    # the Bloom pass over a device image: this rank's ungated local count
     def bloom_device(self, dev_ptr: int, chunks: List[Tuple[int, int, int]], fmt: int, stream: int = 0):
         if not self.cfg.bf_enable:
             raise ValueError("bloom_device needs Config(bf_enable=True)")
         self.engine.bloom(dev_ptr, chunks, fmt, stream)
+        self._bloom_input = (dev_ptr, tuple(map(tuple, chunks)), fmt)
         self._stream = stream
 
     def bloom_finalize(self, stream: int = None) -> int:
-        """End of the Bloom pass (collective): combine the ranks' filters, install the
-        combined filter on every rank and size the tables.  Returns new_in_second (the
-        combined filter's estimate, the same on every rank)."""
+        """End of the Bloom pass (collective): the local tables' records to their owners, the
+        owners' Bloom pass over them, their tables sized (2 x their new_in_second) and the same
+        records counted behind their gates.  Returns new_in_second summed over the owners."""
+        import time
+
         import torch
 
         stream = self._stream if stream is None else stream
-        if self.world > 2 and not self._warned:
-            # the per-bit merge below passes a k-mer seen once on one rank when each of its
-            # filter-1 bits is also set on another rank by other k-mers (probability about
-            # (1 - (1 - rho)^(world - 1))^h at filter-1 fill rho): counts of k-mers seen at
-            # least twice stay exact, but more singletons reach the tables as world grows
-            # (DESIGN.md section 4)
-            import warnings
-
-            warnings.warn(f"sharded Bloom filter over {self.world} ranks: singleton k-mers pass the combined "
-                          "gate more often than on one GPU (tables grow; counts >= 2 stay exact)")
-            self._warned = True
         with _on_stream(self.device, stream):
-            n, unit = self.engine.bloom_words()
-            world = self.world
-            per = -(-max(n, 1) // (unit * world)) * unit  # words of one rank's slice
-            send = self.engine.bloom_copy(per * world, stream)
-            if world > 1:  # rank d receives every rank's copy of slice d, in rank order
-                recv, got = exchange(self.dist, send.view(torch.int64), [per // 2] * world, 1, self.group)
-                parts = recv[:got].view(torch.int32)
-            else:
-                parts = send
-            mine = self.engine.bloom_merge(parts, world, per, stream)
-            full = all_gather_words(self.dist, mine, world, self.group)
-            nis = self.engine.bloom_install(full, n, stream)
-            self.engine.bloom_finalize(owner_share(2 * nis, world))
-        self._inflight = [send, parts, mine, full]
-        return nis
+            recs, counts = self.engine.route_table(self.world, stream)
+            self.engine.clear_local()
+            t0 = time.perf_counter()
+            recv, n, per_rank = exchange(self.dist, recs, counts, self.W + 1, self.group, with_counts=True)
+            rec_bytes = (self.W + 1) * 8
+            self.xstats["bytes_sent"] += sum(c for d, c in enumerate(counts) if d != self.rank) * rec_bytes
+            self.xstats["bytes_recv"] += sum(c for d, c in enumerate(per_rank) if d != self.rank) * rec_bytes
+            self.xstats["exchange_s"] += time.perf_counter() - t0
+            self.xstats["merges"] += 1
+            self.engine.bloom_records(recv, n, stream)
+            nis = self.engine.owner_bloom_finalize()
+            self.engine.count_records(recv, n, stream)
+            tot = torch.tensor([int(nis)], dtype=torch.int64, device=self.device if self.device == "cuda" else "cpu")
+            if self.world > 1:
+                self.dist.all_reduce(tot, group=self.group)
+        self._inflight = [recv]  # the receive buffer must outlive the owner's passes
+        self._counted = True
+        self._pending = False
+        return int(tot.item())
 
     @property
     def kc(self) -> KmerCounter:
@@ -445,6 +405,8 @@ class ShardedCounter:
         self.engine.reset()
         self._pending = False
         self._inflight = []
+        self._bloom_input = None
+        self._counted = False
 
     def sync(self):
         """Completes the job: the (collective) merge if counts are pending, then waits."""
@@ -470,9 +432,13 @@ class ShardedCounter:
         self.sync()
         local, own = self.engine.kc.finish(), self.kc.finish()
         st = dict(own)
-        for key in ("windows", "chunks", "bytes", "bf_windows", "bf_bits", "new_in_first", "new_in_second",
-                    "failed_in_first", "reused_passes"):
+        keys = ("windows", "chunks", "bytes", "reused_passes")
+        if not self.cfg.bf_enable:  # (with the filter, the owner's Bloom counters are its own)
+            keys += ("bf_windows", "bf_bits", "new_in_first", "new_in_second", "failed_in_first")
+        for key in keys:
             st[key] = local[key]
+        if self.cfg.bf_enable:
+            st["bf_windows"] = local["windows"]  # the ungated local count saw every window
         st["local_distinct"] = local["distinct"]
         return st
 

@@ -205,6 +205,26 @@ int kc_bloom_set_device(kc_ctx* ctx, const uint32_t* dev_src, uint64_t n_words, 
                         void* hip_stream);
 int kc_bloom_estimate(kc_ctx* ctx, uint64_t* distinct_in_second, void* hip_stream);
 
+/* Owner-sharded Bloom filter ("the BF is sharded by the same owner"): the two
+ * passes of a Bloom job over pre-aggregated records {W table-key words, raw count} -- what
+ * kc_route_table_device writes from an ungated local count and the exchange delivers to the
+ * k-mers' owner -- on the owner's context (its filter sized for its 1/G share of -u):
+ *   kc_bloom_records_device   Bloom pass 1 (before kc_bloom_finalize): insertion_process
+ *                             (double_bloomfilter.hpp:371-413) once per record, twice for a
+ *                             record of count >= 2 -- the filter updates of a k-mer seen at
+ *                             least twice -- so that, whatever the records' split over the
+ *                             senders, a k-mer seen twice in the whole input sets its filter-2
+ *                             bits and a k-mer seen once is gated exactly as by one filter
+ *                             (parallel_parser.hpp:2788-2940 over the whole input);
+ *   kc_count_records_device   the counting pass (after kc_bloom_finalize, which sizes the table
+ *                             2 * new_in_second, main.cpp:454): adds each record's count when
+ *                             its filter-2 bits pass the gate (parallel_parser.hpp:2436-2453);
+ *                             -m 1 -b and contexts without the filter add every record.
+ * Blocked filter layout only (the reference layout hashes the Rabin-Karp root, which a table
+ * key does not carry): KC_ERR_ARG otherwise. */
+int kc_bloom_records_device(kc_ctx* ctx, const uint64_t* dev_records, uint64_t n_records, void* hip_stream);
+int kc_count_records_device(kc_ctx* ctx, const uint64_t* dev_records, uint64_t n_records, void* hip_stream);
+
 /* Kaarme's compact representation: PointerHashTableCanonicalAV's 8-byte
  * slot words (OneCharacterAndPointerKMerAtomicVariable, kmer.hpp:103-149: occupied, predecessor
  * exists, self / predecessor canonical during insertion, left and right character, 14-bit count,

@@ -89,24 +89,10 @@ def bloom_positions(words, nblocks, nh):
     return [(blk * 16 + (j & 7), (h >> (5 * j)) & 31) for j in range(nh)]
 
 
-def merge_words(parts, nparts, n):
-    """kc_bloom_merge_device's rule on the blocked layout (the checker's restatement)."""
-    p = parts[: nparts * n].reshape(nparts, n // 16, 16)
-    once = np.zeros((n // 16, 8), dtype=np.uint32)
-    twice = np.zeros_like(once)
-    f2 = np.zeros_like(once)
-    for i in range(nparts):
-        x = p[i, :, :8]
-        twice |= once & x
-        once |= x
-        f2 |= p[i, :, 8:]
-    return np.concatenate([once, f2 | twice], axis=1).reshape(-1)
-
-
 class NumpyEngine:
     """Stand-in for sharded.DeviceEngine: same count / route_table / insert_counts contract
-    on CPU tensors (records: W key words + 1 count word), and the Bloom pass contract
-    (bloom / bloom_words / bloom_copy / bloom_merge / bloom_install / bloom_finalize)."""
+    on CPU tensors (records: W key words + 1 count word), and the owner-sharded Bloom contract
+    (bloom = the ungated local count / bloom_records / owner_bloom_finalize / count_records)."""
 
     NBLOCKS, NH, NH_GATE = 40, 7, 6
 
@@ -117,51 +103,49 @@ class NumpyEngine:
         self.kc = _Table()      # local
         self.owner = _Table()
         self.bf = bf
-        self.filter = np.zeros(16 * self.NBLOCKS, dtype=np.uint32)
+        self.filter = np.zeros(16 * self.NBLOCKS, dtype=np.uint32)  # the owner's filter
         self.new_in_second = 0
 
     def _has(self, pos, half):
         return all((int(self.filter[w + half]) >> b) & 1 for w, b in pos)
 
-    def bloom(self, dev_ptr, chunks, fmt, stream=0):
+    def _insert(self, words):
+        """insertion_process (double_bloomfilter.hpp:371-413) on the blocked-layout model."""
+        pos = bloom_positions(words, self.NBLOCKS, self.NH)
+        if self._has(pos, 8):
+            return
+        second = self._has(pos, 0)  # filter 1 complete: the second sighting goes to filter 2
+        for w, b in pos:
+            self.filter[w + (8 if second else 0)] |= np.uint32(1 << b)
+        self.new_in_second += second
+
+    def _rows(self, recs, n):
+        return recs[: n * (self.W + 1)].numpy().view(np.uint64).reshape(n, self.W + 1)
+
+    def bloom(self, dev_ptr, chunks, fmt, stream=0):  # the rank's ungated local count
         for off, ln, _ in chunks:
             for line in self.lines[off:off + ln]:
-                for km in canonical_windows(line, self.k):
-                    pos = bloom_positions(to_words(km, self.W), self.NBLOCKS, self.NH)
-                    half = 8 if self._has(pos, 0) else 0  # insertion_process: second sighting -> filter 2
-                    for w, b in pos:
-                        self.filter[w + half] |= np.uint32(1 << b)
+                self.kc.table.update(canonical_windows(line, self.k))
 
-    def bloom_words(self):
-        return self.filter.size, 16
+    def bloom_records(self, recs, n, stream=0):
+        for row in self._rows(recs, n):
+            ws = [int(x) for x in row[:self.W]]
+            for _ in range(min(2, int(row[self.W]))):  # a record of count >= 2: inserted twice
+                self._insert(ws)
 
-    def bloom_copy(self, n_pad, stream=0):
-        out = np.zeros(n_pad, dtype=np.uint32)
-        out[: self.filter.size] = self.filter
-        return torch.from_numpy(out.view(np.int32))
-
-    def bloom_merge(self, parts, nparts, n, stream=0):
-        return torch.from_numpy(merge_words(parts.numpy().view(np.uint32), nparts, n).view(np.int32))
-
-    def bloom_install(self, full, n, stream=0):
-        self.filter = full[:n].numpy().view(np.uint32).copy()
-        x = sum(bin(int(v)).count("1") for i, v in enumerate(self.filter) if i % 16 >= 8)
-        m = 256 * self.NBLOCKS
-        self.new_in_second = round(-(m / self.NH) * np.log1p(-min(x, m - 1) / m))
+    def owner_bloom_finalize(self):
         return self.new_in_second
 
-    def bloom_finalize(self, owner_slots):
-        self.owner_slots = owner_slots
-        return self.new_in_second
+    def count_records(self, recs, n, stream=0):
+        for row in self._rows(recs, n):
+            ws = [int(x) for x in row[:self.W]]
+            if self._has(bloom_positions(ws, self.NBLOCKS, self.NH)[: self.NH_GATE], 8):
+                self.owner.table[from_words(row[:self.W], self.k)] += int(row[self.W])
 
     def count(self, dev_ptr, chunks, fmt, stream=0):
         for off, ln, _ in chunks:
             for line in self.lines[off:off + ln]:
-                kms = canonical_windows(line, self.k)
-                if self.bf:  # the pass-2 gate: trunc(hf) filter-2 positions
-                    kms = [km for km in kms if self._has(bloom_positions(to_words(km, self.W), self.NBLOCKS,
-                                                                         self.NH)[: self.NH_GATE], 8)]
-                self.kc.table.update(kms)
+                self.kc.table.update(canonical_windows(line, self.k))
 
     def route_table(self, parts, stream=0):
         groups = [[] for _ in range(parts)]
@@ -186,6 +170,8 @@ class NumpyEngine:
     def reset(self):
         self.kc.table.clear()
         self.owner.table.clear()
+        self.filter[:] = 0
+        self.new_in_second = 0
 
 
 def _free_port():
@@ -269,21 +255,23 @@ def _bloom_worker(rank, world, port, k, reads, outdir):
         sc.count_device(0, [(lo, hi - lo, 0)], 2)
         sc.sync()
         with open(os.path.join(outdir, f"shard{rank}.json"), "w") as f:
-            json.dump({"owner": dict(eng.owner.table), "nis": nis, "filter": eng.filter.tolist()}, f)
+            json.dump({"owner": dict(eng.owner.table), "nis": nis, "own_nis": eng.new_in_second}, f)
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("k,world", [(21, 2), (33, 3)])
 def test_sharded_bloom(tmp_path, k, world):
-    """Every rank's Bloom pass fills its own filter; the combined filter gates every rank's
-    counting pass: each k-mer seen twice anywhere (also once on each of two ranks) keeps its
-    exact count, and every rank installs the same filter and the same new_in_second."""
+    """Owner-sharded Bloom filter: every rank counts its reads ungated, the records
+    go to their owners, each owner runs the Bloom pass over its records (twice for a count >= 2)
+    and counts them behind its own filter: each k-mer seen twice anywhere (also once on each of
+    two ranks) keeps its exact count, the owners are disjoint, and every rank returns the same
+    new_in_second, the sum of the owners' counters."""
     reads = make_reads(40, 70, seed=k)
     mp.spawn(_bloom_worker, args=(world, _free_port(), k, reads, str(tmp_path)), nprocs=world, join=True)
     shards = [json.load(open(tmp_path / f"shard{r}.json")) for r in range(world)]
-    assert all(s["filter"] == shards[0]["filter"] for s in shards)
     assert all(s["nis"] == shards[0]["nis"] > 0 for s in shards)
+    assert shards[0]["nis"] == sum(s["own_nis"] for s in shards)
     union = collections.Counter()
     for a in range(world):
         for b in range(a + 1, world):
