@@ -238,9 +238,11 @@ def same_image(a, b):
 FIXTURES = os.path.join(REPO, "tests", "golden", "fullsize.json")
 
 
-def fixture_case(args):
+def fixture_case(args, share=0, first=0, count=None):
     """The tests/golden/fullsize.json case (reference output digest, tests/golden/make_fullsize.py)
-    whose input and options are this workload's at one GPU, or None."""
+    whose input and options are this workload's at one GPU, or None.  share: rank 0's share of
+    a strong preset (--share G): reads [first, first + count) of the whole job, whose local
+    table is sized from the distinct estimate (the reference case's -s only has to hold them)."""
     try:
         with open(FIXTURES) as f:
             doc = json.load(f)
@@ -253,9 +255,13 @@ def fixture_case(args):
         same_in = ((inp["reads"], inp["read_len"], inp["genome"], inp["seed"], inp["err"]) ==
                    (args.reads, args.read_len, args.genome, args.seed, args.err)
                    and (list(skew) if skew else None) == (list(preset["skew"]) if preset.get("skew") else None))
+        if share:
+            same_in = same_in and (inp.get("first"), inp.get("count"), c.get("share")) == (first, count, share)
+        elif "first" in inp:
+            continue
         a = c["args"]
         opt = table_args(args.slots, args.unique)
-        if same_in and c["k"] == args.k and a[:2] == ["-m", "2"] and a[2:-2] == opt:
+        if same_in and c["k"] == args.k and a[:2] == ["-m", "2"] and (share or a[2:-2] == opt):
             return dict(c, name=name, min_abundance=int(a[-1]), input_sha256=inp["sha256"])
     return None
 
@@ -342,7 +348,7 @@ def setup_job(args, env, image=None):
                      f"{sk[3]} in the genome")
     # -a only selects output lines (it does not change counting): the reference fixture's -a when
     # this workload has one, so the parity digest covers the same lines
-    fx = fixture_case(args) if world == 1 and not dist else None
+    fx = fixture_case(args, share, first, N) if world == 1 and not dist else None
     cfg = ka.Config(k=k, mode=2, table_slots=estimate["local_slots"] if share else slots,
                     min_abundance=fx["min_abundance"] if fx else 2, batch_bytes=batch,
                     device=local, bf_enable=bool(args.unique), est_unique=args.unique)

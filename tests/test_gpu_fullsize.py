@@ -29,11 +29,15 @@ def _fixture():
         return json.load(f)
 
 
-def _bench_args(config):
+def _bench_args(config, share=0):
     import bench
     base = argparse.Namespace(config=config, reads=None, read_len=None, genome=None, k=None, slots=None,
-                              unique=None, batch_mib=0, err=0.001, seed=42, share=0)
+                              unique=None, batch_mib=0, err=0.001, seed=42, share=share)
     return bench, bench.resolve(base, config)
+
+
+# fixture name -> (bench preset, --share): the strong presets' rank-0 shares at 8 GPUs
+SHARES = {"C4S": ("C4", 8), "C5S": ("C5", 8)}
 
 
 @pytest.mark.parametrize("n", [0, 1, 7, 1000])
@@ -74,8 +78,13 @@ def test_fixture_cases_match_bench_presets():
     """Every full-size fixture is a bench workload (bench.fixture_case finds it)."""
     doc = _fixture()
     for name, c in doc["cases"].items():
-        bench, args = _bench_args(name)
-        fx = bench.fixture_case(args)
+        config, share = SHARES.get(name, (name, 0))
+        bench, args = _bench_args(config, share)
+        if share:
+            inp = doc["inputs"][c["input"]]
+            fx = bench.fixture_case(args, share, inp["first"], inp["count"])
+        else:
+            fx = bench.fixture_case(args)
         assert fx is not None and fx["name"] == name, name
         assert fx["sorted_sha256"] == c["sorted_sha256"]
 
@@ -116,6 +125,43 @@ def test_bench_job_equals_reference_output(config):
             assert got["sorted_sha256"] == fx["sorted_sha256"], step
             if fx["distinct"] is not None and not args.unique:
                 assert st["distinct"] == fx["distinct"]
+    finally:
+        job.counter.close()
+        del job
+        torch.cuda.empty_cache()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("name", ["C4S", "C5S"])
+def test_bench_share_equals_reference_output(name):
+    """rank 0's share of the strong presets at 8 GPUs (bench.py --config C4|C5
+    --share 8: 12.5 M x 150 bp at k = 51; 125 k x 10 kbp at k = 127), its local table sized from the
+    distinct estimate, against the reference CLI's output on the same reads (make_fullsize.py)."""
+    import torch
+    import kaarme_amd as ka
+    from kaarme_amd.digest import sorted_text_digest
+    doc = _fixture()
+    if name not in doc["cases"]:
+        pytest.skip(f"no {name} fixture")
+    config, share = SHARES[name]
+    bench, args = _bench_args(config, share)
+    env = {"torch": torch, "ka": ka, "lib": ka.load_library(), "dist": None, "rank": 0, "world": 1, "local": 0}
+    torch.cuda.set_device(0)
+    job = bench.setup_job(args, env)
+    fx = job.fixture
+    assert fx is not None and fx["name"] == name
+    try:
+        img = job.image.cpu().numpy()
+        assert hashlib.sha256(memoryview(img)).hexdigest() == fx["input_sha256"], "device image != kc_gen file"
+        del img
+        job.step()
+        st = job.counter.finish()
+        assert st["windows"] == job.windows_expected
+        assert st["distinct"] == fx["distinct"]
+        got = sorted_text_digest(job.counter.dump(), args.k)
+        assert (got["lines"], got["count_sum"]) == (fx["lines"], fx["count_sum"])
+        assert got["sorted_sha256"] == fx["sorted_sha256"]
     finally:
         job.counter.close()
         del job
