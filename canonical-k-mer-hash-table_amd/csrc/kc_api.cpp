@@ -528,9 +528,13 @@ static int tail_needed(kc_ctx* c, hipStream_t s, bool* need) {
     return KC_OK;
 }
 
+// The fused pass is opt-in (KC_FUSE=1): it measured slower than k_b3 + the gated k_p3 over the
+// kept partitions (C3: k_bf3 13.5 ms against 6.3 + 5.5 ms, profiles/r04_ab_fused.txt) -- its
+// filter phase runs 4x the workgroups of k_b3 over 4x smaller filter slices, and the count phase
+// waits for the slowest wave of the filter phase in every workgroup
 static bool fuse_enabled() {
     const char* v = std::getenv("KC_FUSE");
-    return !(v && *v == '0');
+    return v && *v == '1';
 }
 
 // The fused pass's table regions from the probe's sample of the kept fine bins: the distinct
@@ -826,23 +830,38 @@ static int count_reused(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, s
         HIPCHK(c, hipEventRecord(ev[0], s));
         HIPCHK(c, hipEventRecord(ev[1], s));
     }
-    // the bytes must be the Bloom pass's: same checksum
+    // the bytes must be the Bloom pass's: same checksum.  It runs on the aux stream beside the
+    // counting pass from the partitions (which reads no input byte); a mismatch restores the
+    // counters and drops the table before the ordinary pass (C3: 0.35 ms off the step)
     std::memcpy(c->h_desc[c->cur], b.data(), b.size() * sizeof(ChunkDesc));
     HIPCHK(c, hipMemcpyAsync(c->d_chunks, c->h_desc[c->cur], b.size() * sizeof(ChunkDesc), hipMemcpyHostToDevice, s));
-    HIPCHK(c, launch_checksum(img, c->d_chunks, (int)b.size(), max_len, c->d_sum, s));
-    unsigned long long part[CHECKSUM_SLOTS];
-    HIPCHK(c, hipMemcpyAsync(part, c->d_sum, sizeof(part), hipMemcpyDeviceToHost, s));
-    if (ev[2]) HIPCHK(c, hipEventRecord(ev[2], s));
-    HIPCHK(c, hipStreamSynchronize(s));
-    unsigned long long sum = 0;
-    for (auto v : part) sum += v;
-    if (sum != c->reuse_sum) {
-        if (std::getenv("KC_REUSE_DEBUG")) std::fprintf(stderr, "reuse: checksum differs\n");
-        release();
-        return KC_OK;
+    if (!c->aux) {
+        HIPCHK(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+        for (auto& e : c->aev) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
+    HIPCHK(c, hipEventRecord(c->aev[0], s));
+    HIPCHK(c, hipStreamWaitEvent(c->aux, c->aev[0], 0));
+    HIPCHK(c, launch_checksum(img, c->d_chunks, (int)b.size(), max_len, c->d_sum, c->aux));
+    unsigned long long part[CHECKSUM_SLOTS];
+    HIPCHK(c, hipMemcpyAsync(part, c->d_sum, sizeof(part), hipMemcpyDeviceToHost, c->aux));
+    HIPCHK(c, hipEventRecord(c->aev[1], c->aux));
+    auto same_bytes = [&](bool* same) -> int {  // waits for the checksum
+        HIPCHK(c, hipEventSynchronize(c->aev[1]));
+        unsigned long long sum = 0;
+        for (auto v : part) sum += v;
+        *same = sum == c->reuse_sum;
+        if (!*same && std::getenv("KC_REUSE_DEBUG")) std::fprintf(stderr, "reuse: checksum differs\n");
+        return KC_OK;
+    };
+    if (ev[2]) HIPCHK(c, hipEventRecord(ev[2], s));
+    bool same = false;
     const uint64_t syms = used + b.size();
     if (c->reuse_level == 3) {  // the fused pass counted these bytes: its table stands
+        if ((rc = same_bytes(&same))) return rc;
+        if (!same) {
+            release();
+            return KC_OK;
+        }
         HIPCHK(c, launch_spec_commit(c->d_ctr, c->reuse_windows, s));
         if (ev[3]) HIPCHK(c, hipEventRecord(ev[3], s));
         c->spec_table = false;
@@ -870,6 +889,7 @@ static int count_reused(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, s
     if (pr.keys1 != c->pbf.keys1 || (c->reuse_level == 2 && pr.keys2 != c->pbf.keys2) || pr.nblk1 != c->pbf.nblk1 ||
         pr.B2 != c->pbf.B2 || pr.cap1 != c->pbf.cap1 || pr.cap1 == 0 || c->F1 != c->fgeo.F1) {
         if (std::getenv("KC_REUSE_DEBUG")) std::fprintf(stderr, "reuse: partition geometry differs\n");
+        HIPCHK(c, hipEventSynchronize(c->aev[1]));
         release();
         return KC_OK;
     }
@@ -888,11 +908,9 @@ static int count_reused(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, s
     }
     const BloomView bv{c->d_bloom, c->bf_bits ? c->bf_bits - 1 : 0, c->nh, c->nh_gate, c->bloom_blocked,
                        bloom_blocks(c->bf_bits)};
-    // the counters a redo must restore (windows, inserted, overflow: one 128-byte line each)
-    unsigned long long before[3];
-    HIPCHK(c, hipMemcpyAsync(&before[0], &c->d_ctr->windows, 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(c, hipMemcpyAsync(&before[1], &c->d_ctr->inserted, 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(c, hipMemcpyAsync(&before[2], &c->d_ctr->overflow, 8, hipMemcpyDeviceToHost, s));
+    // the counters as they were, for a redo (other bytes, or a table region that overflowed)
+    DevCounters before;
+    HIPCHK(c, hipMemcpyAsync(&before, c->d_ctr, sizeof(before), hipMemcpyDeviceToHost, s));
     // -m 1 -b counts every window (the reference ignores its filter, main.cpp:482-489)
     HIPCHK(c, launch_count_reuse(c->W, table_view(c), bv, c->d_ctr, pr, c->table_fresh, c->reuse_level,
                                  c->cfg.mode != 1, c->reuse_windows, s));
@@ -901,18 +919,14 @@ static int count_reused(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, s
     HIPCHK(c, hipMemcpyAsync(&ovf, &c->d_ctr->part_overflow, sizeof(ovf), hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipMemcpyAsync(&full, &c->d_ctr->overflow, sizeof(full), hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
-    if (ovf) {  // a full skew list: nothing was inserted, the ordinary pass redoes the batch
-        if (std::getenv("KC_REUSE_DEBUG")) std::fprintf(stderr, "reuse: level 2 overflowed\n");
-        release();
-        return KC_OK;
-    }
-    if (full != before[2]) {
-        // a region of the table sized for the gated k-mers overflowed: the ordinary counting pass
-        // redoes the batch into the reference-sized table (2 * new_in_second), counters restored
-        if (std::getenv("KC_REUSE_DEBUG")) std::fprintf(stderr, "reuse: table region overflowed, redo\n");
-        HIPCHK(c, hipMemcpyAsync(&c->d_ctr->windows, &before[0], 8, hipMemcpyHostToDevice, s));
-        HIPCHK(c, hipMemcpyAsync(&c->d_ctr->inserted, &before[1], 8, hipMemcpyHostToDevice, s));
-        HIPCHK(c, hipMemcpyAsync(&c->d_ctr->overflow, &before[2], 8, hipMemcpyHostToDevice, s));
+    if ((rc = same_bytes(&same))) return rc;
+    if (!same || ovf || full != before.overflow) {
+        // other bytes than the Bloom pass's, a full skew list, or a region of the table sized for
+        // the gated k-mers that overflowed: the ordinary counting pass redoes the batch into a
+        // fresh reference-sized table (2 * new_in_second), with the counters as they were
+        if (std::getenv("KC_REUSE_DEBUG") && same)
+            std::fprintf(stderr, "reuse: %s, redo\n", ovf ? "level 2 overflowed" : "table region overflowed");
+        HIPCHK(c, hipMemcpyAsync(c->d_ctr, &before, sizeof(before), hipMemcpyHostToDevice, s));
         HIPCHK(c, hipStreamSynchronize(s));
         release();
         return alloc_table(c, c->min_slots);

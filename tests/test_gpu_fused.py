@@ -3,6 +3,7 @@ k_bf3 / k_bprobe): a one-batch Bloom pass over a device image counts its kept le
 behind the gate in the same workgroup that built the region's filter blocks, into a table
 sized from a sample of the kept bins; the counting pass only confirms the input (checksum).
 
+The fused pass is opt-in (KC_FUSE=1; it measured slower than the two kernels it fuses).
 The filter only gates: every k-mer seen at least twice has its exact count,
 so the fused job's records at -a 2 equal the records of the same job with the fused pass off
 (KC_FUSE=0: k_b3, then the gated k_p3 from the kept partitions), and those of counting without
@@ -49,6 +50,7 @@ def _exact_solid(img, chunks, k):
 @pytest.fixture
 def partitioned(monkeypatch):
     monkeypatch.setenv("KC_INSERT_PATH", "partitioned")
+    monkeypatch.setenv("KC_FUSE", "1")  # (opt-in: kc_api.cpp fuse_enabled)
 
 
 @pytest.mark.parametrize("k,fpr", [(31, 0.01), (51, 0.01), (51, 0.001), (95, 0.05), (127, 0.01)])
