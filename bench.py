@@ -301,9 +301,8 @@ def setup_job(args, env, image=None):
         assert rc == 0, "kc_synth_device failed"
         torch.cuda.synchronize()
     assert image.numel() == nbytes
-    host = image.cpu().numpy().tobytes()  # setup only: the host chunker reads boundary bytes
-    chunks = ka.plan_chunks(host, k, ka.FMT_FASTA)
-    del host
+    # the reference chunk table: the planner reads the bytes around chunk ends from HBM
+    chunks = ka.plan_chunks_device(image.data_ptr(), nbytes, k, ka.FMT_FASTA)
     if args.batch_mib:
         cap = args.batch_mib << 20
     else:

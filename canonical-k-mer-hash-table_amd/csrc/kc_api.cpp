@@ -2201,9 +2201,54 @@ int kc_write(kc_ctx* c, const char* path) {
     return KC_OK;
 }
 
-int kc_plan_chunks(const uint8_t* image, uint64_t size, int k, uint64_t chunk_size, int fmt, kc_chunk** out,
-                   uint64_t* n_out) {
-    if (!out || !n_out || k < 1 || (!image && size)) return KC_ERR_ARG;
+}  // extern "C"
+
+// The chunk planner reads the image only around chunk ends (io_worker / read_chunk_from_file,
+// parallel_parser.hpp:1246-1285, text_reader.h:93-226): templated over how bytes are read --
+// a host pointer, or 64 KiB pages of a device image fetched on demand (kc_plan_chunks_device:
+// a 1.6 GB image costs its ~160 chunk ends, not a copy of the image)
+struct HostImg {
+    const uint8_t* p;
+    uint8_t operator[](uint64_t i) const { return p[i]; }
+    uint64_t find(uint64_t from, uint8_t c, uint64_t size) const {  // first c at >= from, or size
+        const void* q = std::memchr(p + from, c, size - from);
+        return q ? (uint64_t)((const uint8_t*)q - p) : size;
+    }
+};
+struct DeviceImg {
+    static constexpr uint64_t PAGE = 64 << 10;
+    const uint8_t* d;
+    uint64_t size;
+    std::vector<std::pair<uint64_t, std::vector<uint8_t>>> cache;  // a few pages, most recent last
+    bool bad = false;
+    uint64_t fetched = 0;
+    const std::vector<uint8_t>& page(uint64_t pg) {
+        for (size_t i = 0; i < cache.size(); i++)
+            if (cache[i].first == pg) return cache[i].second;
+        if (cache.size() >= 8) cache.erase(cache.begin());
+        const uint64_t off = pg * PAGE, len = std::min(PAGE, size - off);
+        std::vector<uint8_t> buf(len);
+        if (hipMemcpy(buf.data(), d + off, len, hipMemcpyDeviceToHost) != hipSuccess) bad = true;
+        fetched += len;
+        cache.emplace_back(pg, std::move(buf));
+        return cache.back().second;
+    }
+    uint8_t operator[](uint64_t i) { return page(i / PAGE)[i % PAGE]; }
+    uint64_t find(uint64_t from, uint8_t c, uint64_t sz) {
+        while (from < sz) {
+            const auto& pg = page(from / PAGE);
+            const uint64_t o = from % PAGE;
+            const void* q = std::memchr(pg.data() + o, c, pg.size() - o);
+            if (q) return from - o + (uint64_t)((const uint8_t*)q - pg.data());
+            from += pg.size() - o;
+        }
+        return sz;
+    }
+};
+
+template <class Img>
+static int plan_chunks_impl(Img& image, uint64_t size, int k, uint64_t chunk_size, int fmt, kc_chunk** out,
+                            uint64_t* n_out) {
     if (chunk_size == 0) chunk_size = 10ull << 20;  // main.cpp:387
     std::vector<kc_chunk> v;
     if (fmt == KC_FMT_FASTQ) {
@@ -2212,8 +2257,8 @@ int kc_plan_chunks(const uint8_t* image, uint64_t size, int k, uint64_t chunk_si
         // with '@' and whose second next line begins with '+' (a quality line starting
         // with '@' is followed two lines later by a sequence line, never by '+').
         auto line_after = [&](uint64_t p) -> uint64_t {  // start of the line after the one at p
-            const void* q = std::memchr(image + p, '\n', size - p);
-            return q ? (uint64_t)((const uint8_t*)q - image) + 1 : size;
+            const uint64_t q = image.find(p, '\n', size);
+            return q < size ? q + 1 : size;
         };
         auto is_record = [&](uint64_t p) {
             if (p >= size || image[p] != '@') return false;
@@ -2247,20 +2292,20 @@ int kc_plan_chunks(const uint8_t* image, uint64_t size, int k, uint64_t chunk_si
     bool bh = false;
     while (rem >= (int64_t)k) {
         const int64_t n = std::min<int64_t>((int64_t)chunk_size, rem);
-        const uint8_t* b = image + pos;
+        auto b = [&](int64_t i) { return image[pos + (uint64_t)i]; };
         kc_chunk ck{pos, (uint64_t)n, bh ? 1 : 0, 0};
         v.push_back(ck);
         int64_t fake = 0;
         if (start) {
             int64_t real = 0, si = n - 1;
             if (start == '>')
-                for (; real < back && si >= 0; si--) (b[si] != '\n') ? real++ : fake++;  // text_reader.h:143-150
+                for (; real < back && si >= 0; si--) (b(si) != '\n') ? real++ : fake++;  // text_reader.h:143-150
             if (real != back) break;                                                 // text_reader.h:156-160
             // broken header of the NEXT chunk: scan back from the byte before its start
             bh = true;
             for (int64_t i = n - 1 - back - fake; i >= 0; i--) {  // text_reader.h:164-184
-                if (b[i] == start) break;
-                if (b[i] == '\n') { bh = false; break; }
+                if (b(i) == start) break;
+                if (b(i) == '\n') { bh = false; break; }
             }
         }
         if (rem == n) break;                 // text_reader.h:201-204
@@ -2276,6 +2321,30 @@ int kc_plan_chunks(const uint8_t* image, uint64_t size, int k, uint64_t chunk_si
     *out = r;
     *n_out = v.size();
     return KC_OK;
+}
+
+extern "C" {
+
+int kc_plan_chunks(const uint8_t* image, uint64_t size, int k, uint64_t chunk_size, int fmt, kc_chunk** out,
+                   uint64_t* n_out) {
+    if (!out || !n_out || k < 1 || (!image && size)) return KC_ERR_ARG;
+    HostImg img{image};
+    return plan_chunks_impl(img, size, k, chunk_size, fmt, out, n_out);
+}
+
+int kc_plan_chunks_device(const uint8_t* dev_image, uint64_t size, int k, uint64_t chunk_size, int fmt, kc_chunk** out,
+                          uint64_t* n_out) {
+    if (!out || !n_out || k < 1 || (!dev_image && size)) return KC_ERR_ARG;
+    if (hipDeviceSynchronize() != hipSuccess) return KC_ERR_HIP;  // the image's producers are done
+    DeviceImg img{dev_image, size, {}};
+    const int rc = plan_chunks_impl(img, size, k, chunk_size, fmt, out, n_out);
+    if (rc == KC_OK && img.bad) {
+        std::free(*out);
+        *out = nullptr;
+        *n_out = 0;
+        return KC_ERR_HIP;
+    }
+    return rc;
 }
 
 uint64_t kc_table_size_reference(uint64_t at_least) {  // next_prime3mod4, functions_math.cpp:53-96

@@ -352,9 +352,6 @@ template <int W, int OW, int NT>
 constexpr size_t p1_smem(uint32_t F) { return bin_lds_bytes(F) + (size_t)NT * k1_runw<W, NT>() * 8 * OW; }
 // the segmented k_p1's LDS stage of the packed stream: two buffers of the words a tile reads
 // (kc_internal.h p1_stage_words), 8 + 4 bytes per word, after the heavy table
-#ifndef KC_P1_STAGE
-#define KC_P1_STAGE 1  // A/B: 0 = the windows read HBM directly
-#endif
 template <int W, int NT>
 constexpr int k1_stage_words() { return NT * k1_runw<W, NT>() / 32 + W + 3; }
 template <int W, int NT>
@@ -1110,7 +1107,7 @@ __global__ __launch_bounds__(NT, NT >= 1024 ? 8 : 4) void k_p1(PackedView sv, in
     // next tile are loaded while this one is scattered (its rank atomics issue the loads, its
     // placement stores them), so the windows of a tile start without waiting for HBM.  Tile
     // t0 reads words (t0 >> 5) - W - 1 .. (t0 + TW) >> 5 (run_windows, t0 a multiple of 32).
-    constexpr bool STAGE = KC_P1_STAGE && Out::kSeg && !ROLLED;
+    constexpr bool STAGE = Out::kSeg && !ROLLED;  // the segmented level 1 reads its windows from the LDS stage
     constexpr int SW = k1_stage_words<W, NT>();
     static_assert(!STAGE || SW <= NT, "one stage word per thread");
     uint64_t* st_pk = reinterpret_cast<uint64_t*>(smem + p1_smem<W, OW, NT>(F) + heavy_smem<OW>());

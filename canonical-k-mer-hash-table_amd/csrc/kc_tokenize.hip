@@ -19,6 +19,8 @@
 // other byte and every newline is a break -- the counts equal those of the plain-text
 // file of the sequence lines.  The newline count rides in bits 40.. of the tile scan's
 // symbol sum (only its value mod 4 is used; a batch holds < 2^40 symbols).
+#include <cstdlib>
+
 #include "kc_common.h"
 #include "kc_synth.h"
 
@@ -127,6 +129,92 @@ __global__ __launch_bounds__(TILE_THREADS) void k_tile_summary(const uint8_t* __
         ti.avail = avail;
         ti.src = cd.src_off + rel;
         tiles[t] = ti;
+    }
+}
+
+// k_tile_summary_m<TPB>: the same per-tile summary for TPB consecutive tiles per workgroup,
+// every thread's TPB loads (tile map -> chunk descriptor -> 16 bytes of each tile) issued
+// before any is used: one 4 KiB tile per workgroup left a chain of three dependent loads per
+// 16 bytes in flight, the summary ran at ~3.5 TB/s of its 1.6 GB (C2)
+template <int TPB>
+__global__ __launch_bounds__(TILE_THREADS) void k_tile_summary_m(const uint8_t* __restrict__ src,
+                                                                 const ChunkDesc* __restrict__ chunks, uint64_t ntiles,
+                                                                 int fmt, TileInfo* __restrict__ tiles) {
+    __shared__ uint32_t s_nl[TPB][TILE_THREADS / 64];
+    __shared__ uint32_t s_mk[TPB][TILE_THREADS / 64];
+    const int tid = threadIdx.x;
+    const uint64_t t0 = (uint64_t)blockIdx.x * TPB;
+    int ci[TPB];
+#pragma unroll
+    for (int j = 0; j < TPB; j++) ci[j] = t0 + j < ntiles ? (int)tiles[t0 + j].nl : 0;  // k_tile_map
+    ChunkDesc cd[TPB];
+#pragma unroll
+    for (int j = 0; j < TPB; j++) cd[j] = chunks[ci[j]];
+    uint32_t w[TPB][4], vh[TPB], valid[TPB], avail[TPB];
+    uint64_t rel[TPB];
+    const uint32_t my0 = tid * 16;
+#pragma unroll
+    for (int j = 0; j < TPB; j++) {
+        rel[j] = (t0 + j) * TILE - cd[j].stage_off;
+        const bool in = t0 + j < ntiles;
+        valid[j] = in ? (uint32_t)min((uint64_t)TILE, cd[j].len - rel[j]) : 0;
+        avail[j] = in ? (uint32_t)min((uint64_t)TILE + 64, cd[j].len - rel[j]) : 0;
+        vh[j] = valid[j] > my0 ? valid[j] - my0 : 0;
+        w[j][0] = w[j][1] = w[j][2] = w[j][3] = 0;
+        if (fmt != FMT_PLAIN && vh[j]) load16(src + cd[j].src_off + rel[j] + my0, avail[j] - my0, w[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < TPB; j++) {
+        uint32_t nl = 0, mk = 0;
+        if (fmt != FMT_PLAIN && vh[j]) {
+            const uint32_t vmask = vh[j] >= 16 ? 0xFFFFu : ((1u << vh[j]) - 1);
+            const uint32_t nlm = eq_mask16(w[j], 0x0A0A0A0Au) & vmask;
+            nl = __builtin_popcount(nlm);
+            if (fmt == FMT_FASTA) {
+                const uint32_t gtm = eq_mask16(w[j], 0x3E3E3E3Eu) & vmask;
+                const uint32_t any = nlm | gtm;
+                if (any) mk = (gtm >> (31 - __builtin_clz(any))) & 1 ? 2u : 1u;
+            }
+        }
+        for (int d = 32; d >= 1; d >>= 1) nl += __shfl_xor(nl, d, 64);
+        uint32_t tag = mk ? ((uint32_t)tid << 2) | mk : 0;
+        for (int d = 32; d >= 1; d >>= 1) tag = max(tag, (uint32_t)__shfl_xor(tag, d, 64));
+        if ((tid & 63) == 0) {
+            s_nl[j][tid >> 6] = nl;
+            s_mk[j][tid >> 6] = tag;
+        }
+    }
+    __syncthreads();
+    if (tid < TPB && t0 + tid < ntiles) {
+        const int j = tid;
+        uint32_t tn = 0, tm = 0;
+        for (int q = 0; q < TILE_THREADS / 64; q++) {
+            tn += s_nl[j][q];
+            tm = max(tm, s_mk[j][q]);
+        }
+        // (the thread's own copies of tile j's fields: j == tid, registers indexed by the
+        // unrolled loop's constant via a select chain)
+        ChunkDesc c = cd[0];
+        uint64_t r = rel[0];
+        uint32_t v = valid[0], a = avail[0];
+#pragma unroll
+        for (int q = 1; q < TPB; q++)
+            if (q == j) {
+                c = cd[q];
+                r = rel[q];
+                v = valid[q];
+                a = avail[q];
+            }
+        TileInfo ti;
+        ti.nl = tn;
+        ti.valid = v;
+        ti.marker = (uint8_t)(tm & 3);
+        ti.first = r == 0;
+        ti.bh = (uint8_t)c.bh;
+        ti.pad = 0;
+        ti.avail = a;
+        ti.src = c.src_off + r;
+        tiles[t0 + j] = ti;
     }
 }
 
@@ -467,7 +555,18 @@ hipError_t launch_tokenize(const uint8_t* src, uint64_t ntiles, const ChunkDesc*
     const uint64_t nblk = (ntiles + TSCAN - 1) / TSCAN;
     if (n_chunks <= 0) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_tile_map, dim3((unsigned)n_chunks), dim3(256), 0, s, d_chunks, tiles);
-    hipLaunchKernelGGL(k_tile_summary, dim3((unsigned)ntiles), dim3(TILE_THREADS), 0, s, src, d_chunks, n_chunks,
+static const int tpb = [] {  // A/B: KC_TSUM_TPB = tiles per summary workgroup (1 = k_tile_summary)
+        const char* v = std::getenv("KC_TSUM_TPB");
+        return v ? std::atoi(v) : 4;
+    }();
+    if (tpb == 4)
+        hipLaunchKernelGGL(k_tile_summary_m<4>, dim3((unsigned)((ntiles + 3) / 4)), dim3(TILE_THREADS), 0, s, src,
+                           d_chunks, ntiles, fmt, tiles);
+    else if (tpb == 2)
+        hipLaunchKernelGGL(k_tile_summary_m<2>, dim3((unsigned)((ntiles + 1) / 2)), dim3(TILE_THREADS), 0, s, src,
+                           d_chunks, ntiles, fmt, tiles);
+    else
+            hipLaunchKernelGGL(k_tile_summary, dim3((unsigned)ntiles), dim3(TILE_THREADS), 0, s, src, d_chunks, n_chunks,
                        fmt, tiles);
     hipLaunchKernelGGL(k_tscan_block, dim3((unsigned)nblk), dim3(TSCAN), 0, s, tiles, ntiles, fmt, touts, tblk);
     hipLaunchKernelGGL(k_tscan_top, dim3(1), dim3(TSCAN), 0, s, tblk, nblk, fmt, ctr);

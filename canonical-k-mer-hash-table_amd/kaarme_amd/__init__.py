@@ -49,7 +49,7 @@ EXPORTS = (
     "kc_xxh64", "kc_bloom_info", "kc_bloom_read", "kc_bloom_write", "kc_synth_skew_device",
     "kc_table_size_reference", "kc_bloom_get_device", "kc_bloom_merge_device", "kc_bloom_set_device",
     "kc_bloom_estimate", "kc_compact", "kc_compact_dump", "kc_compact_lookup", "kc_compact_read",
-    "kc_estimate_distinct_device", "kc_bloom_records_device", "kc_count_records_device",
+    "kc_estimate_distinct_device", "kc_bloom_records_device", "kc_count_records_device", "kc_plan_chunks_device",
 )
 
 
@@ -138,6 +138,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "kc_free": (None, [P]),
         "kc_plan_chunks": (I32, [P, U64, I32, U64, I32, ctypes.POINTER(ctypes.POINTER(kc_chunk)),
                                  ctypes.POINTER(U64)]),
+        "kc_plan_chunks_device": (I32, [P, U64, I32, U64, I32, ctypes.POINTER(ctypes.POINTER(kc_chunk)),
+                                 ctypes.POINTER(U64)]),
         "kc_synth_bytes": (U64, [U64, U64, ctypes.c_uint32, ctypes.c_uint32]),
         "kc_reset": (I32, [P]),
         "kc_clear_table": (I32, [P]),
@@ -222,6 +224,21 @@ def plan_chunks(image: bytes, k: int, fmt: int, chunk_size: int = 0) -> List[Tup
     rc = lib.kc_plan_chunks(buf, len(image), k, chunk_size, fmt, ctypes.byref(out), ctypes.byref(n))
     if rc:
         raise KcError(rc, "kc_plan_chunks")
+    res = [(out[i].off, out[i].len, out[i].broken_header) for i in range(n.value)]
+    lib.kc_free(out)
+    return res
+
+
+def plan_chunks_device(dev_ptr: int, size: int, k: int, fmt: int, chunk_size: int = 0) -> List[Tuple[int, int, int]]:
+    """plan_chunks for an image in device memory (kc_plan_chunks_device: only the bytes around
+    chunk ends are copied to the host)."""
+    lib = load_library()
+    out = ctypes.POINTER(kc_chunk)()
+    n = ctypes.c_uint64()
+    rc = lib.kc_plan_chunks_device(ctypes.c_void_p(dev_ptr or None), size, k, chunk_size, fmt, ctypes.byref(out),
+                                   ctypes.byref(n))
+    if rc:
+        raise KcError(rc, "kc_plan_chunks_device")
     res = [(out[i].off, out[i].len, out[i].broken_header) for i in range(n.value)]
     lib.kc_free(out)
     return res

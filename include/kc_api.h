@@ -296,6 +296,11 @@ void kc_free(void* p);
  * main.cpp:387).  *chunks is allocated by the library (kc_free). */
 int kc_plan_chunks(const uint8_t* image, uint64_t size, int k, uint64_t chunk_size, int fmt, kc_chunk** chunks,
                    uint64_t* n_chunks);
+/* The same chunk table for an image in device memory (after the device's queued work): the
+ * planner reads only the bytes around chunk ends, copied to the host in 64 KiB pages on demand,
+ * instead of the caller copying the whole image to the host first. */
+int kc_plan_chunks_device(const uint8_t* dev_image, uint64_t size, int k, uint64_t chunk_size, int fmt,
+                          kc_chunk** chunks, uint64_t* n_chunks);
 
 /* The reference's table size for a minimum of `min_slots` slots: the next prime that is
  * 3 mod 4 (next_prime3mod4, functions_math.cpp:53-96; "Hash table size is:").  The device

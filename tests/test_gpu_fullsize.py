@@ -166,3 +166,39 @@ def test_bench_share_equals_reference_output(name):
         job.counter.close()
         del job
         torch.cuda.empty_cache()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_device_writer_at_full_size(tmp_path):
+    """the writer's bytes at full size -- kc_write of the C2 job (86.5 M lines,
+    device formatting + pinned copy-out) sorted and hashed against the reference's output digest
+    (the records' digest is test_bench_job_equals_reference_output's)."""
+    import subprocess
+    import torch
+    import kaarme_amd as ka
+    doc = _fixture()
+    bench, args = _bench_args("C2")
+    env = {"torch": torch, "ka": ka, "lib": ka.load_library(), "dist": None, "rank": 0, "world": 1, "local": 0}
+    torch.cuda.set_device(0)
+    job = bench.setup_job(args, env)
+    fx = job.fixture
+    try:
+        job.step()
+        job.counter.finish()
+        out = tmp_path / "c2.txt"
+        job.counter.write(str(out))
+        p = subprocess.Popen(["sort", "-S", "12G", "--parallel=16", "-T", str(tmp_path), str(out)],
+                             stdout=subprocess.PIPE, env=dict(os.environ, LC_ALL="C"))
+        h = hashlib.sha256()
+        lines = 0
+        for b in iter(lambda: p.stdout.read(1 << 24), b""):
+            h.update(b)
+            lines += b.count(b"\n")
+        assert p.wait() == 0
+        assert lines == fx["lines"] == doc["cases"]["C2"]["lines"]
+        assert h.hexdigest() == fx["sorted_sha256"]
+    finally:
+        job.counter.close()
+        del job
+        torch.cuda.empty_cache()

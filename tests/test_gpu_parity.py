@@ -680,3 +680,31 @@ def test_distinct_estimate(tmp_path, k):
         kc.count_device(img.data_ptr(), chunks[:1], ka.FMT_FASTA)
         exact_small = kc.finish()["distinct"]
     assert abs(est_small - exact_small) / exact_small < 0.04, (est_small, exact_small)
+
+
+@pytest.mark.parametrize("name,k", [("reads_w60.fasta", 31), ("edge.fasta", 25), ("long.fasta", 127),
+                                    ("big_edge.fasta", 51), ("skew.fasta", 31)])
+@pytest.mark.parametrize("chunk_size", [0, 5000, 65537, 100003])
+def test_device_chunk_planner_equals_host(name, k, chunk_size, golden_input):
+    """kc_plan_chunks_device (the planner reading 64 KiB pages around chunk ends from HBM, used by
+    bench.py instead of copying the image to the host) gives kc_plan_chunks' chunk table."""
+    torch = pytest.importorskip("torch")
+    path = golden_input(name)
+    image = open(path, "rb").read()
+    fmt = ka.detect_format(path, image[0])
+    dev = torch.frombuffer(bytearray(image), dtype=torch.uint8).cuda()
+    assert ka.plan_chunks_device(dev.data_ptr(), len(image), k, fmt, chunk_size) == \
+        ka.plan_chunks(image, k, fmt, chunk_size)
+
+
+@pytest.mark.parametrize("chunk_size", [0, 4096, 70000])
+def test_device_chunk_planner_fastq_and_plain(chunk_size, tmp_path):
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(chunk_size)
+    seqs = ["".join("ACGT"[x] for x in rng.integers(0, 4, size=int(rng.integers(20, 300)))) for _ in range(3000)]
+    fq = "".join(f"@r{i}\n{s}\n+\n{'@' * len(s)}\n" for i, s in enumerate(seqs)).encode()
+    plain = "".join(s + "\n" for s in seqs).encode()
+    for data, fmt in ((fq, ka.FMT_FASTQ), (plain, ka.FMT_PLAIN)):
+        dev = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+        assert ka.plan_chunks_device(dev.data_ptr(), len(data), 31, fmt, chunk_size) == \
+            ka.plan_chunks(data, 31, fmt, chunk_size)

