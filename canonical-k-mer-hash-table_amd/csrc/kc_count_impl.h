@@ -171,7 +171,14 @@ DEV bool sb_all(const uint32_t (&f)[8], uint64_t h, int n) {
 // `blk` is the block in HBM (direct pass) or in LDS (k_b3).  A "set" counts as ours only
 // if our atomicOr flipped the bit (MyAtomicBitArrayFT::set, mybitarray.hpp:87-125).
 // Positions j >= 8 share word j - 8 and count once if they repeat its bit.
-DEV void block_insert(uint32_t* blk, uint64_t t0, int nh, BloomLocal& loc) {
+// unique: the key is inserted by no other thread at the same time (pre-aggregated records,
+// kc_bloom_records_device), so a filter-1 bit it needed that another thread set meanwhile was
+// set by ANOTHER key: as if that key had come first.  The insertion then counts as the
+// key's first sighting unless every missing bit was set by others (the filter was complete
+// for it, as a sequential pass would have found it); the reference's rule -- any such bit
+// sends the key to filter 2 -- is for concurrent sightings of one key (windows), and applied
+// to a batch of distinct keys it sent a third of the singletons to filter 2
+DEV void block_insert(uint32_t* blk, uint64_t t0, int nh, BloomLocal& loc, bool unique = false) {
     const uint64_t h = bmix(t0);
     uint32_t f1[8], f2[8];
     load8(blk + 8, f2);
@@ -196,7 +203,7 @@ DEV void block_insert(uint32_t* blk, uint64_t t0, int nh, BloomLocal& loc) {
             const uint32_t m = 1u << sb_bit(h, j);
             if (!dup[j] && !(f1[j & 7] & m)) mine += !(atomicOr(blk + (j & 7), m) & m);
         }
-        if (mine == n - s1) { loc.new_first++; to_second = false; }
+        if (mine == n - s1 || (unique && mine > 0)) { loc.new_first++; to_second = false; }
         else loc.failed++;
     }
     if (to_second) {
@@ -2038,11 +2045,14 @@ template <bool SEG>
 __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView bf, uint32_t bpr, PartBufs pb,
                                                                   DevCounters* __restrict__ ctr,
                                                                   const unsigned long long* gate, int fresh, int is,
-                                                                  int cntw) {
+                                                                  int cntw, int rec_phase) {
     // is: u64 words per item (word 0 is the table key word the filter uses); cntw >= 0: items
     // are pre-aggregated {key, count} records (kc_bloom_records_device) with the count in word
     // cntw, and a record of count >= 2 takes insertion_process twice -- the filter updates of a
-    // k-mer seen twice, as the reference makes them (double_bloomfilter.hpp:371-413)
+    // k-mer seen twice, as the reference makes them (double_bloomfilter.hpp:371-413).  The
+    // records are distinct keys; rec_phase 0 inserts those of count >= 2, rec_phase 1 (a later
+    // launch) those of count 1, with the distinct-key rule of block_insert: the order "the
+    // k-mers seen twice first", one sequential order of the reference's pass
     constexpr int NT = B3_THREADS, KB = 4;  // (8 or 2 keys per round: slower, r02_v21_ab_b3_kb.txt)
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ uint32_t s_pre[MAX_SEG_GROUP + 1];
@@ -2110,7 +2120,11 @@ __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView b
                 } else {
                     const uint64_t t = pb.keys2[i * is];
                     w.v[q] = make_uint3((uint32_t)t, (uint32_t)(t >> 32), 0);
-                    if (cntw >= 0) w.two |= (uint32_t)((pb.keys2[i * is + cntw] & CNT_MASK) >= 2) << q;
+                    if (cntw >= 0) {
+                        const bool two = (pb.keys2[i * is + cntw] & CNT_MASK) >= 2;
+                        w.two |= (uint32_t)two << q;
+                        if (two != (rec_phase == 0)) w.v[q].x = w.v[q].y = 0;  // (the other phase's: skipped)
+                    }
                 }
             }
         }
@@ -2132,7 +2146,7 @@ __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView b
         uint32_t pre[KB], rank[KB], total = 0;
 #pragma unroll
         for (int q = 0; q < KB; q++) {
-            slow[q] = base + threadIdx.x + (uint64_t)q * NT < end &&
+            slow[q] = base + threadIdx.x + (uint64_t)q * NT < end && (cntw < 0 || t0[q] != EMPTY) &&
                       !block_gate(lf + (uint32_t)(bloom_block(t0[q], bf.nblocks) - blk0) * BF_BLOCK_WORDS + 8, t0[q],
                                   bf.nh);
             const uint64_t bal = __ballot(slow[q]);
@@ -2151,8 +2165,8 @@ __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView b
             if (lane < total - r0) {
                 const uint64_t t = wq[lane];
                 const uint32_t lb = (uint32_t)(bloom_block(t, bf.nblocks) - blk0);
-                block_insert(lf + lb * BF_BLOCK_WORDS, t, bf.nh, bl);
-                if (cntw >= 0 && wf[lane]) block_insert(lf + lb * BF_BLOCK_WORDS, t, bf.nh, bl);  // its second sighting
+                block_insert(lf + lb * BF_BLOCK_WORDS, t, bf.nh, bl, cntw >= 0);
+                if (cntw >= 0 && wf[lane]) block_insert(lf + lb * BF_BLOCK_WORDS, t, bf.nh, bl, true);  // its second sighting
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // queue reads done before reuse
         }
@@ -2896,7 +2910,7 @@ static hipError_t part_levels23(TableView t, DevCounters* ctr, PartBufs pb, hipS
 
 template <bool SEG>
 static hipError_t launch_b3(BloomView bf, TableView ft, DevCounters* ctr, PartBufs pb, const unsigned long long* gate,
-                            int fresh, hipStream_t s, int is = 1, int cntw = -1) {
+                            int fresh, hipStream_t s, int is = 1, int cntw = -1, int rec_phase = 0) {
     const uint32_t bpr = (uint32_t)(bf.nblocks / ft.R);
     // + wave queues (+ their count flags for records)
     const size_t sm = (size_t)bpr * BF_BLOCK_WORDS * 4 + (size_t)(B3_THREADS / 64) * 64 * (cntw >= 0 ? 12 : 8);
@@ -2904,7 +2918,7 @@ static hipError_t launch_b3(BloomView bf, TableView ft, DevCounters* ctr, PartBu
     hipError_t e = set_smem(k_b3<SEG>, sm);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_b3<SEG>, dim3((unsigned)ft.R), dim3(B3_THREADS), sm, s, bf, bpr, pb, ctr, gate, fresh, is,
-                       cntw);
+                       cntw, rec_phase);
     return hipGetLastError();
 }
 
@@ -3222,9 +3236,10 @@ static hipError_t insert_items_part(const uint64_t* items, uint64_t n, TableView
 }
 
 
-// Bloom pass 1 over pre-aggregated {key, count} records (kc_bloom_records_device, the owner
-// side of the sharded Bloom filter): the exact levels move whole records into the filter's
-// regions (ft), k_b3 inserts each record once, twice when its count is >= 2
+// Bloom pass 1 over pre-aggregated {key, count} records of distinct keys (kc_bloom_records_device,
+// the owner side of the sharded Bloom filter): the exact levels move whole records into the
+// filter's regions (ft); k_b3 inserts the records of count >= 2 twice, then (a second launch) the
+// others once
 template <int W>
 static hipError_t bloom_records_w(const uint64_t* rec, uint64_t n, BloomView bf, TableView ft, DevCounters* ctr,
                                   PartBufs pb, int fresh, hipStream_t s) {
@@ -3241,7 +3256,9 @@ static hipError_t bloom_records_w(const uint64_t* rec, uint64_t n, BloomView bf,
     hipLaunchKernelGGL((k_p1k<IW, true>), dim3(pb.nblk1), dim3(COUNT_THREADS), sm1, s, rec, n, pb, ft.F1, bin, ctr, -2,
                        DevN{}, IW);
     if ((e = part_level2_exact<IW>(ft, pb, s, nullptr)) != hipSuccess) return e;
-    return launch_b3<false>(bf, ft, ctr, pb, nullptr, fresh, s, IW, W);
+    // the k-mers seen at least twice first (filters 1 and 2), then the singletons
+    if ((e = launch_b3<false>(bf, ft, ctr, pb, nullptr, fresh, s, IW, W, 0)) != hipSuccess) return e;
+    return launch_b3<false>(bf, ft, ctr, pb, nullptr, 0, s, IW, W, 1);
 }
 
 // the counting pass over {key, count} records behind the gate (kc_count_records_device): the

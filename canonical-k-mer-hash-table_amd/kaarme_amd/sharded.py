@@ -213,6 +213,9 @@ class DeviceEngine:
         # receives are region-sorted groups, merged in one pass (kc_insert_counts_runs_device)
         self.same_geometry = local.table_slots == cfg.table_slots
         self.owner = None               # created on first use
+        self._agg = None                # sharded Bloom: the owner's aggregation table
+        self._agg_slots = 0
+        self._uniq, self._nuniq = None, 0
         self.W = words_for_k(cfg.k)
         self.device = "cuda"
         self._buf = None
@@ -277,14 +280,39 @@ class DeviceEngine:
     def bloom(self, dev_ptr: int, chunks, fmt: int, stream: int = 0):
         self.kc.count_device(dev_ptr, chunks, fmt, stream)
 
+    def _distinct_records(self, recs, n: int, stream: int = 0):
+        """The received records with every key once (the senders' records of one k-mer summed):
+        kc_bloom_records_device takes distinct keys.  An aggregation table (kc_insert_counts_device)
+        read back as records (kc_route_table_device, one part)."""
+        import dataclasses
+
+        import torch
+
+        need = max(1 << 16, n)
+        if self._agg is None or self._agg_slots < need:
+            if self._agg is not None:
+                self._agg.close()
+            self._agg_slots = need + need // 4
+            self._agg = KmerCounter(dataclasses.replace(self.cfg, bf_enable=False, table_slots=self._agg_slots))
+        else:
+            self._agg.clear_table()
+        self._agg.insert_counts_device(recs.data_ptr(), n, stream)
+        R = self.W + 1
+        out = torch.empty(max(1, n) * R, dtype=torch.int64, device="cuda")
+        m = self._agg.route_table_device(1, out.data_ptr(), max(1, n), stream)[0]
+        return out, m
+
     def bloom_records(self, recs, n: int, stream: int = 0):
-        self.owner_table().bloom_records_device(recs.data_ptr(), n, stream)
+        self._uniq, self._nuniq = self._distinct_records(recs, n, stream)
+        self.owner_table().bloom_records_device(self._uniq.data_ptr(), self._nuniq, stream)
 
     def owner_bloom_finalize(self) -> int:
         return self.owner_table().bloom_finalize()
 
     def count_records(self, recs, n: int, stream: int = 0):
-        self.owner_table().count_records_device(recs.data_ptr(), n, stream)
+        """(the distinct records of the preceding bloom_records)"""
+        self.owner_table().count_records_device(self._uniq.data_ptr(), self._nuniq, stream)
+        self._uniq = None
 
     def reset(self):
         self.kc.reset()
@@ -295,6 +323,8 @@ class DeviceEngine:
         self.kc.close()
         if self.owner is not None:
             self.owner.close()
+        if self._agg is not None:
+            self._agg.close()
 
 
 class ShardedCounter:

@@ -209,13 +209,14 @@ int kc_bloom_estimate(kc_ctx* ctx, uint64_t* distinct_in_second, void* hip_strea
  * passes of a Bloom job over pre-aggregated records {W table-key words, raw count} -- what
  * kc_route_table_device writes from an ungated local count and the exchange delivers to the
  * k-mers' owner -- on the owner's context (its filter sized for its 1/G share of -u):
- *   kc_bloom_records_device   Bloom pass 1 (before kc_bloom_finalize): insertion_process
- *                             (double_bloomfilter.hpp:371-413) once per record, twice for a
- *                             record of count >= 2 -- the filter updates of a k-mer seen at
- *                             least twice -- so that, whatever the records' split over the
- *                             senders, a k-mer seen twice in the whole input sets its filter-2
- *                             bits and a k-mer seen once is gated exactly as by one filter
- *                             (parallel_parser.hpp:2788-2940 over the whole input);
+ *   kc_bloom_records_device   Bloom pass 1 (before kc_bloom_finalize) over records of
+ *                             DISTINCT keys (the senders' records of one k-mer summed first:
+ *                             kaarme_amd.sharded aggregates them in a table): insertion_process
+ *                             (double_bloomfilter.hpp:371-413) twice for a record of count >= 2
+ *                             -- a k-mer seen at least twice sets its filter-2 bits -- then once
+ *                             for every record of count 1, as in one sequential order of the
+ *                             reference's pass (parallel_parser.hpp:2788-2940), so a singleton
+ *                             meets one filter;
  *   kc_count_records_device   the counting pass (after kc_bloom_finalize, which sizes the table
  *                             2 * new_in_second, main.cpp:454): adds each record's count when
  *                             its filter-2 bits pass the gate (parallel_parser.hpp:2436-2453);

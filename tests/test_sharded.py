@@ -128,19 +128,27 @@ class NumpyEngine:
                 self.kc.table.update(canonical_windows(line, self.k))
 
     def bloom_records(self, recs, n, stream=0):
+        # the senders' records of one k-mer summed (DeviceEngine._distinct_records), then the
+        # k-mers seen at least twice (inserted twice) before the singletons (once)
+        agg = collections.Counter()
         for row in self._rows(recs, n):
-            ws = [int(x) for x in row[:self.W]]
-            for _ in range(min(2, int(row[self.W]))):  # a record of count >= 2: inserted twice
-                self._insert(ws)
+            agg[tuple(int(x) for x in row[:self.W])] += int(row[self.W])
+        self._uniq = agg
+        for ws, c in agg.items():
+            if c >= 2:
+                self._insert(list(ws))
+                self._insert(list(ws))
+        for ws, c in agg.items():
+            if c == 1:
+                self._insert(list(ws))
 
     def owner_bloom_finalize(self):
         return self.new_in_second
 
     def count_records(self, recs, n, stream=0):
-        for row in self._rows(recs, n):
-            ws = [int(x) for x in row[:self.W]]
-            if self._has(bloom_positions(ws, self.NBLOCKS, self.NH)[: self.NH_GATE], 8):
-                self.owner.table[from_words(row[:self.W], self.k)] += int(row[self.W])
+        for ws, c in self._uniq.items():
+            if self._has(bloom_positions(list(ws), self.NBLOCKS, self.NH)[: self.NH_GATE], 8):
+                self.owner.table[from_words(np.array(ws, dtype=np.uint64), self.k)] += c
 
     def count(self, dev_ptr, chunks, fmt, stream=0):
         for off, ln, _ in chunks:
