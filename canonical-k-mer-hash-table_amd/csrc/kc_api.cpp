@@ -1174,6 +1174,7 @@ int kc_create(const kc_config* cfg, kc_ctx** out) {
                     const uint64_t cap = v ? std::max<uint64_t>(1, std::strtoull(v, 0, 10)) : (1ULL << 16);
                     while (fb > rbits && (1ULL << fb) > cap) fb--;
                     f1 = std::min(fb, std::min(8, (fb + 1) / 2 + 1));
+                    if (const char* vf = std::getenv("KC_FGEO_F1")) f1 = std::min(fb, std::max(1, std::atoi(vf)));  // A/B
                     while (f1 > 0 && p1_lds_bytes(c->W, 1u << f1) > p1_cap) f1--;
                     c->fgeo.R = 1ULL << fb;
                     c->fgeo.f2bits = fb - f1;

@@ -213,7 +213,7 @@ DEV void block_insert(uint32_t* blk, uint64_t t0, int nh, BloomLocal& loc, bool 
             const uint32_t m = 1u << sb_bit(h, j);
             if (!dup[j] && !(f2[j & 7] & m)) mine += !(atomicOr(blk + 8 + (j & 7), m) & m);
         }
-        if (mine == n - s2) loc.new_second++;
+        if (unique || mine == n - s2) loc.new_second++;  // (a distinct key was not in filter 2 before)
     }
 }
 
