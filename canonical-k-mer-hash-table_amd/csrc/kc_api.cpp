@@ -1131,7 +1131,10 @@ int kc_create(const kc_config* cfg, kc_ctx** out) {
             // filter regions of up to BF_BLOCKS_PER_REGION (1024) blocks = 64 KiB, F1 x F2 as
             // for the table (all powers of two here)
             const uint64_t nb = bloom_blocks(c->bf_bits);
-            const uint64_t R = std::max<uint64_t>(1, nb / 1024);
+            // (KC_BF_REGION_BLOCKS: A/B of smaller filter regions, more k_b3 workgroups per CU)
+            const char* vr = std::getenv("KC_BF_REGION_BLOCKS");
+            const uint64_t rb = vr ? std::max<uint64_t>(16, std::min<uint64_t>(1024, std::strtoull(vr, 0, 10))) : 1024;
+            const uint64_t R = std::max<uint64_t>(1, nb / rb);
             int rbits = 0;
             while ((1ULL << rbits) < R) rbits++;
             const int f1bits = std::min(10, (rbits + 1) / 2);
@@ -1301,15 +1304,16 @@ int kc_bloom_finalize(kc_ctx* c, uint64_t* new_in_second) {
         HIPCHK(c, hipStreamSynchronize(c->stream));
         return KC_OK;
     }
-    // The counting pass from the kept partitions can redo itself into the reference-sized
-    // table (count_reused: a region that overflowed), so its table is sized for the k-mers the
-    // gate passes -- new_in_second (~ the k-mers seen twice) plus 30 % for the singletons the
-    // filter lets through -- instead of the reference's 2 * new_in_second (C3: 2^15 instead of
-    // 2^16 regions, 2.1 GB less to write).  KC_BF_TABLE=reference keeps 2 * new_in_second.
+    // KC_BF_TABLE=fit: the counting pass from the kept partitions, which can redo itself into the
+    // reference-sized table (count_reused: a region that overflowed), takes a table sized for the
+    // k-mers the gate passes -- new_in_second plus 30 % -- instead of the reference's
+    // 2 * new_in_second.  Not the default: C3's 2^15 instead of 2^16 regions write 2.1 GB less but
+    // give the gated level 3 half the workgroups, twice the keys each (7.4 vs 5.5 ms,
+    // profiles/r04_ab6.txt).  KC_BF_TABLE=tiny (tests) forces the redo.
     uint64_t phys = 0;
     {
         const char* v = std::getenv("KC_BF_TABLE");
-        if (reuse && !(v && !std::strcmp(v, "reference")))
+        if (reuse && v && !std::strcmp(v, "fit"))
             phys = std::min<uint64_t>(slots, h.new_in_second + h.new_in_second * 3 / 10);
         if (reuse && v && !std::strcmp(v, "tiny")) phys = std::max<uint64_t>(64, h.new_in_second / 8);  // (tests)
     }

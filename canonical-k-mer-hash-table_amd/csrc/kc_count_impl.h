@@ -2053,7 +2053,10 @@ __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView b
     // records are distinct keys; rec_phase 0 inserts those of count >= 2, rec_phase 1 (a later
     // launch) those of count 1, with the distinct-key rule of block_insert: the order "the
     // k-mers seen twice first", one sequential order of the reference's pass
-    constexpr int NT = B3_THREADS, KB = 4;  // (8 or 2 keys per round: slower, r02_v21_ab_b3_kb.txt)
+#ifndef KC_B3_KB
+#define KC_B3_KB 4
+#endif
+    constexpr int NT = B3_THREADS, KB = NT >= 1024 ? 2 : KC_B3_KB;  // (8 or 2 keys per round at 512: slower, r02_v21)
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ uint32_t s_pre[MAX_SEG_GROUP + 1];
     if constexpr (SEG) {
