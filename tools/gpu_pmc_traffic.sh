@@ -12,7 +12,7 @@ i=0
 for grp in FETCH_SIZE WRITE_SIZE; do
   i=$((i+1))
   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 240 rocprofv3 --pmc $grp -d "$OUT/pmc$i" -o run --output-format csv -- \
-      python3 "$ROOT/bench.py" --no-cpu-baseline --steps 3 --warmup 1 "$@" > "$OUT/pmc$i.json" 2> "$OUT/pmc$i.err") || exit $?
+      python3 "$ROOT/bench.py" --no-cpu-baseline --no-writer --steps 3 --warmup 1 "$@" > "$OUT/pmc$i.json" 2> "$OUT/pmc$i.err") || exit $?
 done
 python3 "$ROOT/profiles/pmc_summary.py" "$OUT" --write "$ROOT/profiles/pmc_traffic.json" > "$OUT/summary.txt" && \
 cp "$ROOT/profiles/pmc_traffic.json" "$ROOT/gpurun_out/pmc_traffic.json"
