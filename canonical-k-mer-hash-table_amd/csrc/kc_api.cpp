@@ -102,6 +102,11 @@ struct kc_ctx {
     uint64_t* d_roff = nullptr;
     uint64_t* d_rbsum = nullptr;
     uint64_t r_cap = 0;
+    // kc_route_hint: the level-3 passes keep d_rhist for own_parts owners (PartBufs.own_hist);
+    // own_valid = it holds the table's current per-block record counts
+    uint32_t own_parts = 0;
+    bool own_valid = false;
+    uint64_t route_counts_kept = 0;  // kc_route_table_device calls that skipped the count pass
     // kc_insert_counts_runs_device: group offsets, region run starts / lengths
     uint64_t* d_gstart = nullptr;
     uint64_t* d_mstart = nullptr;
@@ -220,6 +225,50 @@ static uint64_t bloom_words(const kc_ctx* c) {
 
 static int alloc_regions(kc_ctx* c);
 
+// kc_route_table_device's buffers for n = parts x blocks entries (d_rhist moves: the level-3
+// passes' pointer follows it and the kept counts are gone)
+static int route_bufs(kc_ctx* c, uint64_t n) {
+    if (n <= c->r_cap) return KC_OK;
+    hipFree(c->d_rhist);
+    hipFree(c->d_roff);
+    hipFree(c->d_rbsum);
+    c->d_rhist = nullptr;
+    c->d_roff = c->d_rbsum = nullptr;
+    c->r_cap = 0;
+    c->own_valid = false;
+    c->pb.own_hist = c->pbf.own_hist = nullptr;
+    c->pb.own_parts = c->pbf.own_parts = 0;
+    if (hipMalloc(&c->d_rhist, n * 4) != hipSuccess || hipMalloc(&c->d_roff, (n + 1) * 8) != hipSuccess ||
+        hipMalloc(&c->d_rbsum, ((n + 4095) / 4096 + 2) * 8) != hipSuccess)
+        return c->fail(KC_ERR_NOMEM, "route buffers allocation failed");
+    c->r_cap = n;
+    return KC_OK;
+}
+
+// Point the level-3 passes at d_rhist for the table's current geometry (kc_route_hint); the
+// counts are valid again after a fresh level-3 pass (which writes every region)
+static int own_prep(kc_ctx* c) {
+    c->own_valid = false;
+    c->pb.own_hist = c->pbf.own_hist = nullptr;
+    c->pb.own_parts = c->pbf.own_parts = 0;
+    if (!c->own_parts || !c->nbuckets) return KC_OK;
+    const uint64_t nblk = (c->nbuckets + 255) / 256;  // = 2 R (BPR = 512)
+    const int rc = route_bufs(c, c->own_parts * nblk);
+    if (rc) return rc;
+    c->pb.own_hist = c->pbf.own_hist = c->d_rhist;
+    c->pb.own_parts = c->pbf.own_parts = c->own_parts;
+    c->pb.own_nblk = c->pbf.own_nblk = nblk;
+    return KC_OK;
+}
+
+// After a write into the table: the kept per-block counts stay valid through level-3 passes
+// (k_p3 rewrites the counts of every region it writes; a fresh pass writes every region) and
+// are lost by any other writer (direct atomics, the fused pass, the merge inserts)
+static void own_after_write(kc_ctx* c, bool level3, bool fresh) {
+    if (!level3) c->own_valid = false;
+    else if (fresh) c->own_valid = c->pb.own_parts != 0;
+}
+
 // pow2_f1 != 0: R = F1 x F2 with F1 = pow2_f1 (the Bloom filter's coarse bins) and F2 a power
 // of two, so the table's coarse bins are the filter's hash-prefix bins (level-1 reuse)
 // phys_slots != 0: size the device table for that many k-mers instead of min_slots (the
@@ -314,7 +363,7 @@ static int alloc_regions(kc_ctx* c) {
     // table first runs materialize_zero
     c->table_zero_pending = true;
     c->table_fresh = true;
-    return KC_OK;
+    return own_prep(c);
 }
 
 // the fused pass's table: exactly R regions (a power of two), coarse bins = min(f1, R) of them
@@ -684,6 +733,7 @@ static int run_batch(kc_ctx* c, const uint8_t* src, uint64_t used, uint64_t nchu
                 pk.B2 = (uint32_t)(c->fgeo.R / rt) * c->pbf.B2;
                 HIPCHK(c, launch_bloom_count_fused(c->W, bv, table_view(c), c->fgeo, pk, c->d_ctr, c->bloom_fresh, s));
                 c->spec_table = true;
+                own_after_write(c, false, true);
                 c->table_fresh = c->table_zero_pending = false;  // every region written
             } else {
                 HIPCHK(c, launch_bloom_partitioned(sv, c->cfg.k, c->W, bv, c->bgeo, c->fgeo, c->d_ctr, c->pbf,
@@ -712,10 +762,12 @@ static int run_batch(kc_ctx* c, const uint8_t* src, uint64_t used, uint64_t nchu
             HIPCHK(c, launch_count_partitioned(sv, syms, c->cfg.k, mode, tv, bv, c->d_ctr, c->pb, c->table_fresh, s,
                                                PH_TAIL));
         c->table_zero_pending = false;  // the fresh pass wrote every region
+        own_after_write(c, true, c->table_fresh);
     } else {
         if (mode != 1) {
             const int rc = materialize_zero(c, s);
             if (rc) return rc;
+            own_after_write(c, false, false);
         }
         HIPCHK(c, launch_count(sv, syms, c->cfg.k, mode, tv, bv, c->d_ctr, s));
         if (mode == 1) c->bloom_fresh = false;
@@ -863,6 +915,7 @@ static int count_reused(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, s
             return KC_OK;
         }
         HIPCHK(c, launch_spec_commit(c->d_ctr, c->reuse_windows, s));
+        own_after_write(c, false, false);
         if (ev[3]) HIPCHK(c, hipEventRecord(ev[3], s));
         c->spec_table = false;
         c->table_fresh = false;
@@ -931,6 +984,7 @@ static int count_reused(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, s
         release();
         return alloc_table(c, c->min_slots);
     }
+    own_after_write(c, true, c->table_fresh);
     c->table_fresh = false;
     c->table_zero_pending = false;  // the fresh level 3 wrote every region
     c->n_chunks += b.size();
@@ -1463,6 +1517,14 @@ int kc_route_device(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, size_
     return KC_OK;
 }
 
+int kc_route_hint(kc_ctx* c, uint32_t nshards) {
+    if (!c || nshards > RT_MAX_PARTS) return KC_ERR_ARG;
+    int rc = kc_sync(c);  // (the level-3 passes in flight keep the previous pointer)
+    if (rc) return rc;
+    c->own_parts = nshards;
+    return own_prep(c);
+}
+
 int kc_route_table_device(kc_ctx* c, uint32_t nshards, uint64_t* dev_out, uint64_t out_capacity, uint64_t* counts,
                           void* sp) {
     if (!c || !counts || nshards == 0 || nshards > 64) return KC_ERR_ARG;
@@ -1477,18 +1539,9 @@ int kc_route_table_device(kc_ctx* c, uint32_t nshards, uint64_t* dev_out, uint64
     rc = materialize_zero(c, s);
     if (rc) return rc;
     const uint64_t nblk = (c->nbuckets + 255) / 256, n = nshards * nblk;
-    if (n > c->r_cap) {
-        hipFree(c->d_rhist);
-        hipFree(c->d_roff);
-        hipFree(c->d_rbsum);
-        c->d_rhist = nullptr;
-        c->d_roff = c->d_rbsum = nullptr;
-        c->r_cap = 0;
-        if (hipMalloc(&c->d_rhist, n * 4) != hipSuccess || hipMalloc(&c->d_roff, (n + 1) * 8) != hipSuccess ||
-            hipMalloc(&c->d_rbsum, ((n + 4095) / 4096 + 2) * 8) != hipSuccess)
-            return c->fail(KC_ERR_NOMEM, "route buffers allocation failed");
-        c->r_cap = n;
-    }
+    rc = route_bufs(c, n);
+    if (rc) return rc;
+    if (c->own_parts && !c->pb.own_parts) own_prep(c);  // (d_rhist moved: the level-3 passes follow it)
     const TableView tv = table_view(c);
     std::array<hipEvent_t, 4> ev{};
     if (c->profiling) {
@@ -1496,7 +1549,11 @@ int kc_route_table_device(kc_ctx* c, uint32_t nshards, uint64_t* dev_out, uint64
         ev[3] = c->get_event();
         HIPCHK(c, hipEventRecord(ev[2], s));
     }
-    HIPCHK(c, launch_route_table(tv, nshards, c->d_rhist, c->d_roff, c->d_rbsum, nullptr, s));
+    // the level-3 passes kept the per-block counts (kc_route_hint): only their scan runs
+    const bool kept = c->own_valid && nshards == c->own_parts && c->pb.own_hist == c->d_rhist;
+    HIPCHK(c, launch_route_table(tv, nshards, c->d_rhist, c->d_roff, c->d_rbsum, nullptr, s, kept ? 1 : 0));
+    c->route_counts_kept += kept;
+    c->own_valid = nshards == c->own_parts && c->pb.own_hist == c->d_rhist;  // (the counts of this table)
     std::vector<uint64_t> offs(nshards + 1);
     for (uint32_t d = 0; d <= nshards; d++)
         HIPCHK(c, hipMemcpyAsync(&offs[d], c->d_roff + d * nblk, 8, hipMemcpyDeviceToHost, s));
@@ -1550,6 +1607,7 @@ int kc_insert_counts_device(kc_ctx* c, const uint64_t* recs, uint64_t n, void* s
         if (rc) return rc;
     }
     HIPCHK(c, launch_insert_counts(recs, n, part, table_view(c), c->d_ctr, c->pb, c->table_fresh, s));
+    own_after_write(c, false, false);
     c->table_fresh = c->table_zero_pending = false;
     if (c->profiling) {
         HIPCHK(c, hipEventRecord(ev[3], s));
@@ -1619,6 +1677,7 @@ int kc_insert_counts_runs_device(kc_ctx* c, const uint64_t* recs, const uint64_t
     HIPCHK(c, launch_insert_counts_runs(recs, c->d_gstart, ngroups, tv, c->d_ctr, c->d_mlen, c->d_mstart,
                                         c->table_fresh, s));
     // records counted like kc_insert_counts_device: inserted += their counts
+    own_after_write(c, false, false);
     c->table_fresh = c->table_zero_pending = false;
     if (c->profiling) {
         HIPCHK(c, hipEventRecord(ev[3], s));
@@ -1697,6 +1756,7 @@ int kc_count_records_device(kc_ctx* c, const uint64_t* recs, uint64_t n, void* s
         HIPCHK(c, hipEventRecord(ev[2], s));
     }
     HIPCHK(c, launch_count_records(c->W, recs, n, table_view(c), bv, c->d_ctr, c->pb, c->table_fresh, gate ? 1 : 0, s));
+    own_after_write(c, false, false);
     c->table_fresh = c->table_zero_pending = false;
     if (c->profiling) {
         HIPCHK(c, hipEventRecord(ev[3], s));
@@ -1740,6 +1800,7 @@ int kc_insert_keys_device(kc_ctx* c, const uint64_t* keys, uint64_t n, void* sp)
         if (rc) return rc;
     }
     HIPCHK(c, launch_insert_keys(keys, n, part, table_view(c), c->d_ctr, c->pb, c->table_fresh, s));
+    own_after_write(c, false, false);
     c->table_fresh = c->table_zero_pending = false;
     if (c->profiling) {
         HIPCHK(c, hipEventRecord(ev[3], s));
@@ -1794,6 +1855,7 @@ int kc_finish(kc_ctx* c, kc_stats* st) {
         st->heavy_records = h.heavy;
         st->reused_passes = c->reuse_hits;
         st->reuse_level = (uint64_t)c->reuse_last_level;
+        st->route_counts_kept = c->route_counts_kept;
         st->bytes = c->n_bytes;
         // occupied slots
         if (c->nbuckets) {
@@ -1842,6 +1904,7 @@ int kc_clear_table(kc_ctx* c) {
     if (!c->nbuckets) return c->fail(KC_ERR_STATE, "no table");
     c->table_zero_pending = true;  // deferred: see materialize_zero
     c->table_fresh = true;
+    c->own_valid = false;
     return KC_OK;
 }
 
@@ -1852,6 +1915,7 @@ int kc_reset(kc_ctx* c) {
     if (c->d_table) {
         c->table_zero_pending = true;  // deferred: see materialize_zero
         c->table_fresh = true;
+        c->own_valid = false;
     }
     if (c->d_bloom) {
         HIPCHK(c, hipMemsetAsync(c->d_bloom, 0, bloom_words(c) * 4, c->stream));
@@ -1884,6 +1948,7 @@ int kc_reset(kc_ctx* c) {
     c->fgeo_next_R = 0;
     c->reuse_hits = 0;
     c->reuse_last_level = 0;
+    c->route_counts_kept = 0;
     return KC_OK;
 }
 

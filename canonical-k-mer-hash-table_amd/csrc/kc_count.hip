@@ -92,9 +92,9 @@ hipError_t launch_insert_keys(const uint64_t* keys, uint64_t n, bool partitioned
 }
 
 hipError_t launch_route_table(TableView t, uint32_t parts, uint32_t* hist, uint64_t* off, uint64_t* bsum,
-                              uint64_t* out, hipStream_t s) {
+                              uint64_t* out, hipStream_t s, int hist_ready) {
     if (parts == 0 || parts > RT_MAX_PARTS) return hipErrorInvalidValue;
-    KC_DISPATCH_W(t.W, route_table(t, parts, hist, off, bsum, out, s));
+    KC_DISPATCH_W(t.W, route_table(t, parts, hist, off, bsum, out, s, hist_ready));
 }
 
 hipError_t launch_insert_counts(const uint64_t* rec, uint64_t n, bool partitioned, TableView t, DevCounters* ctr,

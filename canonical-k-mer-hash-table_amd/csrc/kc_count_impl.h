@@ -2011,7 +2011,26 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
     stp.mark(1);
     __syncthreads();
     stp.mark(2);
+    // kc_route_hint: the region's records per owner shard for each of its two 256-bucket route
+    // blocks, counted in s_pre (dead once the items are inserted)
+    const uint32_t op = pb.own_parts;
+    static_assert(MAX_SEG_GROUP + 1 >= 2 * RT_MAX_PARTS && BPR == 512, "owner counters in s_pre, two route blocks");
+    if (op)
+        for (uint32_t i = threadIdx.x; i < 2 * RT_MAX_PARTS; i += NT) s_pre[i] = 0;
     for (int i = threadIdx.x; i < N4; i += NT) g4[i] = l4[lds_chunk(i >> 3, i & 7)];
+    if (op) {
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < BPR * S; i += NT) {
+            const uint32_t bb = i / S, sl = i % S;
+            const uint64_t w0 = *lds_word(lt, bb, sl * W);
+            if (w0 != EMPTY) atomicAdd(&s_pre[(bb >= BPR / 2 ? RT_MAX_PARTS : 0) + owner_of(w0, op)], 1u);
+        }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < 2 * op; i += NT) {
+            const uint32_t h = i / op, d = i % op;
+            pb.own_hist[(uint64_t)d * pb.own_nblk + 2 * r + h] = s_pre[h * RT_MAX_PARTS + d];
+        }
+    }
     stp.mark(3);
     if (SEG && !CNT && !GATE) stp.flush(2);
     if (n_fail) atomicAdd(&ctr->overflow, (unsigned long long)n_fail);
@@ -3385,10 +3404,11 @@ hipError_t WOps<W>::insert_keys(const uint64_t* keys, uint64_t n, bool partition
 
 template <int W>
 hipError_t WOps<W>::route_table(TableView t, uint32_t parts, uint32_t* hist, uint64_t* off, uint64_t* bsum,
-                                uint64_t* out, hipStream_t s) {
+                                uint64_t* out, hipStream_t s, int hist_ready) {
     const unsigned nblk = (unsigned)((t.nbuckets + 255) / 256);
     if (!out) {
-        hipLaunchKernelGGL((k_route_table<W, false>), dim3(nblk), dim3(256), 0, s, t, parts, hist, off, out);
+        if (!hist_ready)
+            hipLaunchKernelGGL((k_route_table<W, false>), dim3(nblk), dim3(256), 0, s, t, parts, hist, off, out);
         launch_scan(hist, (uint64_t)parts * nblk, off, bsum, s);
     } else {
         hipLaunchKernelGGL((k_route_table<W, true>), dim3(nblk), dim3(256), 0, s, t, parts, hist, off, out);

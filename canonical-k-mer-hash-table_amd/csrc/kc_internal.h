@@ -130,6 +130,12 @@ struct PartBufs {
     int r12_hb;             // bits of table-key word 1 above 32 (2k - 96, or 0)
     int r12_xb1, r12_xb2;   // bits of t0's top half below the level-1 / level-2 bin
     int r12_b2s;            // log2 of the level-2 segments per bin (fine bin of a segment = segment >> r12_b2s)
+    // kc_route_hint: every level-3 workgroup (k_p3) also writes its region's record counts per
+    // owner shard for the two 256-bucket blocks of kc_route_table_device ([own_parts][own_nblk];
+    // own_parts = 0: off), so the route of a table counted by level 3 skips its count pass
+    uint32_t* own_hist;
+    uint32_t own_parts;
+    uint64_t own_nblk;
 };
 constexpr int R12_P1 = 1, R12_IN = 2, R12_OUT = 4, R12_L2 = 8;
 // R12_REG: the records are in the table's own geometry (the counting pass's levels): a bin's
@@ -266,8 +272,10 @@ hipError_t launch_insert_keys(const uint64_t* keys, uint64_t n, bool partitioned
                               PartBufs pb, int fresh, hipStream_t s);
 // pre-aggregated sharding: out == nullptr -> per-(owner, block) record counts into hist and
 // their exclusive scan into off (off[parts * nblk] = total); else scatter the records
+// out == nullptr: the count pass (per-block record counts into hist, skipped when hist_ready:
+// the counting passes kept them, kc_route_hint) and their scan; else the scatter into out
 hipError_t launch_route_table(TableView t, uint32_t parts, uint32_t* hist, uint64_t* off, uint64_t* bsum,
-                              uint64_t* out, hipStream_t s);
+                              uint64_t* out, hipStream_t s, int hist_ready = 0);
 hipError_t launch_insert_counts(const uint64_t* rec, uint64_t n, bool partitioned, TableView t, DevCounters* ctr,
                                 PartBufs pb, int fresh, hipStream_t s);
 // shard merge of records that arrive as G groups each sorted by this table's region
@@ -321,7 +329,7 @@ struct WOps {
     static hipError_t insert_keys(const uint64_t* keys, uint64_t n, bool partitioned, TableView t, DevCounters* ctr,
                                   PartBufs pb, int fresh, hipStream_t s);
     static hipError_t route_table(TableView t, uint32_t parts, uint32_t* hist, uint64_t* off, uint64_t* bsum,
-                                  uint64_t* out, hipStream_t s);
+                                  uint64_t* out, hipStream_t s, int hist_ready);
     static hipError_t insert_counts(const uint64_t* rec, uint64_t n, bool partitioned, TableView t, DevCounters* ctr,
                                     PartBufs pb, int fresh, hipStream_t s);
     static hipError_t check_runs(const uint64_t* rec, const uint64_t* gstart, uint32_t G, uint64_t maxn, TableView t,

@@ -45,7 +45,7 @@ EXPORTS = (
     "kc_count_chunk", "kc_bloom_device", "kc_count_device", "kc_sync", "kc_finish", "kc_dump",
     "kc_write", "kc_key_words", "kc_free", "kc_plan_chunks", "kc_synth_bytes", "kc_synth_device",
     "kc_reset", "kc_profile", "kc_get_timing", "kc_route_device", "kc_insert_keys_device",
-    "kc_route_table_device", "kc_insert_counts_device", "kc_clear_table", "kc_insert_counts_runs_device",
+    "kc_route_table_device", "kc_route_hint", "kc_insert_counts_device", "kc_clear_table", "kc_insert_counts_runs_device",
     "kc_xxh64", "kc_bloom_info", "kc_bloom_read", "kc_bloom_write", "kc_synth_skew_device",
     "kc_table_size_reference", "kc_bloom_get_device", "kc_bloom_merge_device", "kc_bloom_set_device",
     "kc_bloom_estimate", "kc_compact", "kc_compact_dump", "kc_compact_lookup", "kc_compact_read",
@@ -90,7 +90,7 @@ class kc_stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in (
         "windows", "inserted", "distinct", "table_slots", "bf_windows", "bf_bits", "new_in_first",
         "new_in_second", "failed_in_first", "chunks", "bytes", "part_fallbacks", "spilled", "heavy_records",
-        "reused_passes", "reuse_level")]
+        "reused_passes", "reuse_level", "route_counts_kept")]
 
     def as_dict(self) -> dict:
         return {n: int(getattr(self, n)) for n, _ in self._fields_}
@@ -148,6 +148,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                                   ctypes.POINTER(U64), P]),
         "kc_insert_keys_device": (I32, [P, P, U64, P]),
         "kc_route_table_device": (I32, [P, ctypes.c_uint32, P, U64, P, P]),
+        "kc_route_hint": (I32, [P, ctypes.c_uint32]),
         "kc_insert_counts_device": (I32, [P, P, U64, P]),
         "kc_bloom_records_device": (I32, [P, P, U64, P]),
         "kc_count_records_device": (I32, [P, P, U64, P]),
@@ -371,6 +372,11 @@ class KmerCounter:
         self._chk(self.lib.kc_route_table_device(self._ctx, nshards, ctypes.c_void_p(out_ptr or None), out_capacity,
                                                  counts, ctypes.c_void_p(stream or None)), "kc_route_table_device")
         return [int(x) for x in counts]
+
+    def route_hint(self, nshards: int):
+        """The table will be routed to nshards owners: the counting passes keep the per-block
+        owner counts so route_table_device runs no count pass (include/kc_api.h kc_route_hint)."""
+        self._chk(self.lib.kc_route_hint(self._ctx, nshards), "kc_route_hint")
 
     def bloom_records_device(self, rec_ptr: int, n_records: int, stream: int = 0):
         """Bloom pass 1 over {key, count} records (include/kc_api.h kc_bloom_records_device)."""

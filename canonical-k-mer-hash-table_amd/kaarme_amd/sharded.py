@@ -209,6 +209,8 @@ class DeviceEngine:
         else:
             local = dataclasses.replace(cfg, table_slots=max(cfg.table_slots, local_slots))
         self.kc = KmerCounter(local)    # local table (also used by the per-window route path)
+        if world > 1:  # its level-3 passes keep the per-owner counts the merge's route needs
+            self.kc.route_hint(world)
         # every rank's local table has the owner table's geometry: the records a rank
         # receives are region-sorted groups, merged in one pass (kc_insert_counts_runs_device)
         self.same_geometry = local.table_slots == cfg.table_slots

@@ -90,6 +90,8 @@ typedef struct {
     uint64_t reused_passes;   /* counting passes that started from the Bloom pass's kept partitions */
     uint64_t reuse_level;     /* the partition level the last reused pass started from: 2 (level 3 only),
                                  1 (levels 2-3), 0 = no reuse */
+    uint64_t route_counts_kept; /* kc_route_table_device calls that took the per-block owner counts the
+                                   counting passes kept (kc_route_hint) instead of running a count pass */
 } kc_stats;
 
 /* Creates the device table (PointerHashTableCanonicalAV ctor,
@@ -168,6 +170,14 @@ int kc_insert_keys_device(kc_ctx* ctx, const uint64_t* dev_keys, uint64_t n_keys
  * of the owners' tables is the count of the whole input. */
 int kc_route_table_device(kc_ctx* ctx, uint32_t nshards, uint64_t* dev_out, uint64_t out_capacity,
                           uint64_t* counts, void* hip_stream);
+/* Tells the context that its table will be routed to nshards (1..64) owners (0 = off): every
+ * level-3 pass of the counting pipeline then also writes its region's record counts per owner
+ * (the two 256-bucket blocks the route reads), so a kc_route_table_device(nshards) after
+ * counting passes that all went through level 3 (the partitioned path; not the direct
+ * small-batch path or the merge inserts) runs no count pass over the table -- one streaming
+ * read of the table fewer per merge.  kc_stats.route_counts_kept counts
+ * such routes.  The records and counts are the same either way. */
+int kc_route_hint(kc_ctx* ctx, uint32_t nshards);
 int kc_insert_counts_device(kc_ctx* ctx, const uint64_t* dev_records, uint64_t n_records, void* hip_stream);
 /* The same for records that arrive as ngroups (<= 64) consecutive groups of
  * group_counts[g] records (host array), one per sending rank, each in the order

@@ -398,3 +398,91 @@ def test_sharded_bloom_excess_at_design_load(tmp_path, G):
     assert excess <= 1.5 * excess1 + 0.005, (excess, excess1)
     for e in engines:
         e.close()
+
+
+def _routed_groups(kc, G):
+    """kc_route_table_device's records, each owner's group as a sorted array."""
+    import numpy as np
+
+    counts = kc.route_table_device(G, 0, 0)
+    n = sum(counts)
+    st = kc.finish()
+    W = ka.words_for_k(kc.cfg.k)
+    out = torch.empty(max(1, n) * (W + 1), dtype=torch.int64, device="cuda")
+    counts2 = kc.route_table_device(G, out.data_ptr(), max(1, n))
+    assert counts2 == counts
+    recs = out[: n * (W + 1)].view(-1, W + 1).cpu().numpy()
+    groups, lo = [], 0
+    for c in counts:
+        g = recs[lo:lo + c]
+        groups.append(g[np.lexsort(g.T[::-1])])
+        lo += c
+    return counts, groups, st
+
+
+@pytest.mark.parametrize("k,path,batch_mib", [(31, "partitioned", 0), (31, "partitioned", 8), (51, "partitioned", 0),
+                                               (127, "partitioned", 0), (31, "direct", 0)])
+def test_route_hint_keeps_owner_counts(monkeypatch, k, path, batch_mib):
+    """kc_route_hint: the level-3 passes keep the per-block owner counts, so
+    kc_route_table_device runs no count pass -- and routes the same records as without the hint:
+    one batch (fresh level 3), several batches (level 3 over a written table), after
+    kc_clear_table, a route to another number of owners; the direct path keeps none."""
+    import numpy as np
+
+    monkeypatch.setenv("KC_INSERT_PATH", path)
+    G = 4
+    lib = ka.load_library()
+    N, L = 200_000, 150
+    nbytes = lib.kc_synth_bytes(0, N, L, 0)
+    img = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    assert lib.kc_synth_device(img.data_ptr(), 0, N, 5, 2_000_000, L, 0, 0.002, 0.0, 0) == 0
+    torch.cuda.synchronize()
+    chunks = ka.plan_chunks_device(img.data_ptr(), nbytes, k, ka.FMT_FASTA)
+    cfg = ka.Config(k=k, mode=2, table_slots=6_000_000, min_abundance=1, batch_bytes=batch_mib << 20)
+    with ka.KmerCounter(cfg) as want_kc, ka.KmerCounter(cfg) as kc:
+        kc.route_hint(G)
+        for job in range(2):
+            for c in (want_kc, kc):
+                if job:
+                    c.clear_table()
+                c.count_device(img.data_ptr(), chunks if not job else chunks[: len(chunks) // 2], ka.FMT_FASTA)
+            wc, wg, _ = _routed_groups(want_kc, G)
+            gc, gg, st = _routed_groups(kc, G)
+            assert gc == wc and sum(gc) > 0
+            assert all(np.array_equal(a, b) for a, b in zip(gg, wg))
+            # (two routes per job: the count-only call and the scatter)
+            assert st["route_counts_kept"] == (2 * (job + 1) if path == "partitioned" else 0), st
+        # another owner count: the count pass runs, the records are the same
+        wc3, wg3, _ = _routed_groups(want_kc, 3)
+        gc3, gg3, st3 = _routed_groups(kc, 3)
+        assert gc3 == wc3 and all(np.array_equal(a, b) for a, b in zip(gg3, wg3))
+        assert st3["route_counts_kept"] == st["route_counts_kept"]
+
+
+def test_route_hint_bloom_job_from_kept_partitions(monkeypatch):
+    """A Bloom job whose counting pass runs from the Bloom pass's kept partitions (its fresh gated
+    level 3) keeps the owner counts too; the same records as without the hint."""
+    import numpy as np
+
+    monkeypatch.setenv("KC_INSERT_PATH", "partitioned")
+    G, k = 2, 51
+    lib = ka.load_library()
+    N, L = 200_000, 150
+    nbytes = lib.kc_synth_bytes(0, N, L, 0)
+    img = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    assert lib.kc_synth_device(img.data_ptr(), 0, N, 6, 2_000_000, L, 0, 0.002, 0.0, 0) == 0
+    torch.cuda.synchronize()
+    chunks = ka.plan_chunks_device(img.data_ptr(), nbytes, k, ka.FMT_FASTA)
+    cfg = ka.Config(k=k, mode=2, min_abundance=2, bf_enable=True, est_unique=6_000_000, fpr=0.01)
+    res = []
+    for hint in (False, True):
+        with ka.KmerCounter(cfg) as kc:
+            if hint:
+                kc.route_hint(G)
+            kc.bloom_device(img.data_ptr(), chunks, ka.FMT_FASTA)
+            kc.bloom_finalize()
+            kc.count_device(img.data_ptr(), chunks, ka.FMT_FASTA)
+            res.append(_routed_groups(kc, G))
+    (wc, wg, _), (gc, gg, st) = res
+    assert st["reused_passes"] == 1 and st["route_counts_kept"] == 2, st
+    assert gc == wc and all(np.array_equal(a, b) for a, b in zip(gg, wg))
