@@ -406,11 +406,11 @@ def _routed_groups(kc, G):
 
     counts = kc.route_table_device(G, 0, 0)
     n = sum(counts)
-    st = kc.finish()
     W = ka.words_for_k(kc.cfg.k)
     out = torch.empty(max(1, n) * (W + 1), dtype=torch.int64, device="cuda")
     counts2 = kc.route_table_device(G, out.data_ptr(), max(1, n))
     assert counts2 == counts
+    st = kc.finish()
     recs = out[: n * (W + 1)].view(-1, W + 1).cpu().numpy()
     groups, lo = [], 0
     for c in counts:
