@@ -437,7 +437,7 @@ def test_route_hint_keeps_owner_counts(monkeypatch, k, path, batch_mib):
     img = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
     assert lib.kc_synth_device(img.data_ptr(), 0, N, 5, 2_000_000, L, 0, 0.002, 0.0, 0) == 0
     torch.cuda.synchronize()
-    chunks = ka.plan_chunks_device(img.data_ptr(), nbytes, k, ka.FMT_FASTA)
+    chunks = ka.plan_chunks_device(img.data_ptr(), nbytes, k, ka.FMT_FASTA, chunk_size=1 << 20)
     cfg = ka.Config(k=k, mode=2, table_slots=6_000_000, min_abundance=1, batch_bytes=batch_mib << 20)
     with ka.KmerCounter(cfg) as want_kc, ka.KmerCounter(cfg) as kc:
         kc.route_hint(G)
