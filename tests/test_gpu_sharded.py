@@ -450,8 +450,9 @@ def test_route_hint_keeps_owner_counts(monkeypatch, k, path, batch_mib):
             gc, gg, st = _routed_groups(kc, G)
             assert gc == wc and sum(gc) > 0
             assert all(np.array_equal(a, b) for a, b in zip(gg, wg))
-            # (two routes per job: the count-only call and the scatter)
-            assert st["route_counts_kept"] == (2 * (job + 1) if path == "partitioned" else 0), st
+            # two routes per job (the count-only call and the scatter): after level 3 both take the
+            # kept counts; after the direct path the first runs the count pass, which the second reuses
+            assert st["route_counts_kept"] == (2 if path == "partitioned" else 1) * (job + 1), st
         # another owner count: the count pass runs, the records are the same
         wc3, wg3, _ = _routed_groups(want_kc, 3)
         gc3, gg3, st3 = _routed_groups(kc, 3)
