@@ -54,7 +54,7 @@ from . import Config, KmerCounter, words_for_k
 # GPU cannot host two RCCL ranks, so the observation is unconfirmed.  Big exchanges therefore
 # go in rounds of at most this many words per peer, and every exchange checks per-peer sums of
 # what arrived (`verify`) so that a short or corrupt delivery raises instead of miscounting.
-EXCHANGE_CHUNK_WORDS = 1 << 24
+EXCHANGE_CHUNK_WORDS = 1 << 25  # 256 MB: a C2 rank's records to each of 8 peers (~173 MB) in one round
 
 
 def chunk_words_default() -> int:
