@@ -161,7 +161,10 @@ inline int slots_per_bucket(int W) { return BUCKET_WORDS / (W + 1); }
 // Windows rolled per thread in the partitioned kernels, and the workgroup size of the
 // segmented level 1 (tile = threads x windows), by key width: wide keys take fewer
 // windows per thread and smaller groups so that the registers and the LDS tile fit.
-constexpr int run_width(int W) { return W == 1 ? 16 : W == 2 ? 8 : W <= 4 ? 8 : 4; }
+#ifndef KC_RUNW1
+#define KC_RUNW1 16  // (A/B knob: one-word keys' windows per thread)
+#endif
+constexpr int run_width(int W) { return W == 1 ? KC_RUNW1 : W == 2 ? 8 : W <= 4 ? 8 : 4; }
 // The segmented level 1 (k_p1) of one- and two-word keys: 512-thread workgroups, two per CU.
 // (1024 threads with half the windows per thread -- 8 waves per SIMD within 64 VGPRs -- spill
 // and ran 30 % slower: profiles/r03_ab_p1_nt.txt)
