@@ -172,7 +172,12 @@ constexpr int run_width(int W) { return W == 1 ? KC_RUNW1 : W == 2 ? 8 : W <= 4 
 #define KC_P1_NT12 512
 #endif
 constexpr int scatter_threads_w(int W) { return W <= 2 ? KC_P1_NT12 : W <= 4 ? 512 : 256; }
-constexpr int p1_runw(int W) { return W <= 2 ? run_width(W) * 512 / KC_P1_NT12 : run_width(W); }
+#ifndef KC_P1_RUNW1
+#define KC_P1_RUNW1 KC_RUNW1  // (A/B knob: the segmented level 1's one-word windows per thread)
+#endif
+constexpr int p1_runw(int W) {
+    return W == 1 ? KC_P1_RUNW1 * 512 / KC_P1_NT12 : W <= 2 ? run_width(W) * 512 / KC_P1_NT12 : run_width(W);
+}
 constexpr int p1_tile(int W) { return scatter_threads_w(W) * p1_runw(W); }  // windows per segmented level-1 tile
 // level 2 (k_p2f): workgroup size by key width, and its LDS for F2 regions per coarse bin
 #ifndef KC_P2F_NT
