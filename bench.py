@@ -440,6 +440,8 @@ def run_workload(args, env, image=None):
     N, nbytes, strong, workload, tbl = job.N, job.nbytes, job.strong, job.workload, job.tbl
     windows_expected = job.windows_expected
     L, k = args.read_len, args.k
+    if rank == 0:  # progress on stderr (a long setup / digest is not a hang)
+        log(f"{args.config}: job ready ({nbytes} image bytes, {len(chunks)} chunks); warmup")
     for _ in range(args.warmup):
         step()
     counter.profile(True)
@@ -470,8 +472,13 @@ def run_workload(args, env, image=None):
                 "gbs_per_rank": round(sent / max(xsec, 1e-9) / 1e9, 2), "peak_gbs_per_gpu": 7 * 153,
                 "note": "max over ranks; the all-to-all of {key, count} records incl. its count/sum headers"}
     st = counter.finish()  # raises on table overflow
+    if rank == 0:
+        log(f"{args.config}: {args.steps} steps in {elapsed:.3f} s; parity / writer records")
     parity = parity_record(job, k) if args.verify else None
-    writer = writer_record(job, args.verify) if (args.writer and not dist and job.fixture is not None) else None
+    # (the text writer and its sorted-file digest for outputs up to ~8 GB: C2 / C3; a strong
+    # share's 30 GB of text would take minutes to sort)
+    writer = writer_record(job, args.verify) if (args.writer and not dist and job.fixture is not None and
+                                                 job.fixture["lines"] * (k + 8) < 8e9) else None
     compact = None
     if not dist and args.compact:  # the Kaarme slot words built from this table
         torch.cuda.synchronize()

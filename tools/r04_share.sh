@@ -4,5 +4,5 @@
 set -o pipefail
 mkdir -p gpurun_out
 for c in C4 C5; do
-  timeout -k 10 400 python bench.py --config $c --share 8 --no-cpu-baseline > gpurun_out/r04_share_$c.json 2> gpurun_out/r04_share_$c.err || exit 1
+  timeout -k 10 400 python bench.py --config $c --share 8 --no-cpu-baseline --no-writer > gpurun_out/r04_share_$c.json 2> gpurun_out/r04_share_$c.err || exit 1
 done
