@@ -1607,10 +1607,16 @@ DEV uint32_t zero_byte_mask8(uint64_t x) {
 // Exclusive prefix of a level-3 workgroup's n <= MAX_SEG_GROUP segment fills (s_pre[0..n],
 // s_pre[n] = total), by the first wave: two fills per lane, one DPP scan (was a one-thread loop
 // of n dependent-looking loads, ~n HBM latencies at every workgroup's start)
+// (PAIRS: of the segments' record pairs, ceil(fill / 2))
+template <bool PAIRS = false>
 DEV void seg_prefix(uint32_t* s_pre, const uint32_t* __restrict__ fill, uint32_t n) {
     if (threadIdx.x < 64) {
         const uint32_t j = 2 * threadIdx.x;
-        const uint32_t a = j < n ? fill[j] : 0, b = j + 1 < n ? fill[j + 1] : 0;
+        uint32_t a = j < n ? fill[j] : 0, b = j + 1 < n ? fill[j + 1] : 0;
+        if (PAIRS) {
+            a = (a + 1) >> 1;
+            b = (b + 1) >> 1;
+        }
         const uint32_t inc = wave_incl_sum(a + b);
         const uint32_t ex = inc - (a + b);
         if (j < n) s_pre[j] = ex;
@@ -1630,6 +1636,59 @@ DEV void seg_prefix(uint32_t* s_pre, const uint32_t* __restrict__ fill, uint32_t
 // contiguous slice of the filter (bloom_block and region_of share the hash prefix), so
 // the gate reads stay within a few KiB that L2 keeps.
 constexpr int P3_THREADS = 1024;  // two 64 KiB regions per CU: 8 waves per SIMD
+
+// One one-word key into the region's LDS table with 8-bit slot tags (the KC_P3_TAGS probe of
+// k_p3, for its record-pair path): returns false if the region is full.
+DEV bool p3_insert_tagged1(uint64_t* lt, uint64_t* tg, uint64_t R, uint64_t k0) {
+    constexpr int S = BUCKET_WORDS / 2;
+    constexpr uint32_t SMASK = (1u << S) - 1;
+    uint32_t b = bucket_in_region(k0, R);
+    const uint32_t tag = slot_tag(k0);
+    const uint64_t bc = 0x0101010101010101ULL * tag;
+    for (int probe = 0; probe < 4 * BPR;) {
+        const uint64_t tw = tg[b];
+        uint32_t m = zero_byte_mask8(tw ^ bc) & SMASK;
+        int slot = -1;
+        while (m) {
+            const int sl = __builtin_ctz(m);
+            m &= m - 1;
+            if (*lds_word(lt, b, sl) == k0) {
+                slot = sl;
+                break;
+            }
+        }
+        if (slot < 0) {
+            const uint32_t em = zero_byte_mask8(tw) & SMASK;
+            if (!em) {
+                b = (b + 1) & (BPR - 1);
+                probe++;
+                continue;
+            }
+            const int e = __builtin_ctz(em);
+            const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long*>(lds_word(lt, b, e)), 0ULL,
+                                           (unsigned long long)k0);
+            if (old == EMPTY) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __hip_atomic_store(reinterpret_cast<uint8_t*>(tg + b) + e, (uint8_t)tag, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+                slot = e;
+            } else if (old == k0) {
+                slot = e;
+            } else {
+                probe++;
+                continue;
+            }
+        }
+        atomicAdd(reinterpret_cast<unsigned long long*>(lds_word(lt, b, S + slot)), 1ULL);
+        return true;
+    }
+    return false;
+}
+// k_p3's 6-byte records read as whole pairs (one 12-byte load per two keys, KC_P3_PAIRS pairs per
+// thread and round, the next round's loads issued before this round's inserts); 0 = per record
+#ifndef KC_P3_PAIRS
+#define KC_P3_PAIRS 0
+#endif
 // REC6: the segments hold 6-byte level-2 records (StoreRec6; one-word keys, SEG, not CNT)
 template <int W, bool SEG, bool CNT, bool GATE = false, bool REC6 = false>
 __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView tv, PartBufs pb,
@@ -1654,8 +1713,10 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
     uint64_t* tg = lt + BPR * BUCKET_WORDS;             // KC_P3_TAGS: BPR tag words
     const uint64_t r = blockIdx.x;
     uint64_t start, end;
+    // PAIRS: s_pre holds the prefix of the segments' record pairs (zero iff no record)
+    constexpr bool PAIRS = REC6 && !GATE && KC_P3_TAGS && KC_P3_PAIRS > 0;
     if constexpr (SEG) {
-        seg_prefix(s_pre, pb.hist2 + r * pb.B2, pb.B2);
+        seg_prefix<PAIRS>(s_pre, pb.hist2 + r * pb.B2, pb.B2);
         __syncthreads();
         start = 0;
         end = s_pre[pb.B2];
@@ -1803,11 +1864,63 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
             else add[q] = 1;
         }
     };
+    if constexpr (PAIRS) {
+        constexpr int PB = KC_P3_PAIRS > 0 ? KC_P3_PAIRS : 1;
+        const uint32_t np = s_pre[pb.B2];
+        uint32_t pcs = 0, pcb = 0, pnb = s_pre[1];  // pair cursor: segment pcs holds pairs [pcb, pnb)
+        uint32_t pfill = np ? pb.hist2[r * pb.B2] : 0;  // records of segment pcs
+        auto load_pairs = [&](uint32_t base, uint3 (&v)[PB], uint32_t& m) {  // m: bit 2q even / 2q+1 odd valid
+            m = 0;
+#pragma unroll
+            for (int q = 0; q < PB; q++) {
+                const uint32_t i = base + threadIdx.x + q * NT;
+                v[q] = make_uint3(0, 0, 0);
+                if (i < np) {
+                    if (pnb <= i) {
+                        do {
+                            pcs++;
+                            pcb = pnb;
+                            pnb = s_pre[pcs + 1];
+                        } while (pnb <= i);
+                        pfill = pb.hist2[r * pb.B2 + pcs];
+                    }
+                    const uint32_t po = i - pcb;
+                    v[q] = reinterpret_cast<const uint3*>(pb.keys2)[((r * pb.B2 + pcs) * pb.cap2 >> 1) + po];
+                    m |= (1u | (2 * po + 1 < pfill ? 2u : 0u)) << (2 * q);
+                }
+            }
+        };
+        uint3 v[PB];
+        uint32_t m = 0;
+        if (np) load_pairs(0, v, m);
+        for (uint32_t base = 0; base < np; base += PB * NT) {
+            uint3 nv[PB];
+            uint32_t nm = 0;
+            const bool more = base + PB * NT < np;
+            if (more) load_pairs(base + PB * NT, nv, nm);
+#pragma unroll
+            for (int q = 0; q < PB; q++) {
+                if ((m >> (2 * q)) & 1) {
+                    const uint64_t k0 = ((uint64_t)(xlo_r + (v[q].z & 0xFFFFu)) << 32) | v[q].x;
+                    if (!p3_insert_tagged1(lt, tg, tv.R, k0)) n_fail++;
+                }
+                if ((m >> (2 * q + 1)) & 1) {
+                    const uint64_t k1 = ((uint64_t)(xlo_r + (v[q].z >> 16)) << 32) | v[q].y;
+                    if (!p3_insert_tagged1(lt, tg, tv.R, k1)) n_fail++;
+                }
+            }
+            if (more) {
+                m = nm;
+#pragma unroll
+                for (int q = 0; q < PB; q++) v[q] = nv[q];
+            }
+        }
+    }
     uint64_t kk[KB][W];
     uint64_t add[KB];
     uint32_t okm = 0;
-    if (start < vend) load_items(start, kk, add, okm);
-    for (uint64_t base = start; base < vend; base += (uint64_t)KB * NT) {
+    if (!PAIRS && start < vend) load_items(start, kk, add, okm);
+    for (uint64_t base = start; !PAIRS && base < vend; base += (uint64_t)KB * NT) {
         // the next items' loads are issued before this batch's inserts
         uint64_t nkk[KB][W];
         uint64_t nadd[KB];
