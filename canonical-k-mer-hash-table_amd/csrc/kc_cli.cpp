@@ -558,10 +558,21 @@ int main(int argc, char** argv) {
                   << std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0).count() << " microseconds\n";
     }
     std::cout << "Starting " << (a.mode == 0 ? "atomic flag basic" : "atomic variable pointer") << " hash table\n";
+    const bool dbg = std::getenv("KC_CLI_DEBUG") != nullptr;  // phase times on stderr
+    auto us = [](clk::time_point x, clk::time_point y) {
+        return (long long)std::chrono::duration_cast<std::chrono::microseconds>(y - x).count();
+    };
     auto t0 = clk::now();
     load();
+    auto tl = clk::now();
     if (d_img) {
         if (kc_count_device(ctx, d_img, chunks, nch, fmt, nullptr) != KC_OK) die("counting pass");
+        if (dbg) {
+            auto tc = clk::now();
+            (void)kc_sync(ctx);
+            std::cerr << "cli: load " << us(t0, tl) << " us, count call " << us(tl, tc) << " us, its work "
+                      << us(tc, clk::now()) << " us\n";
+        }
     } else {
         for (uint64_t i = 0; i < nch; i++)
             if (kc_count_chunk(ctx, image + chunks[i].off, chunks[i].len, fmt, chunks[i].broken_header) != KC_OK)
