@@ -1244,12 +1244,6 @@ int kc_create(const kc_config* cfg, kc_ctx** out) {
     } else {
         int rc = alloc_table(c, cfg->table_slots);
         if (rc) return bail(rc, "");
-        // a caller that sized its batch (the CLI: its whole image) gets the batch's partition
-        // buffers now rather than inside its first timed pass (several GB of hipMalloc)
-        const uint64_t syms = c->batch_bytes + c->max_chunks;
-        if (cfg->batch_bytes && !std::getenv("KC_NO_PREALLOC") && use_partitioned(c, syms) &&
-            (rc = ensure_part(c, syms, true)))
-            return bail(rc, "");
     }
     if (hipStreamSynchronize(c->stream) != hipSuccess) return bail(KC_ERR_HIP, "stream sync failed");
     *out = c;

@@ -9,11 +9,9 @@ cat $F > /dev/null
 O=gpurun_out/r04_cli_probe2.txt
 : > $O
 for r in 1 2 3; do
-  for pre in 0 1; do
-    for rd in 2 4; do
-      echo "== no_prealloc=$pre readers=$rd" >> $O
-      env $( [ $pre = 1 ] && echo KC_NO_PREALLOC=1 ) KC_CLI_DEBUG=1 KC_CLI_READERS=$rd timeout -k 10 60 $B/kaarme $F 31 \
-          -m 2 -s 156001000 -a 0 -t 18 2>&1 | grep -E "Time used to build|cli:" >> $O || exit 1
-    done
+  for rd in 2 4; do
+    echo "== readers=$rd" >> $O
+    KC_CLI_DEBUG=1 KC_CLI_READERS=$rd timeout -k 10 60 $B/kaarme $F 31 -m 2 -s 156001000 -a 0 -t 18 \
+        2>&1 | grep -E "Time used to build|cli:" >> $O || exit 1
   done
 done
