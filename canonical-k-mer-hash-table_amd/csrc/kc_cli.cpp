@@ -525,8 +525,10 @@ int main(int argc, char** argv) {
     // as the reference's reader thread is.
     const bool host_path = std::getenv("KC_CLI_HOST") && std::atoi(std::getenv("KC_CLI_HOST")) != 0;
     const char* rv = std::getenv("KC_CLI_READERS");
+    // (two readers: 26-31 ms for the C2 sample's 161 MB against 37-46 ms with four,
+    // profiles/r04_cli_probe_phases.txt)
     const unsigned readers = rv ? (unsigned)std::max(1, std::atoi(rv))
-                                : std::max(1u, std::min(4u, std::thread::hardware_concurrency()));
+                                : std::max(1u, std::min(2u, std::thread::hardware_concurrency()));
     Upload up;
     const bool staged = !host_path && up.prepare(isize, a.device, readers);  // (untimed setup)
     uint8_t* d_img = nullptr;
