@@ -525,10 +525,9 @@ int main(int argc, char** argv) {
     // as the reference's reader thread is.
     const bool host_path = std::getenv("KC_CLI_HOST") && std::atoi(std::getenv("KC_CLI_HOST")) != 0;
     const char* rv = std::getenv("KC_CLI_READERS");
-    // (two readers: 26-31 ms for the C2 sample's 161 MB against 37-46 ms with four,
-    // profiles/r04_cli_probe_phases.txt)
-    const unsigned readers = rv ? (unsigned)std::max(1, std::atoi(rv))
-                                : std::max(1u, std::min(2u, std::thread::hardware_concurrency()));
+    // (one reader: the C2 sample's timed build 25-28 ms after the warm-up below, against
+    // 32-35 ms with two and more with four; profiles/r04_cli_probe_{phases,warmup}.txt)
+    const unsigned readers = rv ? (unsigned)std::max(1, std::atoi(rv)) : 1u;
     Upload up;
     const bool staged = !host_path && up.prepare(isize, a.device, readers);  // (untimed setup)
     if (staged && !a.use_bf && !std::getenv("KC_CLI_NO_WARMUP")) {
