@@ -172,8 +172,9 @@ def cli_e2e(fasta, cli_args, windows):
     mw = re.search(r"Time used to write k-mers in a file: (\d+) microseconds", p.stdout)
     return {"value": windows / secs, "unit": "k-mers/s", "build_s": round(secs, 4), "process_wall_s": round(wall, 3),
             "write_s": int(mw.group(1)) / 1e6 if mw else None,
-            "path": "drop-in CLI bin/kaarme on the same sample file: page-cached file -> HBM (parallel pread, "
-                    "pinned slices) -> passes; the reference's own timer lines",
+            "path": "drop-in CLI bin/kaarme on the same sample file: page-cached file -> HBM (pread into pinned "
+                    "slices; -s jobs after an untimed one-read warm-up pass) -> passes; the reference's own "
+                    "timer lines",
             "input_path": "device image" if "Input path: device image" in p.stdout else "host chunks"}
 
 
