@@ -262,7 +262,10 @@ def fixture_case(args, share=0, first=0, count=None):
             continue
         a = c["args"]
         opt = table_args(args.slots, args.unique)
-        if same_in and c["k"] == args.k and a[:2] == ["-m", "2"] and (share or a[2:-2] == opt):
+        # a share's reference case sizes -s for the share alone (its -s is not the run's); its Bloom
+        # filter on / off must still be the run's
+        same_tbl = a[2:-2] == opt or (share and ("-b" in a) == bool(args.unique))
+        if same_in and c["k"] == args.k and a[:2] == ["-m", "2"] and same_tbl:
             return dict(c, name=name, min_abundance=int(a[-1]), input_sha256=inp["sha256"])
     return None
 
@@ -337,7 +340,17 @@ def setup_job(args, env, image=None):
         estimate = {"distinct_estimate": int(est), "local_slots": local_slots,
                     "ms": round((time.perf_counter() - e0) * 1e3, 1),
                     "method": "HyperLogLog, 2^14 registers (~0.8 % std. error); local table = 1.1 x estimate"}
-    tbl = " ".join(["-m", "2"] + table_args(slots, args.unique))
+    if dist and world > 1 and not args.batch_mib:
+        # a rank also holds its owner table (the local table's geometry, sharded.DeviceEngine) and
+        # the merge's record buffers (send x 1.25 + receive: W + 1 words per distinct k-mer of its
+        # input) beside the local count's partition buffers: the batch takes what is left
+        lsl = estimate["local_slots"] if estimate else min(slots or windows_expected, windows_expected)
+        per_table = int(1.25 * max(slots or 0, lsl) / (16 // (W + 1))) * 128
+        recs = int(2.25 * lsl * (W + 1) * 8)
+        free, _ = torch.cuda.mem_get_info()  # (the image is already allocated)
+        fit = int(0.85 * max(0, free - 2 * per_table - recs)) // (21 * W + 3)
+        batch = min(batch, max(64 << 20, min(fit, 1 << 31)) // 4096 * 4096)
+    tbl =" ".join(["-m", "2"] + table_args(slots, args.unique))
     workload = (f"{args.config}: synthetic {N} x {L} bp reads/GPU, k={k}, {tbl}" if not strong else
                 f"{args.config}: synthetic {args.reads} x {L} bp reads over {world} GPU(s), k={k}, {tbl} per GPU")
     if share:
@@ -348,7 +361,10 @@ def setup_job(args, env, image=None):
                      f"{sk[3]} in the genome")
     # -a only selects output lines (it does not change counting): the reference fixture's -a when
     # this workload has one, so the parity digest covers the same lines
-    fx = fixture_case(args, share, first, N) if world == 1 and not dist else None
+    # the whole job's reference digest: one GPU, a share, or a strong preset over all ranks (each
+    # rank's owner table digests its k-mers; parity_record combines them).  A weak job over N > 1
+    # ranks counts N x the preset's reads, which no fixture covers.
+    fx = fixture_case(args, share, first, N) if (world == 1 or strong) else None
     cfg = ka.Config(k=k, mode=2, table_slots=estimate["local_slots"] if share else slots,
                     min_abundance=fx["min_abundance"] if fx else 2, batch_bytes=batch,
                     device=local, bf_enable=bool(args.unique), est_unique=args.unique)
@@ -374,20 +390,38 @@ def setup_job(args, env, image=None):
                               workload=workload, fixture=fx, stream=stream, estimate=estimate, share=share)
 
 
-def parity_record(job, k):
-    """The timed job's output against the reference's (tests/golden/fullsize.json): SHA-256 of the
-    sorted output text from kc_dump, line count, sum of counts; after the timed steps."""
+def parity_record(job, k, dist=None):
+    """The timed job's output against the reference's (tests/golden/fullsize.json), after the timed
+    steps: the order-independent output digest (kc_output_digest: lines, sum of T(c), sum and XOR
+    of XXH64 per line; on N ranks the owners' digests combined, an all-gather) against the case's
+    `digest`, and on one GPU also the SHA-256 of the sorted output text from kc_dump when the case
+    has the reference's sorted digest and its text stays below ~30 GB."""
     fx = job.fixture
     if fx is None:
         return None
-    from kaarme_amd.digest import sorted_text_digest
+    import kaarme_amd as ka
     t0 = time.perf_counter()
-    got = sorted_text_digest(job.counter.dump(), k)
-    ok = (got["sorted_sha256"], got["lines"], got["count_sum"]) == (fx["sorted_sha256"], fx["lines"], fx["count_sum"])
-    return {"reference_case": f"tests/golden/fullsize.json {fx['name']}: oracle/_ref/kaarme "
-                              f"{' '.join(fx['args'])} on the same input", "match": ok,
-            "sorted_sha256": got["sorted_sha256"], "lines": got["lines"], "count_sum": got["count_sum"],
-            "digest_s": round(time.perf_counter() - t0, 2)}
+    rec = {"reference_case": f"tests/golden/fullsize.json {fx['name']}: " + (
+        f"oracle/_ref/kaarme {' '.join(fx['args'])} on the same input" if fx.get("sorted_sha256") else
+        f"{' '.join(fx['args'])}, digest of the pinned CPU restatement (whole job)")}
+    ok = True
+    want = fx.get("digest")
+    if want:
+        got = job.counter.output_digest()
+        ok = ok and ka.same_digest(got, want)
+        rec["digest"] = got
+        rec["digest_source"] = want.get("source")
+    if fx.get("sorted_sha256") and not dist and fx["lines"] * (k + 8) < 30e9:
+        from kaarme_amd.digest import sorted_text_digest
+        got = sorted_text_digest(job.counter.dump(), k)
+        ok = ok and (got["sorted_sha256"], got["lines"], got["count_sum"]) == (fx["sorted_sha256"], fx["lines"],
+                                                                                 fx["count_sum"])
+        rec.update(sorted_sha256=got["sorted_sha256"], lines=got["lines"], count_sum=got["count_sum"])
+    elif not want:
+        return None
+    rec["match"] = ok
+    rec["digest_s"] = round(time.perf_counter() - t0, 2)
+    return rec
 
 
 def writer_record(job, verify):
@@ -475,7 +509,7 @@ def run_workload(args, env, image=None):
     st = counter.finish()  # raises on table overflow
     if rank == 0:
         log(f"{args.config}: {args.steps} steps in {elapsed:.3f} s; parity / writer records")
-    parity = parity_record(job, k) if args.verify else None
+    parity = parity_record(job, k, dist) if args.verify else None
     # (the text writer and its sorted-file digest for outputs up to ~8 GB: C2 / C3; a strong
     # share's 30 GB of text would take minutes to sort)
     writer = writer_record(job, args.verify) if (args.writer and not dist and job.fixture is not None and
@@ -610,16 +644,44 @@ def free_port():
         return so.getsockname()[1]
 
 
+def visible_gpus():
+    """GPUs the rank processes can use, counted without initialising HIP in this process (VERDICT r4
+    item 1, ADVICE r4: torch.cuda.device_count() may fall back to hipGetDeviceCount): the device
+    lists of ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES when set (ROCm
+    applies them in that order, so the smallest count bounds), else the GPU nodes of the kfd
+    topology (sysfs; a node with gpu_id 0 is a CPU).  None when neither tells."""
+    counts = []
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            counts.append(len([x for x in v.split(",") if x.strip()]))
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        nodes = os.listdir(base)
+    except OSError:
+        nodes = None
+    if nodes is not None:
+        n = 0
+        for d in nodes:
+            try:
+                with open(os.path.join(base, d, "gpu_id")) as f:
+                    n += int(f.read().strip() or 0) != 0
+            except (OSError, ValueError):
+                pass
+        counts.append(n)
+    return min(counts) if counts else None
+
+
 def launch_ranks(n, cpu_only):
     """Starts `n` rank processes of this same command line (RANK / LOCAL_RANK / WORLD_SIZE /
     MASTER_ADDR=127.0.0.1 / MASTER_PORT in their environment, as torch.distributed.run would set
-    them) and waits for them.  The launcher itself never touches the GPU: the ranks are children,
-    not an exec.  Rank 0 prints the JSON line on the inherited stdout.  Returns the exit code
-    (the first nonzero rank's; a failed rank stops the others)."""
+    them) and waits for them.  The launcher itself never touches the GPU (it does not import torch:
+    visible_gpus reads the environment and sysfs); the ranks are children, not an exec.  Rank 0
+    prints the JSON line on the inherited stdout.  Returns the exit code (the first nonzero rank's;
+    a failed rank stops the others)."""
     if not cpu_only:
-        import torch  # counting devices does not initialise the GPU on this image
-        have = torch.cuda.device_count()
-        if have < n:
+        have = visible_gpus()
+        if have is not None and have < n:
             log(f"error: --gpus {n} but {have} GPU(s) visible")
             return 2
     port = str(free_port())
@@ -666,7 +728,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="C2", choices=sorted(PRESETS), help="BASELINE.md workload (default C2)")
+    ap.add_argument("--config", default=None, choices=sorted(PRESETS),
+                    help="BASELINE.md workload (default: C2 on one GPU, C4 -- the multi-GPU config BASELINE.json "
+                         "names, strong scaling -- on N > 1)")
     ap.add_argument("--reads", type=int, default=None, help="reads (per GPU for weak, total for strong presets)")
     ap.add_argument("--read-len", type=int, default=None)
     ap.add_argument("--genome", type=int, default=None)
@@ -685,6 +749,12 @@ def main():
                     help="at N=1 with the default C2: also time this workload (the north star's k=51 Bloom "
                          "config) and attach it as a second record ('none' = skip)")
     ap.add_argument("--secondary-cpu-sample-bases", type=int, default=50_000_000)
+    ap.add_argument("--tertiary", default="C4",
+                    help="at N=1 with the default C2: also time this workload on the one GPU ('c4' record: the "
+                         "whole C4 job, the N=1 point of the strong-scaling curve the N > 1 lines time; 'none' = "
+                         "skip)")
+    ap.add_argument("--multi-secondary", default="C2",
+                    help="at N > 1 with the default C4: also time this weak-scaling workload ('none' = skip)")
     ap.add_argument("--no-verify", dest="verify", action="store_false",
                     help="skip the parity digest against the reference's output (tests/golden/fullsize.json)")
     ap.add_argument("--no-writer", dest="writer", action="store_false",
@@ -735,16 +805,30 @@ def main():
 
     env = {"torch": torch, "ka": ka, "lib": ka.load_library(), "dist": dist, "rank": rank, "world": world,
            "local": local}
+    if args.config is None:
+        args.config = "C4" if world > 1 else "C2"
     primary = resolve(args, args.config)
     out, image = run_workload(primary, env)
-    if world == 1 and not dist and args.config == "C2" and args.secondary != "none":
-        sec = resolve(args, args.secondary)
-        sec.cpu_sample_bases = args.secondary_cpu_sample_bases
-        rec, _ = run_workload(sec, env, image if same_image(primary, sec) else None)
-        out[sec.config.lower()] = {key: rec[key] for key in ("value", "unit", "ms_per_step", "config", "roofline",
-                                                            "kernel_ms", "windows_per_step_per_gpu",
-                                                            "distinct_per_gpu", "table_slots", "cpu_baseline",
-                                                            "parity", "compact", "writer") if key in rec}
+    keep = ("value", "unit", "ms_per_step", "scaling", "config", "roofline", "kernel_ms", "windows_per_step_per_gpu",
+            "distinct_per_gpu", "table_slots", "cpu_baseline", "parity", "compact", "writer", "xgmi", "local_table")
+    extra = []
+    if world == 1 and not dist and args.config == "C2":
+        if args.secondary != "none":
+            extra.append((args.secondary, dict(cpu_sample_bases=args.secondary_cpu_sample_bases)))
+        if args.tertiary != "none":
+            # (no CPU baseline or compact figure: the C3 record carries the k = 51 baseline)
+            extra.append((args.tertiary, dict(no_cpu_baseline=True, compact=False)))
+    elif world > 1 and args.config == "C4" and args.multi_secondary != "none":
+        extra.append((args.multi_secondary, {}))
+    for name, over in extra:
+        sec = resolve(args, name)
+        for key, val in over.items():
+            setattr(sec, key, val)
+        if not same_image(primary, sec):
+            image = None
+            torch.cuda.empty_cache()
+        rec, image = run_workload(sec, env, image)
+        out[sec.config.lower()] = {key: rec[key] for key in keep if key in rec}
     del image
     if rank == 0:
         print(json.dumps(out), file=json_out, flush=True)

@@ -2021,6 +2021,31 @@ int kc_dump(kc_ctx* c, uint64_t** records, uint64_t* n_records) {
     return KC_OK;
 }
 
+int kc_output_digest(kc_ctx* c, kc_digest* out) {
+    if (!c || !out) return KC_ERR_ARG;
+    std::memset(out, 0, sizeof(*out));
+    if (c->cfg.min_abundance == 0) return KC_OK;  // no output (parallel_parser.hpp:1536 / 858)
+    int rc = sync_for_read(c);
+    if (rc) return rc;
+    if (!c->nbuckets) return c->fail(KC_ERR_STATE, "no table");
+    unsigned long long* d = nullptr;
+    if (hipMalloc(&d, 4 * sizeof(unsigned long long)) != hipSuccess)
+        return c->fail(KC_ERR_NOMEM, "digest buffer allocation failed");
+    unsigned long long h[4] = {0, 0, 0, 0};
+    hipError_t e = hipMemsetAsync(d, 0, sizeof(h), c->stream);
+    if (e == hipSuccess)
+        e = launch_text_digest(table_view(c), c->cfg.mode == 0 ? 0 : 1, c->cfg.min_abundance, c->cfg.k, d, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    hipFree(d);
+    if (e != hipSuccess) return c->fail(KC_ERR_HIP, std::string("output digest: ") + hipGetErrorString(e));
+    out->lines = h[0];
+    out->count_sum = h[1];
+    out->hash_sum = h[2];
+    out->hash_xor = h[3];
+    return KC_OK;
+}
+
 // ------------------------------------------------------------------------------
 // Kaarme's compact representation: kc_compact_impl.h
 // ------------------------------------------------------------------------------

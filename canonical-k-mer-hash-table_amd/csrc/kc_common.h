@@ -143,6 +143,51 @@ DEV uint64_t xxh64_u64(uint64_t v, uint64_t seed) {
     return h;
 }
 
+// ---- XXH64 of `len` bytes at any alignment (the same spec, every input length): the per-line
+// hash of the output digest (kc_output_digest; oracle/kc_digest.c hashes the reference's text) ----
+DEV uint64_t rd_le(const uint8_t* p, int n) {
+    uint64_t v = 0;
+    for (int i = 0; i < n; i++) v |= (uint64_t)p[i] << (8 * i);
+    return v;
+}
+DEV uint64_t xxh64_bytes(const uint8_t* p, uint32_t len, uint64_t seed) {
+    const uint64_t P1 = 0x9E3779B185EBCA87ULL, P2 = 0xC2B2AE3D27D4EB4FULL, P3 = 0x165667B19E3779F9ULL,
+                   P4 = 0x85EBCA77C2B2AE63ULL, P5 = 0x27D4EB2F165667C5ULL;
+    auto round = [&](uint64_t acc, uint64_t in) { return rotl64(acc + in * P2, 31) * P1; };
+    const uint8_t* end = p + len;
+    uint64_t h;
+    if (len >= 32) {
+        uint64_t v1 = seed + P1 + P2, v2 = seed + P2, v3 = seed, v4 = seed - P1;
+        do {
+            v1 = round(v1, rd_le(p, 8));
+            v2 = round(v2, rd_le(p + 8, 8));
+            v3 = round(v3, rd_le(p + 16, 8));
+            v4 = round(v4, rd_le(p + 24, 8));
+            p += 32;
+        } while (p + 32 <= end);
+        h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
+        h = (h ^ round(0, v1)) * P1 + P4;
+        h = (h ^ round(0, v2)) * P1 + P4;
+        h = (h ^ round(0, v3)) * P1 + P4;
+        h = (h ^ round(0, v4)) * P1 + P4;
+    } else {
+        h = seed + P5;
+    }
+    h += len;
+    for (; p + 8 <= end; p += 8) h = rotl64(h ^ round(0, rd_le(p, 8)), 27) * P1 + P4;
+    if (p + 4 <= end) {
+        h = rotl64(h ^ (rd_le(p, 4) * P1), 23) * P2 + P3;
+        p += 4;
+    }
+    for (; p < end; p++) h = rotl64(h ^ ((uint64_t)*p * P5), 11) * P1;
+    h ^= h >> 33;
+    h *= P2;
+    h ^= h >> 29;
+    h *= P3;
+    h ^= h >> 32;
+    return h;
+}
+
 DEV uint64_t atomic_load_agent(const uint64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

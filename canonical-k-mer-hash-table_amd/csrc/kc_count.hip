@@ -157,6 +157,11 @@ hipError_t launch_text(TableView t, int count_mode, uint64_t a, int k, uint64_t 
     KC_DISPATCH_W(t.W, text(t, count_mode, a, k, blk0, nblk, off, base, out, lds, s));
 }
 
+hipError_t launch_text_digest(TableView t, int count_mode, uint64_t a, int k, unsigned long long* out, hipStream_t s) {
+    if ((t.nbuckets + TEXT_T - 1) / TEXT_T > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    KC_DISPATCH_W(t.W, text_digest(t, count_mode, a, k, out, s));
+}
+
 hipError_t launch_check_runs(const uint64_t* rec, const uint64_t* gstart, uint32_t G, uint64_t maxn, TableView t,
                              unsigned long long* flag, hipStream_t s) {
     if (G == 0) return hipSuccess;

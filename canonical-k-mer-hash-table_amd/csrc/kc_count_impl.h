@@ -2908,21 +2908,10 @@ __global__ __launch_bounds__(TEXT_T) void k_text_bytes(TableView tv, int count_m
     if (threadIdx.x == 0) block_bytes[blockIdx.x] = total;
 }
 
-// blocks [blk0, blk0 + grid) write at out + off[b] - base; dynamic LDS >= the largest
-// block's bytes
-template <int W>
-__global__ __launch_bounds__(TEXT_T) void k_text(TableView tv, int count_mode, uint64_t a, int k, uint64_t blk0,
-                                                 const uint64_t* __restrict__ off, uint64_t base,
-                                                 uint8_t* __restrict__ out) {
-    constexpr int S = BUCKET_WORDS / (W + 1);
-    extern __shared__ uint8_t s_txt[];
-    __shared__ uint32_t s_w[TEXT_T / 64];
-    const uint64_t b = blk0 + blockIdx.x;
-    uint64_t bw[BUCKET_WORDS];
-    uint32_t tc[S];
-    const uint32_t v = text_bucket<W>(tv, b * TEXT_T + threadIdx.x, count_mode, a, k, bw, tc);
-    uint32_t total;
-    uint32_t pos = block_excl_sum<TEXT_T>(v, s_w, total);
+// the lines of one bucket's emitted slots (tc[s] != 0) at p: "<KMER> <T(c)>\n" each, the
+// k-mer's characters int2char'd from the canonical key (functions_strings.cpp:72-90)
+template <int W, int S = BUCKET_WORDS / (W + 1)>
+DEV void format_lines(const uint64_t (&bw)[BUCKET_WORDS], const uint32_t (&tc)[S], int k, uint8_t* p) {
     const int c0 = k - 32 * (W - 1);  // characters in key word 0 (the others hold 32)
 #pragma unroll
     for (int s = 0; s < S; s++) {
@@ -2931,7 +2920,6 @@ __global__ __launch_bounds__(TEXT_T) void k_text(TableView tv, int count_mode, u
 #pragma unroll
         for (int i = 0; i < W; i++) t[i] = bw[s * W + i];
         from_tkey<W>(t, key);
-        uint8_t* p = s_txt + pos;
 #pragma unroll
         for (int w = 0; w < W; w++) {
             const int nc = w == 0 ? c0 : 32;
@@ -2946,8 +2934,90 @@ __global__ __launch_bounds__(TEXT_T) void k_text(TableView tv, int count_mode, u
             cnt /= 10;
         }
         p[nd] = '\n';
-        pos += (uint32_t)k + 2 + nd;
+        p += nd + 1;
     }
+}
+
+// --------------------------------------------------------------------------------
+// Order-independent digest of the output text (kc_output_digest): the lines kc_write would
+// write, each hashed with XXH64 (seed 0) over its bytes incl. '\n', summed mod 2^64 and XORed,
+// plus the line count and the sum of T(c).  Equal for any line order, and additive over tables
+// (the owners of a sharded job) and over partitions of the k-mer space (oracle/kc_digest.c), so a
+// whole-job result is checked without sorting or moving its text.  One TEXT_T-bucket block per
+// workgroup, its lines formatted into LDS as k_text does; out[4] = {lines, count sum, hash sum,
+// hash xor}.
+// --------------------------------------------------------------------------------
+template <int W>
+__global__ __launch_bounds__(TEXT_T) void k_text_digest(TableView tv, int count_mode, uint64_t a, int k,
+                                                        unsigned long long* __restrict__ out) {
+    constexpr int S = BUCKET_WORDS / (W + 1);
+    extern __shared__ uint8_t s_txt[];
+    __shared__ uint32_t s_w[TEXT_T / 64];
+    __shared__ unsigned long long s_red[4][TEXT_T / 64];
+    uint64_t bw[BUCKET_WORDS];
+    uint32_t tc[S];
+    const uint32_t v = text_bucket<W>(tv, (uint64_t)blockIdx.x * TEXT_T + threadIdx.x, count_mode, a, k, bw, tc);
+    uint32_t total;
+    uint32_t pos = block_excl_sum<TEXT_T>(v, s_w, total);
+    format_lines<W>(bw, tc, k, s_txt + pos);
+    uint64_t lines = 0, csum = 0, hsum = 0, hxor = 0;
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+        if (!tc[s]) continue;
+        const uint32_t len = (uint32_t)k + 2 + ndigits(tc[s]);
+        const uint64_t h = xxh64_bytes(s_txt + pos, len, 0);
+        lines++;
+        csum += tc[s];
+        hsum += h;
+        hxor ^= h;
+        pos += len;
+    }
+    for (int d = 32; d >= 1; d >>= 1) {
+        lines += __shfl_xor(lines, d, 64);
+        csum += __shfl_xor(csum, d, 64);
+        hsum += __shfl_xor(hsum, d, 64);
+        hxor ^= __shfl_xor(hxor, d, 64);
+    }
+    const int wid = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        s_red[0][wid] = lines;
+        s_red[1][wid] = csum;
+        s_red[2][wid] = hsum;
+        s_red[3][wid] = hxor;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < TEXT_T / 64; w++) {
+            lines += s_red[0][w];
+            csum += s_red[1][w];
+            hsum += s_red[2][w];
+            hxor ^= s_red[3][w];
+        }
+        if (lines) {
+            atomicAdd(&out[0], (unsigned long long)lines);
+            atomicAdd(&out[1], (unsigned long long)csum);
+            atomicAdd(&out[2], (unsigned long long)hsum);
+            atomicXor(&out[3], (unsigned long long)hxor);
+        }
+    }
+}
+
+// blocks [blk0, blk0 + grid) write at out + off[b] - base; dynamic LDS >= the largest
+// block's bytes
+template <int W>
+__global__ __launch_bounds__(TEXT_T) void k_text(TableView tv, int count_mode, uint64_t a, int k, uint64_t blk0,
+                                                 const uint64_t* __restrict__ off, uint64_t base,
+                                                 uint8_t* __restrict__ out) {
+    constexpr int S = BUCKET_WORDS / (W + 1);
+    extern __shared__ uint8_t s_txt[];
+    __shared__ uint32_t s_w[TEXT_T / 64];
+    const uint64_t b = blk0 + blockIdx.x;
+    uint64_t bw[BUCKET_WORDS];
+    uint32_t tc[S];
+    const uint32_t v = text_bucket<W>(tv, b * TEXT_T + threadIdx.x, count_mode, a, k, bw, tc);
+    uint32_t total;
+    const uint32_t pos = block_excl_sum<TEXT_T>(v, s_w, total);
+    format_lines<W>(bw, tc, k, s_txt + pos);
     __syncthreads();
     uint8_t* o = out + (off[b] - base);
     // copy out: byte head up to a 4-byte boundary of the destination, then dwords
@@ -3574,6 +3644,20 @@ template <int W>
 hipError_t WOps<W>::text(TableView t, int count_mode, uint64_t a, int k, uint64_t blk0, uint64_t nblk,
                          const uint64_t* off, uint64_t base, uint8_t* out, size_t lds, hipStream_t s) {
     return text_w<W>(t, count_mode, a, k, blk0, nblk, off, base, out, lds, s);
+}
+
+template <int W>
+hipError_t WOps<W>::text_digest(TableView t, int count_mode, uint64_t a, int k, unsigned long long* out,
+                                hipStream_t s) {
+    // every block's lines fit: TEXT_T buckets x S slots x (k + 2 + 5) bytes (<= 124 KiB for k <= 479)
+    const size_t lds = ((size_t)TEXT_T * (BUCKET_WORDS / (W + 1)) * ((size_t)k + 7) + 15) / 16 * 16;
+    const uint64_t nblk = (t.nbuckets + TEXT_T - 1) / TEXT_T;
+    if (nblk == 0) return hipSuccess;
+    auto kern = k_text_digest<W>;
+    hipError_t e = set_smem(kern, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(TEXT_T), lds, s, t, count_mode, a, k, out);
+    return hipGetLastError();
 }
 
 // --------------------------------------------------------------------------------

@@ -308,6 +308,9 @@ hipError_t launch_text_bytes(TableView t, int count_mode, uint64_t a, int k, uin
                              uint64_t* bsum, hipStream_t s);
 hipError_t launch_text(TableView t, int count_mode, uint64_t a, int k, uint64_t blk0, uint64_t nblk,
                        const uint64_t* off, uint64_t base, uint8_t* out, size_t lds, hipStream_t s);
+// order-independent digest of those lines (kc_output_digest): out[4] += {lines, sum T(c), sum of
+// XXH64(line), xor of XXH64(line)} (out zeroed by the caller)
+hipError_t launch_text_digest(TableView t, int count_mode, uint64_t a, int k, unsigned long long* out, hipStream_t s);
 hipError_t launch_xxh64(const uint64_t* v, const uint64_t* seed, uint64_t n, uint64_t* out, hipStream_t s);
 hipError_t launch_synth(uint8_t* dst, uint64_t first_read, uint64_t n_reads, uint64_t seed, uint64_t genome_len,
                         uint32_t read_len, uint32_t wrap, double err_rate, double n_rate, const kc_synth_skew* skew,
@@ -351,6 +354,8 @@ struct WOps {
                                  uint64_t* bsum, hipStream_t s);
     static hipError_t text(TableView t, int count_mode, uint64_t a, int k, uint64_t blk0, uint64_t nblk,
                            const uint64_t* off, uint64_t base, uint8_t* out, size_t lds, hipStream_t s);
+    static hipError_t text_digest(TableView t, int count_mode, uint64_t a, int k, unsigned long long* out,
+                                  hipStream_t s);
 };
 // Kaarme's compact representation, built after counting (kc_compact_impl.h)
 struct CompactView {

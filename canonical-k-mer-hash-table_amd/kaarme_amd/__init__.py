@@ -50,6 +50,7 @@ EXPORTS = (
     "kc_table_size_reference", "kc_bloom_get_device", "kc_bloom_merge_device", "kc_bloom_set_device",
     "kc_bloom_estimate", "kc_compact", "kc_compact_dump", "kc_compact_lookup", "kc_compact_read",
     "kc_estimate_distinct_device", "kc_bloom_records_device", "kc_count_records_device", "kc_plan_chunks_device",
+    "kc_output_digest",
 )
 
 
@@ -84,6 +85,10 @@ class kc_synth_skew(ctypes.Structure):
 
 class kc_compact_info(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in ("slots", "kmers", "chain_starts", "bytes", "table_bytes")]
+
+
+class kc_digest(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in ("lines", "count_sum", "hash_sum", "hash_xor")]
 
 
 class kc_stats(ctypes.Structure):
@@ -134,6 +139,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "kc_finish": (I32, [P, ctypes.POINTER(kc_stats)]),
         "kc_dump": (I32, [P, ctypes.POINTER(ctypes.POINTER(U64)), ctypes.POINTER(U64)]),
         "kc_write": (I32, [P, ctypes.c_char_p]),
+        "kc_output_digest": (I32, [P, ctypes.POINTER(kc_digest)]),
         "kc_key_words": (I32, [P]),
         "kc_free": (None, [P]),
         "kc_plan_chunks": (I32, [P, U64, I32, U64, I32, ctypes.POINTER(ctypes.POINTER(kc_chunk)),
@@ -526,6 +532,34 @@ class KmerCounter:
 
     def write(self, path: str):
         self._chk(self.lib.kc_write(self._ctx, path.encode()), "kc_write")
+
+    def output_digest(self) -> dict:
+        """Order-independent digest of the output text (kc_output_digest): lines, sum of T(c), and
+        the sum mod 2^64 / XOR of XXH64 over every line (hash_sum / hash_xor as 16 hex digits, the
+        format of oracle/kc_digest.c and tests/golden/fullsize.json)."""
+        d = kc_digest()
+        self._chk(self.lib.kc_output_digest(self._ctx, ctypes.byref(d)), "kc_output_digest")
+        return digest_dict(d.lines, d.count_sum, d.hash_sum, d.hash_xor)
+
+
+def digest_dict(lines: int, count_sum: int, hash_sum: int, hash_xor: int) -> dict:
+    return {"lines": int(lines), "count_sum": int(count_sum), "hash_sum": f"{int(hash_sum) & (2**64 - 1):016x}",
+            "hash_xor": f"{int(hash_xor) & (2**64 - 1):016x}"}
+
+
+def combine_digests(parts: Iterable[dict]) -> dict:
+    """The digest of the union of disjoint line sets (e.g. the owners of a sharded job)."""
+    n = c = s = x = 0
+    for d in parts:
+        n += d["lines"]
+        c += d["count_sum"]
+        s += int(d["hash_sum"], 16)
+        x ^= int(d["hash_xor"], 16)
+    return digest_dict(n, c, s, x)
+
+
+def same_digest(a: dict, b: dict) -> bool:
+    return all(a[key] == b[key] for key in ("lines", "count_sum", "hash_sum", "hash_xor"))
 
 
 def count_file(path: str, k: int, mode: int = 2, min_abundance: int = 2, table_slots: int = 1 << 20,

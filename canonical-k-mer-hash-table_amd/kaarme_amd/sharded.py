@@ -202,12 +202,18 @@ class DeviceEngine:
         # owner share does not bound (a rank sees ~all k-mers of the genome at low
         # per-rank coverage): local_slots, e.g. min(-s total, this rank's windows).  With the
         # Bloom filter the local count is ungated (the owners gate): it holds every distinct
-        # k-mer of the rank's input, -u unless local_slots is given
+        # k-mer of the rank's input -- local_slots when given (e.g. bench.py's distinct estimate;
+        # -u overstates it ~8x for C3), else -u
         if cfg.bf_enable:
             local = dataclasses.replace(cfg, bf_enable=False,
-                                        table_slots=max(local_slots, cfg.est_unique, cfg.table_slots))
+                                        table_slots=local_slots or max(cfg.est_unique, cfg.table_slots))
         else:
             local = dataclasses.replace(cfg, table_slots=max(cfg.table_slots, local_slots))
+            # the owner table takes the same size: the records a rank receives are then region-sorted
+            # groups merged by one level-3 pass (kc_insert_counts_runs_device), with no partition
+            # buffers beside the two tables (a local table larger than the owner's share is the
+            # strong presets' case: C4 at 8 ranks 567 M local vs 406 M owner slots)
+            self.cfg = cfg = dataclasses.replace(cfg, table_slots=local.table_slots)
         self.kc = KmerCounter(local)    # local table (also used by the per-window route path)
         if world > 1:  # its level-3 passes keep the per-owner counts the merge's route needs
             self.kc.route_hint(world)
@@ -499,6 +505,26 @@ class ShardedCounter:
         close = getattr(self.engine, "close", None)
         if close:
             close()
+
+    def output_digest(self, combine: bool = True) -> dict:
+        """Digest of this rank's output (its owner table, kc_output_digest) or, with combine
+        (collective), of the whole job's: the owners' digests add up (their k-mers are disjoint),
+        gathered over the group.  The whole job's output is the concatenation of the owners'
+        outputs, so this is the digest a single table of the whole input would give."""
+        from . import combine_digests, digest_dict
+
+        self.sync()
+        d = self.kc.output_digest()
+        if not combine or self.world == 1:
+            return d
+        import torch
+
+        vals = [d["lines"], d["count_sum"], int(d["hash_sum"], 16), int(d["hash_xor"], 16)]
+        dev = "cuda" if self.device == "cuda" and self.dist.get_backend(self.group) != "gloo" else "cpu"
+        t = torch.tensor([v - (1 << 64) if v >= (1 << 63) else v for v in vals], dtype=torch.int64, device=dev)
+        got = [torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(got, t, group=self.group)
+        return combine_digests(digest_dict(*[int(v) & (2**64 - 1) for v in g.tolist()]) for g in got)
 
     def dump(self):
         return self.kc.dump()

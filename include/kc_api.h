@@ -299,6 +299,20 @@ int kc_dump(kc_ctx* ctx, uint64_t** records, uint64_t* n_records);
  * write_kmers_on_disk_separately_even_faster (kmer_hash_table.cpp:4318-4524) /
  * write_kmers (2013-2050).  Line order is unspecified, as in the reference. */
 int kc_write(kc_ctx* ctx, const char* path);
+/* Order-independent digest of the text kc_write would write (the reference has none; its
+ * output order is unspecified): every line "<CANONICAL_KMER> <T(c)>\n" is
+ * hashed with XXH64 (seed 0) over its bytes incl. the '\n'; hash_sum is the sum of those
+ * hashes mod 2^64 and hash_xor their XOR.  Any line order gives the same digest, and the digests
+ * of disjoint line sets add up (lines, count_sum, hash_sum by addition mod 2^64, hash_xor by XOR),
+ * so the owners of a sharded job combine theirs into the whole job's, comparable with a digest of
+ * the reference's output file (oracle/kc_digest.c lines).  a == 0: all zero (no output). */
+typedef struct {
+    uint64_t lines;      /* lines (k-mers with T(c) >= a) */
+    uint64_t count_sum;  /* sum of T(c) over the lines */
+    uint64_t hash_sum;   /* sum of XXH64(line) mod 2^64 */
+    uint64_t hash_xor;   /* XOR of XXH64(line) */
+} kc_digest;
+int kc_output_digest(kc_ctx* ctx, kc_digest* out);
 int kc_key_words(const kc_ctx* ctx);
 void kc_free(void* p);
 

@@ -98,6 +98,32 @@ def golden_input(tmp_path_factory):
     return get
 
 
+def lines_digest(lines):
+    """The output digest (include/kc_api.h kc_output_digest: lines, sum of T(c), sum mod 2^64 and XOR
+    of XXH64 over every "<KMER> <T(c)>\\n" line) of lines given as bytes with or without their '\\n'."""
+    import xxhash
+    n = c = s = x = 0
+    for line in lines:
+        if isinstance(line, str):
+            line = line.encode()
+        if not line.endswith(b"\n"):
+            line += b"\n"
+        h = xxhash.xxh64_intdigest(line)
+        n += 1
+        c += int(line.split()[1])
+        s += h
+        x ^= h
+    return {"lines": n, "count_sum": c, "hash_sum": f"{s % 2**64:016x}", "hash_xor": f"{x:016x}"}
+
+
+def text_digest(path):
+    """lines_digest of a text file (no file: the empty digest)."""
+    if not os.path.exists(path):
+        return lines_digest([])
+    with open(path, "rb") as f:
+        return lines_digest(f.read().splitlines(keepends=True))
+
+
 def oracle_count(path, k, args, out):
     """Run the C oracle; returns its stats line as a dict."""
     p = subprocess.run([ORACLE, "count", path, str(k)] + list(args) + ["-o", str(out)],

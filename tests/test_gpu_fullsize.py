@@ -87,6 +87,8 @@ def test_fixture_cases_match_bench_presets():
             fx = bench.fixture_case(args)
         assert fx is not None and fx["name"] == name, name
         assert fx["sorted_sha256"] == c["sorted_sha256"]
+        # the whole strong jobs are found at every world size (bench.py's N > 1 parity)
+        assert bool(c.get("whole_job")) == (name in ("C4", "C5")), name
 
 
 @pytest.mark.gpu
@@ -125,6 +127,8 @@ def test_bench_job_equals_reference_output(config):
             assert got["sorted_sha256"] == fx["sorted_sha256"], step
             if fx["distinct"] is not None and not args.unique:
                 assert st["distinct"] == fx["distinct"]
+            if fx.get("digest"):  # the order-independent digest of the same output (make_digests.py)
+                assert ka.same_digest(job.counter.output_digest(), fx["digest"]), step
     finally:
         job.counter.close()
         del job
@@ -162,6 +166,41 @@ def test_bench_share_equals_reference_output(name):
         got = sorted_text_digest(job.counter.dump(), args.k)
         assert (got["lines"], got["count_sum"]) == (fx["lines"], fx["count_sum"])
         assert got["sorted_sha256"] == fx["sorted_sha256"]
+        if fx.get("digest"):
+            assert ka.same_digest(job.counter.output_digest(), fx["digest"])
+    finally:
+        job.counter.close()
+        del job
+        torch.cuda.empty_cache()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("name", ["C4", "C5"])
+def test_whole_strong_job_on_one_gpu(name):
+    """the whole C4 (100 M x 150 bp, k = 51, -s 2.6e9) and C5 (1 M x 10 kbp,
+    k = 127, -s 3.6e9) jobs on one GPU -- bench.py's N = 1 point of the strong-scaling curve, many
+    staging batches into one table -- against the whole-job digest of tests/golden/fullsize.json (the
+    pinned CPU restatement, partitioned: make_digests.py; no reference run covers these sizes here).
+    Two steps on one context, as bench.py times them."""
+    import torch
+    import kaarme_amd as ka
+    doc = _fixture()
+    if name not in doc["cases"]:
+        pytest.skip(f"no {name} fixture")
+    bench, args = _bench_args(name)
+    env = {"torch": torch, "ka": ka, "lib": ka.load_library(), "dist": None, "rank": 0, "world": 1, "local": 0}
+    torch.cuda.set_device(0)
+    job = bench.setup_job(args, env)
+    fx = job.fixture
+    assert fx is not None and fx["name"] == name and fx.get("whole_job")
+    try:
+        for step in range(2):
+            job.step()
+            st = job.counter.finish()
+            assert st["windows"] == job.windows_expected == fx["count_sum"]
+            assert st["distinct"] == fx["distinct"], step
+            assert ka.same_digest(job.counter.output_digest(), fx["digest"]), step
     finally:
         job.counter.close()
         del job

@@ -12,7 +12,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from conftest import CLI, GEN, load_cases, oracle_count, sorted_digest_file, sorted_digest_lines
+from conftest import CLI, GEN, load_cases, oracle_count, sorted_digest_file, sorted_digest_lines, text_digest
 import kaarme_amd as ka
 
 pytestmark = pytest.mark.gpu
@@ -100,6 +100,9 @@ def check_golden_case(case, golden_input, tmp_path):
         out = tmp_path / "out.txt"
         kc.write(str(out))
         assert sorted(open(out).read().splitlines()) == sorted(lines)
+        # the order-independent digest (kc_output_digest, the whole-job parity of bench.py's N > 1
+        # lines) is the written text's
+        assert kc.output_digest() == text_digest(str(out))
 
 
 @pytest.mark.parametrize("name,k,args", [

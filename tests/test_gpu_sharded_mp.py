@@ -6,13 +6,14 @@ count, the pre-aggregated merge (kc_route_table_device -> all-to-all -> kc_inser
 The union of the owners' outputs must equal the reference's output on the whole input
 (tests/golden/cases.json); the reference's single shared table is kmer_hash_table.cpp:2207.
 """
+import json
 import os
 import socket
 
 import numpy as np
 import pytest
 
-from conftest import load_cases, sorted_digest_lines
+from conftest import lines_digest, load_cases, sorted_digest_lines
 
 pytestmark = pytest.mark.gpu
 
@@ -69,7 +70,10 @@ def _rank(rank, world, port, path, k, args, out_dir):
         sc.bloom_finalize()
     sc.count_device(img.data_ptr(), mine, ka.FMT_FASTA, stream)
     st = sc.finish()
+    d = sc.output_digest()  # collective: the owners' digests combined (bench.py's N > 1 parity)
     np.save(os.path.join(out_dir, f"r{rank}.npy"), sc.dump())
+    with open(os.path.join(out_dir, f"dg{rank}.json"), "w") as f:
+        json.dump(d, f)
     with open(os.path.join(out_dir, f"st{rank}.txt"), "w") as f:
         f.write(f"{st['windows']} {st['chunks']}\n")
     sc.close()
@@ -95,5 +99,8 @@ def test_two_processes_equal_the_reference(name, k, args, golden_input, tmp_path
     for r in recs:
         lines += [f"{s} {c}" for s, c in ka.decode_records(r.reshape(-1), k)]
     assert sorted_digest_lines(lines) == (case["sorted_sha256"], case["lines"])
+    want = lines_digest(lines)
+    for r in range(2):
+        assert json.load(open(tmp_path / f"dg{r}.json")) == want, r
     windows = sum(int(open(tmp_path / f"st{r}.txt").read().split()[0]) for r in range(2))
     assert windows > 0

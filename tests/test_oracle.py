@@ -11,7 +11,10 @@ import subprocess
 
 import pytest
 
-from conftest import (GOLDEN, ORACLE, REF_BIN, GEN, load_cases, oracle_count, sorted_digest_file)
+from conftest import (GOLDEN, ORACLE, ORACLE_DIR, REF_BIN, GEN, load_cases, oracle_count, sorted_digest_file,
+                      text_digest)
+
+DIGEST = os.path.join(ORACLE_DIR, "_ref", "kc_digest")
 
 CASES = load_cases()["cases"]
 
@@ -80,3 +83,55 @@ def test_bloom_model_xxh64_matches_golden_vectors():
     from conftest import GOLDEN
     vec = json.load(open(os.path.join(GOLDEN, "xxh64.json")))["vectors"]
     assert all(bm.xxh64_u64(v["value"], v["seed"]) == v["xxh64"] for v in vec)
+
+
+def _digest_json(args):
+    return json.loads(subprocess.run([DIGEST] + args, capture_output=True, text=True, check=True).stdout)
+
+
+def _same(a, b):
+    return all(a[key] == b[key] for key in ("lines", "count_sum", "hash_sum", "hash_xor"))
+
+
+# the whole-job digests of tests/golden/fullsize.json (C4, C5) come from `kc_digest count`: it must give
+# the digest of the reference's output on every golden case it can restate (no Bloom filter, or a >= 2,
+# where the reference's Bloom output equals the unfiltered count)
+DIGEST_CASES = [c for c in CASES if "-b" not in c["args"] or int(c["args"][c["args"].index("-a") + 1]) >= 2]
+
+
+@pytest.mark.parametrize("case", DIGEST_CASES, ids=_case_id)
+def test_partitioned_digest_matches_reference_output(case, golden_input, tmp_path):
+    path = golden_input(case["input"])
+    args = case["args"]
+    out = tmp_path / "o.txt"
+    oracle_count(path, case["k"], args, out)  # sorted-equal to the reference's output (test above)
+    want = text_digest(str(out))
+    assert want["lines"] == case["lines"]
+    assert _same(_digest_json(["lines", str(out)]) if out.exists() else want, want)
+    m = args[args.index("-m") + 1] if "-m" in args else "2"
+    a = args[args.index("-a") + 1] if "-a" in args else "2"
+    got = _digest_json(["count", path, str(case["k"]), "-m", m, "-a", a, "-p", "3", "-j", "2"])
+    assert _same(got, want), (got, want)
+
+
+def test_digest_is_order_independent(tmp_path):
+    p = tmp_path / "o.txt"
+    lines = [b"ACGT 3\n", b"CCCA 1\n", b"AAAA 16383\n"]
+    p.write_bytes(b"".join(lines))
+    q = tmp_path / "r.txt"
+    q.write_bytes(b"".join(reversed(lines)))
+    assert _same(_digest_json(["lines", str(p)]), _digest_json(["lines", str(q)]))
+    assert _same(_digest_json(["lines", str(p)]), text_digest(str(p)))
+
+
+def test_fullsize_digests_are_consistent():
+    """Every full-size fixture with a digest: the digest's lines / count sum are the case's (for the
+    reference-run cases these come from the reference's own output), and --ref runs agree."""
+    doc = json.load(open(os.path.join(GOLDEN, "fullsize.json")))
+    for name, c in doc["cases"].items():
+        d = c.get("digest")
+        if not d:
+            continue
+        assert (d["lines"], d["count_sum"]) == (c["lines"], c["count_sum"]), name
+        if c.get("ref_digest"):
+            assert _same(c["ref_digest"], d), name

@@ -76,6 +76,11 @@ class _Table:
     def sync(self):
         pass
 
+    def output_digest(self):
+        """kc_output_digest of this table's lines (T(c) = c mod 65536, -m 0; a = 1)."""
+        from conftest import lines_digest
+        return lines_digest(f"{km} {c & 0xFFFF}" for km, c in self.table.items())
+
 
 def bloom_positions(words, nblocks, nh):
     """Blocked-layout model: one 16-word block per k-mer, position j = a 5-bit field of
@@ -230,6 +235,10 @@ def _worker(rank, world, port, k, reads, outdir, rounds):
         sc.sync()                  # nothing pending: no third exchange
         with open(os.path.join(outdir, f"shard{rank}.json"), "w") as f:
             json.dump(dict(eng.owner.table), f)
+        # the whole job's output digest: the owners' digests gathered and combined (bench.py's N > 1
+        # parity record)
+        with open(os.path.join(outdir, f"digest{rank}.json"), "w") as f:
+            json.dump(sc.output_digest(), f)
     finally:
         dist.destroy_process_group()
 
@@ -247,6 +256,10 @@ def test_sharded_union_equals_single(tmp_path, k):
     truth = collections.Counter(km for r in reads for km in canonical_windows(r, k))
     assert union == truth
     assert all(len(s) > 0 for s in shards)
+    from conftest import lines_digest
+    want = lines_digest(f"{km} {c & 0xFFFF}" for km, c in truth.items())
+    for r in range(world):
+        assert json.load(open(tmp_path / f"digest{r}.json")) == want
 
 
 def _bloom_worker(rank, world, port, k, reads, outdir):
