@@ -165,6 +165,16 @@ struct kc_ctx {
 
     uint64_t n_chunks = 0, n_bytes = 0;
 
+    // Deferred level 3 (device_pass / run_deferred): a counting pass over an image of several
+    // batches keeps the level-2 segments of up to defer_g batches in keys2 and inserts them with one
+    // level-3 pass -- one sweep of the table per group instead of per batch
+    bool defer_on = false;     // the current device_pass defers (set per pass)
+    bool defer_last = false;   // the batch being launched is the pass's last
+    uint32_t defer_g = 0;      // batches per group
+    uint32_t defer_n = 0;      // batches of the current group whose segments wait
+    uint64_t defer_syms = 0;   // the group's segment geometry is sized for batches of this bound
+    uint64_t defer_groups = 0; // level-3 passes the deferral ran (kc_stats)
+
     // profiling: event quadruples {start, after gather, after tokenize, after count}
     bool profiling = false;
     std::vector<hipEvent_t> ev_pool;
@@ -433,15 +443,17 @@ struct PartGeo {
 };
 static PartGeo table_geo(const kc_ctx* c) { return PartGeo{c->F1, c->F2, c->R, c->W}; }
 
+// slots > 1: the level-2 histogram and key buffers hold that many batches' segments (a deferred
+// level 3, run_deferred)
 static int ensure_part_geo(kc_ctx* c, uint64_t syms, bool seg, const PartGeo& g, PartBufs& pb, PartCap& cap,
-                           uint32_t bins1 = 0) {
+                           uint32_t bins1 = 0, uint32_t slots = 1) {
     const uint64_t tile = (uint64_t)COUNT_THREADS * run_width(c->W);
     const uint32_t nblk1 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(2048, (syms + tile - 1) / tile));
     const uint32_t B2 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(64, 2048 / g.F1));
     // every array is sized for the geometry of THIS call (a Bloom job re-sizes the table
     // after each Bloom pass, so F1 and R may grow between calls on one context)
     const uint64_t n1 = (uint64_t)std::max<uint32_t>(g.F1, bins1) * 2048;  // level-1 bins x max workgroups
-    const uint64_t n2 = g.R * B2;
+    const uint64_t n2 = g.R * B2 * slots;
     const uint64_t nbs = (std::max(n1, n2) + 4095) / 4096 + 2;
     if (n1 > cap.h1) {
         hipFree(pb.hist1);
@@ -493,7 +505,7 @@ static int ensure_part_geo(kc_ctx* c, uint64_t syms, bool seg, const PartGeo& g,
     }
     const uint64_t spill_words = spill_cap * (g.IW + 1);
     const uint64_t need1 = std::max(std::max<uint64_t>(syms, (uint64_t)g.F1 * nblk1 * cap1) * g.IW, spill_words);
-    const uint64_t need2 = std::max(std::max<uint64_t>(syms, g.R * B2 * cap2) * g.IW, spill_words);
+    const uint64_t need2 = std::max(std::max<uint64_t>(syms, g.R * B2 * cap2 * slots) * g.IW, spill_words);
     auto grow = [&](uint64_t** buf, uint64_t* have, uint64_t need) -> int {
         if (need <= *have) return KC_OK;
         hipFree(*buf);
@@ -521,9 +533,9 @@ static int ensure_part_geo(kc_ctx* c, uint64_t syms, bool seg, const PartGeo& g,
     return KC_OK;
 }
 // the table's levels
-static int ensure_part(kc_ctx* c, uint64_t syms, bool seg, uint32_t bins1 = 0) {
+static int ensure_part(kc_ctx* c, uint64_t syms, bool seg, uint32_t bins1 = 0, uint32_t slots = 1) {
     seg = seg && c->seg_ok;
-    return ensure_part_geo(c, syms, seg, table_geo(c), c->pb, c->pb_cap, bins1);
+    return ensure_part_geo(c, syms, seg, table_geo(c), c->pb, c->pb_cap, bins1, slots);
 }
 
 // Insert path per batch: the partitioned pipeline moves ~(4W+1)*8 bytes per window
@@ -574,6 +586,53 @@ static int tail_needed(kc_ctx* c, hipStream_t s, bool* need) {
     HIPCHK(c, hipMemcpyAsync(&f[1], &c->d_ctr->spill_n, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
     *need = f[0] != 0 || f[1] != 0;
+    return KC_OK;
+}
+
+// The level-3 pass of the deferred group (run_deferred): the waiting batches' segments, slots of
+// batches that did not fill the group zeroed first (their fills are a previous group's)
+static int flush_deferred(kc_ctx* c, const PackedView& sv, uint64_t syms, int mode, const TableView& tv,
+                          const BloomView& bv, PartBufs pb, hipStream_t s, bool overflowed) {
+    const uint32_t G = c->defer_g, B2 = c->pb.B2;
+    // (the batch that overflowed: its segments are not all written; its tail redoes it)
+    const uint32_t keep = overflowed ? c->defer_n - 1 : c->defer_n;
+    if (keep < G)
+        HIPCHK(c, hipMemset2DAsync(c->pb.hist2 + (uint64_t)keep * B2, (size_t)G * B2 * 4, 0, (size_t)(G - keep) * B2 * 4,
+                                   c->R, s));
+    if (overflowed) HIPCHK(c, launch_hold_overflow(c->d_ctr, 0, s));
+    HIPCHK(c, launch_count_partitioned(sv, syms, c->cfg.k, mode, tv, bv, c->d_ctr, pb, c->table_fresh, s, PH_L3));
+    if (overflowed) HIPCHK(c, launch_hold_overflow(c->d_ctr, 1, s));
+    c->table_zero_pending = false;  // a fresh level 3 writes every region
+    own_after_write(c, true, c->table_fresh);
+    c->table_fresh = false;
+    c->defer_n = 0;
+    c->defer_groups++;
+    return KC_OK;
+}
+
+// One batch of a deferred counting pass: levels 1-2 into the batch's slot of the group's level-2
+// segments; the group's level 3 when the group is full, at the pass's last batch, or when this
+// batch needs its tail (a skew list, or segments that overflowed: the tail's exact pipeline uses
+// the key buffers as scratch, so the waiting segments are inserted first).  The host reads the
+// batch's two flags (it waits for the batch) before queueing the next one.
+static int run_deferred(kc_ctx* c, const PackedView& sv, uint64_t syms, int mode, const TableView& tv,
+                        const BloomView& bv, hipStream_t s) {
+    PartBufs pb = c->pb;
+    pb.b2t = c->defer_g * pb.B2;
+    pb.b2off = c->defer_n * pb.B2;
+    HIPCHK(c, launch_count_partitioned(sv, syms, c->cfg.k, mode, tv, bv, c->d_ctr, pb, c->table_fresh, s, PH_L12));
+    c->defer_n++;
+    unsigned long long f[2] = {0, 0};
+    HIPCHK(c, hipMemcpyAsync(&f[0], &c->d_ctr->part_overflow, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(&f[1], &c->d_ctr->spill_n, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    const bool tail = f[0] != 0 || f[1] != 0;
+    if (!tail && c->defer_n < c->defer_g && !c->defer_last) return KC_OK;
+    int rc = flush_deferred(c, sv, syms, mode, tv, bv, pb, s, f[0] != 0);
+    if (rc) return rc;
+    if (tail)
+        HIPCHK(c, launch_count_partitioned(sv, syms, c->cfg.k, mode, tv, bv, c->d_ctr, c->pb, c->table_fresh, s,
+                                           PH_TAIL));
     return KC_OK;
 }
 
@@ -749,6 +808,11 @@ static int run_batch(kc_ctx* c, const uint8_t* src, uint64_t used, uint64_t nchu
                                                c->bloom_fresh, keep ? 1 : 0, s, PH_TAIL));
         c->bloom_fresh = false;
         c->reuse_kept = keep;
+    } else if (mode != 1 && c->defer_on) {  // (device_pass chose the partitioned segmented path)
+        int rc = ensure_part(c, std::max(syms, c->defer_syms), true, 0, c->defer_g);
+        if (rc) return rc;
+        if (c->pb.cap1 == 0) return c->fail(KC_ERR_STATE, "deferred level 3 without segmented levels");
+        if ((rc = run_deferred(c, sv, syms, mode, tv, bv, s))) return rc;
     } else if (mode != 1 && use_partitioned(c, syms)) {
         const char* env = std::getenv("KC_INSERT_PATH");
         int rc = ensure_part(c, syms, !(env && !std::strcmp(env, "exact")));
@@ -1003,6 +1067,55 @@ static int count_reused(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, s
     return KC_OK;
 }
 
+// The deferred level 3's group size for a counting pass over chunks (device_pass splits them into
+// batches of batch_bytes / max_chunks): the batches' largest symbol bound fixes the segment
+// geometry of every slot; a group takes as many batches as KC_DEFER_FRAC (0.5) of the free HBM
+// holds level-2 segments for, at most MAX_SEG_GROUP segments per region.  KC_DEFER=0: off.
+static int plan_deferral(kc_ctx* c, const kc_chunk* chunks, size_t n) {
+    static const double frac = [] {
+        const char* v = std::getenv("KC_DEFER");
+        if (v && *v == '0') return 0.0;
+        const char* f = std::getenv("KC_DEFER_FRAC");
+        const double x = f ? std::atof(f) : 0.5;
+        return x >= 0 && x <= 0.9 ? x : 0.5;
+    }();
+    if (frac == 0 || !c->nbuckets || !c->seg_ok) return KC_OK;
+    const char* env = std::getenv("KC_INSERT_PATH");
+    if (env && (!std::strcmp(env, "direct") || !std::strcmp(env, "exact"))) return KC_OK;
+    if (c->cfg.bf_enable && !c->bloom_blocked && c->cfg.mode != 1) return KC_OK;  // (gate at level 1: not deferred)
+    uint64_t nb = 0, syms = 0, used = 0, cnt = 0;
+    for (size_t i = 0; i <= n; i++) {
+        const bool end = i == n;
+        const uint64_t need = end ? 0 : round_up(chunks[i].len, TILE);
+        if (!end && chunks[i].len == 0) continue;
+        if (end || used + need > c->batch_bytes || cnt + 1 > c->max_chunks) {
+            if (cnt) {
+                nb++;
+                syms = std::max(syms, used + cnt);
+            }
+            used = cnt = 0;
+        }
+        used += need;
+        cnt++;
+    }
+    if (nb < 2 || !use_partitioned(c, syms)) return KC_OK;
+    int rc = ensure_part(c, syms, true);  // one slot: the segment geometry
+    if (rc) return rc;
+    if (c->pb.cap1 == 0) return KC_OK;
+    const uint64_t slot_bytes = c->R * c->pb.B2 * c->pb.cap2 * c->W * 8;
+    size_t fr = 0, tot = 0;
+    HIPCHK(c, hipMemGetInfo(&fr, &tot));
+    const double avail = frac * ((double)fr + (double)c->k2_words * 8.0 - (double)(2ull << 30));
+    uint64_t g = avail > 0 ? (uint64_t)(avail / (double)slot_bytes) : 0;
+    if (const char* v = std::getenv("KC_DEFER_G")) g = std::strtoull(v, nullptr, 10);  // (tests: small groups)
+    g = std::min<uint64_t>({g, nb, MAX_SEG_GROUP / std::max<uint32_t>(1, c->pb.B2)});
+    if (g < 2) return KC_OK;
+    c->defer_on = true;
+    c->defer_g = (uint32_t)g;
+    c->defer_syms = syms;
+    return KC_OK;
+}
+
 static int device_pass(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, size_t n, int fmt, int pass,
                        hipStream_t s) {
     if (fmt != KC_FMT_FASTA && fmt != KC_FMT_FASTQ && fmt != KC_FMT_PLAIN) return c->fail(KC_ERR_ARG, "unknown format");
@@ -1027,6 +1140,15 @@ static int device_pass(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, si
     }
     // level-1 reuse: the Bloom pass keeps its level-1 output if it is the job's only batch
     const bool keep = pass == 1 && c->bloom_batches == 0 && reuse_enabled() && single;
+    // a counting pass of several batches defers level 3 (kc_ctx defer_*) when the segmented levels
+    // run and HBM holds at least two batches' level-2 segments beside everything else
+    c->defer_on = false;
+    c->defer_n = 0;
+    if (pass == 0 && !single) {
+        rc = plan_deferral(c, chunks, n);
+        if (rc) return rc;
+    }
+    bool last = false;
     auto launch = [&]() -> int {
         if (batch.empty()) return KC_OK;
         // descriptors go through the (idle) pinned desc buffer of the current slot
@@ -1060,6 +1182,8 @@ static int device_pass(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, si
         }
         // the host gate of the batch's tail (the call waits for the batch) only for a one-batch
         // image; the batches of a larger image keep the device gate (kc_api.h: kc_count_device)
+        // -- or a deferred pass, which reads each batch's flags
+        c->defer_last = last;
         int r = run_batch(c, img, used, batch.size(), fmt, pass, s, e0, e1, keep, single);
         if (keep) HIPCHK(c, hipStreamWaitEvent(s, c->aev[1], 0));  // (before an error return, too)
         if (r) return r;
@@ -1092,7 +1216,9 @@ static int device_pass(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, si
         used += need;
         if (pass == 0) { c->n_chunks++; c->n_bytes += chunks[i].len; }
     }
+    last = true;
     rc = launch();
+    c->defer_on = false;
     if (rc) return rc;
     if (s != c->stream) {
         HIPCHK(c, hipEventRecord(c->xev, s));
@@ -1856,6 +1982,7 @@ int kc_finish(kc_ctx* c, kc_stats* st) {
         st->reused_passes = c->reuse_hits;
         st->reuse_level = (uint64_t)c->reuse_last_level;
         st->route_counts_kept = c->route_counts_kept;
+        st->deferred_level3 = c->defer_groups;
         st->bytes = c->n_bytes;
         // occupied slots
         if (c->nbuckets) {
@@ -1949,6 +2076,8 @@ int kc_reset(kc_ctx* c) {
     c->reuse_hits = 0;
     c->reuse_last_level = 0;
     c->route_counts_kept = 0;
+    c->defer_groups = 0;
+    c->defer_n = 0;
     return KC_OK;
 }
 

@@ -1484,7 +1484,9 @@ __global__ __launch_bounds__(NT, (2048 / NT > 8 ? 8 : 2048 / NT)) void k_p2f(Tab
     const uint32_t s_lo = (uint32_t)((uint64_t)j * pb.nblk1 / pb.B2);
     const uint32_t nseg = (uint32_t)((uint64_t)(j + 1) * pb.nblk1 / pb.B2) - s_lo;
     const uint64_t seg0 = (uint64_t)c * pb.nblk1 + s_lo;  // level-1 segment index of cursor 0
-    const OutSeg o{(uint64_t)pb.B2 * pb.cap2, ((uint64_t)c * F * pb.B2 + j) * pb.cap2, pb.cap2,
+    // output segment of region r: r * B2T + jo (a deferred level 3 keeps several batches' segments)
+    const uint32_t B2T = pb.b2t ? pb.b2t : pb.B2, jo = pb.b2off + j;
+    const OutSeg o{(uint64_t)B2T * pb.cap2, ((uint64_t)c * F * B2T + jo) * pb.cap2, pb.cap2,
                    pb.spill, pb.spill_cap, &ctr->spill_n, &ctr->part_overflow, REC};
     for (uint32_t i = tid; i <= nseg; i += NT) pre[i] = i < nseg ? pb.hist1[seg0 + i] : 0;
     uint32_t* xlo = pre + nseg + 1;  // REC6: xlo of the F regions of coarse bin c
@@ -1576,7 +1578,7 @@ __global__ __launch_bounds__(NT, (2048 / NT > 8 ? 8 : 2048 / NT)) void k_p2f(Tab
     __syncthreads();  // the last write-out read lim / gbase
     stp.flush(1);
     for (uint32_t b = tid; b < F; b += NT)
-        pb.hist2[((uint64_t)c * F + b) * pb.B2 + j] = (uint32_t)(scatter_seg_next(l, b) - o.start(b));
+        pb.hist2[((uint64_t)c * F + b) * B2T + jo] = (uint32_t)(scatter_seg_next(l, b) - o.start(b));
 }
 
 // LDS image of a region: the 16-byte chunks of each 128-byte bucket are XOR-swizzled
@@ -3257,7 +3259,13 @@ static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf
     pb.rec6 = W == 1 && t.R >= (1ULL << 16) && !std::getenv("KC_NO_REC6");
     // two-word keys: 12-byte records at each level whose bins span few enough values of x
     if constexpr (W == 2) set_rec12_table(pb, t, k);
-    if (phase & PH_MAIN) {
+    if (phase & PH_L3) {  // the deferred level 3 of a group of batches: B2 = the group's segments
+        PartBufs p3 = pb;
+        p3.B2 = pb.b2t;
+        p3.b2t = p3.b2off = 0;
+        if ((e = launch_p3<W, true, false, GATE3>(t, ctr, p3, nullptr, fresh, s, bf)) != hipSuccess) return e;
+    }
+    if (phase & (PH_MAIN | PH_L12)) {
     hipLaunchKernelGGL(k_batch_begin, dim3(1), dim3(1), 0, s, ctr);
     const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
     auto k1 = k_p1<W, MODE, true, BinRegion, OutSeg, scatter_threads<W>()>;
@@ -3283,7 +3291,8 @@ static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf
     hipLaunchKernelGGL(k1, dim3(pb.nblk1), dim3(scatter_threads<W>()), sm1, s, sym, k, bf, ctr, pb, t.F1, coarse_bins(t),
                        pb.keys1, pk, pkm1, o1, (const unsigned long long*)nullptr, 1);
     if ((e = launch_p2f<W>(t, pb, ctr, 1, s, p2f_pad)) != hipSuccess) return e;
-    if ((e = launch_p3<W, true, false, GATE3>(t, ctr, pb, nullptr, fresh, s, bf)) != hipSuccess) return e;
+    if (phase & PH_MAIN)
+        if ((e = launch_p3<W, true, false, GATE3>(t, ctr, pb, nullptr, fresh, s, bf)) != hipSuccess) return e;
     }
     if (!(phase & PH_TAIL)) return hipGetLastError();
     // the skew lists (MODE 2 rolls its windows: no heavy records); the segmented level 3

@@ -82,6 +82,8 @@ struct DevCounters {
     // table, added to `inserted` when the counting pass confirms the same input (kc_api.cpp)
     unsigned long long spec_inserted;   uint64_t _p17[15];
     unsigned long long spec_overflow;   uint64_t _p18[15];  // keys the fused pass could not place
+    // deferred level 3: a batch's part_overflow held aside while the group's level 3 runs
+    unsigned long long held_overflow;   uint64_t _p19[15];
 };
 
 // The symbol stream: 32 symbols per word, symbol j of word w at bits 62-2j of pk[w]
@@ -136,6 +138,12 @@ struct PartBufs {
     uint32_t* own_hist;
     uint32_t own_parts;
     uint64_t own_nblk;
+    // deferred level 3 (kc_api.cpp run_batch): the level-2 segments of several batches of one image
+    // stay in keys2 and one level-3 pass inserts them all, i.e. one sweep of the table per group of
+    // batches instead of per batch.  Level 2 writes segment r * b2t + b2off + j of region r (b2t = 0:
+    // B2 and no offset, one batch); the deferred level 3 runs with B2 = b2t.
+    uint32_t b2t;
+    uint32_t b2off;
 };
 constexpr int R12_P1 = 1, R12_IN = 2, R12_OUT = 4, R12_L2 = 8;
 // R12_REG: the records are in the table's own geometry (the counting pass's levels): a bin's
@@ -219,6 +227,9 @@ constexpr int PH_MAIN = 1, PH_TAIL = 2, PH_ALL = 3;
 // Bloom pass only: the main phase's partition levels without its level 3 (k_b3), and k_b3 alone
 // (the host runs the fused pass, launch_bloom_count_fused, or k_b3 in between)
 constexpr int PH_LEVELS = 4, PH_B3 = 8;
+// Counting pass, deferred level 3 (segmented layout): the batch's levels 1-2 into its slot of the
+// group's level-2 segments (PartBufs b2t / b2off), and level 3 over the whole group (pb.B2 = b2t)
+constexpr int PH_L12 = 16, PH_L3 = 32;
 hipError_t launch_count_partitioned(PackedView sv, uint64_t sym_bound, int k, int mode, TableView t,
                                     BloomView bf, DevCounters* ctr, PartBufs pb, int fresh, hipStream_t s,
                                     int phase = PH_ALL);
@@ -259,6 +270,8 @@ hipError_t launch_count_records(int W, const uint64_t* rec, uint64_t n, TableVie
                                 PartBufs pb, int fresh, int gate, hipStream_t s);
 // ctr->inserted += ctr->spec_inserted (the counting pass confirmed the fused pass's input)
 hipError_t launch_spec_commit(DevCounters* ctr, uint64_t windows, hipStream_t s);
+// deferred level 3: part_overflow -> held_overflow (and cleared), or back (restore)
+hipError_t launch_hold_overflow(DevCounters* ctr, int restore, hipStream_t s);
 // 64-bit checksum of the chunks' bytes (a promise check between two passes over one image):
 // CHECKSUM_SLOTS partial sums in out (their sum is the checksum)
 constexpr int CHECKSUM_SLOTS = 64;

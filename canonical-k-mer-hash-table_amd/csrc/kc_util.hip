@@ -147,4 +147,22 @@ hipError_t launch_spec_commit(DevCounters* ctr, uint64_t windows, hipStream_t s)
     return hipGetLastError();
 }
 
+// deferred level 3 (kc_api.cpp run_deferred): a batch whose segments overflowed holds its
+// part_overflow aside while the group's level 3 inserts the other batches (k_p3 skips on the
+// flag), then gets it back for its tail (the exact pipeline redoes that batch)
+__global__ void k_hold_overflow(DevCounters* ctr, int restore) {
+    if (restore) {
+        ctr->part_overflow = ctr->held_overflow;
+        ctr->held_overflow = 0;
+    } else {
+        ctr->held_overflow = ctr->part_overflow;
+        ctr->part_overflow = 0;
+    }
+}
+
+hipError_t launch_hold_overflow(DevCounters* ctr, int restore, hipStream_t s) {
+    hipLaunchKernelGGL(k_hold_overflow, dim3(1), dim3(1), 0, s, ctr, restore);
+    return hipGetLastError();
+}
+
 }  // namespace kc

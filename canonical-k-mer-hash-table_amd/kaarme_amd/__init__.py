@@ -95,7 +95,7 @@ class kc_stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in (
         "windows", "inserted", "distinct", "table_slots", "bf_windows", "bf_bits", "new_in_first",
         "new_in_second", "failed_in_first", "chunks", "bytes", "part_fallbacks", "spilled", "heavy_records",
-        "reused_passes", "reuse_level", "route_counts_kept")]
+        "reused_passes", "reuse_level", "route_counts_kept", "deferred_level3")]
 
     def as_dict(self) -> dict:
         return {n: int(getattr(self, n)) for n, _ in self._fields_}

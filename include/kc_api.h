@@ -92,6 +92,9 @@ typedef struct {
                                  1 (levels 2-3), 0 = no reuse */
     uint64_t route_counts_kept; /* kc_route_table_device calls that took the per-block owner counts the
                                    counting passes kept (kc_route_hint) instead of running a count pass */
+    uint64_t deferred_level3;   /* level-3 passes of counting passes over several staging batches that
+                                   inserted a group of batches' level-2 partitions at once (one table
+                                   sweep per group, not per batch; KC_DEFER=0 disables it) */
 } kc_stats;
 
 /* Creates the device table (PointerHashTableCanonicalAV ctor,
