@@ -138,6 +138,9 @@ struct kc_ctx {
     unsigned long long reuse_sum = 0; // checksum of the Bloom pass's chunk bytes
     uint64_t reuse_windows = 0;       // windows of that batch
     unsigned long long* d_sum = nullptr;  // CHECKSUM_SLOTS partial sums (+ CHECKSUM_SLOTS for kc_bloom_estimate)
+    // the counting pass's checksum of its bytes, copied back on the aux stream: context memory, so
+    // a call that returns before waiting for that copy leaves it no dangling destination
+    unsigned long long h_part[CHECKSUM_SLOTS] = {};
     uint32_t* d_hll = nullptr;            // HLL_M registers of kc_estimate_distinct_device
     // compact representation (kc_compact): slot words, chain-start keys, counters
     uint64_t* d_cwords = nullptr;
@@ -151,15 +154,7 @@ struct kc_ctx {
     TableView fgeo{};                     // the kept partitions' fine geometry (powers of two)
     uint64_t fgeo_max_R = 0;              // the create-time fine regions (the most the LDS fits)
     uint64_t fgeo_next_R = 0;             // fine regions learned from the last finalize (0 = keep)
-    int reuse_level = 0;                  // kc_bloom_finalize: 3 = counted by the fused pass, 2 = from level 2,
-                                          // 1 = from level 1
-    // Fused Bloom + counting pass (run_batch): the kept batch's table counted during the Bloom
-    // pass itself (launch_bloom_count_fused), "speculatively": it stands only if the counting
-    // pass presents the same input (count_reused, level 3); any other use of the table first
-    // drops it (settle_spec).  The table's size comes from a sample of the kept fine bins
-    // (launch_bloom_probe); the reference's 2 * new_in_second stays the job's min_slots.
-    bool spec_table = false;
-    uint32_t* d_probe = nullptr;          // PROBE_BINS sample counts
+    int reuse_level = 0;                  // kc_bloom_finalize: 2 = from level 2, 1 = from level 1
     uint64_t reuse_hits = 0;          // counting passes that reused (kc_stats.reused_passes)
     int reuse_last_level = 0;         // the level the last reused pass started from (kc_stats.reuse_level)
 
@@ -273,7 +268,7 @@ static int own_prep(kc_ctx* c) {
 
 // After a write into the table: the kept per-block counts stay valid through level-3 passes
 // (k_p3 rewrites the counts of every region it writes; a fresh pass writes every region) and
-// are lost by any other writer (direct atomics, the fused pass, the merge inserts)
+// are lost by any other writer (direct atomics, the merge inserts)
 static void own_after_write(kc_ctx* c, bool level3, bool fresh) {
     if (!level3) c->own_valid = false;
     else if (fresh) c->own_valid = c->pb.own_parts != 0;
@@ -376,34 +371,6 @@ static int alloc_regions(kc_ctx* c) {
     return own_prep(c);
 }
 
-// the fused pass's table: exactly R regions (a power of two), coarse bins = min(f1, R) of them
-static int alloc_table_pow2(kc_ctx* c, uint64_t R, uint32_t f1) {
-    int rb = 0, fb = 0;
-    while ((1ULL << rb) < R) rb++;
-    while ((1u << fb) < f1) fb++;
-    fb = std::min(fb, rb);
-    c->f2bits = rb - fb;
-    c->F2 = 1u << c->f2bits;
-    c->F1 = 1u << fb;
-    c->R = R;
-    c->seg_ok = true;
-    return alloc_regions(c);
-}
-
-// Drop the fused pass's speculative table before anything but the confirming counting pass
-// uses the table: before kc_bloom_finalize there is no table yet; after it, the table the
-// reference would have (2 * new_in_second slots), fresh.
-static int settle_spec(kc_ctx* c) {
-    if (!c->spec_table) return KC_OK;
-    c->spec_table = false;
-    c->reuse_ok = false;
-    if (!c->bloom_final) {
-        c->nbuckets = 0;
-        return KC_OK;
-    }
-    return alloc_table(c, c->min_slots);
-}
-
 static TableView table_view(const kc_ctx* c) {
     TableView tv;
     tv.buckets = c->d_table;
@@ -420,8 +387,6 @@ static TableView table_view(const kc_ctx* c) {
 // Perform a deferred table reset before the table is read or updated by anything but a
 // fresh level-3 pass.
 static int materialize_zero(kc_ctx* c, hipStream_t s) {
-    const int rc = settle_spec(c);
-    if (rc) return rc;
     if (!c->table_zero_pending || !c->d_table) return KC_OK;
     HIPCHK(c, hipMemsetAsync(c->d_table, 0, c->nbuckets * BUCKET_WORDS * sizeof(uint64_t), s));
     c->table_zero_pending = false;
@@ -538,13 +503,29 @@ static int ensure_part(kc_ctx* c, uint64_t syms, bool seg, uint32_t bins1 = 0, u
     return ensure_part_geo(c, syms, seg, table_geo(c), c->pb, c->pb_cap, bins1, slots);
 }
 
+// KC_INSERT_PATH (tests, include/kc_api.h knobs): direct | partitioned | exact forces one insert
+// path for every batch; unset = chosen per batch by the cost rules below
+enum class PathKnob { Auto, Direct, Partitioned, Exact };
+static PathKnob insert_path_knob() {
+    const char* v = std::getenv("KC_INSERT_PATH");
+    if (!v) return PathKnob::Auto;
+    if (!std::strcmp(v, "direct")) return PathKnob::Direct;
+    if (!std::strcmp(v, "partitioned")) return PathKnob::Partitioned;
+    if (!std::strcmp(v, "exact")) return PathKnob::Exact;
+    return PathKnob::Auto;
+}
+// KC_DEBUG=1: the host's decisions (partition reuse, deferred level 3) on stderr
+static bool debug_on() {
+    const char* v = std::getenv("KC_DEBUG");
+    return v && *v && *v != '0';
+}
+
 // Insert path per batch: the partitioned pipeline moves ~(4W+1)*8 bytes per window
 // plus two sweeps of the table; the direct path is bound by scattered device atomics
 // (~20 G/s on MI355X, i.e. ~275 bytes-equivalent per window at ~5.5 TB/s).
 static bool use_partitioned(const kc_ctx* c, uint64_t syms) {
-    const char* env = std::getenv("KC_INSERT_PATH");
-    if (env && !std::strcmp(env, "direct")) return false;
-    if (env && (!std::strcmp(env, "partitioned") || !std::strcmp(env, "exact"))) return true;
+    const PathKnob p = insert_path_knob();
+    if (p != PathKnob::Auto) return p != PathKnob::Direct;
     const double table_bytes = (double)c->nbuckets * 128.0;
     return (double)syms * 275.0 > (double)syms * (4.0 * c->W + 1) * 8.0 + 2.0 * table_bytes;
 }
@@ -553,9 +534,8 @@ static bool use_partitioned(const kc_ctx* c, uint64_t syms) {
 // times plus two sweeps of the filter; the direct pass costs a scattered 64-byte line
 // RMW with up to ceil(hf) device-scope atomics per window.
 static bool use_partitioned_bloom(const kc_ctx* c, uint64_t syms) {
-    const char* env = std::getenv("KC_INSERT_PATH");
-    if (env && !std::strcmp(env, "direct")) return false;
-    if (env && (!std::strcmp(env, "partitioned") || !std::strcmp(env, "exact"))) return true;
+    const PathKnob p = insert_path_knob();
+    if (p != PathKnob::Auto) return p != PathKnob::Direct;
     const double filter_bytes = (double)bloom_words(c) * 4.0;
     return (double)syms * 275.0 > (double)syms * 5.0 * 8.0 + 2.0 * filter_bytes;
 }
@@ -579,7 +559,7 @@ static hipStream_t pick_stream(kc_ctx* c, void* s) {
 // (the call waits for its batch) and launches the tail only when needed: ~20 idle kernel
 // launches and two region-grid passes less per batch (0.25 ms of C2's 15.9 ms step).  Images
 // of several batches and host chunks keep the device gate (their batches queue behind each
-// other).  KC_DEVICE_GATE=1 forces the device gate everywhere.
+// other).
 static int tail_needed(kc_ctx* c, hipStream_t s, bool* need) {
     unsigned long long f[2] = {0, 0};
     HIPCHK(c, hipMemcpyAsync(&f[0], &c->d_ctr->part_overflow, 8, hipMemcpyDeviceToHost, s));
@@ -636,56 +616,9 @@ static int run_deferred(kc_ctx* c, const PackedView& sv, uint64_t syms, int mode
     return KC_OK;
 }
 
-// The fused pass is opt-in (KC_FUSE=1): it measured slower than k_b3 + the gated k_p3 over the
-// kept partitions (C3: k_bf3 13.5 ms against 6.3 + 5.5 ms, profiles/r04_ab_fused.txt) -- its
-// filter phase runs 4x the workgroups of k_b3 over 4x smaller filter slices, and the count phase
-// waits for the slowest wave of the filter phase in every workgroup
-static bool fuse_enabled() {
-    const char* v = std::getenv("KC_FUSE");
-    return v && *v == '1';
-}
-
-// The fused pass's table regions from the probe's sample of the kept fine bins: the distinct
-// keys passing the gate, scaled to all fine bins, at a mean load of KC_FUSE_LOAD (0.7) of a
-// region's slots, as a power of two between the bounds the fused kernel needs (regions =
-// unions of fine bins, of whole filter blocks, <= 1024 blocks and MAX_SEG_GROUP segments
-// each).  0 = no fused pass (a sampled bin outgrew the probe, or the bounds cross).
-// KC_FUSE_R forces the region count (tests, A/B).
-static uint64_t fused_regions(const kc_ctx* c, const uint32_t* probe, uint32_t ns) {
-    uint64_t sum = 0;
-    for (uint32_t i = 0; i < ns; i++) {
-        if (probe[i] == ~0u) return 0;
-        sum += probe[i];
-    }
-    static const double load = [] {
-        const char* v = std::getenv("KC_FUSE_LOAD");
-        const double x = v ? std::atof(v) : 0.7;
-        return x > 0.05 && x <= 1.0 ? x : 0.7;
-    }();
-    const uint64_t nblocks = bloom_blocks(c->bf_bits), fine = c->fgeo.R;
-    const double est = (double)sum * (double)(fine / ns);
-    const uint64_t need = (uint64_t)std::ceil(est / (load * c->S * BPR));
-    uint64_t lo = std::max<uint64_t>(nblocks / BF_BLOCKS_PER_REGION,
-                                     fine * c->pbf.B2 / MAX_SEG_GROUP + (fine * c->pbf.B2 % MAX_SEG_GROUP != 0));
-    uint64_t rt = 1;
-    while (rt < std::max<uint64_t>(need, lo)) rt <<= 1;
-    // regions no finer than the fine bins: a fuller table (mean load up to 0.9; a region that
-    // overflows still only costs the fallback) rather than no fused pass
-    if (rt > fine && est <= 0.9 * (double)fine * c->S * BPR) rt = fine;
-    if (const char* v = std::getenv("KC_FUSE_R")) rt = std::strtoull(v, 0, 10);
-    if (std::getenv("KC_REUSE_DEBUG"))
-        std::fprintf(stderr, "fused sizing: probe sum %llu of %u bins, est %.0f, need %llu, lo %llu, rt %llu, fine %llu, "
-                     "nblocks %llu, B2 %u\n", (unsigned long long)sum, ns, est, (unsigned long long)need,
-                     (unsigned long long)lo, (unsigned long long)rt, (unsigned long long)fine,
-                     (unsigned long long)nblocks, c->pbf.B2);
-    if (rt == 0 || (rt & (rt - 1)) || rt > fine || rt > nblocks || rt < lo) return 0;
-    return rt;
-}
-
 static int run_batch(kc_ctx* c, const uint8_t* src, uint64_t used, uint64_t nchunks, int fmt, int pass, hipStream_t s,
                      hipEvent_t ev_start = nullptr, hipEvent_t ev_gather = nullptr, bool keep = false,
                      bool host_gate = false) {
-    if (std::getenv("KC_DEVICE_GATE")) host_gate = false;
     const uint64_t ntiles = used / TILE;
     if (ntiles == 0) return KC_OK;
     if (pass == 3) {  // the distinct-count sketch (kc_estimate_distinct_device): tokenize + k_hll
@@ -720,13 +653,8 @@ static int run_batch(kc_ctx* c, const uint8_t* src, uint64_t used, uint64_t nchu
         c->bloom_batches++;
         c->reuse_kept = false;
     }
-    {
-        const int rc = settle_spec(c);  // a second Bloom batch or a counting batch: not the fused pass's
-        if (rc) return rc;
-    }
     if (mode == 1 && c->bloom_blocked && use_partitioned_bloom(c, syms)) {
-        const char* env = std::getenv("KC_INSERT_PATH");
-        const bool seg = !(env && !std::strcmp(env, "exact"));
+        const bool seg = insert_path_knob() != PathKnob::Exact;
         keep = keep && seg;  // (the exact layout does not keep: its level 1 moves word 0 only)
         keep = keep && c->fgeo.R != 0;
         const PartGeo g = keep ? PartGeo{c->fgeo.F1, c->fgeo.F2, c->fgeo.R, c->W}
@@ -753,7 +681,7 @@ static int run_batch(kc_ctx* c, const uint8_t* src, uint64_t used, uint64_t nchu
         // two-word keys: the kept levels as 12-byte records (kc_count_impl.h Rec12) when a record
         // holds the table key's bits below its bin: hb + 1 + xb <= 32 at both levels
         c->pbf.rec12 = 0;
-        if (keep && c->W == 2 && !std::getenv("KC_NO_REC12")) {
+        if (keep && c->W == 2) {
             int f1 = 0, rb = 0;
             while ((1u << f1) < c->fgeo.F1) f1++;
             while ((1ULL << rb) < c->fgeo.R) rb++;
@@ -769,40 +697,10 @@ static int run_batch(kc_ctx* c, const uint8_t* src, uint64_t used, uint64_t nchu
             }
         }
         const bool split = host_gate && c->pbf.cap1 != 0;
-        // the fused Bloom + counting pass (k_bf3): the kept levels, a sizing probe, then one
-        // workgroup per table region does both passes -- unless the levels left a skew list
-        const bool fuse = split && keep && fuse_enabled() && c->cfg.mode != 1 && c->fgeo.R <= bv.nblocks;
-        if (std::getenv("KC_REUSE_DEBUG"))
-            std::fprintf(stderr, "bloom batch: split %d keep %d fine %llu nblocks %llu -> fuse %d\n", (int)split,
-                         (int)keep, (unsigned long long)c->fgeo.R, (unsigned long long)bv.nblocks, (int)fuse);
         bool tail = false;
-        if (fuse) {
-            HIPCHK(c, launch_bloom_partitioned(sv, c->cfg.k, c->W, bv, c->bgeo, c->fgeo, c->d_ctr, c->pbf,
-                                               c->bloom_fresh, 1, s, PH_LEVELS));
-            PartBufs pk = c->pbf;
-            pk.hist2 = c->d_keep_fill2;  // the kept fills (hist2 itself is the skew pass's scratch)
-            const uint32_t ns = (uint32_t)std::min<uint64_t>(PROBE_BINS, c->fgeo.R);
-            HIPCHK(c, launch_bloom_probe(c->W, bv, c->fgeo, pk, ns, c->bloom_fresh, c->d_probe, s));
-            uint32_t probe[PROBE_BINS];
-            HIPCHK(c, hipMemcpyAsync(probe, c->d_probe, ns * 4, hipMemcpyDeviceToHost, s));
-            if ((rc = tail_needed(c, s, &tail))) return rc;  // (its sync covers the probe's copy)
-            const uint64_t rt = tail ? 0 : fused_regions(c, probe, ns);
-            if (rt) {
-                if ((rc = alloc_table_pow2(c, rt, c->fgeo.F1))) return rc;
-                pk.B2 = (uint32_t)(c->fgeo.R / rt) * c->pbf.B2;
-                HIPCHK(c, launch_bloom_count_fused(c->W, bv, table_view(c), c->fgeo, pk, c->d_ctr, c->bloom_fresh, s));
-                c->spec_table = true;
-                own_after_write(c, false, true);
-                c->table_fresh = c->table_zero_pending = false;  // every region written
-            } else {
-                HIPCHK(c, launch_bloom_partitioned(sv, c->cfg.k, c->W, bv, c->bgeo, c->fgeo, c->d_ctr, c->pbf,
-                                                   c->bloom_fresh, 1, s, PH_B3));
-            }
-        } else {
-            HIPCHK(c, launch_bloom_partitioned(sv, c->cfg.k, c->W, bv, c->bgeo, c->fgeo, c->d_ctr, c->pbf,
-                                               c->bloom_fresh, keep ? 1 : 0, s, split ? PH_MAIN : PH_ALL));
-            if (split && (rc = tail_needed(c, s, &tail))) return rc;
-        }
+        HIPCHK(c, launch_bloom_partitioned(sv, c->cfg.k, c->W, bv, c->bgeo, c->fgeo, c->d_ctr, c->pbf, c->bloom_fresh,
+                                           keep ? 1 : 0, s, split ? PH_MAIN : PH_ALL));
+        if (split && (rc = tail_needed(c, s, &tail))) return rc;
         if (tail)
             HIPCHK(c, launch_bloom_partitioned(sv, c->cfg.k, c->W, bv, c->bgeo, c->fgeo, c->d_ctr, c->pbf,
                                                c->bloom_fresh, keep ? 1 : 0, s, PH_TAIL));
@@ -814,8 +712,7 @@ static int run_batch(kc_ctx* c, const uint8_t* src, uint64_t used, uint64_t nchu
         if (c->pb.cap1 == 0) return c->fail(KC_ERR_STATE, "deferred level 3 without segmented levels");
         if ((rc = run_deferred(c, sv, syms, mode, tv, bv, s))) return rc;
     } else if (mode != 1 && use_partitioned(c, syms)) {
-        const char* env = std::getenv("KC_INSERT_PATH");
-        int rc = ensure_part(c, syms, !(env && !std::strcmp(env, "exact")));
+        int rc = ensure_part(c, syms, insert_path_knob() != PathKnob::Exact);
         if (rc) return rc;
         const bool split = host_gate && c->pb.cap1 != 0;
         HIPCHK(c, launch_count_partitioned(sv, syms, c->cfg.k, mode, tv, bv, c->d_ctr, c->pb, c->table_fresh, s,
@@ -836,7 +733,7 @@ static int run_batch(kc_ctx* c, const uint8_t* src, uint64_t used, uint64_t nchu
         HIPCHK(c, launch_count(sv, syms, c->cfg.k, mode, tv, bv, c->d_ctr, s));
         if (mode == 1) c->bloom_fresh = false;
     }
-    if (mode != 1) c->table_fresh = false;
+    if (mode != 1 && !c->defer_on) c->table_fresh = false;  // (a deferred pass: its level 3 clears it)
     if (c->profiling) {
         HIPCHK(c, hipEventRecord(ev[3], s));
         c->ev_pending.push_back(ev);
@@ -906,7 +803,7 @@ static int count_reused(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, s
                         bool* done) {
     *done = false;
     if (img != c->reuse_img || fmt != c->reuse_fmt) {
-        if (std::getenv("KC_REUSE_DEBUG")) std::fprintf(stderr, "reuse: another image or format\n");
+        if (debug_on()) std::fprintf(stderr, "reuse: another image or format\n");
         return KC_OK;
     }
     std::vector<ChunkDesc> b;
@@ -958,54 +855,26 @@ static int count_reused(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, s
     HIPCHK(c, hipEventRecord(c->aev[0], s));
     HIPCHK(c, hipStreamWaitEvent(c->aux, c->aev[0], 0));
     HIPCHK(c, launch_checksum(img, c->d_chunks, (int)b.size(), max_len, c->d_sum, c->aux));
-    unsigned long long part[CHECKSUM_SLOTS];
-    HIPCHK(c, hipMemcpyAsync(part, c->d_sum, sizeof(part), hipMemcpyDeviceToHost, c->aux));
+    HIPCHK(c, hipMemcpyAsync(c->h_part, c->d_sum, sizeof(c->h_part), hipMemcpyDeviceToHost, c->aux));
     HIPCHK(c, hipEventRecord(c->aev[1], c->aux));
     auto same_bytes = [&](bool* same) -> int {  // waits for the checksum
         HIPCHK(c, hipEventSynchronize(c->aev[1]));
         unsigned long long sum = 0;
-        for (auto v : part) sum += v;
+        for (auto v : c->h_part) sum += v;
         *same = sum == c->reuse_sum;
-        if (!*same && std::getenv("KC_REUSE_DEBUG")) std::fprintf(stderr, "reuse: checksum differs\n");
+        if (!*same && debug_on()) std::fprintf(stderr, "reuse: checksum differs\n");
         return KC_OK;
     };
     if (ev[2]) HIPCHK(c, hipEventRecord(ev[2], s));
     bool same = false;
     const uint64_t syms = used + b.size();
-    if (c->reuse_level == 3) {  // the fused pass counted these bytes: its table stands
-        if ((rc = same_bytes(&same))) return rc;
-        if (!same) {
-            release();
-            return KC_OK;
-        }
-        HIPCHK(c, launch_spec_commit(c->d_ctr, c->reuse_windows, s));
-        own_after_write(c, false, false);
-        if (ev[3]) HIPCHK(c, hipEventRecord(ev[3], s));
-        c->spec_table = false;
-        c->table_fresh = false;
-        c->table_zero_pending = false;
-        c->n_chunks += b.size();
-        c->n_bytes += bytes;
-        c->reuse_hits++;
-        c->reuse_last_level = 3;
-        if (c->profiling) {
-            c->ev_pending.push_back(ev);
-            c->pending_symbols_bound.push_back(syms);
-        }
-        if (s != c->stream) {
-            HIPCHK(c, hipEventRecord(c->xev, s));
-            HIPCHK(c, hipStreamWaitEvent(c->stream, c->xev, 0));
-        }
-        *done = true;
-        return KC_OK;
-    }
     // the table's partition buffers for this batch, with the Bloom pass's partitions as its
     // level 1 (and level 2); the kept buffers must not have moved
     if ((rc = ensure_part(c, syms, true))) return rc;
     PartBufs pr = c->pb;
     if (pr.keys1 != c->pbf.keys1 || (c->reuse_level == 2 && pr.keys2 != c->pbf.keys2) || pr.nblk1 != c->pbf.nblk1 ||
         pr.B2 != c->pbf.B2 || pr.cap1 != c->pbf.cap1 || pr.cap1 == 0 || c->F1 != c->fgeo.F1) {
-        if (std::getenv("KC_REUSE_DEBUG")) std::fprintf(stderr, "reuse: partition geometry differs\n");
+        if (debug_on()) std::fprintf(stderr, "reuse: partition geometry differs\n");
         HIPCHK(c, hipEventSynchronize(c->aev[1]));
         release();
         return KC_OK;
@@ -1041,7 +910,7 @@ static int count_reused(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, s
         // other bytes than the Bloom pass's, a full skew list, or a region of the table sized for
         // the gated k-mers that overflowed: the ordinary counting pass redoes the batch into a
         // fresh reference-sized table (2 * new_in_second), with the counters as they were
-        if (std::getenv("KC_REUSE_DEBUG") && same)
+        if (debug_on() && same)
             std::fprintf(stderr, "reuse: %s, redo\n", ovf ? "level 2 overflowed" : "table region overflowed");
         HIPCHK(c, hipMemcpyAsync(c->d_ctr, &before, sizeof(before), hipMemcpyHostToDevice, s));
         HIPCHK(c, hipStreamSynchronize(s));
@@ -1072,17 +941,12 @@ static int count_reused(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, s
 // geometry of every slot; a group takes as many batches as KC_DEFER_FRAC (0.5) of the free HBM
 // holds level-2 segments for, at most MAX_SEG_GROUP segments per region.  KC_DEFER=0: off.
 static int plan_deferral(kc_ctx* c, const kc_chunk* chunks, size_t n) {
-    static const double frac = [] {
-        const char* v = std::getenv("KC_DEFER");
-        if (v && *v == '0') return 0.0;
-        const char* f = std::getenv("KC_DEFER_FRAC");
-        const double x = f ? std::atof(f) : 0.5;
-        return x >= 0 && x <= 0.9 ? x : 0.5;
-    }();
-    if (frac == 0 || !c->nbuckets || !c->seg_ok) return KC_OK;
-    const char* env = std::getenv("KC_INSERT_PATH");
-    if (env && (!std::strcmp(env, "direct") || !std::strcmp(env, "exact"))) return KC_OK;
-    if (c->cfg.bf_enable && !c->bloom_blocked && c->cfg.mode != 1) return KC_OK;  // (gate at level 1: not deferred)
+    // KC_DEFER: 0 = off, N = groups of at most N batches (tests)
+    const char* kd = std::getenv("KC_DEFER");
+    const uint64_t kmax = kd ? std::strtoull(kd, nullptr, 10) : ~0ULL;
+    if (kmax == 0 || !c->nbuckets || !c->seg_ok) return KC_OK;
+    const PathKnob pk = insert_path_knob();
+    if (pk == PathKnob::Direct || pk == PathKnob::Exact) return KC_OK;
     uint64_t nb = 0, syms = 0, used = 0, cnt = 0;
     for (size_t i = 0; i <= n; i++) {
         const bool end = i == n;
@@ -1105,10 +969,12 @@ static int plan_deferral(kc_ctx* c, const kc_chunk* chunks, size_t n) {
     const uint64_t slot_bytes = c->R * c->pb.B2 * c->pb.cap2 * c->W * 8;
     size_t fr = 0, tot = 0;
     HIPCHK(c, hipMemGetInfo(&fr, &tot));
-    const double avail = frac * ((double)fr + (double)c->k2_words * 8.0 - (double)(2ull << 30));
+    const double avail = 0.5 * ((double)fr + (double)c->k2_words * 8.0 - (double)(2ull << 30));
     uint64_t g = avail > 0 ? (uint64_t)(avail / (double)slot_bytes) : 0;
-    if (const char* v = std::getenv("KC_DEFER_G")) g = std::strtoull(v, nullptr, 10);  // (tests: small groups)
-    g = std::min<uint64_t>({g, nb, MAX_SEG_GROUP / std::max<uint32_t>(1, c->pb.B2)});
+    g = std::min<uint64_t>({g, kmax, nb, MAX_SEG_GROUP / std::max<uint32_t>(1, c->pb.B2)});
+    if (debug_on())
+        std::fprintf(stderr, "deferred level 3: %llu batches, slot %.2f GB, free %.1f GB -> groups of %llu\n",
+                     (unsigned long long)nb, slot_bytes / 1e9, fr / 1e9, (unsigned long long)g);
     if (g < 2) return KC_OK;
     c->defer_on = true;
     c->defer_g = (uint32_t)g;
@@ -1305,16 +1171,12 @@ int kc_create(const kc_config* cfg, kc_ctx** out) {
         if (hipMalloc(&c->d_bloom, words * 4) != hipSuccess)
             return bail(KC_ERR_NOMEM, "Bloom filter allocation failed");
         if (hipMemsetAsync(c->d_bloom, 0, words * 4, c->stream) != hipSuccess) return bail(KC_ERR_HIP, "memset");
-        if (hipMalloc(&c->d_probe, PROBE_BINS * 4) != hipSuccess) return bail(KC_ERR_NOMEM, "probe allocation failed");
         c->bloom_fresh = true;
         if (c->bloom_blocked) {
             // filter regions of up to BF_BLOCKS_PER_REGION (1024) blocks = 64 KiB, F1 x F2 as
             // for the table (all powers of two here)
             const uint64_t nb = bloom_blocks(c->bf_bits);
-            // (KC_BF_REGION_BLOCKS: A/B of smaller filter regions, more k_b3 workgroups per CU)
-            const char* vr = std::getenv("KC_BF_REGION_BLOCKS");
-            const uint64_t rb = vr ? std::max<uint64_t>(16, std::min<uint64_t>(1024, std::strtoull(vr, 0, 10))) : 1024;
-            const uint64_t R = std::max<uint64_t>(1, nb / rb);
+            const uint64_t R = std::max<uint64_t>(1, nb / BF_BLOCKS_PER_REGION);
             int rbits = 0;
             while ((1ULL << rbits) < R) rbits++;
             const int f1bits = std::min(10, (rbits + 1) / 2);
@@ -1349,15 +1211,11 @@ int kc_create(const kc_config* cfg, kc_ctx** out) {
                 }
                 if (fb >= rbits) {
                     c->fgeo_max_R = 1ULL << fb;
-                    // the job starts at no more than 2^16 fine bins (KC_FGEO_R): -u usually
-                    // overstates the k-mers that pass the gate (C3: -u 4e8 for 50 M), and
-                    // level 2's 256-bin scatter of C2's table is the fastest shape; the fused
-                    // pass sizes its table from the data and takes these bins whole
-                    const char* v = std::getenv("KC_FGEO_R");
-                    const uint64_t cap = v ? std::max<uint64_t>(1, std::strtoull(v, 0, 10)) : (1ULL << 16);
-                    while (fb > rbits && (1ULL << fb) > cap) fb--;
+                    // the job starts at no more than 2^16 fine bins: -u usually overstates the
+                    // k-mers that pass the gate (C3: -u 4e8 for 50 M), and level 2's 256-bin
+                    // scatter of C2's table is the fastest shape
+                    while (fb > rbits && (1ULL << fb) > (1ULL << 16)) fb--;
                     f1 = std::min(fb, std::min(8, (fb + 1) / 2 + 1));
-                    if (const char* vf = std::getenv("KC_FGEO_F1")) f1 = std::min(fb, std::max(1, std::atoi(vf)));  // A/B
                     while (f1 > 0 && p1_lds_bytes(c->W, 1u << f1) > p1_cap) f1--;
                     c->fgeo.R = 1ULL << fb;
                     c->fgeo.f2bits = fb - f1;
@@ -1394,7 +1252,6 @@ void kc_destroy(kc_ctx* c) {
     hipFree(c->d_ctr);
     hipFree(c->d_sum);
     hipFree(c->d_hll);
-    hipFree(c->d_probe);
     hipFree(c->d_cwords);
     hipFree(c->d_csecond);
     hipFree(c->d_cstat);
@@ -1463,42 +1320,8 @@ int kc_bloom_finalize(kc_ctx* c, uint64_t* new_in_second) {
     bool reuse = c->reuse_kept && c->bloom_batches == 1 && h.part_fallbacks == 0 && h.spilled == 0 && h.heavy == 0;
     const uint64_t slots = 2 * h.new_in_second;  // main.cpp:454
     c->reuse_level = 0;
-    if (c->spec_table && (!reuse || h.spec_overflow)) {
-        // a region of the fused pass's table overflowed (the probe underestimated it): the
-        // counting pass runs from the kept level 2 into the reference-sized table instead
-        c->spec_table = false;
-        if (std::getenv("KC_REUSE_DEBUG"))
-            std::fprintf(stderr, "fused pass dropped: %llu keys did not fit\n", (unsigned long long)h.spec_overflow);
-    }
-    if (c->spec_table) {
-        // the fused pass counted the batch: the table stands if the counting pass presents the
-        // same input (count_reused); min_slots stays the reference's 2 * new_in_second
-        unsigned long long part[CHECKSUM_SLOTS];
-        HIPCHK(c, hipMemcpy(part, c->d_sum, sizeof(part), hipMemcpyDeviceToHost));
-        c->reuse_sum = 0;
-        for (auto v : part) c->reuse_sum += v;
-        c->reuse_windows = h.bf_windows;
-        c->reuse_level = 3;
-        c->reuse_ok = true;
-        c->min_slots = slots;
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        return KC_OK;
-    }
-    // KC_BF_TABLE=fit: the counting pass from the kept partitions, which can redo itself into the
-    // reference-sized table (count_reused: a region that overflowed), takes a table sized for the
-    // k-mers the gate passes -- new_in_second plus 30 % -- instead of the reference's
-    // 2 * new_in_second.  Not the default: C3's 2^15 instead of 2^16 regions write 2.1 GB less but
-    // give the gated level 3 half the workgroups, twice the keys each (7.4 vs 5.5 ms,
-    // profiles/r04_ab6.txt).  KC_BF_TABLE=tiny (tests) forces the redo.
-    uint64_t phys = 0;
-    {
-        const char* v = std::getenv("KC_BF_TABLE");
-        if (reuse && v && !std::strcmp(v, "fit"))
-            phys = std::min<uint64_t>(slots, h.new_in_second + h.new_in_second * 3 / 10);
-        if (reuse && v && !std::strcmp(v, "tiny")) phys = std::max<uint64_t>(64, h.new_in_second / 8);  // (tests)
-    }
     if (reuse) {
-        uint64_t want = std::max<uint64_t>(phys ? phys : slots, 64);
+        uint64_t want = std::max<uint64_t>(slots, 64);
         want += want / 4;
         const uint64_t regions = std::max<uint64_t>(1, ((want + c->S - 1) / c->S + BPR - 1) / BPR);
         uint64_t rt = c->fgeo.F1;
@@ -1528,11 +1351,11 @@ int kc_bloom_finalize(kc_ctx* c, uint64_t* new_in_second) {
         c->reuse_windows = h.bf_windows;
     }
     c->reuse_ok = reuse;
-    if (std::getenv("KC_REUSE_DEBUG"))
+    if (debug_on())
         std::fprintf(stderr, "reuse finalize: kept %d batches %d fallbacks %llu spilled %llu heavy %llu -> level %d\n",
                      (int)c->reuse_kept, c->bloom_batches, (unsigned long long)h.part_fallbacks,
                      (unsigned long long)h.spilled, (unsigned long long)h.heavy, c->reuse_level);
-    rc = alloc_table(c, slots, reuse ? c->fgeo.F1 : 0, reuse ? phys : 0);
+    rc = alloc_table(c, slots, reuse ? c->fgeo.F1 : 0);
     if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return KC_OK;
@@ -1541,8 +1364,6 @@ int kc_bloom_finalize(kc_ctx* c, uint64_t* new_in_second) {
 int kc_count_chunk(kc_ctx* c, const uint8_t* buf, size_t len, int fmt, int bh) {
     if (!c) return KC_ERR_ARG;
     if (!c->nbuckets) return c->fail(KC_ERR_STATE, "kc_bloom_finalize must precede the counting pass");
-    const int rc = settle_spec(c);
-    if (rc) return rc;
     return add_host_chunk(c, buf, len, fmt, bh, 0);
 }
 
@@ -1555,8 +1376,6 @@ int kc_count_device(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, size_
         const int rc = count_reused(c, img, chunks, n, fmt, pick_stream(c, s), &done);
         if (rc || done) return rc;
     }
-    const int rc = settle_spec(c);  // (another input than the fused pass's)
-    if (rc) return rc;
     return device_pass(c, img, chunks, n, fmt, 0, pick_stream(c, s));
 }
 
@@ -1704,10 +1523,6 @@ int kc_route_table_device(kc_ctx* c, uint32_t nshards, uint64_t* dev_out, uint64
 
 int kc_insert_counts_device(kc_ctx* c, const uint64_t* recs, uint64_t n, void* sp) {
     if (!c || (!recs && n)) return KC_ERR_ARG;
-    {
-        const int r0 = settle_spec(c);
-        if (r0) return r0;
-    }
     if (!c->nbuckets) return c->fail(KC_ERR_STATE, "no table");
     hipStream_t s = pick_stream(c, sp);
     int rc = flush_host(c);
@@ -1749,10 +1564,6 @@ int kc_insert_counts_device(kc_ctx* c, const uint64_t* recs, uint64_t n, void* s
 int kc_insert_counts_runs_device(kc_ctx* c, const uint64_t* recs, const uint64_t* group_counts, uint32_t ngroups,
                                  void* sp) {
     if (!c || !group_counts || ngroups == 0 || ngroups > 64) return KC_ERR_ARG;
-    {
-        const int r0 = settle_spec(c);
-        if (r0) return r0;
-    }
     if (!c->nbuckets) return c->fail(KC_ERR_STATE, "no table");
     std::vector<uint64_t> gs(ngroups + 1, 0);
     uint64_t maxn = 0;
@@ -1823,7 +1634,6 @@ int kc_bloom_records_device(kc_ctx* c, const uint64_t* recs, uint64_t n, void* s
     hipStream_t s = pick_stream(c, sp);
     int rc = flush_host(c);
     if (rc) return rc;
-    if ((rc = settle_spec(c))) return rc;
     c->bloom_batches++;  // (a Bloom pass of records keeps no partitions)
     c->reuse_kept = false;
     if (n == 0) return KC_OK;
@@ -1857,10 +1667,6 @@ int kc_bloom_records_device(kc_ctx* c, const uint64_t* recs, uint64_t n, void* s
 
 int kc_count_records_device(kc_ctx* c, const uint64_t* recs, uint64_t n, void* sp) {
     if (!c || (!recs && n)) return KC_ERR_ARG;
-    {
-        const int r0 = settle_spec(c);
-        if (r0) return r0;
-    }
     if (!c->nbuckets) return c->fail(KC_ERR_STATE, "no table (kc_bloom_finalize must precede the counting pass)");
     const bool gate = c->cfg.bf_enable && c->cfg.mode != 1;  // -m 1 -b ignores the filter (main.cpp:482-489)
     if (gate && !c->bloom_blocked) return c->fail(KC_ERR_ARG, "records need the blocked Bloom layout");
@@ -1897,10 +1703,6 @@ int kc_count_records_device(kc_ctx* c, const uint64_t* recs, uint64_t n, void* s
 
 int kc_insert_keys_device(kc_ctx* c, const uint64_t* keys, uint64_t n, void* sp) {
     if (!c || (!keys && n)) return KC_ERR_ARG;
-    {
-        const int r0 = settle_spec(c);
-        if (r0) return r0;
-    }
     if (!c->nbuckets) return c->fail(KC_ERR_STATE, "no table");
     hipStream_t s = pick_stream(c, sp);
     int rc = flush_host(c);
@@ -2026,8 +1828,6 @@ static void drop_compact(kc_ctx* c) {
 
 int kc_clear_table(kc_ctx* c) {
     if (!c) return KC_ERR_ARG;
-    const int rc = settle_spec(c);
-    if (rc) return rc;
     if (!c->nbuckets) return c->fail(KC_ERR_STATE, "no table");
     c->table_zero_pending = true;  // deferred: see materialize_zero
     c->table_fresh = true;
@@ -2060,10 +1860,6 @@ int kc_reset(kc_ctx* c) {
     drop_compact(c);
     c->reuse_kept = c->reuse_ok = false;
     c->reuse_level = 0;
-    if (c->spec_table) {  // (a job's table is sized again after its Bloom pass)
-        c->spec_table = false;
-        if (!c->bloom_final) c->nbuckets = 0;
-    }
     if (c->fgeo_next_R && c->fgeo_next_R != c->fgeo.R && c->fgeo_next_R <= c->fgeo_max_R) {
         int fb = 0, f1 = 0;
         while ((1ULL << fb) < c->fgeo_next_R) fb++;
@@ -2622,7 +2418,6 @@ int kc_bloom_write(kc_ctx* c, const uint32_t* words, uint64_t n) {
     if (n > bloom_words(c)) return c->fail(KC_ERR_ARG, "more words than the filter holds");
     int rc = kc_sync(c);
     if (rc) return rc;
-    if ((rc = settle_spec(c))) return rc;  // the fused pass gated by the filter being replaced
     HIPCHK(c, hipMemcpy(c->d_bloom, words, n * 4, hipMemcpyHostToDevice));
     c->bloom_fresh = false;
     return KC_OK;
@@ -2683,7 +2478,6 @@ int kc_bloom_set_device(kc_ctx* c, const uint32_t* dev_src, uint64_t n_words, ui
     hipStream_t s = pick_stream(c, sp);
     int rc = after_host_work(c, s);
     if (rc) return rc;
-    if ((rc = settle_spec(c))) return rc;  // the fused pass gated by the local filter
     HIPCHK(c, hipMemcpyAsync(c->d_bloom, dev_src, n_words * 4, hipMemcpyDeviceToDevice, s));
     c->bloom_fresh = false;
     uint64_t est = 0;

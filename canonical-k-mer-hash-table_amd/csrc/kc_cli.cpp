@@ -48,6 +48,11 @@ struct Args {
     unsigned long long slots = 0, unique = 0;
     int device = 0;
     std::string gunzip_to;  // test hook: write the decompressed input there and exit (no GPU)
+    // extensions, not in --help: --host-chunks stages host chunks instead of one
+    // device image; --no-warmup skips the untimed warm-up pass; --readers N upload threads; --phases
+    // prints the counting pass's phase times on stderr
+    bool host_chunks = false, no_warmup = false, phases = false;
+    unsigned readers = 1;
 };
 
 void usage(const char* prog) {
@@ -188,6 +193,9 @@ int parse(int argc, char** argv, Args* a) {
         if (o == "-h" || o == "--help") { usage(argv[0]); return 0; }
         if (o == "-b" || o == "--use-bfilter") { a->use_bf = true; continue; }
         if (o == "--strict-capacity") { setenv("KC_STRICT_CAPACITY", "1", 1); continue; }  // kc_api.h
+        if (o == "--host-chunks") { a->host_chunks = true; continue; }
+        if (o == "--no-warmup") { a->no_warmup = true; continue; }
+        if (o == "--phases") { a->phases = true; continue; }
         if (o.size() > 1 && o[0] == '-' && !(o.size() > 1 && std::isdigit((unsigned char)o[1]))) {
             std::string v;
             if (!next(&v)) return cli_error(kRequired, o + " requires an argument");
@@ -226,6 +234,9 @@ int parse(int argc, char** argv, Args* a) {
             } else if (o == "--device") {
                 if (!parse_int(v, &si) || si < 0) return cli_error(kConversion, "Could not convert: " + o + " = " + v);
                 a->device = (int)si;
+            } else if (o == "--readers") {
+                if (!parse_int(v, &si) || si < 1 || si > 16) return cli_error(kConversion, "Could not convert: " + o + " = " + v);
+                a->readers = (unsigned)si;
             } else {
                 return cli_error(kExtras, "The following argument was not expected: " + o);
             }
@@ -295,8 +306,7 @@ struct Upload {
             d = nullptr;
             return false;
         }
-        const char* sv = std::getenv("KC_CLI_SLICE_MB");
-        slice = (uint64_t)std::max(1, sv ? std::atoi(sv) : 8) << 20;
+        slice = 8ull << 20;
         nslices = (size + slice - 1) / slice;
         readers = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(readers, nslices));
         // a slice per buffer no larger than the image: small inputs pin little
@@ -519,18 +529,16 @@ int main(int argc, char** argv) {
         std::exit(1);
     };
     using clk = std::chrono::high_resolution_clock;
-    // The image goes to HBM once (KC_CLI_HOST=1: stage host chunks instead): both passes
+    // The image goes to HBM once (--host-chunks: stage host chunks instead): both passes
     // then read it in place, and a Bloom job counts from the Bloom pass's partitions
     // (kc_api.h, partition reuse).  Its read is timed with the pass that needs it first,
-    // as the reference's reader thread is.
-    const bool host_path = std::getenv("KC_CLI_HOST") && std::atoi(std::getenv("KC_CLI_HOST")) != 0;
-    const char* rv = std::getenv("KC_CLI_READERS");
-    // (one reader: the C2 sample's timed build 25-28 ms after the warm-up below, against
-    // 32-35 ms with two and more with four; profiles/r04_cli_probe_{phases,warmup}.txt)
-    const unsigned readers = rv ? (unsigned)std::max(1, std::atoi(rv)) : 1u;
+    // as the reference's reader thread is.  (One reader by default: the C2 sample's timed build
+    // 25-28 ms after the warm-up below, against 32-35 ms with two and more with four;
+    // profiles/r04_cli_probe_{phases,warmup}.txt)
+    const bool host_path = a.host_chunks;
     Upload up;
-    const bool staged = !host_path && up.prepare(isize, a.device, readers);  // (untimed setup)
-    if (staged && !a.use_bf && !std::getenv("KC_CLI_NO_WARMUP")) {
+    const bool staged = !host_path && up.prepare(isize, a.device, a.readers);  // (untimed setup)
+    if (staged && !a.use_bf && !a.no_warmup) {
         // (untimed setup, as the reference's table allocation is) the GPU runtime's one-time
         // work -- loading the counting kernels' code, first launches -- on a one-read input,
         // then kc_reset: the timed pass starts on a warm device
@@ -574,7 +582,7 @@ int main(int argc, char** argv) {
                   << std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0).count() << " microseconds\n";
     }
     std::cout << "Starting " << (a.mode == 0 ? "atomic flag basic" : "atomic variable pointer") << " hash table\n";
-    const bool dbg = std::getenv("KC_CLI_DEBUG") != nullptr;  // phase times on stderr
+    const bool dbg = a.phases;  // phase times on stderr
     auto us = [](clk::time_point x, clk::time_point y) {
         return (long long)std::chrono::duration_cast<std::chrono::microseconds>(y - x).count();
     };

@@ -51,23 +51,6 @@ hipError_t launch_count_reuse(int W, TableView t, BloomView bf, DevCounters* ctr
     KC_DISPATCH_W(W, count_reuse(t, bf, ctr, pb, fresh, level, gate, windows, s));
 }
 
-hipError_t launch_bloom_count_fused(int W, BloomView bf, TableView t, TableView fg, PartBufs pb, DevCounters* ctr,
-                                    int fresh_filter, hipStream_t s) {
-    // table regions: a power of two, unions of fine bins, each the hash prefix of whole filter blocks
-    if (!bf.blocked || t.R == 0 || (t.R & (t.R - 1)) || fg.R % t.R || bf.nblocks % t.R || pb.B2 == 0 ||
-        pb.B2 > MAX_SEG_GROUP || bf.nblocks / t.R > (uint64_t)BF_BLOCKS_PER_REGION)
-        return hipErrorInvalidValue;
-    KC_DISPATCH_W(W, bloom_count_fused(bf, t, fg, pb, ctr, fresh_filter, s));
-}
-
-hipError_t launch_bloom_probe(int W, BloomView bf, TableView fg, PartBufs pb, uint32_t nsample, int fresh_filter,
-                              uint32_t* out, hipStream_t s) {
-    if (!bf.blocked || nsample == 0 || fg.R % nsample || bf.nblocks % fg.R || pb.B2 == 0 || pb.B2 > MAX_SEG_GROUP ||
-        bf.nblocks / fg.R > (uint64_t)BF_BLOCKS_PER_REGION)
-        return hipErrorInvalidValue;
-    KC_DISPATCH_W(W, bloom_probe(bf, fg, pb, nsample, fresh_filter, out, s));
-}
-
 hipError_t launch_bloom_records(int W, const uint64_t* rec, uint64_t n, BloomView bf, TableView ft, DevCounters* ctr,
                                 PartBufs pb, int fresh, hipStream_t s) {
     if (!bf.blocked || ft.R == 0 || bf.nblocks % ft.R || bf.nblocks / ft.R > (uint64_t)BF_BLOCKS_PER_REGION)

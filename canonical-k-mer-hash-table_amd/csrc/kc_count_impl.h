@@ -557,44 +557,6 @@ struct OutSeg {
 DEV uint64_t ks_load(const uint64_t* p) { return *p; }
 DEV void ks_store(uint64_t* p, uint64_t v) { *p = v; }
 
-// In-kernel phase stamps (measurement builds only, tools/probe: -DKC_STAMP=1): wave 0 of
-// each workgroup adds the cycles of every phase of the scatter into g_stamp[block][phase].
-#ifndef KC_STAMP
-#define KC_STAMP 0
-#endif
-struct Stamps {
-    unsigned long long last, acc[8];
-    DEV void init() {
-#if KC_STAMP
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(last)::"memory");
-        for (int i = 0; i < 8; i++) acc[i] = 0;
-#endif
-    }
-    DEV void mark(int i) {
-#if KC_STAMP
-        __builtin_amdgcn_sched_barrier(0);
-        unsigned long long t;
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-        __builtin_amdgcn_sched_barrier(0);
-        acc[i] += t - last;
-        last = t;
-#endif
-    }
-    DEV void flush(int part) {  // part 0: level 1, 1: level 2, 2: level 3
-#if KC_STAMP
-        if (threadIdx.x == 0)
-            for (int i = 0; i < 8; i++) atomicAdd(&g_stamp_buf()[(part * 2048 + (blockIdx.x & 2047)) * 8 + i], acc[i]);
-#endif
-    }
-#if KC_STAMP
-    static DEV unsigned long long* g_stamp_buf();
-#endif
-};
-#if KC_STAMP
-__device__ unsigned long long g_stamp[6144 * 8];
-DEV unsigned long long* Stamps::g_stamp_buf() { return g_stamp; }
-#endif
-
 // rank of this lane among the set lanes of a wave mask
 DEV uint32_t lane_rank(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -621,19 +583,16 @@ struct NoMid {
 // may load its next tile into them)
 template <int W, int RUNW, class Bin, class Out, int NT = COUNT_THREADS, class Mid = NoMid>
 DEV bool scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const Out& o, uint64_t (&tk)[RUNW][W],
-                      bool (&ok)[RUNW], uint64_t* __restrict__ out, Mid&& mid = Mid(), Stamps* stp = nullptr) {
+                      bool (&ok)[RUNW], uint64_t* __restrict__ out, Mid&& mid = Mid()) {
     __shared__ unsigned long long s_spbase;
     __shared__ uint32_t s_spills;  // some bin of the tile spills (set by the setup, read after a barrier)
     const int tid = threadIdx.x;
     uint32_t rank[RUNW];  // (the bins are recomputed below: one multiply, fewer registers)
-    if (KC_STAMP && stp) stp->mark(0);
     if (Out::kSeg && tid == 0) s_spills = 0;
 #pragma unroll
     for (int j = 0; j < RUNW; j++) rank[j] = ok[j] ? atomicAdd(&l.hist[bin(tk[j][0])], 1u) : 0;
-    if (KC_STAMP && stp) stp->mark(1);
     __syncthreads();
     block_excl_scan_lds<NT>(l.hist, l.start, F);
-    if (KC_STAMP && stp) stp->mark(2);
 #pragma unroll
     for (int j = 0; j < RUNW; j++)
         if (ok[j]) {
@@ -641,7 +600,6 @@ DEV bool scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const Out& o
 #pragma unroll
             for (int w = 0; w < W; w++) l.keys[slot * W + w] = tk[j][w];
         }
-    if (KC_STAMP && stp) stp->mark(3);
     // per bin: destination minus tile slot, the tile slots that fit the bin's output, and
     // the keys past its end
     bool spills = false;
@@ -655,7 +613,6 @@ DEV bool scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const Out& o
         spills |= fit < h;
     }
     if (Out::kSeg && spills) s_spills = 1;
-    if (KC_STAMP && stp) stp->mark(4);
     mid();
     __syncthreads();
     if constexpr (Out::kSeg) {
@@ -668,7 +625,6 @@ DEV bool scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const Out& o
             __syncthreads();
         }
     }
-    if (KC_STAMP && stp) stp->mark(5);
     const uint32_t n = l.start[F - 1] + l.hist[F - 1];
     for (uint32_t i = tid; i < n; i += NT) {
         uint64_t key[W];
@@ -692,14 +648,12 @@ DEV bool scatter_tile(const PartLds& l, uint32_t F, const Bin& bin, const Out& o
             }
         }
     }
-    if (KC_STAMP && stp) stp->mark(6);
     __syncthreads();
     for (uint32_t b = tid; b < F; b += NT) {
         l.gbase[b] += l.lim[b];  // past the keys written (a segment's fill never passes its end)
         l.hist[b] = 0;
     }
     __syncthreads();
-    if (KC_STAMP && stp) stp->mark(7);
     return false;
 }
 
@@ -791,23 +745,20 @@ struct StoreRec12 {
 
 template <int W, int RUNW, class Bin, class Out, int NT, class Mid = NoMid, class St = StoreWords, class Pre = NoMid>
 DEV void scatter_seg(const PartLds& l, uint32_t F, const Bin& bin, const Out& o, uint64_t (&tk)[RUNW][W],
-                     bool (&ok)[RUNW], uint64_t* __restrict__ out, Mid&& mid = Mid(), Stamps* stp = nullptr,
+                     bool (&ok)[RUNW], uint64_t* __restrict__ out, Mid&& mid = Mid(),
                      const St& store = St(), Pre&& pre = Pre()) {
     static_assert(NT * RUNW <= 65536, "ranks ride in 16 bits");
     __shared__ unsigned long long s_spbase;
     __shared__ uint32_t s_spills, s_n;
     const int tid = threadIdx.x, lane = tid & 63;
     uint32_t pk[RUNW];  // bin << 16 | rank in the bin, ~0 = no key
-    if (KC_STAMP && stp) stp->mark(0);
 #pragma unroll
     for (int j = 0; j < RUNW; j++) {
         const uint32_t b = bin(tk[j][0]);
         pk[j] = ok[j] ? (b << 16) | atomicAdd(&l.hist[b], 1u) : ~0u;
     }
     pre();
-    if (KC_STAMP && stp) stp->mark(1);
     __syncthreads();  // 1
-    if (KC_STAMP && stp) stp->mark(2);
     if (tid < 64) {
         if (F % 4 == 0) {  // (hist and start 16-byte aligned) four bins per 16-byte LDS access
             const uint32_t per = (F / 4 + 63) / 64, lo = min(F / 4, lane * per), hi = min(F / 4, lo + per);
@@ -841,7 +792,6 @@ DEV void scatter_seg(const PartLds& l, uint32_t F, const Bin& bin, const Out& o,
         if (Out::kSeg && lane == 0) s_spills = 0;
     }
     __syncthreads();  // 2
-    if (KC_STAMP && stp) stp->mark(3);
 #pragma unroll
     for (int j = 0; j < RUNW; j++)
         if (pk[j] != ~0u) {
@@ -862,7 +812,6 @@ DEV void scatter_seg(const PartLds& l, uint32_t F, const Bin& bin, const Out& o,
     }
     if (Out::kSeg && spills) s_spills = 1;
     mid();
-    if (KC_STAMP && stp) stp->mark(4);
     __syncthreads();  // 3
     if constexpr (Out::kSeg) {
         if (s_spills) {
@@ -874,7 +823,6 @@ DEV void scatter_seg(const PartLds& l, uint32_t F, const Bin& bin, const Out& o,
             __syncthreads();
         }
     }
-    if (KC_STAMP && stp) stp->mark(5);
     const uint32_t n = s_n;
     auto emit = [&](uint32_t i, const uint64_t (&key)[W], uint32_t b, uint32_t lim, uint64_t g) {
         if (i < lim) {
@@ -907,7 +855,6 @@ DEV void scatter_seg(const PartLds& l, uint32_t F, const Bin& bin, const Out& o,
         emit(i0, k0, b0, lim0, g0);
         if (has1) emit(i1, k1, b1, lim1, g1);
     }
-    if (KC_STAMP && stp) stp->mark(6);
 }
 
 // MODE 3 and 5 are Bloom pass 1 (MODE 5 writes the whole table key: its level-1 output is
@@ -1142,8 +1089,6 @@ __global__ __launch_bounds__(NT, NT >= 1024 ? 8 : 4) void k_p1(PackedView sv, in
     __syncthreads();
     const RollConst rk = make_roll<W>(k, pow5_k, pow5_km1);
     uint32_t n_win = 0, n_ins = 0;
-    Stamps stp;
-    stp.init();
     for (uint64_t t0 = lo; t0 < hi; t0 += TW) {
         const uint64_t t1 = min(t0 + TW, hi);
         uint64_t tk[RUNW][OW];
@@ -1213,16 +1158,16 @@ __global__ __launch_bounds__(NT, NT >= 1024 ? 8 : 4) void k_p1(PackedView sv, in
                 };
                 if constexpr (OW == 2) {  // level 1 as 12-byte records (the kept Bloom levels, the table's)
                     if (pb.rec12 & R12_P1) {
-                        scatter_seg<OW, RUNW, Bin, Out, NT>(l, F, bin, ob, tk, ok, out, mid, &stp,
+                        scatter_seg<OW, RUNW, Bin, Out, NT>(l, F, bin, ob, tk, ok, out, mid,
                                                             StoreRec12{Rec12{pb.r12_hb, pb.r12_xb1}}, pre);
                         par ^= 1;
                         continue;
                     }
                 }
-                scatter_seg<OW, RUNW, Bin, Out, NT>(l, F, bin, ob, tk, ok, out, mid, &stp, StoreWords(), pre);
+                scatter_seg<OW, RUNW, Bin, Out, NT>(l, F, bin, ob, tk, ok, out, mid, StoreWords(), pre);
                 par ^= 1;
             } else {
-                scatter_tile<OW, RUNW, Bin, Out, NT>(l, F, bin, ob, tk, ok, out, NoMid(), &stp);
+                scatter_tile<OW, RUNW, Bin, Out, NT>(l, F, bin, ob, tk, ok, out, NoMid());
             }
         } else {
 #pragma unroll
@@ -1239,7 +1184,6 @@ __global__ __launch_bounds__(NT, NT >= 1024 ? 8 : 4) void k_p1(PackedView sv, in
         for (uint32_t b = tid; b < F; b += NT)
             pb.hist1[(uint64_t)b * pb.nblk1 + blockIdx.x] = (uint32_t)(scatter_seg_next(l, b) - ob.start(b));
     }
-    if constexpr (SCATTER && Out::kSeg) stp.flush(0);
     if constexpr (HEAVY) heavy_flush<OW, MODE>(ht, pb, ctr);
     // routing (owner bins) counts windows here and insertions at the owner; the Bloom
     // pass counts its windows apart
@@ -1462,9 +1406,6 @@ __global__ __launch_bounds__(COUNT_THREADS, 4) void k_p2(TableView tv, PartBufs 
 template <int W, int NT>
 constexpr size_t p2f_smem(uint32_t F, uint32_t nseg_max) { return part_smem<W, NT>(F) + (size_t)(nseg_max + 1) * 4; }
 
-#ifndef KC_PREFETCH
-#define KC_PREFETCH 1
-#endif
 // IS: u64 words per level-1 item (W, or the whole table key of a kept level-1 output when
 // the Bloom pass reads only its word 0)
 // REC6: write 6-byte level-2 records (StoreRec6) instead of whole keys (one-word keys)
@@ -1541,15 +1482,13 @@ __global__ __launch_bounds__(NT, (2048 / NT > 8 ? 8 : 2048 / NT)) void k_p2f(Tab
     };
     uint64_t tk[RUNW][W];
     bool ok[RUNW];
-    Stamps stp;
-    stp.init();
     if (total) load_tile(0, tk, ok);
     for (uint32_t t0 = 0; t0 < total; t0 += TW) {
         // the next tile is loaded into the same registers as soon as this tile's keys sit
         // in LDS, so its loads overlap this tile's write-out (barriers wait for LDS only)
         const bool more = t0 + TW < total;
         auto mid = [&]() {
-            if (KC_PREFETCH && more) load_tile(t0 + TW, tk, ok);
+            if (more) load_tile(t0 + TW, tk, ok);
         };
         if constexpr (W == 2) {
             if (rin) {  // the level-1 records of coarse bin c
@@ -1562,21 +1501,19 @@ __global__ __launch_bounds__(NT, (2048 / NT > 8 ? 8 : 2048 / NT)) void k_p2f(Tab
             }
         }
         if constexpr (REC6) {
-            scatter_seg<W, RUNW, BinRegion, OutSeg, NT>(l, F, bin, o, tk, ok, pb.keys2, mid, &stp,
+            scatter_seg<W, RUNW, BinRegion, OutSeg, NT>(l, F, bin, o, tk, ok, pb.keys2, mid,
                                                         StoreRec6{xlo});
         } else if constexpr (W == 2) {
             if (rout)
-                scatter_seg<W, RUNW, BinRegion, OutSeg, NT>(l, F, bin, o, tk, ok, pb.keys2, mid, &stp,
+                scatter_seg<W, RUNW, BinRegion, OutSeg, NT>(l, F, bin, o, tk, ok, pb.keys2, mid,
                                                             StoreRec12{Rec12{pb.r12_hb, pb.r12_xb2}});
             else
-                scatter_seg<W, RUNW, BinRegion, OutSeg, NT>(l, F, bin, o, tk, ok, pb.keys2, mid, &stp);
+                scatter_seg<W, RUNW, BinRegion, OutSeg, NT>(l, F, bin, o, tk, ok, pb.keys2, mid);
         } else {
-            scatter_seg<W, RUNW, BinRegion, OutSeg, NT>(l, F, bin, o, tk, ok, pb.keys2, mid, &stp);
+            scatter_seg<W, RUNW, BinRegion, OutSeg, NT>(l, F, bin, o, tk, ok, pb.keys2, mid);
         }
-        if (!KC_PREFETCH && more) load_tile(t0 + TW, tk, ok);
     }
     __syncthreads();  // the last write-out read lim / gbase
-    stp.flush(1);
     for (uint32_t b = tid; b < F; b += NT)
         pb.hist2[((uint64_t)c * F + b) * B2T + jo] = (uint32_t)(scatter_seg_next(l, b) - o.start(b));
 }
@@ -1593,9 +1530,6 @@ DEV uint64_t* lds_word(uint64_t* lt, uint32_t b, uint32_t word) {
 // 8-bit slot tags (LDS only, beside the region image): one u64 per bucket, byte s = the tag
 // of slot s, 0 = empty.  A probe reads the bucket's tags (one ds_read_b64) and the key words
 // of the slots whose tag matches, instead of every key word of the bucket.
-#ifndef KC_P3_TAGS
-#define KC_P3_TAGS 1
-#endif
 DEV uint32_t slot_tag(uint64_t t0) { return 1u + (((uint32_t)t0 & 0xFFu) * 255u >> 8); }
 // bit i set iff byte i of x is zero (exact: no borrow between bytes)
 DEV uint32_t zero_byte_mask4(uint32_t x) {
@@ -1609,16 +1543,10 @@ DEV uint32_t zero_byte_mask8(uint64_t x) {
 // Exclusive prefix of a level-3 workgroup's n <= MAX_SEG_GROUP segment fills (s_pre[0..n],
 // s_pre[n] = total), by the first wave: two fills per lane, one DPP scan (was a one-thread loop
 // of n dependent-looking loads, ~n HBM latencies at every workgroup's start)
-// (PAIRS: of the segments' record pairs, ceil(fill / 2))
-template <bool PAIRS = false>
 DEV void seg_prefix(uint32_t* s_pre, const uint32_t* __restrict__ fill, uint32_t n) {
     if (threadIdx.x < 64) {
         const uint32_t j = 2 * threadIdx.x;
-        uint32_t a = j < n ? fill[j] : 0, b = j + 1 < n ? fill[j + 1] : 0;
-        if (PAIRS) {
-            a = (a + 1) >> 1;
-            b = (b + 1) >> 1;
-        }
+        const uint32_t a = j < n ? fill[j] : 0, b = j + 1 < n ? fill[j + 1] : 0;
         const uint32_t inc = wave_incl_sum(a + b);
         const uint32_t ex = inc - (a + b);
         if (j < n) s_pre[j] = ex;
@@ -1639,58 +1567,6 @@ DEV void seg_prefix(uint32_t* s_pre, const uint32_t* __restrict__ fill, uint32_t
 // the gate reads stay within a few KiB that L2 keeps.
 constexpr int P3_THREADS = 1024;  // two 64 KiB regions per CU: 8 waves per SIMD
 
-// One one-word key into the region's LDS table with 8-bit slot tags (the KC_P3_TAGS probe of
-// k_p3, for its record-pair path): returns false if the region is full.
-DEV bool p3_insert_tagged1(uint64_t* lt, uint64_t* tg, uint64_t R, uint64_t k0) {
-    constexpr int S = BUCKET_WORDS / 2;
-    constexpr uint32_t SMASK = (1u << S) - 1;
-    uint32_t b = bucket_in_region(k0, R);
-    const uint32_t tag = slot_tag(k0);
-    const uint64_t bc = 0x0101010101010101ULL * tag;
-    for (int probe = 0; probe < 4 * BPR;) {
-        const uint64_t tw = tg[b];
-        uint32_t m = zero_byte_mask8(tw ^ bc) & SMASK;
-        int slot = -1;
-        while (m) {
-            const int sl = __builtin_ctz(m);
-            m &= m - 1;
-            if (*lds_word(lt, b, sl) == k0) {
-                slot = sl;
-                break;
-            }
-        }
-        if (slot < 0) {
-            const uint32_t em = zero_byte_mask8(tw) & SMASK;
-            if (!em) {
-                b = (b + 1) & (BPR - 1);
-                probe++;
-                continue;
-            }
-            const int e = __builtin_ctz(em);
-            const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long*>(lds_word(lt, b, e)), 0ULL,
-                                           (unsigned long long)k0);
-            if (old == EMPTY) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                __hip_atomic_store(reinterpret_cast<uint8_t*>(tg + b) + e, (uint8_t)tag, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-                slot = e;
-            } else if (old == k0) {
-                slot = e;
-            } else {
-                probe++;
-                continue;
-            }
-        }
-        atomicAdd(reinterpret_cast<unsigned long long*>(lds_word(lt, b, S + slot)), 1ULL);
-        return true;
-    }
-    return false;
-}
-// k_p3's 6-byte records read as whole pairs (one 12-byte load per two keys, KC_P3_PAIRS pairs per
-// thread and round, the next round's loads issued before this round's inserts); 0 = per record
-#ifndef KC_P3_PAIRS
-#define KC_P3_PAIRS 0
-#endif
 // REC6: the segments hold 6-byte level-2 records (StoreRec6; one-word keys, SEG, not CNT)
 template <int W, bool SEG, bool CNT, bool GATE = false, bool REC6 = false>
 __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView tv, PartBufs pb,
@@ -1712,13 +1588,11 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
         if (gated_off(gate)) return;
     }
     uint64_t* lt = reinterpret_cast<uint64_t*>(smem);  // BPR * BUCKET_WORDS words
-    uint64_t* tg = lt + BPR * BUCKET_WORDS;             // KC_P3_TAGS: BPR tag words
+    uint64_t* tg = lt + BPR * BUCKET_WORDS;             // BPR tag words (slot_tag of each slot's word 0)
     const uint64_t r = blockIdx.x;
     uint64_t start, end;
-    // PAIRS: s_pre holds the prefix of the segments' record pairs (zero iff no record)
-    constexpr bool PAIRS = REC6 && !GATE && KC_P3_TAGS && KC_P3_PAIRS > 0;
     if constexpr (SEG) {
-        seg_prefix<PAIRS>(s_pre, pb.hist2 + r * pb.B2, pb.B2);
+        seg_prefix(s_pre, pb.hist2 + r * pb.B2, pb.B2);
         __syncthreads();
         start = 0;
         end = s_pre[pb.B2];
@@ -1732,16 +1606,14 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
     uint4* g4 = reinterpret_cast<uint4*>(tv.buckets + r * BPR * BUCKET_WORDS);
     uint4* l4 = reinterpret_cast<uint4*>(lt);
     constexpr int N4 = BPR * BUCKET_WORDS / 2;
-    constexpr int NT4 = KC_P3_TAGS ? BPR / 2 : 0;  // tag words, as uint4
-    Stamps stp;
-    stp.init();
+    constexpr int NT4 = BPR / 2;  // tag words, as uint4
     if (fresh) {
         for (int i = threadIdx.x; i < N4 + NT4; i += NT) l4[i] = make_uint4(0, 0, 0, 0);
         __syncthreads();
     } else {
         for (int i = threadIdx.x; i < N4; i += NT) l4[lds_chunk(i >> 3, i & 7)] = g4[i];
         __syncthreads();
-        if constexpr (KC_P3_TAGS) {
+        {
             for (int bb = threadIdx.x; bb < BPR; bb += NT) {
                 uint64_t t = 0;
 #pragma unroll
@@ -1755,7 +1627,7 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
         }
     }
     // GATE with an LDS slice: the filter-2 bits of the region's blocks, 8 words per block
-    uint32_t* gs = reinterpret_cast<uint32_t*>(tg + (KC_P3_TAGS ? BPR : 0));
+    uint32_t* gs = reinterpret_cast<uint32_t*>(tg + BPR);
     uint64_t gblo = 0;
     if constexpr (GATE) {
         if (bf.slice_blocks) {
@@ -1768,7 +1640,6 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
             __syncthreads();
         }
     }
-    stp.mark(0);
     uint32_t n_fail = 0, n_ins = 0;
     unsigned long long n_add = 0;  // CNT: the records' counts (the runs merge counts them here)
     // SEG: segment cursor of this thread (indices grow monotonically): segment cs holds
@@ -1866,69 +1737,18 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
             else add[q] = 1;
         }
     };
-    if constexpr (PAIRS) {
-        constexpr int PB = KC_P3_PAIRS > 0 ? KC_P3_PAIRS : 1;
-        const uint32_t np = s_pre[pb.B2];
-        uint32_t pcs = 0, pcb = 0, pnb = s_pre[1];  // pair cursor: segment pcs holds pairs [pcb, pnb)
-        uint32_t pfill = np ? pb.hist2[r * pb.B2] : 0;  // records of segment pcs
-        auto load_pairs = [&](uint32_t base, uint3 (&v)[PB], uint32_t& m) {  // m: bit 2q even / 2q+1 odd valid
-            m = 0;
-#pragma unroll
-            for (int q = 0; q < PB; q++) {
-                const uint32_t i = base + threadIdx.x + q * NT;
-                v[q] = make_uint3(0, 0, 0);
-                if (i < np) {
-                    if (pnb <= i) {
-                        do {
-                            pcs++;
-                            pcb = pnb;
-                            pnb = s_pre[pcs + 1];
-                        } while (pnb <= i);
-                        pfill = pb.hist2[r * pb.B2 + pcs];
-                    }
-                    const uint32_t po = i - pcb;
-                    v[q] = reinterpret_cast<const uint3*>(pb.keys2)[((r * pb.B2 + pcs) * pb.cap2 >> 1) + po];
-                    m |= (1u | (2 * po + 1 < pfill ? 2u : 0u)) << (2 * q);
-                }
-            }
-        };
-        uint3 v[PB];
-        uint32_t m = 0;
-        if (np) load_pairs(0, v, m);
-        for (uint32_t base = 0; base < np; base += PB * NT) {
-            uint3 nv[PB];
-            uint32_t nm = 0;
-            const bool more = base + PB * NT < np;
-            if (more) load_pairs(base + PB * NT, nv, nm);
-#pragma unroll
-            for (int q = 0; q < PB; q++) {
-                if ((m >> (2 * q)) & 1) {
-                    const uint64_t k0 = ((uint64_t)(xlo_r + (v[q].z & 0xFFFFu)) << 32) | v[q].x;
-                    if (!p3_insert_tagged1(lt, tg, tv.R, k0)) n_fail++;
-                }
-                if ((m >> (2 * q + 1)) & 1) {
-                    const uint64_t k1 = ((uint64_t)(xlo_r + (v[q].z >> 16)) << 32) | v[q].y;
-                    if (!p3_insert_tagged1(lt, tg, tv.R, k1)) n_fail++;
-                }
-            }
-            if (more) {
-                m = nm;
-#pragma unroll
-                for (int q = 0; q < PB; q++) v[q] = nv[q];
-            }
-        }
-    }
+
     uint64_t kk[KB][W];
     uint64_t add[KB];
     uint32_t okm = 0;
-    if (!PAIRS && start < vend) load_items(start, kk, add, okm);
-    for (uint64_t base = start; !PAIRS && base < vend; base += (uint64_t)KB * NT) {
+    if (start < vend) load_items(start, kk, add, okm);
+    for (uint64_t base = start; base < vend; base += (uint64_t)KB * NT) {
         // the next items' loads are issued before this batch's inserts
         uint64_t nkk[KB][W];
         uint64_t nadd[KB];
         uint32_t nokm = 0;
         const uint64_t nbase = base + (uint64_t)KB * NT;
-        const bool more = KC_PREFETCH && W <= 2 && nbase < vend;  // W > 2: no spare registers
+        const bool more = W <= 2 && nbase < vend;  // W > 2: no spare registers
         if (more) load_items(nbase, nkk, nadd, nokm);
         if constexpr (REC6) {
 #pragma unroll
@@ -1964,7 +1784,7 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
             const uint64_t k0 = kk[q][0];
             uint32_t b = bucket_in_region(k0, tv.R);
             bool done = false;
-            if constexpr (KC_P3_TAGS) {
+            {
                 constexpr uint32_t SMASK = (1u << S) - 1;
                 const uint32_t tag = slot_tag(k0);
                 const uint64_t bc = 0x0101010101010101ULL * tag;
@@ -2017,98 +1837,8 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
                               (unsigned long long)a);
                     done = true;
                 }
-            } else if constexpr (W == 1) {
-                // branch-light probe: match / first-empty masks over the 8 slots of a bucket
-                for (int probe = 0; probe < 2 * BPR && !done;) {
-                    uint32_t eqm = 0, emm = 0;
-#pragma unroll
-                    for (int c = 0; c < 4; c++) {
-                        const uint4 v = l4[lds_chunk(b, c)];
-                        const uint64_t x0 = ((uint64_t)v.y << 32) | v.x, x1 = ((uint64_t)v.w << 32) | v.z;
-                        eqm |= (uint32_t)(x0 == k0) << (2 * c) | (uint32_t)(x1 == k0) << (2 * c + 1);
-                        emm |= (uint32_t)(x0 == 0) << (2 * c) | (uint32_t)(x1 == 0) << (2 * c + 1);
-                    }
-                    int slot = -1;
-                    if (eqm) {
-                        slot = __builtin_ctz(eqm);
-                    } else if (emm) {
-                        const int e = __builtin_ctz(emm);
-                        const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long*>(lds_word(lt, b, e)), 0ULL,
-                                                       (unsigned long long)k0);
-                        if (old == 0 || old == k0) slot = e;
-                        else { probe++; continue; }  // lost the slot to another key: re-read this bucket
-                    }
-                    if (slot >= 0) {
-                        atomicAdd(reinterpret_cast<unsigned long long*>(lds_word(lt, b, S + slot)),
-                                  (unsigned long long)add[q]);
-                        done = true;
-                    } else {
-                        b = (b + 1) & (BPR - 1);
-                        probe++;
-                    }
-                }
             }
-            if constexpr (!KC_P3_TAGS && W > 1) {
-                // branch-light probe over a whole bucket: the count words are read first and
-                // the key words after a wait, so a READY count guarantees that the key words
-                // read after it are published (the claimer stores them before setting READY)
-                constexpr int C0 = S * W / 2;  // first 16-byte chunk holding counts
-                static_assert((S * W) % 2 == 0, "keys end on a chunk boundary");
-                for (int probe = 0; probe < 4 * BPR && !done;) {
-                    uint64_t bw[BUCKET_WORDS];
-#pragma unroll
-                    for (int c = C0; c < BUCKET_WORDS / 2; c++) {
-                        const uint4 v = l4[lds_chunk(b, c)];
-                        bw[2 * c] = ((uint64_t)v.y << 32) | v.x;
-                        bw[2 * c + 1] = ((uint64_t)v.w << 32) | v.z;
-                    }
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-                    for (int c = 0; c < C0; c++) {
-                        const uint4 v = l4[lds_chunk(b, c)];
-                        bw[2 * c] = ((uint64_t)v.y << 32) | v.x;
-                        bw[2 * c + 1] = ((uint64_t)v.w << 32) | v.z;
-                    }
-                    uint32_t eqm = 0, pend = 0, emm = 0;
-#pragma unroll
-                    for (int sl = 0; sl < S; sl++) {
-                        const bool w0eq = bw[sl * W] == k0;
-                        bool rest = true;
-#pragma unroll
-                        for (int w = 1; w < W; w++) rest &= bw[sl * W + w] == kk[q][w];
-                        const bool ready = (bw[S * W + sl] & READY) != 0;
-                        eqm |= (uint32_t)(w0eq && rest && ready) << sl;
-                        pend |= (uint32_t)(w0eq && !ready) << sl;
-                        emm |= (uint32_t)(bw[sl * W] == EMPTY) << sl;
-                    }
-                    if (eqm) {
-                        atomicAdd(reinterpret_cast<unsigned long long*>(lds_word(lt, b, S * W + __builtin_ctz(eqm))),
-                                  (unsigned long long)add[q]);
-                        done = true;
-                    } else if (pend) {
-                        probe++;  // another wave is publishing a key with this word 0: read again
-                    } else if (emm) {
-                        const int e = __builtin_ctz(emm);
-                        const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long*>(lds_word(lt, b, e * W)),
-                                                       0ULL, (unsigned long long)k0);
-                        if (old == EMPTY) {
-#pragma unroll
-                            for (int w = 1; w < W; w++)
-                                __hip_atomic_store(lds_word(lt, b, e * W + w), kk[q][w], __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-                            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                            atomicAdd(reinterpret_cast<unsigned long long*>(lds_word(lt, b, S * W + e)),
-                                      (unsigned long long)(READY + add[q]));
-                            done = true;
-                        } else {
-                            probe++;  // lost the slot: read the bucket again
-                        }
-                    } else {
-                        b = (b + 1) & (BPR - 1);  // bucket full, key absent: next bucket
-                        probe++;
-                    }
-                }
-            }
+
             if (!done) n_fail++;
         }
         if (more) {
@@ -2123,9 +1853,7 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
             load_items(nbase, kk, add, okm);
         }
     }
-    stp.mark(1);
     __syncthreads();
-    stp.mark(2);
     // kc_route_hint: the region's records per owner shard for each of its two 256-bucket route
     // blocks, counted in s_pre (dead once the items are inserted)
     const uint32_t op = pb.own_parts;
@@ -2146,8 +1874,6 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
             pb.own_hist[(uint64_t)d * pb.own_nblk + 2 * r + h] = s_pre[h * RT_MAX_PARTS + d];
         }
     }
-    stp.mark(3);
-    if (SEG && !CNT && !GATE) stp.flush(2);
     if (n_fail) atomicAdd(&ctr->overflow, (unsigned long long)n_fail);
     if constexpr (GATE || CNT) {
         // GATE: the gated insertions (level 1 counted the windows); CNT over runs: the
@@ -2168,13 +1894,7 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
 // contiguous run [off2[r * B2], off2[(r + 1) * B2]).
 // keys per thread per round and workgroup size: 512 threads keep the insertion path within
 // its registers (72 VGPRs, no scratch spills; 1024-thread groups would be capped at 64)
-#ifndef KC_B3_NT
-#define KC_B3_NT 512
-#endif
-constexpr int B3_THREADS = KC_B3_NT;  // two 64 KiB regions per CU
-#ifndef KC_B3_PREFETCH
-#define KC_B3_PREFETCH 1
-#endif
+constexpr int B3_THREADS = 512;  // two 64 KiB regions per CU
 template <bool SEG>
 __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView bf, uint32_t bpr, PartBufs pb,
                                                                   DevCounters* __restrict__ ctr,
@@ -2187,10 +1907,7 @@ __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView b
     // records are distinct keys; rec_phase 0 inserts those of count >= 2, rec_phase 1 (a later
     // launch) those of count 1, with the distinct-key rule of block_insert: the order "the
     // k-mers seen twice first", one sequential order of the reference's pass
-#ifndef KC_B3_KB
-#define KC_B3_KB 4
-#endif
-    constexpr int NT = B3_THREADS, KB = NT >= 1024 ? 2 : KC_B3_KB;  // (8 or 2 keys per round at 512: slower, r02_v21)
+    constexpr int NT = B3_THREADS, KB = 4;  // (8 or 2 keys per round: slower, r02_v21)
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ uint32_t s_pre[MAX_SEG_GROUP + 1];
     if constexpr (SEG) {
@@ -2225,8 +1942,8 @@ __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView b
     uint32_t cs = 0, cb = 0, nb = 0;  // SEG: segment cursor (indices grow monotonically)
     if constexpr (SEG) nb = s_pre[1];
     const bool r12 = SEG && (pb.rec12 & R12_L2);  // 12-byte records of fine bin seg >> r12_b2s (Rec12)
-    // the next round's items are loaded while this round's are tested and inserted (KC_B3_PREFETCH:
-    // the loads' latency was exposed once per round; raw records, decoded when used)
+    // the next round's items are loaded while this round's are tested and inserted (the loads'
+    // latency was exposed once per round; raw records, decoded when used)
     struct Raw {
         uint3 v[KB];
         uint32_t xhi[KB];
@@ -2270,7 +1987,7 @@ __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView b
     if (start < end) fetch(start, cur);
     for (uint64_t base = start; base < end; base += (uint64_t)KB * NT) {
         const uint64_t nbase = base + (uint64_t)KB * NT;
-        if (KC_B3_PREFETCH && nbase < end) fetch(nbase, nxt);
+        if (nbase < end) fetch(nbase, nxt);
         uint64_t t0[KB];
 #pragma unroll
         for (int q = 0; q < KB; q++)
@@ -2307,373 +2024,13 @@ __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView b
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // queue reads done before reuse
         }
-        if (KC_B3_PREFETCH) cur = nxt;
-        else if (nbase < end) fetch(nbase, cur);
+        cur = nxt;
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < n4; i += NT) g4[i] = l4[i];
     // one atomic per counter and workgroup (per-wave adds to one address serialise)
     block_add4(bl.new_first, bl.new_second, bl.failed, 0, &ctr->new_in_first, &ctr->new_in_second,
                &ctr->failed_in_first, nullptr);
-}
-
-// --------------------------------------------------------------------------------
-// Fused Bloom pass 1 + gated counting pass (kc_api.cpp run_batch: a one-batch Bloom pass
-// over a device image whose kept level-2 partitions are clean, with the table sized from a
-// sample of them before the Bloom pass ends).  The reference runs pass 1 over the whole input
-// and then a second pass that counts the k-mers whose filter-2 bits are all set
-// (parallel_parser.hpp:2680-2974, the gate at 2436-2453).  A k-mer's filter block and its
-// table region are the same hash prefix (bloom_block, region_of): once every key of one table
-// region has been through insertion_process, that region's blocks are final, so the same
-// workgroup gates the same keys and counts them into the region.  The keys are read twice,
-// the second time right after the first (a workgroup's ~0.2-0.4 MB stays in the Infinity
-// Cache), instead of by two launches 12 GB of records apart (k_b3 in the Bloom pass, then
-// k_p3<GATE> in the counting pass).
-// --------------------------------------------------------------------------------
-// a kept level-2 item (segment seg of the fine bins, entry j): word 0 of its table key, or
-// the whole key (Rec12 records decoded against their fine bin's lowest x)
-template <int W>
-DEV uint64_t kept_t0(const PartBufs& pb, uint64_t seg, uint64_t j) {
-    if constexpr (W == 2) {
-        if (pb.rec12 & R12_L2) {
-            const uint3 v = reinterpret_cast<const uint3*>(pb.keys2)[seg * pb.cap2 + j];
-            const uint32_t x = (uint32_t)(seg >> pb.r12_b2s) << pb.r12_xb2 | v.z >> (pb.r12_hb + 1);
-            return (uint64_t)x << 32 | v.x;
-        }
-    }
-    return pb.keys2[(seg * pb.cap2 + j) * W];
-}
-template <int W>
-DEV void kept_key(const PartBufs& pb, uint64_t seg, uint64_t j, uint64_t (&t)[W]) {
-    if constexpr (W == 2) {
-        if (pb.rec12 & R12_L2) {
-            const uint3 v = reinterpret_cast<const uint3*>(pb.keys2)[seg * pb.cap2 + j];
-            const Rec12 rc{pb.r12_hb, pb.r12_xb2};
-            rc.dec(v, (uint32_t)(seg >> pb.r12_b2s) << pb.r12_xb2, t[0], t[1]);
-            return;
-        }
-    }
-    const uint64_t* src = pb.keys2 + (seg * pb.cap2 + j) * W;
-#pragma unroll
-    for (int w = 0; w < W; w++) t[w] = src[w];
-}
-
-// insert one table key with count `add` into an LDS region with slot tags (k_p3's tagged
-// probe): false when the region is full
-template <int W>
-DEV bool lds_insert_tagged(uint64_t* lt, uint64_t* tg, uint64_t R, const uint64_t (&kk)[W], uint64_t add) {
-    constexpr int S = BUCKET_WORDS / (W + 1);
-    constexpr uint32_t SMASK = (1u << S) - 1;
-    const uint64_t k0 = kk[0];
-    uint32_t b = bucket_in_region(k0, R);
-    const uint32_t tag = slot_tag(k0);
-    const uint64_t bc = 0x0101010101010101ULL * tag;
-    for (int probe = 0; probe < 4 * BPR;) {
-        const uint64_t tw = tg[b];
-        uint32_t m = zero_byte_mask8(tw ^ bc) & SMASK;
-        int slot = -1;
-        while (m) {
-            const int sl = __builtin_ctz(m);
-            m &= m - 1;
-            bool eq = *lds_word(lt, b, sl * W) == k0;
-#pragma unroll
-            for (int w = 1; w < W; w++) eq &= *lds_word(lt, b, sl * W + w) == kk[w];
-            if (eq) {
-                slot = sl;
-                break;
-            }
-        }
-        uint64_t a = add;
-        if (slot < 0) {
-            const uint32_t em = zero_byte_mask8(tw) & SMASK;
-            if (!em) {
-                b = (b + 1) & (BPR - 1);
-                probe++;
-                continue;
-            }
-            const int e = __builtin_ctz(em);
-            const uint64_t old =
-                atomicCAS(reinterpret_cast<unsigned long long*>(lds_word(lt, b, e * W)), 0ULL, (unsigned long long)k0);
-            if (old == EMPTY) {
-#pragma unroll
-                for (int w = 1; w < W; w++)
-                    __hip_atomic_store(lds_word(lt, b, e * W + w), kk[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                __hip_atomic_store(reinterpret_cast<uint8_t*>(tg + b) + e, (uint8_t)tag, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-                if constexpr (W > 1) a += READY;
-                slot = e;
-            } else if (W == 1 && old == k0) {
-                slot = e;
-            } else {
-                probe++;
-                continue;
-            }
-        }
-        atomicAdd(reinterpret_cast<unsigned long long*>(lds_word(lt, b, S * W + slot)), (unsigned long long)a);
-        return true;
-    }
-    return false;
-}
-
-// One workgroup per table region r (tv.R a power of two): segments [r * B2, (r + 1) * B2) of
-// the kept fine bins (pb.B2 = fine bins per region x their segments, fills in pb.hist2), filter
-// blocks [r * bpr, (r + 1) * bpr), bpr = nblocks / R.  Phase 1 = k_b3 on the region's blocks;
-// the blocks go back to HBM; phase 2 = k_p3<GATE> on the region (the table is fresh: zero-filled,
-// every region written).  LGATE: the blocks' filter-2 halves stay in LDS for the gate
-// (bpr * 32 bytes beside the 68 KiB table image); otherwise the gate reads the blocks just
-// written (L2).  Region overflow -> ctr->spec_overflow (the host then drops the table).
-#ifndef KC_BF3_NT
-#define KC_BF3_NT 1024
-#endif
-constexpr int BF3_THREADS = KC_BF3_NT;  // two per CU: 8 waves per SIMD for the count phase's latency
-template <int W, bool LGATE>
-__global__ __launch_bounds__(BF3_THREADS, BF3_THREADS / 128) void k_bf3(BloomView bf, TableView tv, PartBufs pb,
-                                                                    DevCounters* __restrict__ ctr, int fresh_filter) {
-    constexpr int NT = BF3_THREADS, KB1 = NT >= 1024 ? 2 : 4, KB2 = W > 2 ? 1 : NT >= 1024 ? 2 : 4;
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    __shared__ uint32_t s_pre[MAX_SEG_GROUP + 1];
-    const uint64_t r = blockIdx.x;
-    const uint32_t bpr = (uint32_t)(bf.nblocks / tv.R);
-    seg_prefix(s_pre, pb.hist2 + r * pb.B2, pb.B2);
-    __syncthreads();
-    const uint32_t end = s_pre[pb.B2];
-    const uint64_t seg0 = r * pb.B2;
-    // ---- phase 1: insertion_process for every key of the region (k_b3)
-    uint32_t* lf = reinterpret_cast<uint32_t*>(smem);
-    uint4* l4 = reinterpret_cast<uint4*>(smem);
-    const uint32_t n4f = bpr * BF_BLOCK_WORDS / 4;
-    uint4* g4f = reinterpret_cast<uint4*>(bf.bits + r * bpr * BF_BLOCK_WORDS);
-    for (uint32_t i = threadIdx.x; i < n4f; i += NT) l4[i] = (fresh_filter & 1) ? make_uint4(0, 0, 0, 0) : g4f[i];
-    __syncthreads();
-    const uint64_t blk0 = r * bpr;
-    const int lane = threadIdx.x & 63;
-    BloomLocal bl = {0, 0, 0};
-    {
-        uint64_t* wq = reinterpret_cast<uint64_t*>(smem + (size_t)bpr * BF_BLOCK_WORDS * 4) + (threadIdx.x >> 6) * 64;
-        uint32_t cs = 0, cb = 0, nb = s_pre[1];
-        for (uint32_t base = 0; base < end; base += KB1 * NT) {
-            uint64_t t0[KB1];
-#pragma unroll
-            for (int q = 0; q < KB1; q++) {
-                const uint32_t i = base + threadIdx.x + q * NT;
-                t0[q] = EMPTY;
-                if (i < end) {
-                    while (nb <= i) {
-                        cs++;
-                        cb = nb;
-                        nb = s_pre[cs + 1];
-                    }
-                    t0[q] = kept_t0<W>(pb, seg0 + cs, i - cb);
-                }
-            }
-            bool slow[KB1];
-            uint32_t pre[KB1], rank[KB1], total = 0;
-#pragma unroll
-            for (int q = 0; q < KB1; q++) {
-                slow[q] = base + threadIdx.x + q * NT < end &&
-                          !block_gate(lf + (uint32_t)(bloom_block(t0[q], bf.nblocks) - blk0) * BF_BLOCK_WORDS + 8, t0[q],
-                                      bf.nh);
-                const uint64_t bal = __ballot(slow[q]);
-                pre[q] = total;
-                rank[q] = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                total += (uint32_t)__popcll(bal);
-            }
-            for (uint32_t r0 = 0; r0 < total; r0 += 64) {
-#pragma unroll
-                for (int q = 0; q < KB1; q++)
-                    if (slow[q] && pre[q] + rank[q] - r0 < 64) wq[pre[q] + rank[q] - r0] = t0[q];
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                if (lane < total - r0) {
-                    const uint64_t t = wq[lane];
-                    block_insert(lf + (uint32_t)(bloom_block(t, bf.nblocks) - blk0) * BF_BLOCK_WORDS, t, bf.nh, bl);
-                }
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            }
-        }
-    }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < n4f; i += NT) g4f[i] = l4[i];  // the final blocks
-    if constexpr (LGATE) {  // block b's filter-2 words to gs + 8 b (host: 2 * bpr <= 2 * NT)
-        const uint32_t i0 = threadIdx.x, i1 = threadIdx.x + NT;
-        const uint4 v0 = i0 < 2 * bpr ? l4[(i0 >> 1) * 4 + 2 + (i0 & 1)] : make_uint4(0, 0, 0, 0);
-        const uint4 v1 = i1 < 2 * bpr ? l4[(i1 >> 1) * 4 + 2 + (i1 & 1)] : make_uint4(0, 0, 0, 0);
-        __syncthreads();
-        if (i0 < 2 * bpr) l4[i0] = v0;
-        if (i1 < 2 * bpr) l4[i1] = v1;
-    } else {
-        __syncthreads();  // the write-back's LDS reads before the table image overwrites them
-    }
-    // ---- phase 2: the same keys behind the gate into the region's LDS table (k_p3<GATE>)
-    if (fresh_filter & 2) return;  // (A/B: KC_FUSE_PHASES=1 times phase 1 alone)
-    const uint32_t* gs = reinterpret_cast<const uint32_t*>(smem);
-    uint64_t* lt = reinterpret_cast<uint64_t*>(smem + (LGATE ? (size_t)bpr * 32 : 0));
-    uint64_t* tg = lt + BPR * BUCKET_WORDS;
-    uint4* t4 = reinterpret_cast<uint4*>(lt);
-    constexpr int N4 = BPR * BUCKET_WORDS / 2, NT4 = BPR / 2;
-    for (int i = threadIdx.x; i < N4 + NT4; i += NT) t4[i] = make_uint4(0, 0, 0, 0);
-    __syncthreads();
-    uint32_t n_fail = 0, n_ins = 0;
-    uint32_t cs = 0, cb = 0, nb = s_pre[1];
-    auto load = [&](uint32_t base, uint64_t (&kk)[KB2][W], uint32_t& ok) {
-        ok = 0;
-#pragma unroll
-        for (int q = 0; q < KB2; q++) {
-            const uint32_t i = base + threadIdx.x + q * NT;
-#pragma unroll
-            for (int w = 0; w < W; w++) kk[q][w] = 0;
-            if (i < end) {
-                while (nb <= i) {
-                    cs++;
-                    cb = nb;
-                    nb = s_pre[cs + 1];
-                }
-                kept_key<W>(pb, seg0 + cs, i - cb, kk[q]);
-                ok |= 1u << q;
-            }
-        }
-    };
-    uint64_t kk[KB2][W];
-    uint32_t okm = 0;
-    if (end) load(0, kk, okm);
-    for (uint32_t base = 0; base < end; base += KB2 * NT) {
-        uint64_t nkk[KB2][W];
-        uint32_t nokm = 0;
-        const uint32_t nbase = base + KB2 * NT;
-        const bool more = W <= 2 && nbase < end;  // the next round's loads in flight during this one's inserts
-        if (more) load(nbase, nkk, nokm);
-        bool pass[KB2];
-#pragma unroll
-        for (int q = 0; q < KB2; q++) {
-            const uint64_t t0 = kk[q][0];
-            pass[q] = (okm >> q) & 1;
-            if (LGATE)
-                pass[q] = pass[q] && block_gate(gs + (uint32_t)(bloom_block(t0, bf.nblocks) - blk0) * 8, t0, bf.nh_gate);
-            else
-                pass[q] = pass[q] && block_gate(bloom_block_ptr(bf, t0) + 8, t0, bf.nh_gate);
-            n_ins += pass[q];
-        }
-#pragma unroll
-        for (int q = 0; q < KB2; q++)
-            if (pass[q] && !lds_insert_tagged<W>(lt, tg, tv.R, kk[q], 1)) n_fail++;
-        if (more) {
-            okm = nokm;
-#pragma unroll
-            for (int q = 0; q < KB2; q++)
-#pragma unroll
-                for (int w = 0; w < W; w++) kk[q][w] = nkk[q][w];
-        } else if (nbase < end) {
-            load(nbase, kk, okm);
-        }
-    }
-    __syncthreads();
-    uint4* g4 = reinterpret_cast<uint4*>(tv.buckets + r * BPR * BUCKET_WORDS);
-    for (int i = threadIdx.x; i < N4; i += NT) g4[i] = t4[lds_chunk(i >> 3, i & 7)];
-    block_add4(bl.new_first, bl.new_second, bl.failed, n_ins, &ctr->new_in_first, &ctr->new_in_second,
-               &ctr->failed_in_first, &ctr->spec_inserted);
-    if (n_fail) atomicAdd(&ctr->spec_overflow, (unsigned long long)n_fail);
-}
-
-// The fused pass's sizing probe: one workgroup per sampled fine bin fb = blockIdx.x * stride
-// (segments [fb * B2, (fb + 1) * B2) of the kept level 2): the bin's Bloom pass on its own
-// blocks in LDS (insertion_process per key), then the distinct word-0 table keys that pass
-// the gate, counted in an LDS set.  out[blockIdx.x] = that count, ~0u past 3/4 of the set.
-constexpr int PROBE_THREADS = 512;
-constexpr uint32_t PROBE_SET = 4096;
-template <int W>
-__global__ __launch_bounds__(PROBE_THREADS) void k_bprobe(BloomView bf, uint64_t fineR, uint32_t stride, PartBufs pb,
-                                                       int fresh_filter, uint32_t* __restrict__ out) {
-    constexpr int NT = PROBE_THREADS;
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    __shared__ uint32_t s_pre[MAX_SEG_GROUP + 1];
-    __shared__ uint32_t s_cnt, s_sat;
-    const uint64_t fb = (uint64_t)blockIdx.x * stride;
-    const uint32_t bpf = (uint32_t)(bf.nblocks / fineR);
-    seg_prefix(s_pre, pb.hist2 + fb * pb.B2, pb.B2);
-    if (threadIdx.x == 0) {
-        s_cnt = 0;
-        s_sat = 0;
-    }
-    uint32_t* lf = reinterpret_cast<uint32_t*>(smem);
-    uint64_t* set = reinterpret_cast<uint64_t*>(smem + (size_t)bpf * BF_BLOCK_WORDS * 4);
-    const uint32_t* g = bf.bits + fb * bpf * BF_BLOCK_WORDS;
-    for (uint32_t i = threadIdx.x; i < bpf * BF_BLOCK_WORDS; i += NT) lf[i] = fresh_filter ? 0u : g[i];
-    for (uint32_t i = threadIdx.x; i < PROBE_SET; i += NT) set[i] = EMPTY;
-    __syncthreads();
-    const uint32_t end = s_pre[pb.B2];
-    const uint64_t blk0 = fb * bpf, seg0 = fb * pb.B2;
-    BloomLocal bl = {0, 0, 0};
-    auto item = [&](uint32_t i) {
-        uint32_t lo = 0, hi = pb.B2;  // the segment holding item i
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (s_pre[mid] <= i) lo = mid;
-            else hi = mid;
-        }
-        return kept_t0<W>(pb, seg0 + lo, i - s_pre[lo]);
-    };
-    for (uint32_t i = threadIdx.x; i < end; i += NT) {
-        const uint64_t t = item(i);
-        block_insert(lf + (uint32_t)(bloom_block(t, bf.nblocks) - blk0) * BF_BLOCK_WORDS, t, bf.nh, bl);
-    }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < end && !*(volatile uint32_t*)&s_sat; i += NT) {
-        const uint64_t t = item(i);
-        if (!block_gate(lf + (uint32_t)(bloom_block(t, bf.nblocks) - blk0) * BF_BLOCK_WORDS + 8, t, bf.nh_gate))
-            continue;
-        uint32_t h = (uint32_t)((t * 0x9E3779B97F4A7C15ULL) >> 52);  // 12 bits: PROBE_SET slots
-        bool done = false;
-        for (uint32_t p = 0; p < PROBE_SET && !done; p++, h = (h + 1) & (PROBE_SET - 1)) {
-            const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long*>(set + h), 0ULL, (unsigned long long)t);
-            if (old == EMPTY) {
-                if (atomicAdd(&s_cnt, 1u) + 1 > PROBE_SET / 4 * 3) s_sat = 1;
-                done = true;
-            } else if (old == t) {
-                done = true;
-            }
-        }
-        if (!done) s_sat = 1;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) out[blockIdx.x] = s_sat ? ~0u : s_cnt;
-}
-
-template <int W>
-static hipError_t bloom_count_fused_w(BloomView bf, TableView t, TableView fg, PartBufs pb, DevCounters* ctr,
-                                      int fresh_filter, hipStream_t s) {
-    (void)fg;
-    const uint64_t bpr = bf.nblocks / t.R;
-    const size_t tbl = (size_t)BPR * BUCKET_WORDS * 8 + (size_t)BPR * 8;
-    const size_t ph1 = (size_t)bpr * BF_BLOCK_WORDS * 4 + (size_t)(BF3_THREADS / 64) * 64 * 8;
-    // the filter-2 slice beside the table image if two workgroups still fit a CU (KC_FUSE_GATE:
-    // lds / global forces one)
-    const size_t lg = (size_t)bpr * 32 + tbl;
-    static const int knob = [] {
-        const char* v = std::getenv("KC_FUSE_GATE");
-        return v ? (!std::strcmp(v, "lds") ? 1 : !std::strcmp(v, "global") ? 0 : -1) : -1;
-    }();
-    const bool lgate = bpr <= BF3_THREADS && (knob == 1 || (knob < 0 && std::max(lg, ph1) + 2048 <= 80 * 1024));
-    const size_t sm = std::max(ph1, lgate ? lg : tbl);
-    auto kern = lgate ? k_bf3<W, true> : k_bf3<W, false>;
-    hipError_t e = set_smem(kern, sm);
-    if (e != hipSuccess) return e;
-    static const int ph1_only = [] {
-        const char* v = std::getenv("KC_FUSE_PHASES");
-        return v && *v == '1' ? 2 : 0;
-    }();
-    hipLaunchKernelGGL(kern, dim3((unsigned)t.R), dim3(BF3_THREADS), sm, s, bf, t, pb, ctr, fresh_filter | ph1_only);
-    return hipGetLastError();
-}
-
-template <int W>
-static hipError_t bloom_probe_w(BloomView bf, TableView fg, PartBufs pb, uint32_t nsample, int fresh_filter,
-                                uint32_t* out, hipStream_t s) {
-    const size_t sm = (size_t)(bf.nblocks / fg.R) * BF_BLOCK_WORDS * 4 + (size_t)PROBE_SET * 8;
-    hipError_t e = set_smem(k_bprobe<W>, sm);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_bprobe<W>, dim3(nsample), dim3(PROBE_THREADS), sm, s, bf, fg.R, (uint32_t)(fg.R / nsample), pb,
-                       fresh_filter, out);
-    return hipGetLastError();
 }
 
 // --------------------------------------------------------------------------------
@@ -3073,7 +2430,7 @@ static BinRegion coarse_bins(const TableView& t) { return BinRegion{t.R, t.f2bit
 template <int W, bool SEG, bool CNT = false, bool GATE = false>
 static hipError_t launch_p3(TableView t, DevCounters* ctr, PartBufs pb, const unsigned long long* gate, int fresh,
                             hipStream_t s, BloomView bf = BloomView{}) {
-    size_t sm3 = (size_t)BPR * BUCKET_WORDS * 8 + (KC_P3_TAGS ? (size_t)BPR * 8 : 0);
+    size_t sm3 = (size_t)BPR * BUCKET_WORDS * 8 + (size_t)BPR * 8;
     if (GATE) {
         // the filter-2 slice goes to LDS if two workgroups still fit a CU (80 KiB each)
         const uint64_t maxb = bf.nblocks / t.R + 2;
@@ -3215,10 +2572,10 @@ static __global__ void k_batch_end(DevCounters* ctr) {
 
 // Rec12 in the table's geometry (R12_REG): a coarse bin spans at most ceil(F2 * 2^32 / R) values
 // of x, a region ceil(2^32 / R); level 1 (k_p1 -> k_p2f) and level 2 (k_p2f -> k_p3) take the
-// 12-byte records independently, each when hb + 1 + xb <= 32 (KC_NO_REC12: 16-byte records)
+// 12-byte records independently, each when hb + 1 + xb <= 32 (else 16-byte records)
 static inline void set_rec12_table(PartBufs& pb, const TableView& t, int k) {
     pb.rec12 = 0;
-    if (std::getenv("KC_NO_REC12") || t.R == 0) return;
+    if (t.R == 0) return;
     const int hb = std::max(0, 2 * k - 96);
     auto span_bits = [](uint64_t span) {
         int b = 0;
@@ -3256,7 +2613,7 @@ static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf
     hipError_t e;
     const unsigned long long* gate = &ctr->part_overflow;
     // one-word keys in a table of >= 2^16 regions: 6-byte level-2 records (StoreRec6)
-    pb.rec6 = W == 1 && t.R >= (1ULL << 16) && !std::getenv("KC_NO_REC6");
+    pb.rec6 = W == 1 && t.R >= (1ULL << 16);
     // two-word keys: 12-byte records at each level whose bins span few enough values of x
     if constexpr (W == 2) set_rec12_table(pb, t, k);
     if (phase & PH_L3) {  // the deferred level 3 of a group of batches: B2 = the group's segments
@@ -3269,20 +2626,11 @@ static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf
     hipLaunchKernelGGL(k_batch_begin, dim3(1), dim3(1), 0, s, ctr);
     const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
     auto k1 = k_p1<W, MODE, true, BinRegion, OutSeg, scatter_threads<W>()>;
-    static const uint32_t p2f_pad = [] {  // A/B knob: reserve LDS as if for this many segments
-        const char* v = std::getenv("KC_P2F_SEGS");
-        return v ? (uint32_t)std::atoi(v) : 0u;
-    }();
     // Short level-1 runs (fewer than 8 keys per bin and tile: big tables, C4 shares) leave
     // partial 128-byte lines that L2 merges only while they stay resident: one workgroup per
     // CU halves the open lines (C4 share: k_p1 writes 33 GB for 20 GB of keys; count
     // 41.0 -> 40.15 ms; C2's 34-key runs lose 18 % that way, profiles/r02_v16_ab_p1_lds.txt)
-    static const long p1_lds_knob = [] {  // A/B knob: reserve at least this much LDS
-        const char* v = std::getenv("KC_P1_LDS_MIN");
-        return v ? std::atol(v) : -1L;
-    }();
-    const size_t p1_lds_min = p1_lds_knob >= 0 ? std::min(LDS_BYTES, (size_t)p1_lds_knob)
-                              : (size_t)p1_tile(W) < 8 * (size_t)t.F1 ? LDS_BYTES / 2 + 16 : 0;
+    const size_t p1_lds_min = (size_t)p1_tile(W) < 8 * (size_t)t.F1 ? LDS_BYTES / 2 + 16 : 0;
     const size_t sm1 = std::max(p1_lds_min, p1_smem<W, W, scatter_threads<W>()>(t.F1) + heavy_smem<W>() +
                                                 p1_stage_smem<W, scatter_threads<W>()>());
     if ((e = set_smem(k1, sm1)) != hipSuccess) return e;
@@ -3290,7 +2638,7 @@ static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf
                     &ctr->part_overflow, 1};
     hipLaunchKernelGGL(k1, dim3(pb.nblk1), dim3(scatter_threads<W>()), sm1, s, sym, k, bf, ctr, pb, t.F1, coarse_bins(t),
                        pb.keys1, pk, pkm1, o1, (const unsigned long long*)nullptr, 1);
-    if ((e = launch_p2f<W>(t, pb, ctr, 1, s, p2f_pad)) != hipSuccess) return e;
+    if ((e = launch_p2f<W>(t, pb, ctr, 1, s)) != hipSuccess) return e;
     if (phase & PH_MAIN)
         if ((e = launch_p3<W, true, false, GATE3>(t, ctr, pb, nullptr, fresh, s, bf)) != hipSuccess) return e;
     }
@@ -3339,7 +2687,7 @@ static hipError_t bloom_part_w(PackedView sym, int k, BloomView bf, TableView ft
     const TableView& lg = KEEP ? fg : ft;  // the partition levels' geometry
     hipError_t e;
     const unsigned long long* gate = &ctr->part_overflow;
-    if (phase & (PH_MAIN | PH_LEVELS)) {
+    if (phase & PH_MAIN) {
     hipLaunchKernelGGL(k_batch_begin, dim3(1), dim3(1), 0, s, ctr);
     const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
     constexpr int NT = scatter_threads<W>(), NT2 = p2f_threads<OW>();
@@ -3363,7 +2711,7 @@ static hipError_t bloom_part_w(PackedView sym, int k, BloomView bf, TableView ft
             return e;
     }
     }
-    if (phase & (PH_MAIN | PH_B3)) {  // (PH_B3 alone: after PH_LEVELS, hist2 untouched in between)
+    if (phase & PH_MAIN) {
         PartBufs p3 = pb;  // k_b3's view: a filter region = R_fine / R_f consecutive fine bins
         if constexpr (KEEP) p3.B2 = (uint32_t)(fg.R / ft.R) * pb.B2;
         if ((e = launch_b3<true>(bf, ft, ctr, p3, nullptr, fresh, s, OW)) != hipSuccess) return e;
@@ -3558,17 +2906,6 @@ hipError_t WOps<W>::count_reuse(TableView t, BloomView bf, DevCounters* ctr, Par
                                 int gate, uint64_t windows, hipStream_t s) {
     if (gate) return count_reuse_w<W, true>(t, bf, ctr, pb, fresh, level, windows, s);
     return count_reuse_w<W, false>(t, bf, ctr, pb, fresh, level, windows, s);
-}
-
-template <int W>
-hipError_t WOps<W>::bloom_count_fused(BloomView bf, TableView t, TableView fg, PartBufs pb, DevCounters* ctr,
-                                      int fresh_filter, hipStream_t s) {
-    return bloom_count_fused_w<W>(bf, t, fg, pb, ctr, fresh_filter, s);
-}
-template <int W>
-hipError_t WOps<W>::bloom_probe(BloomView bf, TableView fg, PartBufs pb, uint32_t nsample, int fresh_filter,
-                                uint32_t* out, hipStream_t s) {
-    return bloom_probe_w<W>(bf, fg, pb, nsample, fresh_filter, out, s);
 }
 
 template <int W>

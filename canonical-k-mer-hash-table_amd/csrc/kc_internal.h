@@ -78,10 +78,6 @@ struct DevCounters {
     unsigned long long heavy_n;         uint64_t _p14[15];
     unsigned long long spilled;         uint64_t _p15[15];
     unsigned long long heavy;           uint64_t _p16[15];
-    // fused Bloom + counting pass (k_bf3): the gated insertions it made into the speculative
-    // table, added to `inserted` when the counting pass confirms the same input (kc_api.cpp)
-    unsigned long long spec_inserted;   uint64_t _p17[15];
-    unsigned long long spec_overflow;   uint64_t _p18[15];  // keys the fused pass could not place
     // deferred level 3: a batch's part_overflow held aside while the group's level 3 runs
     unsigned long long held_overflow;   uint64_t _p19[15];
 };
@@ -169,32 +165,18 @@ inline int slots_per_bucket(int W) { return BUCKET_WORDS / (W + 1); }
 // Windows rolled per thread in the partitioned kernels, and the workgroup size of the
 // segmented level 1 (tile = threads x windows), by key width: wide keys take fewer
 // windows per thread and smaller groups so that the registers and the LDS tile fit.
-#ifndef KC_RUNW1
-#define KC_RUNW1 16  // (A/B knob: one-word keys' windows per thread)
-#endif
-constexpr int run_width(int W) { return W == 1 ? KC_RUNW1 : W == 2 ? 8 : W <= 4 ? 8 : 4; }
-// The segmented level 1 (k_p1) of one- and two-word keys: 512-thread workgroups, two per CU.
+constexpr int run_width(int W) { return W == 1 ? 16 : W == 2 ? 8 : W <= 4 ? 8 : 4; }
+// The segmented level 1 (k_p1) of one- to four-word keys: 512-thread workgroups, two per CU.
 // (1024 threads with half the windows per thread -- 8 waves per SIMD within 64 VGPRs -- spill
 // and ran 30 % slower: profiles/r03_ab_p1_nt.txt)
-#ifndef KC_P1_NT12
-#define KC_P1_NT12 512
-#endif
-constexpr int scatter_threads_w(int W) { return W <= 2 ? KC_P1_NT12 : W <= 4 ? 512 : 256; }
-#ifndef KC_P1_RUNW1
-#define KC_P1_RUNW1 KC_RUNW1  // (A/B knob: the segmented level 1's one-word windows per thread)
-#endif
-constexpr int p1_runw(int W) {
-    return W == 1 ? KC_P1_RUNW1 * 512 / KC_P1_NT12 : W <= 2 ? run_width(W) * 512 / KC_P1_NT12 : run_width(W);
-}
+constexpr int scatter_threads_w(int W) { return W <= 4 ? 512 : 256; }
+constexpr int p1_runw(int W) { return run_width(W); }
 constexpr int p1_tile(int W) { return scatter_threads_w(W) * p1_runw(W); }  // windows per segmented level-1 tile
 // level 2 (k_p2f): workgroup size by key width, and its LDS for F2 regions per coarse bin
-#ifndef KC_P2F_NT
-#define KC_P2F_NT 0  // 0: the default below
-#endif
 // a scatter's per-bin LDS arrays (k_count_impl.h PartLds: 4 x u32 + 1 x u64 per bin, the
 // tile's keys after them at a 16-byte boundary) and its static extras
 constexpr size_t bin_lds_bytes(uint32_t F) { return ((size_t)F * 24 + 15) / 16 * 16 + 16; }
-constexpr int p2f_threads_w(int W) { return KC_P2F_NT ? KC_P2F_NT : (W <= 2 ? 1024 : W <= 4 ? 512 : 256); }
+constexpr int p2f_threads_w(int W) { return W <= 2 ? 1024 : W <= 4 ? 512 : 256; }
 // k_p1's LDS stage of the packed stream: two buffers of the words one tile reads, 12 bytes each
 constexpr size_t p1_stage_bytes(int W) { return (size_t)(p1_tile(W) / 32 + W + 3) * 24; }
 // segmented level 1 (k_p1, W-word output keys + the heavy table + the stage) for F1 coarse bins
@@ -224,9 +206,6 @@ hipError_t launch_count(PackedView sv, uint64_t sym_bound, int k, int mode, Tabl
 // overflow gate (PH_TAIL).  The host may run the tail only when the main phase left a skew
 // list or an overflow (kc_api.cpp); with both empty every tail kernel is a no-op.
 constexpr int PH_MAIN = 1, PH_TAIL = 2, PH_ALL = 3;
-// Bloom pass only: the main phase's partition levels without its level 3 (k_b3), and k_b3 alone
-// (the host runs the fused pass, launch_bloom_count_fused, or k_b3 in between)
-constexpr int PH_LEVELS = 4, PH_B3 = 8;
 // Counting pass, deferred level 3 (segmented layout): the batch's levels 1-2 into its slot of the
 // group's level-2 segments (PartBufs b2t / b2off), and level 3 over the whole group (pb.B2 = b2t)
 constexpr int PH_L12 = 16, PH_L3 = 32;
@@ -246,20 +225,6 @@ hipError_t launch_bloom_partitioned(PackedView sv, int k, int W, BloomView bf, T
 // filter is ignored); windows: the batch's windows (counted by the Bloom pass)
 hipError_t launch_count_reuse(int W, TableView t, BloomView bf, DevCounters* ctr, PartBufs pb, int fresh, int level,
                               int gate, uint64_t windows, hipStream_t s);
-// Fused Bloom pass 1 + gated counting pass over the kept level-2 fine bins (partition reuse with
-// the table sized before the Bloom pass ends): one workgroup per table region r of t (R a power
-// of two <= fg.R, <= nblocks): the region's filter blocks in LDS take insertion_process for every
-// key of its fine bins, then the same keys behind the gate go into the region's LDS table.
-// pb: the kept partitions (keys2 / hist2 = fills / cap2 / B2 = segments per fine bin / rec12).
-// The table must be fresh (every region is written); inserted counts go to ctr->spec_inserted.
-hipError_t launch_bloom_count_fused(int W, BloomView bf, TableView t, TableView fg, PartBufs pb, DevCounters* ctr,
-                                    int fresh_filter, hipStream_t s);
-// The fused pass's table size from a sample of the kept fine bins: for nsample fine bins spread
-// over fg (fresh filter), the distinct table-key words that pass the gate after the bin's own
-// Bloom pass; out[i] = that count, or ~0u when the bin's keys outgrew the probe's set
-constexpr uint32_t PROBE_BINS = 64;
-hipError_t launch_bloom_probe(int W, BloomView bf, TableView fg, PartBufs pb, uint32_t nsample, int fresh_filter,
-                              uint32_t* out, hipStream_t s);
 // The two passes over pre-aggregated {W key words, count} records (the owner side of the sharded
 // Bloom filter, kaarme_amd/sharded.py): Bloom pass 1 (a record of count >= 2 inserted twice) into
 // the filter's regions ft, and the gated (gate = 1) or plain counting pass into the table t.
@@ -268,8 +233,6 @@ hipError_t launch_bloom_records(int W, const uint64_t* rec, uint64_t n, BloomVie
                                 PartBufs pb, int fresh, hipStream_t s);
 hipError_t launch_count_records(int W, const uint64_t* rec, uint64_t n, TableView t, BloomView bf, DevCounters* ctr,
                                 PartBufs pb, int fresh, int gate, hipStream_t s);
-// ctr->inserted += ctr->spec_inserted (the counting pass confirmed the fused pass's input)
-hipError_t launch_spec_commit(DevCounters* ctr, uint64_t windows, hipStream_t s);
 // deferred level 3: part_overflow -> held_overflow (and cleared), or back (restore)
 hipError_t launch_hold_overflow(DevCounters* ctr, int restore, hipStream_t s);
 // 64-bit checksum of the chunks' bytes (a promise check between two passes over one image):
@@ -340,10 +303,6 @@ struct WOps {
                                         DevCounters* ctr, PartBufs pb, int fresh, int keep, hipStream_t s, int phase);
     static hipError_t count_reuse(TableView t, BloomView bf, DevCounters* ctr, PartBufs pb, int fresh, int level,
                                   int gate, uint64_t windows, hipStream_t s);
-    static hipError_t bloom_count_fused(BloomView bf, TableView t, TableView fg, PartBufs pb, DevCounters* ctr,
-                                        int fresh_filter, hipStream_t s);
-    static hipError_t bloom_probe(BloomView bf, TableView fg, PartBufs pb, uint32_t nsample, int fresh_filter,
-                                  uint32_t* out, hipStream_t s);
     static hipError_t bloom_records(const uint64_t* rec, uint64_t n, BloomView bf, TableView ft, DevCounters* ctr,
                                     PartBufs pb, int fresh, hipStream_t s);
     static hipError_t count_records(const uint64_t* rec, uint64_t n, TableView t, BloomView bf, DevCounters* ctr,

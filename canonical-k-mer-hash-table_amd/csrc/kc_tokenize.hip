@@ -77,62 +77,8 @@ __global__ __launch_bounds__(256) void k_tile_map(const ChunkDesc* __restrict__ 
 }
 
 // --------------------------------------------------------------------------------
-// k_tile_summary
-// --------------------------------------------------------------------------------
-__global__ __launch_bounds__(TILE_THREADS) void k_tile_summary(const uint8_t* __restrict__ src,
-                                                               const ChunkDesc* __restrict__ chunks, int n_chunks,
-                                                               int fmt, TileInfo* __restrict__ tiles) {
-    __shared__ uint32_t s_nl[TILE_THREADS / 64];
-    __shared__ uint32_t s_mk[TILE_THREADS / 64];
-    __shared__ int s_c;
-    const uint64_t t = blockIdx.x;
-    const uint64_t base = t * TILE;
-    (void)n_chunks;
-    if (threadIdx.x == 0) s_c = (int)tiles[t].nl;  // k_tile_map
-    __syncthreads();
-    const ChunkDesc cd = chunks[s_c];
-    const uint64_t rel = base - cd.stage_off;
-    const uint32_t valid = (uint32_t)min((uint64_t)TILE, cd.len - rel);
-    const uint32_t avail = (uint32_t)min((uint64_t)TILE + 64, cd.len - rel);
-    const int tid = threadIdx.x;
-    const uint32_t my0 = tid * 16;
-    const uint32_t vh = valid > my0 ? valid - my0 : 0;
-    uint32_t nl = 0, mk = 0;
-    if (fmt != FMT_PLAIN && vh) {
-        uint32_t w[4];
-        load16(src + cd.src_off + rel + my0, avail - my0, w);
-        const uint32_t vmask = vh >= 16 ? 0xFFFFu : ((1u << vh) - 1);
-        const uint32_t nlm = eq_mask16(w, 0x0A0A0A0Au) & vmask;
-        nl = __builtin_popcount(nlm);
-        if (fmt == FMT_FASTA) {
-            const uint32_t gtm = eq_mask16(w, 0x3E3E3E3Eu) & vmask;
-            const uint32_t any = nlm | gtm;
-            if (any) mk = (gtm >> (31 - __builtin_clz(any))) & 1 ? 2u : 1u;
-        }
-    }
-    // block reductions: sum of nl, last marker
-    for (int d = 32; d >= 1; d >>= 1) nl += __shfl_xor(nl, d, 64);
-    uint32_t tag = mk ? ((uint32_t)tid << 2) | mk : 0;
-    for (int d = 32; d >= 1; d >>= 1) tag = max(tag, (uint32_t)__shfl_xor(tag, d, 64));
-    if ((tid & 63) == 0) { s_nl[tid >> 6] = nl; s_mk[tid >> 6] = tag; }
-    __syncthreads();
-    if (tid == 0) {
-        uint32_t tn = 0, tm = 0;
-        for (int w = 0; w < TILE_THREADS / 64; w++) { tn += s_nl[w]; tm = max(tm, s_mk[w]); }
-        TileInfo ti;
-        ti.nl = tn;
-        ti.valid = valid;
-        ti.marker = (uint8_t)(tm & 3);
-        ti.first = rel == 0;
-        ti.bh = (uint8_t)cd.bh;
-        ti.pad = 0;
-        ti.avail = avail;
-        ti.src = cd.src_off + rel;
-        tiles[t] = ti;
-    }
-}
-
-// k_tile_summary_m<TPB>: the same per-tile summary for TPB consecutive tiles per workgroup,
+// k_tile_summary_m<TPB>: per 4 KiB tile the FASTA/FASTQ newline count and the last FASTA header
+// marker, for TPB consecutive tiles per workgroup,
 // every thread's TPB loads (tile map -> chunk descriptor -> 16 bytes of each tile) issued
 // before any is used: one 4 KiB tile per workgroup left a chain of three dependent loads per
 // 16 bytes in flight, the summary ran at ~3.5 TB/s of its 1.6 GB (C2)
@@ -555,19 +501,8 @@ hipError_t launch_tokenize(const uint8_t* src, uint64_t ntiles, const ChunkDesc*
     const uint64_t nblk = (ntiles + TSCAN - 1) / TSCAN;
     if (n_chunks <= 0) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_tile_map, dim3((unsigned)n_chunks), dim3(256), 0, s, d_chunks, tiles);
-static const int tpb = [] {  // A/B: KC_TSUM_TPB = tiles per summary workgroup (1 = k_tile_summary)
-        const char* v = std::getenv("KC_TSUM_TPB");
-        return v ? std::atoi(v) : 4;
-    }();
-    if (tpb == 4)
-        hipLaunchKernelGGL(k_tile_summary_m<4>, dim3((unsigned)((ntiles + 3) / 4)), dim3(TILE_THREADS), 0, s, src,
-                           d_chunks, ntiles, fmt, tiles);
-    else if (tpb == 2)
-        hipLaunchKernelGGL(k_tile_summary_m<2>, dim3((unsigned)((ntiles + 1) / 2)), dim3(TILE_THREADS), 0, s, src,
-                           d_chunks, ntiles, fmt, tiles);
-    else
-            hipLaunchKernelGGL(k_tile_summary, dim3((unsigned)ntiles), dim3(TILE_THREADS), 0, s, src, d_chunks, n_chunks,
-                       fmt, tiles);
+    hipLaunchKernelGGL(k_tile_summary_m<4>, dim3((unsigned)((ntiles + 3) / 4)), dim3(TILE_THREADS), 0, s, src,
+                       d_chunks, ntiles, fmt, tiles);
     hipLaunchKernelGGL(k_tscan_block, dim3((unsigned)nblk), dim3(TSCAN), 0, s, tiles, ntiles, fmt, touts, tblk);
     hipLaunchKernelGGL(k_tscan_top, dim3(1), dim3(TSCAN), 0, s, tblk, nblk, fmt, ctr);
     hipLaunchKernelGGL(k_zero_edges, dim3((unsigned)((ntiles + 255) / 256)), dim3(256), 0, s, tiles, touts, tblk,

@@ -134,19 +134,6 @@ hipError_t launch_bloom_popcount2(const uint32_t* words, uint64_t n, int blocked
     return hipGetLastError();
 }
 
-// the counting pass confirmed the fused Bloom + counting pass's input (kc_api.cpp count_reused):
-// its gated insertions and the batch's windows become the counting pass's
-__global__ void k_spec_commit(DevCounters* ctr, unsigned long long windows) {
-    ctr->inserted += ctr->spec_inserted;
-    ctr->spec_inserted = 0;
-    ctr->windows += windows;
-}
-
-hipError_t launch_spec_commit(DevCounters* ctr, uint64_t windows, hipStream_t s) {
-    hipLaunchKernelGGL(k_spec_commit, dim3(1), dim3(1), 0, s, ctr, (unsigned long long)windows);
-    return hipGetLastError();
-}
-
 // deferred level 3 (kc_api.cpp run_deferred): a batch whose segments overflowed holds its
 // part_overflow aside while the group's level 3 inserts the other batches (k_p3 skips on the
 // flag), then gets it back for its tail (the exact pipeline redoes that batch)

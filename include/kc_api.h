@@ -40,7 +40,9 @@ extern "C" {
 #define KC_ERR_STATE (-4)       /* call out of order (e.g. count before bloom finalize) */
 #define KC_ERR_IO (-5)          /* file error */
 #define KC_ERR_NOMEM (-6)       /* host or device allocation failed */
-#define KC_ERR_UNSUPPORTED (-7) /* the Bloom filter on the per-window routing entry point kc_route_device (the sharded Bloom pass is pre-aggregated: kc_bloom_merge_device) */
+#define KC_ERR_UNSUPPORTED (-7) /* the Bloom filter on the per-window routing entry point kc_route_device (a sharded
+                                   Bloom job routes {key, count} records to the filter's owner instead:
+                                   kc_bloom_records_device); the compact representation of a -m 0 table */
 
 /* input_mode of main.cpp:178-189 */
 #define KC_FMT_FASTA 0
@@ -128,7 +130,11 @@ int kc_count_chunk(kc_ctx* ctx, const uint8_t* buf, size_t len, int fmt, int bro
  *     segment overflow) to launch the batch's fallback work only when it is needed;
  *   - an image of several batches: before batch i+1 is queued, the call waits until batch i's
  *     chunk descriptors have reached the device (queued after the work before it), so at most
- *     one batch is queued ahead; the fallback work stays behind a device-side gate;
+ *     one batch is queued ahead; the fallback work stays behind a device-side gate.  A counting
+ *     pass of several batches defers level 3 (kc_stats.deferred_level3): the level-2 partitions
+ *     of a group of batches wait in HBM and one level-3 pass inserts them (one sweep of the
+ *     table per group, not per batch; KC_DEFER=0 disables it); the call then waits for each
+ *     batch's partition levels (it reads the batch's skew-list and overflow counters);
  *   - the counting pass that reuses the Bloom pass's partitions waits for its work (below).
  * Level-1 reuse: when the Bloom pass is one staging batch, it keeps its window
  * partition, and a counting pass given the same image pointer, chunk table and format
@@ -191,11 +197,12 @@ int kc_insert_counts_device(kc_ctx* ctx, const uint64_t* dev_records, uint64_t n
 int kc_insert_counts_runs_device(kc_ctx* ctx, const uint64_t* dev_records, const uint64_t* group_counts,
                                  uint32_t ngroups, void* hip_stream);
 
-/* Sharded Bloom filter (the reference has one filter,
+/* Whole-filter primitives (the reference has one filter,
  * DoubleAtomicDoubleBloomFilter, double_bloomfilter.hpp:233-260, filled by every worker of
- * the Bloom pass, parallel_parser.hpp:2788-2940).  Every rank runs kc_bloom_device over its
- * own input; the ranks' filters are then combined and every rank gates its counting pass
- * with the combined filter before the pre-aggregated merge:
+ * the Bloom pass, parallel_parser.hpp:2788-2940), for a caller that runs kc_bloom_device on
+ * every rank and combines the ranks' whole filters itself.  (kaarme_amd.sharded does not: it
+ * shards the filter by the k-mers' owner, kc_bloom_records_device / kc_count_records_device
+ * below, so no filter crosses xGMI.)  The primitives:
  *   kc_bloom_get_device   copies words [first_word, first_word + n_words) of the filter to
  *                         dev_dst (after the work queued on hip_stream and the context);
  *   kc_bloom_merge_device combines nparts copies of one word range (consecutive in

@@ -164,12 +164,12 @@ def test_synth_device_matches_cpu_generator(tmp_path):
 def test_cli_end_to_end(case, cli_path, golden_input, tmp_path):
     """The drop-in CLI: the input read into HBM by parallel pinned slices and counted from
     there (device; Bloom jobs count from the Bloom pass's partitions), or staged as host
-    chunks (KC_CLI_HOST=1)."""
+    chunks (--host-chunks)."""
     path = golden_input(case["input"])
     out = tmp_path / "out.kaarme_counts"
-    env = dict(os.environ, KC_CLI_HOST="1" if cli_path == "host" else "0")
-    r = subprocess.run([CLI, path, str(case["k"]), "-t", "3", "-o", str(out)] + case["args"],
-                       capture_output=True, text=True, env=env)
+    extra = ["--host-chunks"] if cli_path == "host" else []
+    r = subprocess.run([CLI, path, str(case["k"]), "-t", "3", "-o", str(out)] + case["args"] + extra,
+                       capture_output=True, text=True)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert sorted_digest_file(out) == (case["sorted_sha256"], case["lines"])
     assert "Time used to build hash table" in r.stdout
@@ -634,7 +634,7 @@ def test_twelve_byte_table_records(tmp_path, k, seg, slots, monkeypatch):
     regions, -s 3e8 146 485) move 12-byte level records (kc_count_impl.h Rec12, R12_REG: x
     recovered from x mod 2^xb and the bin's lowest x) where the bins are narrow enough: k = 33 at
     both levels; k = 51 at level 2 (and level 1 of the big table); k = 55 at level 2 of the big
-    table only.  Compared with the oracle and with the 16-byte records (KC_NO_REC12)."""
+    table only.  Compared with the oracle."""
     torch = pytest.importorskip("torch")
     monkeypatch.setenv("KC_INSERT_PATH", "partitioned")
     if seg == "tiny":
@@ -644,21 +644,16 @@ def test_twelve_byte_table_records(tmp_path, k, seg, slots, monkeypatch):
     subprocess.run([GEN, str(fa), "30000", "150", "200000", "-s", "7", "-n", "0.001"], check=True)
     data = open(fa, "rb").read()
     img = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
-    got = {}
-    for rec in ("12", "16"):
-        if rec == "16":
-            monkeypatch.setenv("KC_NO_REC12", "1")
-        with ka.KmerCounter(ka.Config(k=k, mode=2, min_abundance=1, table_slots=slots)) as kc:
-            kc.count_device(img.data_ptr(), ka.plan_chunks(data, k, ka.FMT_FASTA), ka.FMT_FASTA)
-            st = kc.finish()
-            assert st["part_fallbacks"] == 0
-            if seg == "tiny" and slots < 10 ** 8:  # (146 485 regions leave every segment short)
-                assert st["spilled"] > 0
-            got[rec] = sorted_digest_lines(kc.lines())
+    with ka.KmerCounter(ka.Config(k=k, mode=2, min_abundance=1, table_slots=slots)) as kc:
+        kc.count_device(img.data_ptr(), ka.plan_chunks(data, k, ka.FMT_FASTA), ka.FMT_FASTA)
+        st = kc.finish()
+        assert st["part_fallbacks"] == 0
+        if seg == "tiny" and slots < 10 ** 8:  # (146 485 regions leave every segment short)
+            assert st["spilled"] > 0
+        got = sorted_digest_lines(kc.lines())
     out = tmp_path / "oracle.txt"
     oracle_count(str(fa), k, ["-m", "2", "-a", "1"], out)
-    assert got["12"] == sorted_digest_file(out)
-    assert got["16"] == got["12"]
+    assert got == sorted_digest_file(out)
 
 
 @pytest.mark.parametrize("k", [15, 31, 51, 127])
