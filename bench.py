@@ -404,7 +404,11 @@ def setup_job(args, env, image=None):
     batch = min((nbytes + len(chunks) * 4096 + (1 << 20)) // 4096 * 4096, cap // 4096 * 4096)
     windows_expected = N * (L - k + 1)
     estimate = None
-    if (strong and (share or (dist and world > 1))) or (dist and args.unique):
+    # (strong presets on one GPU too, unless --s-table: the job's table is then sized from the
+    # estimate -- C4 holds 1.0 G distinct k-mers in a -s 2.6e9 table, C5 1.5 G in -s 3.6e9, which as
+    # 25 % headroom over -s take 83 / 192 GB of HBM for 35 / 86 GB of need)
+    est_table = strong and not dist and not share and not args.s_table
+    if (strong and (share or est_table or (dist and world > 1))) or (dist and args.unique):
         # (sharded Bloom jobs too: the rank's ungated local count holds all its distinct k-mers)
         # a rank's local table holds its own input's distinct k-mers, which its 1/G share of -s
         # does not bound: sized from a HyperLogLog estimate of them (kc_estimate_distinct_device,
@@ -431,6 +435,8 @@ def setup_job(args, env, image=None):
     tbl =" ".join(["-m", "2"] + table_args(slots, args.unique))
     workload = (f"{args.config}: synthetic {N} x {L} bp reads/GPU, k={k}, {tbl}" if not strong else
                 f"{args.config}: synthetic {args.reads} x {L} bp reads over {world} GPU(s), k={k}, {tbl} per GPU")
+    if est_table:
+        workload += " (device table sized from the distinct estimate, 1.1 x HLL, not 1.25 x -s)"
     if share:
         workload = (f"{args.config} share 1/{share}: synthetic {N} x {L} bp reads (rank 0 of {args.reads} over "
                     f"{share} GPUs), k={k}, -m 2, local table from the distinct estimate, no exchange")
@@ -443,7 +449,7 @@ def setup_job(args, env, image=None):
     # rank's owner table digests its k-mers; parity_record combines them).  A weak job over N > 1
     # ranks counts N x the preset's reads, which no fixture covers.
     fx = fixture_case(args, share, first, N) if (world == 1 or strong) else None
-    cfg = ka.Config(k=k, mode=2, table_slots=estimate["local_slots"] if share else slots,
+    cfg = ka.Config(k=k, mode=2, table_slots=estimate["local_slots"] if (share or est_table) else slots,
                     min_abundance=fx["min_abundance"] if fx else 2, batch_bytes=batch,
                     device=local, bf_enable=bool(args.unique), est_unique=args.unique)
     if dist:
@@ -596,10 +602,13 @@ def run_workload(args, env, image=None):
     if not dist and args.compact:  # the Kaarme slot words built from this table
         torch.cuda.synchronize()
         c0 = time.perf_counter()
-        info = counter.compact()
+        try:
+            info = counter.compact()
+        except ka.KcError as e:  # (the compact words need HBM beside the table: none left by C5's)
+            info = {"error": str(e)}
         c1 = time.perf_counter()
-        n = max(1, info["kmers"])
-        compact = {"build_ms": round((c1 - c0) * 1e3, 2), "kmers": info["kmers"],
+        n = max(1, info.get("kmers", 0))
+        compact = {"error": info["error"]} if "error" in info else {"build_ms": round((c1 - c0) * 1e3, 2), "kmers": info["kmers"],
                    "chain_starts": info["chain_starts"], "bytes_per_kmer": round(info["bytes"] / n, 2),
                    "table_bytes_per_kmer": round(info["table_bytes"] / n, 2),
                    "note": "kc_compact after the timed steps (not in value): 8-byte slot words at load 0.8 + "
@@ -845,6 +854,8 @@ def main():
     ap.add_argument("--share", type=int, default=0,
                     help="strong presets on one GPU: time rank 0's share of a G-rank job (its reads, its local "
                          "table sized from the distinct estimate; no exchange)")
+    ap.add_argument("--s-table", action="store_true",
+                    help="strong presets on one GPU: size the table from -s (1.25 x) instead of the distinct estimate")
     ap.add_argument("--force-sharded", action="store_true",
                     help="use the sharded (RCCL) path even at one rank (testing)")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),

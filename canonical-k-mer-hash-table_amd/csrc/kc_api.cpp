@@ -944,7 +944,11 @@ static int plan_deferral(kc_ctx* c, const kc_chunk* chunks, size_t n) {
     // KC_DEFER: 0 = off, N = groups of at most N batches (tests)
     const char* kd = std::getenv("KC_DEFER");
     const uint64_t kmax = kd ? std::strtoull(kd, nullptr, 10) : ~0ULL;
-    if (kmax == 0 || !c->nbuckets || !c->seg_ok) return KC_OK;
+    if (kmax == 0 || !c->nbuckets || !c->seg_ok) {
+        if (debug_on()) std::fprintf(stderr, "deferred level 3: off (knob %d, table %d, segmented levels %d)\n",
+                                     kmax != 0, c->nbuckets != 0, (int)c->seg_ok);
+        return KC_OK;
+    }
     const PathKnob pk = insert_path_knob();
     if (pk == PathKnob::Direct || pk == PathKnob::Exact) return KC_OK;
     uint64_t nb = 0, syms = 0, used = 0, cnt = 0;
@@ -965,7 +969,10 @@ static int plan_deferral(kc_ctx* c, const kc_chunk* chunks, size_t n) {
     if (nb < 2 || !use_partitioned(c, syms)) return KC_OK;
     int rc = ensure_part(c, syms, true);  // one slot: the segment geometry
     if (rc) return rc;
-    if (c->pb.cap1 == 0) return KC_OK;
+    if (c->pb.cap1 == 0) {
+        if (debug_on()) std::fprintf(stderr, "deferred level 3: off (exact layout for this batch size)\n");
+        return KC_OK;
+    }
     const uint64_t slot_bytes = c->R * c->pb.B2 * c->pb.cap2 * c->W * 8;
     size_t fr = 0, tot = 0;
     HIPCHK(c, hipMemGetInfo(&fr, &tot));

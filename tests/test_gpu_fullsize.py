@@ -32,7 +32,7 @@ def _fixture():
 def _bench_args(config, share=0):
     import bench
     base = argparse.Namespace(config=config, reads=None, read_len=None, genome=None, k=None, slots=None,
-                              unique=None, batch_mib=0, err=0.001, seed=42, share=share)
+                              unique=None, batch_mib=0, err=0.001, seed=42, share=share, s_table=False)
     return bench, bench.resolve(base, config)
 
 
