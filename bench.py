@@ -419,6 +419,12 @@ def setup_job(args, env, image=None):
         est = probe.estimate_distinct_device(image.data_ptr(), chunks, ka.FMT_FASTA, stream.cuda_stream)
         probe.close()
         local_slots = min(windows_expected, int(1.1 * est) + (1 << 20))
+        if dist and world > 1:
+            # one size for every rank's local (and owner) table: the groups a rank receives are then
+            # sorted by its own table's regions, and merge in one level-3 pass (sharded.DeviceEngine)
+            t = torch.tensor([local_slots], dtype=torch.int64, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            local_slots = int(t.item())
         estimate = {"distinct_estimate": int(est), "local_slots": local_slots,
                     "ms": round((time.perf_counter() - e0) * 1e3, 1),
                     "method": "HyperLogLog, 2^14 registers (~0.8 % std. error); local table = 1.1 x estimate"}
