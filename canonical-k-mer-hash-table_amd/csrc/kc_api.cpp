@@ -408,18 +408,59 @@ struct PartGeo {
 };
 static PartGeo table_geo(const kc_ctx* c) { return PartGeo{c->F1, c->F2, c->R, c->W}; }
 
-// slots > 1: the level-2 histogram and key buffers hold that many batches' segments (a deferred
-// level 3, run_deferred)
-static int ensure_part_geo(kc_ctx* c, uint64_t syms, bool seg, const PartGeo& g, PartBufs& pb, PartCap& cap,
-                           uint32_t bins1 = 0, uint32_t slots = 1) {
+// The sizes of a partitioned pass over a batch of up to `syms` symbols (no allocation):
+// level-1 workgroups, level-2 segments per bin, the segment capacities, the skew list and the key
+// buffers' words.  slots > 1: the level-2 histogram and key buffers hold that many batches'
+// segments (a deferred level 3, run_deferred), each record rec2 bytes (level2_record_bytes)
+struct PartPlan {
+    uint32_t nblk1, B2;
+    uint64_t n1, n2, nbs;     // histogram entries: level 1, level 2, block sums
+    uint64_t cap1, cap2;      // segment capacities (0: the exact layout)
+    uint64_t spill_cap, spill_words, need1, need2;
+};
+static PartPlan part_plan(const kc_ctx* c, uint64_t syms, bool seg, const PartGeo& g, uint32_t bins1, uint32_t slots,
+                          uint64_t rec2 = 0) {
+    PartPlan p{};
     const uint64_t tile = (uint64_t)COUNT_THREADS * run_width(c->W);
-    const uint32_t nblk1 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(2048, (syms + tile - 1) / tile));
-    const uint32_t B2 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(64, 2048 / g.F1));
+    p.nblk1 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(2048, (syms + tile - 1) / tile));
+    p.B2 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(64, 2048 / g.F1));
     // every array is sized for the geometry of THIS call (a Bloom job re-sizes the table
     // after each Bloom pass, so F1 and R may grow between calls on one context)
-    const uint64_t n1 = (uint64_t)std::max<uint32_t>(g.F1, bins1) * 2048;  // level-1 bins x max workgroups
-    const uint64_t n2 = g.R * B2 * slots;
-    const uint64_t nbs = (std::max(n1, n2) + 4095) / 4096 + 2;
+    p.n1 = (uint64_t)std::max<uint32_t>(g.F1, bins1) * 2048;  // level-1 bins x max workgroups
+    p.n2 = g.R * p.B2 * slots;
+    p.nbs = (std::max(p.n1, p.n2) + 4095) / 4096 + 2;
+    if (seg) {
+        auto capacity = [](double e) { return ((uint64_t)std::ceil(e + 8.0 * std::sqrt(e) + 32.0) + 7) / 8 * 8; };
+        const uint64_t t1 = (uint64_t)p1_tile(c->W);  // k_p1<..., OutSeg> rounds block ranges to its tile
+        const uint64_t per1 = ((syms + p.nblk1 - 1) / p.nblk1 + t1 - 1) / t1 * t1;  // windows per level-1 block
+        const uint64_t nseg = (p.nblk1 + p.B2 - 1) / p.B2;                           // level-1 segments per p2 block
+        p.cap1 = capacity((double)per1 / g.F1);
+        p.cap2 = capacity((double)nseg * per1 / g.F1 / g.F2);
+        if (const char* v = std::getenv("KC_SEG_CAP")) p.cap1 = p.cap2 = std::max<uint64_t>(1, std::strtoull(v, 0, 10));
+        // the segment walks index a virtual run with 32-bit offsets
+        if (nseg * p.cap1 >= (1ULL << 31) || (uint64_t)p.B2 * p.cap2 * slots >= (1ULL << 31)) p.cap1 = p.cap2 = 0;
+    }
+    // the skew list of a segmented batch: {key words, count} records of keys past a segment's
+    // end and of repeated windows (Bloom pass: plain keys), an eighth of the windows before the
+    // batch falls back to the exact layout; its exact pipeline runs through the key buffers
+    if (p.cap1) {
+        p.spill_cap = std::max<uint64_t>(1 << 16, syms / 8);
+        if (const char* v = std::getenv("KC_SPILL_CAP")) p.spill_cap = std::strtoull(v, 0, 10);  // tests
+    }
+    p.spill_words = p.spill_cap * (g.IW + 1);
+    p.need1 = std::max(std::max<uint64_t>(syms, (uint64_t)g.F1 * p.nblk1 * p.cap1) * g.IW, p.spill_words);
+    // one batch's level 2 in W-word items; a deferred group's slots in level-2 records (the exact
+    // pipeline of a batch's tail, which writes W-word items, runs after its group's level 3)
+    const uint64_t l2 = slots > 1 && rec2 ? (g.R * p.B2 * p.cap2 * slots * rec2 + 7) / 8 : g.R * p.B2 * p.cap2 * g.IW;
+    p.need2 = std::max(std::max<uint64_t>(syms * g.IW, l2), p.spill_words);
+    return p;
+}
+
+// Partition buffers for a batch of up to `syms` symbols (lazily grown): part_plan's sizes
+static int ensure_part_geo(kc_ctx* c, uint64_t syms, bool seg, const PartGeo& g, PartBufs& pb, PartCap& cap,
+                           uint32_t bins1 = 0, uint32_t slots = 1, uint64_t rec2 = 0) {
+    const PartPlan p = part_plan(c, syms, seg, g, bins1, slots, rec2);
+    const uint64_t n1 = p.n1, n2 = p.n2, nbs = p.nbs;
     if (n1 > cap.h1) {
         hipFree(pb.hist1);
         hipFree(pb.off1);
@@ -448,29 +489,9 @@ static int ensure_part_geo(kc_ctx* c, uint64_t syms, bool seg, const PartGeo& g,
             return c->fail(KC_ERR_NOMEM, "partition histogram allocation failed");
         cap.bs = nbs;
     }
-    uint64_t cap1 = 0, cap2 = 0;
-    if (seg) {
-        auto capacity = [](double e) { return ((uint64_t)std::ceil(e + 8.0 * std::sqrt(e) + 32.0) + 7) / 8 * 8; };
-        const uint64_t t1 = (uint64_t)p1_tile(c->W);  // k_p1<..., OutSeg> rounds block ranges to its tile
-        const uint64_t per1 = ((syms + nblk1 - 1) / nblk1 + t1 - 1) / t1 * t1;  // windows per level-1 block
-        const uint64_t nseg = (nblk1 + B2 - 1) / B2;                               // level-1 segments per p2 block
-        cap1 = capacity((double)per1 / g.F1);
-        cap2 = capacity((double)nseg * per1 / g.F1 / g.F2);
-        if (const char* v = std::getenv("KC_SEG_CAP")) cap1 = cap2 = std::max<uint64_t>(1, std::strtoull(v, 0, 10));
-        // the segment walks index a virtual run with 32-bit offsets
-        if (nseg * cap1 >= (1ULL << 31) || (uint64_t)B2 * cap2 >= (1ULL << 31)) cap1 = cap2 = 0;
-    }
-    // the skew list of a segmented batch: {key words, count} records of keys past a segment's
-    // end and of repeated windows (Bloom pass: plain keys), an eighth of the windows before the
-    // batch falls back to the exact layout; its exact pipeline runs through the key buffers
-    uint64_t spill_cap = 0;
-    if (cap1) {
-        spill_cap = std::max<uint64_t>(1 << 16, syms / 8);
-        if (const char* v = std::getenv("KC_SPILL_CAP")) spill_cap = std::strtoull(v, 0, 10);  // tests
-    }
-    const uint64_t spill_words = spill_cap * (g.IW + 1);
-    const uint64_t need1 = std::max(std::max<uint64_t>(syms, (uint64_t)g.F1 * nblk1 * cap1) * g.IW, spill_words);
-    const uint64_t need2 = std::max(std::max<uint64_t>(syms, g.R * B2 * cap2 * slots) * g.IW, spill_words);
+    const uint64_t cap1 = p.cap1, cap2 = p.cap2, spill_cap = p.spill_cap, spill_words = p.spill_words;
+    const uint64_t need1 = p.need1, need2 = p.need2;
+    const uint32_t nblk1 = p.nblk1, B2 = p.B2;
     auto grow = [&](uint64_t** buf, uint64_t* have, uint64_t need) -> int {
         if (need <= *have) return KC_OK;
         hipFree(*buf);
@@ -500,7 +521,8 @@ static int ensure_part_geo(kc_ctx* c, uint64_t syms, bool seg, const PartGeo& g,
 // the table's levels
 static int ensure_part(kc_ctx* c, uint64_t syms, bool seg, uint32_t bins1 = 0, uint32_t slots = 1) {
     seg = seg && c->seg_ok;
-    return ensure_part_geo(c, syms, seg, table_geo(c), c->pb, c->pb_cap, bins1, slots);
+    return ensure_part_geo(c, syms, seg, table_geo(c), c->pb, c->pb_cap, bins1, slots,
+                           slots > 1 ? level2_record_bytes(c->W, c->cfg.k, c->R) : 0);
 }
 
 // KC_INSERT_PATH (tests, include/kc_api.h knobs): direct | partitioned | exact forces one insert
@@ -938,8 +960,12 @@ static int count_reused(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, s
 
 // The deferred level 3's group size for a counting pass over chunks (device_pass splits them into
 // batches of batch_bytes / max_chunks): the batches' largest symbol bound fixes the segment
-// geometry of every slot; a group takes as many batches as KC_DEFER_FRAC (0.5) of the free HBM
-// holds level-2 segments for, at most MAX_SEG_GROUP segments per region.  KC_DEFER=0: off.
+// geometry of every slot (part_plan, level-2 records of level2_record_bytes); a group takes as many
+// batches as 85 % of the HBM left beside the level-1 buffers and the skew list (free + the
+// partition buffers held now, less 2 GiB) holds level-2 slots for, at most MAX_SEG_GROUP segments
+// per region.  The pass then runs partitioned when one sweep of the table per group beats the
+// direct inserts (use_partitioned's rule with the table's bytes spread over the group), e.g. C5's
+// one-GPU job, whose table is too large for a sweep per batch.  KC_DEFER=0: off.
 static int plan_deferral(kc_ctx* c, const kc_chunk* chunks, size_t n) {
     // KC_DEFER: 0 = off, N = groups of at most N batches (tests)
     const char* kd = std::getenv("KC_DEFER");
@@ -966,23 +992,34 @@ static int plan_deferral(kc_ctx* c, const kc_chunk* chunks, size_t n) {
         used += need;
         cnt++;
     }
-    if (nb < 2 || !use_partitioned(c, syms)) return KC_OK;
-    int rc = ensure_part(c, syms, true);  // one slot: the segment geometry
-    if (rc) return rc;
-    if (c->pb.cap1 == 0) {
+    if (nb < 2) return KC_OK;
+    const PartPlan p = part_plan(c, syms, true, table_geo(c), 0, 1);
+    if (p.cap1 == 0) {
         if (debug_on()) std::fprintf(stderr, "deferred level 3: off (exact layout for this batch size)\n");
         return KC_OK;
     }
-    const uint64_t slot_bytes = c->R * c->pb.B2 * c->pb.cap2 * c->W * 8;
+    const uint64_t rec2 = level2_record_bytes(c->W, c->cfg.k, c->R);
+    const double slot_bytes = (double)c->R * p.B2 * p.cap2 * rec2;
     size_t fr = 0, tot = 0;
     HIPCHK(c, hipMemGetInfo(&fr, &tot));
-    const double avail = 0.5 * ((double)fr + (double)c->k2_words * 8.0 - (double)(2ull << 30));
-    uint64_t g = avail > 0 ? (uint64_t)(avail / (double)slot_bytes) : 0;
-    g = std::min<uint64_t>({g, kmax, nb, MAX_SEG_GROUP / std::max<uint32_t>(1, c->pb.B2)});
+    const double held = (double)(c->k1_words + c->k2_words + c->spill_words) * 8.0;
+    const double fixed = (double)(std::max(p.need1, c->k1_words) + std::max(p.spill_words, c->spill_words)) * 8.0;
+    const double avail = 0.85 * ((double)fr + held - fixed) - (double)(2ull << 30);
+    uint64_t g = avail > 0 ? (uint64_t)(avail / slot_bytes) : 0;
+    g = std::min<uint64_t>({g, kmax, nb, MAX_SEG_GROUP / std::max<uint32_t>(1, p.B2),
+                            ((1ULL << 31) - 1) / ((uint64_t)p.B2 * p.cap2)});
+    // per batch: the direct inserts against the levels' key traffic + the group's table sweep
+    const double table_bytes = (double)c->nbuckets * 128.0;
+    const bool part_wins = pk == PathKnob::Partitioned || use_partitioned(c, syms) ||
+                           (g >= 2 && (double)syms * 275.0 > (double)syms * (4.0 * c->W + 1) * 8.0 +
+                                                                  2.0 * table_bytes / (double)g);
     if (debug_on())
-        std::fprintf(stderr, "deferred level 3: %llu batches, slot %.2f GB, free %.1f GB -> groups of %llu\n",
-                     (unsigned long long)nb, slot_bytes / 1e9, fr / 1e9, (unsigned long long)g);
-    if (g < 2) return KC_OK;
+        std::fprintf(stderr,
+                     "deferred level 3: %llu batches, slot %.2f GB (%llu-byte records), free %.1f GB -> groups of "
+                     "%llu%s\n",
+                     (unsigned long long)nb, slot_bytes / 1e9, (unsigned long long)rec2, fr / 1e9,
+                     (unsigned long long)g, part_wins ? "" : " (direct inserts cheaper: off)");
+    if (g < 2 || !part_wins) return KC_OK;
     c->defer_on = true;
     c->defer_g = (uint32_t)g;
     c->defer_syms = syms;
@@ -1826,6 +1863,27 @@ int kc_finish(kc_ctx* c, kc_stats* st) {
 }
 
 // the compact representation is a snapshot of the table (kc_compact); kc_reset drops it
+// The counting passes' key buffers and skew list are scratch that stays allocated between
+// batches and jobs (a deferred group holds several batches' level-2 segments: C5 on one GPU,
+// ~150 GB).  Before an allocation that would not fit beside them (the compact representation, a
+// full dump) they are released; the next counting pass allocates them again (and cannot count
+// from a Bloom pass's partitions released this way).
+static void make_room(kc_ctx* c, uint64_t bytes) {
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess || (double)fr >= (double)bytes + (double)(1ull << 30)) return;
+    if (!c->d_keys1 && !c->d_keys2 && !c->d_spill) return;
+    (void)hipDeviceSynchronize();
+    hipFree(c->d_keys1);
+    hipFree(c->d_keys2);
+    hipFree(c->d_spill);
+    c->d_keys1 = c->d_keys2 = c->d_spill = nullptr;
+    c->k1_words = c->k2_words = c->spill_words = 0;
+    c->pb.keys1 = c->pb.keys2 = c->pb.spill = nullptr;
+    c->pbf.keys1 = c->pbf.keys2 = c->pbf.spill = nullptr;
+    c->reuse_img = nullptr;  // (the kept partitions are gone)
+    if (debug_on()) std::fprintf(stderr, "released the partition key buffers for %.1f GB\n", bytes / 1e9);
+}
+
 static void drop_compact(kc_ctx* c) {
     hipFree(c->d_cwords);
     hipFree(c->d_csecond);
@@ -1940,6 +1998,7 @@ int kc_dump(kc_ctx* c, uint64_t** records, uint64_t* n_records) {
     if (!h) return c->fail(KC_ERR_NOMEM, "host allocation failed");
     if (n) {
         uint64_t* d = nullptr;
+        make_room(c, n * rec);
         hipError_t e = hipMalloc(&d, n * rec);
         if (e != hipSuccess) { std::free(h); return c->fail(KC_ERR_NOMEM, "dump buffer allocation failed"); }
         HIPCHK(c, hipMemsetAsync(&c->d_ctr->dump_n, 0, 16 * 8 * 2, c->stream));
@@ -2005,6 +2064,7 @@ int kc_compact(kc_ctx* c, double load, kc_compact_info* info) {
     uint64_t *src = nullptr, *second = nullptr, *inv = nullptr;
     if (!c->d_cstat && hipMalloc(&c->d_cstat, 4 * sizeof(unsigned long long)) != hipSuccess)
         return c->fail(KC_ERR_NOMEM, "compact counters");
+    make_room(c, nslots * 16 + std::max<uint64_t>(1, occ) * c->W * 8 + c->nbuckets * c->S * 8);
     if (hipMalloc(&c->d_cwords, nslots * 8) != hipSuccess || hipMalloc(&src, nslots * 8) != hipSuccess ||
         hipMalloc(&second, std::max<uint64_t>(1, occ) * c->W * 8) != hipSuccess ||
         hipMalloc(&inv, c->nbuckets * c->S * 8) != hipSuccess) {
@@ -2071,6 +2131,7 @@ int kc_compact_dump(kc_ctx* c, uint64_t** records, uint64_t* n_records, uint64_t
     if (!h) return c->fail(KC_ERR_NOMEM, "host allocation failed");
     if (n) {
         uint64_t* d = nullptr;
+        make_room(c, n * rec);
         if (hipMalloc(&d, n * rec) != hipSuccess) {
             std::free(h);
             return c->fail(KC_ERR_NOMEM, "dump buffer allocation failed");

@@ -2577,13 +2577,8 @@ static inline void set_rec12_table(PartBufs& pb, const TableView& t, int k) {
     pb.rec12 = 0;
     if (t.R == 0) return;
     const int hb = std::max(0, 2 * k - 96);
-    auto span_bits = [](uint64_t span) {
-        int b = 0;
-        while (b < 32 && (1ULL << b) < span) b++;
-        return b;
-    };
     const uint64_t f2 = 1ULL << t.f2bits;
-    const int xb1 = span_bits(((f2 << 32) + t.R - 1) / t.R), xb2 = span_bits(((1ULL << 32) + t.R - 1) / t.R);
+    const int xb1 = span_bits32(((f2 << 32) + t.R - 1) / t.R), xb2 = span_bits32(((1ULL << 32) + t.R - 1) / t.R);
     if (hb + 1 + xb1 <= 32) {
         pb.rec12 |= R12_P1 | R12_IN;
         pb.r12_xb1 = xb1;

@@ -145,6 +145,23 @@ constexpr int R12_P1 = 1, R12_IN = 2, R12_OUT = 4, R12_L2 = 8;
 // R12_REG: the records are in the table's own geometry (the counting pass's levels): a bin's
 // lowest x is region_xlo of its first region, not bin << xb
 constexpr int R12_REG = 16;
+// bits that hold every value of a span (ceil(log2(span)), at most 32)
+inline int span_bits32(uint64_t span) {
+    int b = 0;
+    while (b < 32 && (1ULL << b) < span) b++;
+    return b;
+}
+// the level-2 record of the counting pass in a table of R regions (kc_count_impl.h
+// launch_part_w): 6 bytes for one-word keys once R >= 2^16 (StoreRec6), 12 for two-word keys
+// whose region spans few enough values of x (Rec12: hb + 1 + xb2 <= 32), else the W key words
+inline uint64_t level2_record_bytes(int W, int k, uint64_t R) {
+    if (W == 1) return R >= (1ULL << 16) ? 6 : 8;
+    if (W == 2 && R) {
+        const int hb = 2 * k - 96 > 0 ? 2 * k - 96 : 0;
+        if (hb + 1 + span_bits32(((1ULL << 32) + R - 1) / R) <= 32) return 12;
+    }
+    return 8ull * (uint64_t)W;
+}
 
 struct BloomView {
     uint32_t* bits;         // 2 * nbits filter bits, interleaved: bit 2h = filter 1, 2h+1 = filter 2
