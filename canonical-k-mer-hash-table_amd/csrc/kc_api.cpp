@@ -431,7 +431,7 @@ static PartPlan part_plan(const kc_ctx* c, uint64_t syms, bool seg, const PartGe
     p.nbs = (std::max(p.n1, p.n2) + 4095) / 4096 + 2;
     if (seg) {
         auto capacity = [](double e) { return ((uint64_t)std::ceil(e + 8.0 * std::sqrt(e) + 32.0) + 7) / 8 * 8; };
-        const uint64_t t1 = (uint64_t)p1_tile(c->W);  // k_p1<..., OutSeg> rounds block ranges to its tile
+        const uint64_t t1 = (uint64_t)p1_tile_max(c->W);  // k_p1<..., OutSeg> rounds block ranges to its tile
         const uint64_t per1 = ((syms + p.nblk1 - 1) / p.nblk1 + t1 - 1) / t1 * t1;  // windows per level-1 block
         const uint64_t nseg = (p.nblk1 + p.B2 - 1) / p.B2;                           // level-1 segments per p2 block
         p.cap1 = capacity((double)per1 / g.F1);

@@ -1034,7 +1034,7 @@ constexpr int p1_out_words(int W, int MODE) { return MODE == 3 ? 1 : W; }
 // fill counts go to hist1).  `count`: add windows / inserted to the counters (off for
 // the histogram pass of a fallback, whose windows the segmented pass counted already).
 template <int W, int MODE, bool SCATTER, class Bin, class Out, int NT = COUNT_THREADS>
-__global__ __launch_bounds__(NT, NT >= 1024 ? 8 : 4) void k_p1(PackedView sv, int k, BloomView bf,
+__global__ __launch_bounds__(NT, 4) void k_p1(PackedView sv, int k, BloomView bf,
                                                       DevCounters* __restrict__ ctr, PartBufs pb, uint32_t F, Bin bin_arg,
                                                       uint64_t* __restrict__ out, uint64_t pow5_k, uint64_t pow5_km1,
                                                       Out o, const unsigned long long* gate, int count) {
@@ -2628,11 +2628,24 @@ static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf
     const size_t p1_lds_min = (size_t)p1_tile(W) < 8 * (size_t)t.F1 ? LDS_BYTES / 2 + 16 : 0;
     const size_t sm1 = std::max(p1_lds_min, p1_smem<W, W, scatter_threads<W>()>(t.F1) + heavy_smem<W>() +
                                                 p1_stage_smem<W, scatter_threads<W>()>());
-    if ((e = set_smem(k1, sm1)) != hipSuccess) return e;
     const OutSeg o1{(uint64_t)pb.nblk1 * pb.cap1, 0, pb.cap1, pb.spill, pb.spill_cap, &ctr->spill_n,
                     &ctr->part_overflow, 1};
-    hipLaunchKernelGGL(k1, dim3(pb.nblk1), dim3(scatter_threads<W>()), sm1, s, sym, k, bf, ctr, pb, t.F1, coarse_bins(t),
-                       pb.keys1, pk, pkm1, o1, (const unsigned long long*)nullptr, 1);
+    bool wide = false;
+    if constexpr (W == 2) {  // (kc_internal.h p1_wide: big tables' two-word level 1)
+        if (p1_wide(W, t.F1)) {
+            wide = true;
+            auto kw = k_p1<W, MODE, true, BinRegion, OutSeg, P1_WIDE_THREADS>;
+            const size_t smw = p1_smem<W, W, P1_WIDE_THREADS>(t.F1) + heavy_smem<W>() + p1_stage_smem<W, P1_WIDE_THREADS>();
+            if ((e = set_smem(kw, smw)) != hipSuccess) return e;
+            hipLaunchKernelGGL(kw, dim3(pb.nblk1), dim3(P1_WIDE_THREADS), smw, s, sym, k, bf, ctr, pb, t.F1,
+                               coarse_bins(t), pb.keys1, pk, pkm1, o1, (const unsigned long long*)nullptr, 1);
+        }
+    }
+    if (!wide) {
+        if ((e = set_smem(k1, sm1)) != hipSuccess) return e;
+        hipLaunchKernelGGL(k1, dim3(pb.nblk1), dim3(scatter_threads<W>()), sm1, s, sym, k, bf, ctr, pb, t.F1,
+                           coarse_bins(t), pb.keys1, pk, pkm1, o1, (const unsigned long long*)nullptr, 1);
+    }
     if ((e = launch_p2f<W>(t, pb, ctr, 1, s)) != hipSuccess) return e;
     if (phase & PH_MAIN)
         if ((e = launch_p3<W, true, false, GATE3>(t, ctr, pb, nullptr, fresh, s, bf)) != hipSuccess) return e;

@@ -206,6 +206,22 @@ constexpr size_t p2f_lds_bytes(int W, uint32_t F2, uint32_t nseg, int nt = 0) {
     return bin_lds_bytes(F2) + (size_t)(nt ? nt : p2f_threads_w(W)) * run_width(W) * 8 * W + ((size_t)nseg + 1) * 4;
 }
 constexpr size_t LDS_BYTES = 160 * 1024;  // per CU (one workgroup may take all of it)
+// Big tables (the whole C4 job on one GPU: 525 coarse bins) leave the 4096-window tile of the
+// two-word level 1 runs of fewer than 8 keys per bin, and the launcher then keeps one 512-thread
+// workgroup per CU (8 waves) so that L2 merges the partial lines.  Two-word keys take a
+// 1024-thread level 1 instead (one workgroup per CU, 16 waves, 128 VGPRs): an 8192-window
+// tile, runs twice as long, when its LDS fits beside the bins.
+constexpr int P1_WIDE_THREADS = 1024;
+constexpr size_t p1_lds_bytes_nt(int W, uint32_t F1, int nt) {
+    return bin_lds_bytes(F1) + (size_t)nt * p1_runw(W) * 8 * W + (size_t)64 * (W + 1) * 8 +
+           (size_t)(nt * p1_runw(W) / 32 + W + 3) * 24;
+}
+constexpr bool p1_wide(int W, uint32_t F1) {
+    return W == 2 && (uint64_t)p1_tile(W) < 8ULL * F1 && p1_lds_bytes_nt(W, F1, P1_WIDE_THREADS) <= LDS_BYTES;
+}
+// the largest level-1 tile a table pass of W-word keys may run (the host's segment sizing rounds
+// block ranges to it)
+constexpr int p1_tile_max(int W) { return W == 2 ? P1_WIDE_THREADS * p1_runw(W) : p1_tile(W); }
 
 // ---- launchers (kc_tokenize.hip, kc_count.hip) -------------------------------------------------
 // src: bytes the chunk descriptors' src_off point into (host stage or device image)

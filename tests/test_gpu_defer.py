@@ -35,8 +35,10 @@ def _count(img, host, k, slots, batch, mode=2):
 
 
 # (k, table slots): one-word keys in a >= 2^16-region table take 6-byte level-2 records, two-word
-# keys 12-byte records, k = 127 whole 32-byte keys
-@pytest.mark.parametrize("k,slots", [(31, 40_000_000), (31, 2_000_000), (51, 6_000_000), (127, 3_000_000)])
+# keys 12-byte records, k = 127 whole 32-byte keys; 1.4 G two-word slots (a 35 GB table of 525 coarse
+# bins, as the whole C4 job's) run the 1024-thread level 1 (kc_internal.h p1_wide)
+@pytest.mark.parametrize("k,slots", [(31, 40_000_000), (31, 2_000_000), (51, 6_000_000), (127, 3_000_000),
+                                     (51, 1_400_000_000)])
 @pytest.mark.parametrize("group", ["auto", "2"])
 def test_deferred_level3_equals_oracle(k, slots, group, tmp_path, monkeypatch):
     monkeypatch.setenv("KC_INSERT_PATH", "partitioned")
