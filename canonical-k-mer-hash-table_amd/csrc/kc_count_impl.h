@@ -1023,6 +1023,16 @@ DEV bool gated_off(const unsigned long long* gate) { return gate && *gate == 0; 
 
 // words per level-1 output key: the Bloom pass (MODE 3) moves table key word 0 only
 constexpr int p1_out_words(int W, int MODE) { return MODE == 3 ? 1 : W; }
+// The waves per SIMD a scatter kernel can have resident: its LDS tile (NT threads x RUNW keys of
+// OW words) bounds the workgroups per CU.  Its launch bound asks for no more (capped by `cap`),
+// so the register budget is what that occupancy leaves: wide keys at one workgroup per CU got 64
+// VGPRs and 316 bytes of scratch per lane from a bound of 8 waves (C5's level 2) -- registers
+// the LDS would never let other waves use
+constexpr int scatter_waves(int NT, int RUNW, int OW, int cap) {
+    const int wg = (int)(LDS_BYTES / ((size_t)NT * RUNW * 8 * OW));
+    const int w = (wg < 1 ? 1 : wg) * NT / 256;
+    return w < 1 ? 1 : w > cap ? cap : w;
+}
 
 
 // Level 1: windows of a contiguous symbol range -> coarse bins (region >> f2bits).
@@ -1034,7 +1044,7 @@ constexpr int p1_out_words(int W, int MODE) { return MODE == 3 ? 1 : W; }
 // fill counts go to hist1).  `count`: add windows / inserted to the counters (off for
 // the histogram pass of a fallback, whose windows the segmented pass counted already).
 template <int W, int MODE, bool SCATTER, class Bin, class Out, int NT = COUNT_THREADS>
-__global__ __launch_bounds__(NT, 4) void k_p1(PackedView sv, int k, BloomView bf,
+__global__ __launch_bounds__(NT, scatter_waves(NT, k1_runw<W, NT>(), p1_out_words(W, MODE), 4)) void k_p1(PackedView sv, int k, BloomView bf,
                                                       DevCounters* __restrict__ ctr, PartBufs pb, uint32_t F, Bin bin_arg,
                                                       uint64_t* __restrict__ out, uint64_t pow5_k, uint64_t pow5_km1,
                                                       Out o, const unsigned long long* gate, int count) {
@@ -1410,7 +1420,7 @@ constexpr size_t p2f_smem(uint32_t F, uint32_t nseg_max) { return part_smem<W, N
 // the Bloom pass reads only its word 0)
 // REC6: write 6-byte level-2 records (StoreRec6) instead of whole keys (one-word keys)
 template <int W, int NT, int IS = W, bool REC6 = false>
-__global__ __launch_bounds__(NT, (2048 / NT > 8 ? 8 : 2048 / NT)) void k_p2f(TableView tv, PartBufs pb, DevCounters* __restrict__ ctr,
+__global__ __launch_bounds__(NT, scatter_waves(NT, run_w<W>(), W, 2048 / NT > 8 ? 8 : 2048 / NT)) void k_p2f(TableView tv, PartBufs pb, DevCounters* __restrict__ ctr,
                                                           int REC) {
     static_assert(!REC6 || W == 1, "6-byte records hold one-word keys");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
