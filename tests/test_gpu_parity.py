@@ -706,3 +706,26 @@ def test_device_chunk_planner_fastq_and_plain(chunk_size, tmp_path):
         dev = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
         assert ka.plan_chunks_device(dev.data_ptr(), len(data), 31, fmt, chunk_size) == \
             ka.plan_chunks(data, 31, fmt, chunk_size)
+
+
+def test_cli_overlapped_upload_equals_one_pass(tmp_path):
+    """A -s job on an input of >= 512 MiB counts the image's first half while the second half
+    uploads (two counting passes into one table, kc_cli.cpp): the output equals the single-pass
+    library run's over the same bytes (digest of every line), and the CLI says it split."""
+    import torch
+    n, L = 4_000_000, 150  # 0.64 GB of FASTA
+    p = tmp_path / "big.fasta"
+    subprocess.run([GEN, str(p), str(n), str(L), "5000000", "-s", "7", "-e", "0.001"], check=True)
+    out = tmp_path / "out.txt"
+    r = subprocess.run([CLI, str(p), "31", "-m", "2", "-s", "60000000", "-a", "1", "-t", "3", "-o", str(out), "--phases"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "overlapped upload" in r.stderr, r.stderr[-2000:]
+    host = open(p, "rb").read()
+    img = torch.frombuffer(bytearray(host), dtype=torch.uint8).cuda()
+    chunks = ka.plan_chunks(host, 31, ka.FMT_FASTA)
+    with ka.KmerCounter(ka.Config(k=31, mode=2, min_abundance=1, table_slots=60_000_000)) as kc:
+        kc.count_device(img.data_ptr(), chunks, ka.FMT_FASTA)
+        kc.finish()
+        want = kc.output_digest()
+    assert ka.same_digest(text_digest(str(out)), want)
