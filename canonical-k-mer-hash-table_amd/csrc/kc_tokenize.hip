@@ -314,31 +314,20 @@ __global__ __launch_bounds__(256) void k_zero_edges(const TileInfo* __restrict__
 // thread's (at most 16) symbols land in one or two words of the tile's LDS image.
 // --------------------------------------------------------------------------------
 DEV uint32_t swap_pairs(uint32_t x) { return ((x >> 1) & 0x55555555u) | ((x & 0x55555555u) << 1); }
+// tiles per k_emit workgroup: 2 or 4 with their loads issued first were slower (tokenize 1.36 ->
+// 1.38 / 1.42 ms on C2, profiles/r05_ab_emit_tiles.txt): k_emit is not bound by its load chain
+constexpr int EMIT_TPB = 1;
 
-__global__ __launch_bounds__(TILE_THREADS) void k_emit(const uint8_t* __restrict__ src,
-                                                       const TileInfo* __restrict__ tiles,
-                                                       const TileOut* __restrict__ touts,
-                                                       const TileOut* __restrict__ bpre, int fmt,
-                                                       uint64_t* __restrict__ pk, uint32_t* __restrict__ bk) {
-    constexpr int NW = TILE / 32 + 2;  // output words a tile can touch
-    __shared__ unsigned long long s_pk[NW];
-    __shared__ uint32_t s_bk[NW];
-    __shared__ uint32_t s_wsum[TILE_THREADS / 64];
-    __shared__ uint32_t s_wmk[TILE_THREADS / 64];  // FASTA: last marker per wave; FASTQ: newlines per wave
-    const uint64_t t = blockIdx.x;
-    const TileInfo ti = tiles[t];
-    const TileOut to = touts[t];
-    const TileOut bp = bpre[t / TSCAN];
+// one tile's symbols into the tile's LDS image (s_pk / s_bk, zeroed) and out: w = the thread's
+// 16 bytes (vh of them valid); s_wsum / s_wmk: per-wave scratch of this tile
+DEV void emit_tile(const TileInfo& ti, const TileOut& to, const TileOut& bp, int fmt, const uint32_t (&w)[4],
+                   uint32_t vh, unsigned long long* s_pk, uint32_t* s_bk, uint32_t* s_wsum, uint32_t* s_wmk,
+                   uint64_t* __restrict__ pk, uint32_t* __restrict__ bk) {
     const uint64_t gsum = bp.out_off + to.out_off;
     const uint64_t g0 = fmt == FMT_FASTQ ? (gsum & FQ_MASK) : gsum;  // global index of the tile's first symbol
     uint32_t hs_in = to.hs_in ? (to.hs_in == 2 ? 1u : 0u) : bp.hs_in;
     if (ti.first) hs_in = ti.bh;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    for (int i = tid; i < NW; i += TILE_THREADS) { s_pk[i] = 0; s_bk[i] = 0; }
-    const uint32_t my0 = tid * 16;
-    const uint32_t vh = ti.valid > my0 ? min(ti.valid - my0, 16u) : 0;
-    uint32_t w[4] = {0, 0, 0, 0};
-    if (vh) load16(src + ti.src + my0, ti.avail - my0, w);
     const bool fasta = fmt == FMT_FASTA;
     const uint32_t vmask = vh >= 16 ? 0xFFFFu : ((1u << vh) - 1);
     const uint32_t nlm = eq_mask16(w, 0x0A0A0A0Au) & vmask, gtm = eq_mask16(w, 0x3E3E3E3Eu) & vmask;
@@ -418,7 +407,7 @@ __global__ __launch_bounds__(TILE_THREADS) void k_emit(const uint8_t* __restrict
         if (ww < wid) pos += s_wsum[ww];
         total += s_wsum[ww];
     }
-    if (total == 0) return;
+    if (total == 0) return;  // (uniform over the workgroup)
     const uint64_t wbase = g0 >> 5;
     const uint32_t o0 = (uint32_t)(g0 & 31) + pos;  // slot of my first symbol, relative to wbase
     const uint32_t wa = o0 >> 5, r = o0 & 31;
@@ -458,6 +447,51 @@ __global__ __launch_bounds__(TILE_THREADS) void k_emit(const uint8_t* __restrict
     }
 }
 
+// TPB consecutive tiles per workgroup: every thread's loads for all of them (tile info, scan
+// outputs, then its 16 bytes of each tile) are issued before the first tile is emitted
+template <int TPB>
+__global__ __launch_bounds__(TILE_THREADS) void k_emit(const uint8_t* __restrict__ src,
+                                                       const TileInfo* __restrict__ tiles,
+                                                       const TileOut* __restrict__ touts,
+                                                       const TileOut* __restrict__ bpre, uint64_t ntiles, int fmt,
+                                                       uint64_t* __restrict__ pk, uint32_t* __restrict__ bk) {
+    constexpr int NW = TILE / 32 + 2;  // output words a tile can touch
+    __shared__ unsigned long long s_pk[TPB][NW];
+    __shared__ uint32_t s_bk[TPB][NW];
+    __shared__ uint32_t s_wsum[TPB][TILE_THREADS / 64];
+    __shared__ uint32_t s_wmk[TPB][TILE_THREADS / 64];  // FASTA: last marker per wave; FASTQ: newlines per wave
+    const uint64_t t0 = (uint64_t)blockIdx.x * TPB;
+    const int tid = threadIdx.x;
+    TileInfo ti[TPB];
+    TileOut to[TPB], bp[TPB];
+#pragma unroll
+    for (int j = 0; j < TPB; j++) {
+        if (t0 + j < ntiles) {
+            ti[j] = tiles[t0 + j];
+            to[j] = touts[t0 + j];
+            bp[j] = bpre[(t0 + j) / TSCAN];
+        } else {
+            ti[j] = TileInfo{};
+            to[j] = bp[j] = TileOut{};
+        }
+    }
+    const uint32_t my0 = tid * 16;
+    uint32_t w[TPB][4], vh[TPB];
+#pragma unroll
+    for (int j = 0; j < TPB; j++) {
+        vh[j] = ti[j].valid > my0 ? min(ti[j].valid - my0, 16u) : 0;
+        w[j][0] = w[j][1] = w[j][2] = w[j][3] = 0;
+        if (vh[j]) load16(src + ti[j].src + my0, ti[j].avail - my0, w[j]);
+    }
+    for (int i = tid; i < TPB * NW; i += TILE_THREADS) {
+        (&s_pk[0][0])[i] = 0;
+        (&s_bk[0][0])[i] = 0;
+    }
+#pragma unroll
+    for (int j = 0; j < TPB; j++)
+        if (t0 + j < ntiles)  // (uniform)
+            emit_tile(ti[j], to[j], bp[j], fmt, w[j], vh[j], s_pk[j], s_bk[j], s_wsum[j], s_wmk[j], pk, bk);
+}
 
 // --------------------------------------------------------------------------------
 // k_synth: device twin of tools/kc_gen.c (one thread per read)
@@ -507,8 +541,8 @@ hipError_t launch_tokenize(const uint8_t* src, uint64_t ntiles, const ChunkDesc*
     hipLaunchKernelGGL(k_tscan_top, dim3(1), dim3(TSCAN), 0, s, tblk, nblk, fmt, ctr);
     hipLaunchKernelGGL(k_zero_edges, dim3((unsigned)((ntiles + 255) / 256)), dim3(256), 0, s, tiles, touts, tblk,
                        ntiles, fmt, sv.pk, sv.bk);
-    hipLaunchKernelGGL(k_emit, dim3((unsigned)ntiles), dim3(TILE_THREADS), 0, s, src, tiles, touts, tblk, fmt,
-                       sv.pk, sv.bk);
+    hipLaunchKernelGGL(k_emit<EMIT_TPB>, dim3((unsigned)((ntiles + EMIT_TPB - 1) / EMIT_TPB)), dim3(TILE_THREADS), 0, s,
+                       src, tiles, touts, tblk, ntiles, fmt, sv.pk, sv.bk);
     return hipGetLastError();
 }
 
