@@ -589,13 +589,18 @@ def run_workload(args, env, image=None):
     xgmi = None
     if dist and world > 1:  # the merge's exchange, per rank and step, beside the HBM figures
         xs = counter.xstats
-        t = torch.tensor([xs["bytes_sent"], xs["exchange_s"]], dtype=torch.float64, device="cuda")
+        t = torch.tensor([xs["bytes_sent"], xs["exchange_s"], xs.get("route_s", 0.0), xs.get("insert_s", 0.0)],
+                         dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        sent, xsec = float(t[0].item()), float(t[1].item())
+        sent, xsec, rsec, isec = (float(v) for v in t.tolist())
         xgmi = {"sent_bytes_per_step_per_rank": int(sent / args.steps),
                 "exchange_ms_per_step": round(xsec / args.steps * 1e3, 3),
                 "gbs_per_rank": round(sent / max(xsec, 1e-9) / 1e9, 2), "peak_gbs_per_gpu": 7 * 153,
-                "note": "max over ranks; the all-to-all of {key, count} records incl. its count/sum headers"}
+                "route_ms_per_step": round(rsec / args.steps * 1e3, 3),
+                "owner_insert_ms_per_step": round(isec / args.steps * 1e3, 3),
+                "note": "max over ranks; the all-to-all of {key, count} records incl. its count/sum headers; "
+                        "route = the local table as owner-grouped records (host waits for its counts), "
+                        "owner insert = the received records into the owner table (waited for)"}
     st = counter.finish()  # raises on table overflow
     if rank == 0:
         log(f"{args.config}: {args.steps} steps in {elapsed:.3f} s; parity / writer records")

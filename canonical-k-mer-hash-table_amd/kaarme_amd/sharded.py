@@ -359,7 +359,11 @@ class ShardedCounter:
         self._bloom_input = None  # the Bloom pass's (image, chunks, format): the owners count it
         self._counted = False
         # exchange traffic of the merges (xGMI bytes reported beside HBM bytes)
-        self.xstats = {"bytes_sent": 0, "bytes_recv": 0, "exchange_s": 0.0, "merges": 0}
+        # with profile(True) the merge's phases are timed too (route / exchange / owner insert; the
+        # insert waits for its kernels, which the step's end would wait for anyway)
+        self.xstats = {"bytes_sent": 0, "bytes_recv": 0, "exchange_s": 0.0, "route_s": 0.0, "insert_s": 0.0,
+                       "merges": 0}
+        self._profiling = False
 
     # the counting pass over a device image (chunks from kaarme_amd.plan_chunks): local
     def count_device(self, dev_ptr: int, chunks: List[Tuple[int, int, int]], fmt: int, stream: int = 0):
@@ -388,7 +392,9 @@ class ShardedCounter:
             self._pending = False
             return
         with _on_stream(self.device, stream):
-            recs, counts = self.engine.route_table(self.world, stream)
+            tr = time.perf_counter()
+            recs, counts = self.engine.route_table(self.world, stream)  # (the counts come back to the host)
+            self.xstats["route_s"] += time.perf_counter() - tr
             # the records hold the local counts now: a later merge must route only what is
             # counted after this one
             self.engine.clear_local()
@@ -399,7 +405,13 @@ class ShardedCounter:
             self.xstats["bytes_recv"] += sum(c for d, c in enumerate(per_rank) if d != self.rank) * rec_bytes
             self.xstats["exchange_s"] += time.perf_counter() - t0  # (route synced before, the sums check after)
             self.xstats["merges"] += 1
+            ti = time.perf_counter()
             self.engine.insert_counts(recv, n, stream, group_counts=per_rank)
+            if self._profiling and self.device == "cuda":
+                import torch
+
+                torch.cuda.synchronize()
+                self.xstats["insert_s"] += time.perf_counter() - ti
         self._inflight = [recv]  # the receive buffer must outlive the insert
         self._pending = False
 
@@ -469,6 +481,7 @@ class ShardedCounter:
         self._inflight = []
 
     def profile(self, enable: bool = True):
+        self._profiling = enable
         self.engine.kc.profile(enable)
         if not self._local_owner():
             self.kc.profile(enable)
