@@ -422,7 +422,7 @@ def setup_job(args, env, image=None):
         if dist and world > 1:
             # one size for every rank's local (and owner) table: the groups a rank receives are then
             # sorted by its own table's regions, and merge in one level-3 pass (sharded.DeviceEngine)
-            t = torch.tensor([local_slots], dtype=torch.int64, device="cuda")
+            t = torch.tensor([local_slots], dtype=torch.int64, device=coll_device(dist))
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             local_slots = int(t.item())
         estimate = {"distinct_estimate": int(est), "local_slots": local_slots,
@@ -590,7 +590,7 @@ def run_workload(args, env, image=None):
     if dist and world > 1:  # the merge's exchange, per rank and step, beside the HBM figures
         xs = counter.xstats
         t = torch.tensor([xs["bytes_sent"], xs["exchange_s"], xs.get("route_s", 0.0), xs.get("insert_s", 0.0)],
-                         dtype=torch.float64, device="cuda")
+                         dtype=torch.float64, device=coll_device(dist))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         sent, xsec, rsec, isec = (float(v) for v in t.tolist())
         xgmi = {"sent_bytes_per_step_per_rank": int(sent / args.steps),
@@ -626,14 +626,14 @@ def run_workload(args, env, image=None):
                            "chain-start keys, vs the full-key table sized by -s"}
     counter.close()
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_device(dist))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     windows_step = st["windows"]
     assert windows_step == windows_expected, (windows_step, windows_expected)
     total_windows = windows_step * args.steps
     if dist:
-        t = torch.tensor([total_windows], dtype=torch.float64, device="cuda")
+        t = torch.tensor([total_windows], dtype=torch.float64, device=coll_device(dist))
         dist.all_reduce(t)
         total_windows = float(t.item())
     value = total_windows / elapsed
@@ -772,6 +772,12 @@ def visible_gpus():
     return min(counts) if counts else None
 
 
+def coll_device(dist):
+    """Where the line's own collectives keep their tensors: the GPU over RCCL, the host over gloo
+    (--rehearse-one-gpu)."""
+    return "cpu" if dist.get_backend() == "gloo" else "cuda"
+
+
 def launch_ranks(n, cpu_only):
     """Starts `n` rank processes of this same command line (RANK / LOCAL_RANK / WORLD_SIZE /
     MASTER_ADDR=127.0.0.1 / MASTER_PORT in their environment, as torch.distributed.run would set
@@ -779,7 +785,7 @@ def launch_ranks(n, cpu_only):
     visible_gpus reads the environment and sysfs); the ranks are children, not an exec.  Rank 0
     prints the JSON line on the inherited stdout.  Returns the exit code (the first nonzero rank's;
     a failed rank stops the others)."""
-    if not cpu_only:
+    if not cpu_only and "--rehearse-one-gpu" not in sys.argv:
         have = visible_gpus()
         if have is not None and have < n:
             log(f"error: --gpus {n} but {have} GPU(s) visible")
@@ -871,6 +877,9 @@ def main():
                     help="use the sharded (RCCL) path even at one rank (testing)")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="torch.distributed backend of the ranks (nccl = RCCL; gloo only with --launch-only)")
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="N > 1 on a one-GPU box: every rank on cuda:0, gloo instead of RCCL (the exchange goes "
+                         "through host memory) -- runs the multi-GPU line's code path end to end (testing)")
     ap.add_argument("--launch-only", action="store_true",
                     help="start the ranks, join the process group and print the line without any GPU work "
                          "(tests the N-rank launch on CPU)")
@@ -898,13 +907,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    if args.rehearse_one_gpu:
+        local = 0
     torch.cuda.set_device(local)
     dist = None
     if world > 1 or args.force_sharded:
         import torch.distributed as dist
         for key, val in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29531"), ("RANK", "0"), ("WORLD_SIZE", "1")):
             os.environ.setdefault(key, val)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.rehearse_one_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import kaarme_amd as ka
 
