@@ -487,10 +487,11 @@ def parity_record(job, k, dist=None):
     `digest`, and on one GPU also the SHA-256 of the sorted output text from kc_dump when the case
     has the reference's sorted digest and its text stays below ~30 GB."""
     fx = job.fixture
-    if fx is None:
-        return None
     import kaarme_amd as ka
     t0 = time.perf_counter()
+    if fx is None:  # (no reference case for this input: the digest alone, e.g. to compare N = 1 with N > 1)
+        return {"reference_case": None, "digest": job.counter.output_digest(), "match": None,
+                "digest_s": round(time.perf_counter() - t0, 2)}
     rec = {"reference_case": f"tests/golden/fullsize.json {fx['name']}: " + (
         f"oracle/_ref/kaarme {' '.join(fx['args'])} on the same input" if fx.get("sorted_sha256") else
         f"{' '.join(fx['args'])}, digest of the pinned CPU restatement (whole job)")}
