@@ -433,7 +433,7 @@ def setup_job(args, env, image=None):
         # the merge's record buffers (send x 1.25 + receive: W + 1 words per distinct k-mer of its
         # input) beside the local count's partition buffers: the batch takes what is left
         lsl = estimate["local_slots"] if estimate else min(slots or windows_expected, windows_expected)
-        per_table = int(1.25 * max(slots or 0, lsl) / (16 // (W + 1))) * 128
+        per_table = int(1.25 * (lsl if estimate else max(slots or 0, lsl)) / (16 // (W + 1))) * 128
         recs = int(2.25 * lsl * (W + 1) * 8)
         free, _ = torch.cuda.mem_get_info()  # (the image is already allocated)
         fit = int(0.85 * max(0, free - 2 * per_table - recs)) // (21 * W + 3)
@@ -455,7 +455,12 @@ def setup_job(args, env, image=None):
     # rank's owner table digests its k-mers; parity_record combines them).  A weak job over N > 1
     # ranks counts N x the preset's reads, which no fixture covers.
     fx = fixture_case(args, share, first, N) if (world == 1 or strong) else None
-    cfg = ka.Config(k=k, mode=2, table_slots=estimate["local_slots"] if (share or est_table) else slots,
+    # (N > 1 strong: the owner table takes the local table's estimate-sized geometry, not the 1/G share
+    # of -s -- the largest rank's distinct k-mers bound an owner's, about the job's 1/G, from above)
+    tslots = slots
+    if share or est_table or (dist and world > 1 and strong and estimate):
+        tslots = estimate["local_slots"] if (share or est_table) else min(slots, estimate["local_slots"])
+    cfg = ka.Config(k=k, mode=2, table_slots=tslots,
                     min_abundance=fx["min_abundance"] if fx else 2, batch_bytes=batch,
                     device=local, bf_enable=bool(args.unique), est_unique=args.unique)
     if dist:
