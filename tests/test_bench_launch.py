@@ -73,3 +73,25 @@ def test_gpus_two_on_a_one_gpu_box_fails_without_a_line():
                        text=True, timeout=300, env=_env())
     assert p.returncode != 0
     assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_two_rank_line_rehearsed_on_one_gpu_matches_one_gpu():
+    """The N > 1 line's code path end to end (--rehearse-one-gpu: two ranks on cuda:0 over gloo):
+    the default strong C4 line at a small read count with its c2 record and xgmi record, whose
+    combined owner digest equals the same job's on one GPU."""
+    common = ["--reads", "200000", "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--no-compact",
+              "--no-writer", "--no-cli-fullsize"]
+    p2 = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--rehearse-one-gpu"] + common, capture_output=True,
+                        text=True, timeout=500, env=_env())
+    assert p2.returncode == 0, p2.stderr[-3000:]
+    d2 = _json_line(p2.stdout)
+    assert d2["n_gpus"] == 2 and d2["scaling"] == "strong" and d2["config"]["workload"].startswith("C4")
+    assert "xgmi" in d2 and d2["xgmi"]["sent_bytes_per_step_per_rank"] > 0 and "c2" in d2
+    p1 = subprocess.run([sys.executable, BENCH, "--config", "C4"] + common, capture_output=True, text=True,
+                        timeout=300, env=_env())
+    assert p1.returncode == 0, p1.stderr[-3000:]
+    d1 = _json_line(p1.stdout)
+    assert d2["parity"]["digest"] == d1["parity"]["digest"]
+    assert d2["windows_per_step_per_gpu"] * 2 == d1["windows_per_step_per_gpu"]
