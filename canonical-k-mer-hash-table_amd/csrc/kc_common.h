@@ -407,11 +407,11 @@ DEV void run_windows_src(const Src& sv, uint64_t r0, uint64_t t1, const RollCons
     const uint64_t pa = sv.pk(wa), pb = sv.pk(wa + 1);
     const uint32_t ba = sv.bk(wa), bb = sv.bk(wa + 1);
     const int o0 = (int)(r0 & 31);
+    // the run's RUNW incoming symbols and break bits, funnel-shifted into one register each, so
+    // every step reads them at a constant position
+    const uint64_t ins = o0 ? (pa << (2 * o0)) | (pb >> (64 - 2 * o0)) : pa;  // symbol j at bits 63-2j:62-2j
+    const uint32_t inb = o0 ? (ba << o0) | (bb >> (32 - o0)) : ba;            // break j at bit 31-j
     if constexpr (W == 1) {
-        // one-word keys: the run's RUNW incoming symbols and break bits are funnel-shifted
-        // into one register each, so every step reads them at a constant position
-        const uint64_t ins = o0 ? (pa << (2 * o0)) | (pb >> (64 - 2 * o0)) : pa;  // symbol j at bits 63-2j:62-2j
-        const uint32_t inb = o0 ? (ba << o0) | (bb >> (32 - o0)) : ba;            // break j at bit 31-j
         const uint64_t top = rk.topmask;
         const int rcb = rk.rc_bit;
         uint64_t f = fwd[0], r = rc[0];
@@ -429,12 +429,8 @@ DEV void run_windows_src(const Src& sv, uint64_t r0, uint64_t t1, const RollCons
     }
 #pragma unroll
     for (int j = 0; j < RUNW; j++) {
-        const int o = o0 + j;
-        const uint64_t pw = o < 32 ? pa : pb;
-        const uint32_t bw = o < 32 ? ba : bb;
-        const int oo = o & 31;
-        const uint32_t c = (uint32_t)(pw >> (62 - 2 * oo)) & 3;
-        const bool br = (bw >> (31 - oo)) & 1;
+        const uint32_t c = (uint32_t)(ins >> (62 - 2 * j)) & 3;
+        const bool br = (inb >> (31 - j)) & 1;
         since = br ? 0 : min(since + 1, k);
 #pragma unroll
         for (int i = 0; i < W - 1; i++) fwd[i] = (fwd[i] << 2) | (fwd[i + 1] >> 62);
