@@ -453,6 +453,10 @@ static PartPlan part_plan(const kc_ctx* c, uint64_t syms, bool seg, const PartGe
     // pipeline of a batch's tail, which writes W-word items, runs after its group's level 3)
     const uint64_t l2 = slots > 1 && rec2 ? (g.R * p.B2 * p.cap2 * slots * rec2 + 7) / 8 : g.R * p.B2 * p.cap2 * g.IW;
     p.need2 = std::max(std::max<uint64_t>(syms * g.IW, l2), p.spill_words);
+    // (the levels' record loads are 12 or 16 bytes wide whatever the record: a last 8- or
+    // 12-byte record's load reads past it)
+    p.need1 += 2;
+    p.need2 += 2;
     return p;
 }
 

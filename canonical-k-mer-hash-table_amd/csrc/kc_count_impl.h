@@ -1241,14 +1241,21 @@ __global__ __launch_bounds__(COUNT_THREADS, 4) void k_p1k(const uint64_t* __rest
     for (uint64_t t0 = lo; t0 < hi; t0 += TW) {
         uint64_t tk[RUNW][W];
         bool ok[RUNW];
+        uint32_t inr = 0;  // the tile's loads first (past hi: item lo), then their use
 #pragma unroll
         for (int q = 0; q < RUNW; q++) {
             const uint64_t i = t0 + tid + (uint64_t)q * COUNT_THREADS;
+            const uint64_t ii = i < hi ? i : lo;
+            inr |= (uint32_t)(i < hi) << q;
 #pragma unroll
-            for (int w = 0; w < W; w++) tk[q][w] = i < hi ? in[i * istride + w] : 0;
-            ok[q] = tk[q][0] != EMPTY;  // 0 is never a table key: skip (counted as invalid)
+            for (int w = 0; w < W; w++) tk[q][w] = in[ii * istride + w];
+        }
+#pragma unroll
+        for (int q = 0; q < RUNW; q++) {
+            const bool inq = (inr >> q) & 1;
+            ok[q] = inq && tk[q][0] != EMPTY;  // 0 is never a table key: skip (counted as invalid)
             if constexpr (!SCATTER) {
-                n_inv += (i < hi) & !ok[q];
+                n_inv += inq & !ok[q];
 #pragma unroll
                 for (int w = 0; w < W; w++)
                     if (w == cnt_word && ok[q]) added += tk[q][w] & CNT_MASK;
@@ -1390,8 +1397,9 @@ __global__ __launch_bounds__(COUNT_THREADS, 4) void k_p2(TableView tv, PartBufs 
         for (int q = 0; q < RUNW; q++) {
             const uint64_t i = t0 + tid + (uint64_t)q * COUNT_THREADS;
             ok[q] = i < hi;
+            const uint64_t ii = ok[q] ? i : lo;  // (the select on the address: nothing waits for the loads)
 #pragma unroll
-            for (int w = 0; w < W; w++) tk[q][w] = ok[q] ? pb.keys1[i * W + w] : 0;
+            for (int w = 0; w < W; w++) tk[q][w] = pb.keys1[ii * W + w];
         }
         if constexpr (SCATTER) {
             scatter_tile<W, RUNW>(l, F, bin, OutExact{}, tk, ok, pb.keys2);
@@ -1464,8 +1472,8 @@ __global__ __launch_bounds__(NT, scatter_waves(NT, run_w<W>(), W, 2048 / NT > 8 
         for (int q = 0; q < RUNW; q++) {
             const uint32_t i = t0 + wpos + q * 64;
             ok[q] = i < total;
-            const uint64_t* src = pb.keys1;
-            uint64_t item = 0;
+            const uint64_t* src = sp;  // (past the total: the current segment's first item)
+            uint64_t item = (seg0 + cs) * pb.cap1;
             if (ok[q]) {
                 if (nb <= i) {
                     do {
@@ -1479,12 +1487,19 @@ __global__ __launch_bounds__(NT, scatter_waves(NT, run_w<W>(), W, 2048 / NT > 8 
                 item = (seg0 + cs) * pb.cap1 + (i - cb);
             }
             if constexpr (W == 2) {
-                if (rin) {  // a 12-byte record, kept raw (decoded when the tile is scattered)
-                    const uint3 v = reinterpret_cast<const uint3*>(pb.keys1)[item];
-                    tk[q][0] = v.x | (uint64_t)v.y << 32;
-                    tk[q][1] = v.z;
-                    continue;
-                }
+                // one 16-byte load for either format at the format's byte offset, into the same
+                // registers (a 12-byte record is kept raw, decoded when the tile is scattered; its
+                // load reads 4 bytes of the next, inside buffers of 16 bytes per item).  Loads into
+                // format-specific registers left a copy after each, and the copy made every load
+                // wait for all the tile's earlier ones (s_waitcnt vmcnt(0)): 8 serialised latencies
+                // per tile
+                const uint64_t off = rin ? item * 12 : item * (8 * IS);
+                uint32_t v[4];
+                __builtin_memcpy(v, reinterpret_cast<const uint8_t*>(pb.keys1) + off, 16);
+                tk[q][0] = v[0] | (uint64_t)v[1] << 32;
+                tk[q][1] = v[2] | (uint64_t)v[3] << 32;
+                (void)src;
+                continue;
             }
 #pragma unroll
             for (int w = 0; w < W; w++) tk[q][w] = ks_load(src + w);
@@ -1601,8 +1616,16 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
     uint64_t* tg = lt + BPR * BUCKET_WORDS;             // BPR tag words (slot_tag of each slot's word 0)
     const uint64_t r = blockIdx.x;
     uint64_t start, end;
+    // runs (the merge over region-sorted groups): each group's first record in LDS, so an item's
+    // address needs no dependent global load
+    // (runs are count records: the other variants keep their static LDS, which the gate's filter
+    // slice budget counts on)
+    __shared__ uint64_t s_gst[SEG && CNT ? MAX_SEG_GROUP : 1];
     if constexpr (SEG) {
         seg_prefix(s_pre, pb.hist2 + r * pb.B2, pb.B2);
+        if constexpr (CNT)
+            if (pb.seg_start)
+                for (uint32_t g = threadIdx.x; g < pb.B2; g += NT) s_gst[g] = pb.seg_start[r * pb.B2 + g];
         __syncthreads();
         start = 0;
         end = s_pre[pb.B2];
@@ -1675,31 +1698,40 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
     // pass's fine bins: against the fine bin's)
     const bool r12_reg = r12 && (pb.rec12 & R12_REG);
     const uint32_t xlo_r = REC6 || r12_reg ? (uint32_t)region_xlo(r, tv.R) : 0;
-    auto load_items = [&](uint64_t base, uint64_t (&kk)[KB][W], uint64_t (&add)[KB], uint32_t& ok) {
+    // sg: Rec12 items' fine bin (seg >> r12_b2s), beside the raw record
+    auto load_items = [&](uint64_t base, uint64_t (&kk)[KB][W], uint64_t (&add)[KB], uint32_t& ok,
+                          uint32_t (&sg)[KB]) {
         ok = 0;
 #pragma unroll
         for (int q = 0; q < KB; q++) {
             const uint64_t i = base + threadIdx.x + (uint64_t)q * NT;
             if constexpr (W == 2 && SEG && !CNT) {
-                if (r12) {  // a 12-byte record, kept raw with its fine bin (decoded when used)
-                    kk[q][0] = kk[q][1] = 0;
-                    if (i < end) {
-                        while (nb <= i) {
-                            cs++;
-                            cb = nb;
-                            nb = s_pre[cs + 1];
-                        }
-                        const uint64_t seg = r * pb.B2 + cs;
-                        const uint3 v = reinterpret_cast<const uint3*>(pb.keys2)[seg * pb.cap2 + (i - cb)];
-                        kk[q][0] = v.x | (uint64_t)v.y << 32;
-                        kk[q][1] = v.z | (uint64_t)(seg >> pb.r12_b2s) << 32;
-                        ok |= 1u << q;
+                // either format (a 12-byte record, kept raw with its fine bin and decoded when
+                // used, or two whole words) by one 16-byte load into the same registers, at the
+                // format's byte offset (k_p2f load_tile: format-specific registers made every load
+                // wait for the earlier ones); lanes past the end load their segment's first item
+                uint64_t seg = r * pb.B2 + cs, item = seg * pb.cap2;
+                if (i < end) {
+                    while (nb <= i) {
+                        cs++;
+                        cb = nb;
+                        nb = s_pre[cs + 1];
                     }
-                    add[q] = 1;
-                    continue;
+                    seg = r * pb.B2 + cs;
+                    item = seg * pb.cap2 + (i - cb);
+                    ok |= 1u << q;
                 }
+                uint32_t v[4];
+                __builtin_memcpy(v, reinterpret_cast<const uint8_t*>(pb.keys2) + (r12 ? item * 12 : item * 16), 16);
+                kk[q][0] = v[0] | (uint64_t)v[1] << 32;
+                kk[q][1] = v[2] | (uint64_t)v[3] << 32;
+                sg[q] = (uint32_t)(seg >> pb.r12_b2s);
+                add[q] = 1;
+                continue;
             }
             if constexpr (REC6) {
+                // (loads only in range: the unconditional form of the two-word path measured 2 %
+                // slower here, profiles/r05_ab_load_merge.txt)
                 kk[q][0] = 0;
                 if (i < end) {
                     while (nb <= i) {
@@ -1714,6 +1746,9 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
                 add[q] = 1;
                 continue;
             }
+            // every lane loads (past the end: a nearby item) into the same registers, its validity in
+            // ok and its count masked where it is used: a value merged after a load made every
+            // load wait for the earlier ones
             const uint64_t* src = nullptr;
             if (runs) {
                 uint32_t j = ((uint32_t)i * 0x9E3779B1u) & pmask;
@@ -1726,7 +1761,7 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
                         if (s_pre[mid] <= j) lo = mid;
                         else hi = mid;
                     }
-                    src = pb.keys2 + (pb.seg_start[r * pb.B2 + lo] + (j - s_pre[lo])) * IW;
+                    src = pb.keys2 + ((CNT ? s_gst[lo] : pb.seg_start[r * pb.B2 + lo]) + (j - s_pre[lo])) * IW;
                 }
             } else if (i < end) {
                 if constexpr (SEG) {
@@ -1741,25 +1776,26 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
                 }
             }
             ok |= (src != nullptr) << q;
+            if (!src) src = pb.keys2 + (SEG ? (r * pb.B2 + cs) * pb.cap2 * IW : start * IW);  // (a nearby item)
 #pragma unroll
-            for (int w = 0; w < W; w++) kk[q][w] = src ? ks_load(src + w) : 0;
-            if constexpr (CNT) add[q] = src ? src[W] & CNT_MASK : 0;
+            for (int w = 0; w < W; w++) kk[q][w] = ks_load(src + w);
+            if constexpr (CNT) add[q] = src[W];  // (raw: CNT_MASK applied where it is used)
             else add[q] = 1;
         }
     };
 
     uint64_t kk[KB][W];
     uint64_t add[KB];
-    uint32_t okm = 0;
-    if (start < vend) load_items(start, kk, add, okm);
+    uint32_t okm = 0, sg[KB];
+    if (start < vend) load_items(start, kk, add, okm, sg);
     for (uint64_t base = start; base < vend; base += (uint64_t)KB * NT) {
         // the next items' loads are issued before this batch's inserts
         uint64_t nkk[KB][W];
         uint64_t nadd[KB];
-        uint32_t nokm = 0;
+        uint32_t nokm = 0, nsg[KB];
         const uint64_t nbase = base + (uint64_t)KB * NT;
         const bool more = W <= 2 && nbase < vend;  // W > 2: no spare registers
-        if (more) load_items(nbase, nkk, nadd, nokm);
+        if (more) load_items(nbase, nkk, nadd, nokm, nsg);
         if constexpr (REC6) {
 #pragma unroll
             for (int q = 0; q < KB; q++) kk[q][0] = rec6_key(kk[q][0], (okm >> (16 + q)) & 1, xlo_r);
@@ -1770,7 +1806,7 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
 #pragma unroll
                 for (int q = 0; q < KB; q++) {
                     const uint3 v = make_uint3((uint32_t)kk[q][0], (uint32_t)(kk[q][0] >> 32), (uint32_t)kk[q][1]);
-                    rc.dec(v, r12_reg ? xlo_r : (uint32_t)(kk[q][1] >> 32) << pb.r12_xb2, kk[q][0], kk[q][1]);
+                    rc.dec(v, r12_reg ? xlo_r : sg[q] << pb.r12_xb2, kk[q][0], kk[q][1]);
                 }
             }
         }
@@ -1786,7 +1822,10 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
                     pass[q] = pass[q] && block_gate(bloom_block_ptr(bf, t0) + 8, t0, bf.nh_gate);
             }
             n_ins += pass[q];
-            if constexpr (CNT) n_add += pass[q] ? add[q] : 0;
+            if constexpr (CNT) {
+                add[q] &= CNT_MASK;
+                n_add += pass[q] ? add[q] : 0;
+            }
         }
 #pragma unroll
         for (int q = 0; q < KB; q++) {
@@ -1856,11 +1895,12 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
 #pragma unroll
             for (int q = 0; q < KB; q++) {
                 add[q] = nadd[q];
+                sg[q] = nsg[q];
 #pragma unroll
                 for (int w = 0; w < W; w++) kk[q][w] = nkk[q][w];
             }
         } else if (nbase < vend) {
-            load_items(nbase, kk, add, okm);
+            load_items(nbase, kk, add, okm, sg);
         }
     }
     __syncthreads();
@@ -1957,40 +1997,40 @@ __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView b
     struct Raw {
         uint3 v[KB];
         uint32_t xhi[KB];
-        uint32_t two;  // bit q: item q is a record of count >= 2
+        uint64_t cnt[KB];  // cntw >= 0: the records' count words
     };
     auto fetch = [&](uint64_t base, Raw& w) {
-        w.two = 0;
 #pragma unroll
         for (int q = 0; q < KB; q++) {
             const uint64_t i = base + threadIdx.x + (uint64_t)q * NT;
-            w.v[q] = make_uint3(0, 0, 0);
-            w.xhi[q] = 0;
-            if (i < end) {
-                if constexpr (SEG) {
+            if constexpr (SEG) {
+                // either format by one 12-byte load into the same registers at the format's byte
+                // offset (k_p2f load_tile: format-specific registers made every load wait for the
+                // earlier ones); lanes past the end load their segment's first item, a whole word's load reads 4 bytes
+                // of the next item (z, unused)
+                uint64_t seg = r * pb.B2 + cs, item = seg * pb.cap2;  // (past the end: the segment's first)
+                if (i < end) {
                     while (nb <= i) {
                         cs++;
                         cb = nb;
                         nb = s_pre[cs + 1];
                     }
-                    const uint64_t seg = r * pb.B2 + cs, item = seg * pb.cap2 + (i - cb);
-                    if (r12) {
-                        w.v[q] = reinterpret_cast<const uint3*>(pb.keys2)[item];
-                        w.xhi[q] = (uint32_t)(seg >> pb.r12_b2s) << pb.r12_xb2;
-                    } else {
-                        const uint64_t t = pb.keys2[item * is];
-                        w.v[q] = make_uint3((uint32_t)t, (uint32_t)(t >> 32), 0);
-                    }
-                } else {
-                    const uint64_t t = pb.keys2[i * is];
-                    w.v[q] = make_uint3((uint32_t)t, (uint32_t)(t >> 32), 0);
-                    if (cntw >= 0) {
-                        const bool two = (pb.keys2[i * is + cntw] & CNT_MASK) >= 2;
-                        w.two |= (uint32_t)two << q;
-                        if (two != (rec_phase == 0)) w.v[q].x = w.v[q].y = 0;  // (the other phase's: skipped)
-                    }
+                    seg = r * pb.B2 + cs;
+                    item = seg * pb.cap2 + (i - cb);
                 }
+                uint32_t v[3];
+                __builtin_memcpy(v, reinterpret_cast<const uint8_t*>(pb.keys2) + (r12 ? item * 12 : item * is * 8), 12);
+                w.v[q] = make_uint3(v[0], v[1], v[2]);
+                w.xhi[q] = r12 ? (uint32_t)(seg >> pb.r12_b2s) << pb.r12_xb2 : 0;
+                continue;
             }
+            // the contiguous run (exact layout, or {key, count} records): the count word raw, its
+            // phase test made when the round uses it (a test here would wait for the load)
+            const uint64_t ii = i < end ? i : 0;
+            const uint64_t t = pb.keys2[ii * is];
+            w.v[q] = make_uint3((uint32_t)t, (uint32_t)(t >> 32), 0);
+            w.xhi[q] = 0;
+            w.cnt[q] = cntw >= 0 ? pb.keys2[ii * is + cntw] : 0;
         }
     };
     Raw cur, nxt;
@@ -1999,10 +2039,17 @@ __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView b
         const uint64_t nbase = base + (uint64_t)KB * NT;
         if (nbase < end) fetch(nbase, nxt);
         uint64_t t0[KB];
+        uint32_t two = 0;  // bit q: item q is a record of count >= 2
 #pragma unroll
-        for (int q = 0; q < KB; q++)
+        for (int q = 0; q < KB; q++) {
             t0[q] = r12 ? (uint64_t)(cur.xhi[q] | cur.v[q].z >> (pb.r12_hb + 1)) << 32 | cur.v[q].x
                         : (uint64_t)cur.v[q].y << 32 | cur.v[q].x;
+            if (cntw >= 0) {
+                const bool tw = (cur.cnt[q] & CNT_MASK) >= 2;
+                two |= (uint32_t)tw << q;
+                if (tw != (rec_phase == 0)) t0[q] = EMPTY;  // (the other phase's: skipped)
+            }
+        }
         // fast path: a k-mer whose filter-2 bits are all set changes nothing (most
         // occurrences of a k-mer seen before); the others are packed into the wave's queue
         // so the insertion path runs on dense lanes instead of once per item slot
@@ -2023,7 +2070,7 @@ __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView b
             for (int q = 0; q < KB; q++)
                 if (slow[q] && pre[q] + rank[q] - r0 < 64) {
                     wq[pre[q] + rank[q] - r0] = t0[q];
-                    if (cntw >= 0) wf[pre[q] + rank[q] - r0] = (cur.two >> q) & 1;
+                    if (cntw >= 0) wf[pre[q] + rank[q] - r0] = (two >> q) & 1;
                 }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's queue writes land
             if (lane < total - r0) {
