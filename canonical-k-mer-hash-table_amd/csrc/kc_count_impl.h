@@ -3078,16 +3078,18 @@ hipError_t WOps<W>::text_digest(TableView t, int count_mode, uint64_t a, int k, 
 // key's word 0 (a bijective mix of the key; for W >= 2 of its last word and a hash of the
 // others), value = 1 + the leading zeros of its other bits; merged into the context's
 // registers with atomicMax.  Grid-stride over the batch's tiles, one tile per round.
+// 1024-thread workgroups: the 64 KiB of registers allow two workgroups per CU, and the
+// windows' symbol loads want the 8 waves per SIMD that two 256-thread ones left at 2.
 // --------------------------------------------------------------------------------
+constexpr int HLL_T = 1024;
 template <int W>
-__global__ __launch_bounds__(COUNT_THREADS) void k_hll(PackedView sv, int k, const DevCounters* __restrict__ ctr,
-                                                       uint32_t* __restrict__ regs, uint64_t pow5_k,
-                                                       uint64_t pow5_km1) {
+__global__ __launch_bounds__(HLL_T) void k_hll(PackedView sv, int k, const DevCounters* __restrict__ ctr,
+                                               uint32_t* __restrict__ regs, uint64_t pow5_k, uint64_t pow5_km1) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint32_t* r = reinterpret_cast<uint32_t*>(smem);
-    for (uint32_t i = threadIdx.x; i < HLL_M; i += COUNT_THREADS) r[i] = 0;
+    for (uint32_t i = threadIdx.x; i < HLL_M; i += HLL_T) r[i] = 0;
     __syncthreads();
-    constexpr int TW = tile_win<W>(), RUNW = run_w<W>();
+    constexpr int RUNW = run_w<W>(), TW = HLL_T * RUNW;
     const uint64_t M = ctr->stream_len;
     const RollConst rk = make_roll<W>(k, pow5_k, pow5_km1);
     for (uint64_t t0 = (uint64_t)blockIdx.x * TW; t0 < M; t0 += (uint64_t)gridDim.x * TW) {
@@ -3105,7 +3107,7 @@ __global__ __launch_bounds__(COUNT_THREADS) void k_hll(PackedView sv, int k, con
             });
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < HLL_M; i += COUNT_THREADS)
+    for (uint32_t i = threadIdx.x; i < HLL_M; i += HLL_T)
         if (r[i]) atomicMax(&regs[i], r[i]);
 }
 
@@ -3114,7 +3116,7 @@ hipError_t WOps<W>::hll(PackedView sym, int k, DevCounters* ctr, uint32_t* regs,
     const size_t sm = (size_t)HLL_M * 4;
     hipError_t e = set_smem(k_hll<W>, sm);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_hll<W>, dim3(512), dim3(COUNT_THREADS), sm, s, sym, k, ctr, regs, pow5_mod54(k),
+    hipLaunchKernelGGL(k_hll<W>, dim3(512), dim3(HLL_T), sm, s, sym, k, ctr, regs, pow5_mod54(k),
                        pow5_mod54(k - 1));
     return hipGetLastError();
 }

@@ -30,14 +30,22 @@ namespace kc {
 // the chunk's offset, which has any alignment: five aligned dwords are funnel-shifted.
 // The fast path needs 3 readable bytes past the 16 (still inside the chunk), so the
 // last few bytes of a chunk take the byte path and nothing is read past a chunk.
-DEV void load16(const uint8_t* __restrict__ p, uint32_t vh, uint32_t (&w)[4]) {
-    if (vh >= 19) {
-        const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-        const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
-        const uint32_t sh = (uint32_t)(a & 3);
-        uint32_t x[5];
+// Two phases, so that a workgroup's loads for several tiles are all issued before the
+// first is used (a funnel shift right after its loads makes the compiler wait for them):
+// load16_issue loads the five dwords of the fast path (a lane whose 16 bytes are not
+// followed by 3 readable ones issues nothing), load16_finish shifts them, or reads the
+// bytes of the rare short case.
+DEV bool load16_fast(uint32_t vh) { return vh >= 19; }
+DEV void load16_issue(const uint8_t* __restrict__ p, uint32_t (&x)[5]) {
+    // (p minus its misalignment, not the masked integer, so the compiler still sees a global
+    // pointer: a flat load also counts against lgkmcnt, and the next scalar load's wait stalls on it)
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(p - (reinterpret_cast<uintptr_t>(p) & 3));
 #pragma unroll
-        for (int i = 0; i < 5; i++) x[i] = q[i];
+    for (int i = 0; i < 5; i++) x[i] = q[i];
+}
+DEV void load16_finish(const uint8_t* __restrict__ p, uint32_t vh, const uint32_t (&x)[5], uint32_t (&w)[4]) {
+    if (load16_fast(vh)) {
+        const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
 #pragma unroll
         for (int i = 0; i < 4; i++) w[i] = __builtin_amdgcn_alignbyte(x[i + 1], x[i], sh);
     } else {
@@ -96,18 +104,23 @@ __global__ __launch_bounds__(TILE_THREADS) void k_tile_summary_m(const uint8_t* 
     ChunkDesc cd[TPB];
 #pragma unroll
     for (int j = 0; j < TPB; j++) cd[j] = chunks[ci[j]];
-    uint32_t w[TPB][4], vh[TPB], valid[TPB], avail[TPB];
+    uint32_t w[TPB][4], vh[TPB], valid[TPB], avail[TPB], x[TPB][5];
     uint64_t rel[TPB];
     const uint32_t my0 = tid * 16;
 #pragma unroll
-    for (int j = 0; j < TPB; j++) {
+    for (int j = 0; j < TPB; j++) {  // every tile's dword loads first (load16_issue)
         rel[j] = (t0 + j) * TILE - cd[j].stage_off;
         const bool in = t0 + j < ntiles;
         valid[j] = in ? (uint32_t)min((uint64_t)TILE, cd[j].len - rel[j]) : 0;
         avail[j] = in ? (uint32_t)min((uint64_t)TILE + 64, cd[j].len - rel[j]) : 0;
         vh[j] = valid[j] > my0 ? valid[j] - my0 : 0;
+        if (fmt != FMT_PLAIN && vh[j] && load16_fast(avail[j] - my0))
+            load16_issue(src + cd[j].src_off + rel[j] + my0, x[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < TPB; j++) {
         w[j][0] = w[j][1] = w[j][2] = w[j][3] = 0;
-        if (fmt != FMT_PLAIN && vh[j]) load16(src + cd[j].src_off + rel[j] + my0, avail[j] - my0, w[j]);
+        if (fmt != FMT_PLAIN && vh[j]) load16_finish(src + cd[j].src_off + rel[j] + my0, avail[j] - my0, x[j], w[j]);
     }
 #pragma unroll
     for (int j = 0; j < TPB; j++) {
@@ -314,9 +327,11 @@ __global__ __launch_bounds__(256) void k_zero_edges(const TileInfo* __restrict__
 // thread's (at most 16) symbols land in one or two words of the tile's LDS image.
 // --------------------------------------------------------------------------------
 DEV uint32_t swap_pairs(uint32_t x) { return ((x >> 1) & 0x55555555u) | ((x & 0x55555555u) << 1); }
-// tiles per k_emit workgroup: 2 or 4 with their loads issued first were slower (tokenize 1.36 ->
-// 1.38 / 1.42 ms on C2, profiles/r05_ab_emit_tiles.txt): k_emit is not bound by its load chain
-constexpr int EMIT_TPB = 1;
+// tiles per k_emit workgroup: with every tile's loads issued before the first funnel shift
+// (load16_issue / load16_finish), 2 tiles take tokenize 1.31 -> 1.27 ms on C2; 4 tiles, and the
+// tiles' phases merged under one set of barriers, gained nothing (1.34 / 1.27 ms;
+// profiles/r05_ab_tokenizer_loads.txt)
+constexpr int EMIT_TPB = 2;
 
 // one tile's symbols into the tile's LDS image (s_pk / s_bk, zeroed) and out: w = the thread's
 // 16 bytes (vh of them valid); s_wsum / s_wmk: per-wave scratch of this tile
@@ -476,12 +491,16 @@ __global__ __launch_bounds__(TILE_THREADS) void k_emit(const uint8_t* __restrict
         }
     }
     const uint32_t my0 = tid * 16;
-    uint32_t w[TPB][4], vh[TPB];
+    uint32_t w[TPB][4], vh[TPB], x[TPB][5];
+#pragma unroll
+    for (int j = 0; j < TPB; j++) {  // every tile's dword loads first (load16_issue)
+        vh[j] = ti[j].valid > my0 ? min(ti[j].valid - my0, 16u) : 0;
+        if (vh[j] && load16_fast(ti[j].avail - my0)) load16_issue(src + ti[j].src + my0, x[j]);
+    }
 #pragma unroll
     for (int j = 0; j < TPB; j++) {
-        vh[j] = ti[j].valid > my0 ? min(ti[j].valid - my0, 16u) : 0;
         w[j][0] = w[j][1] = w[j][2] = w[j][3] = 0;
-        if (vh[j]) load16(src + ti[j].src + my0, ti[j].avail - my0, w[j]);
+        if (vh[j]) load16_finish(src + ti[j].src + my0, ti[j].avail - my0, x[j], w[j]);
     }
     for (int i = tid; i < TPB * NW; i += TILE_THREADS) {
         (&s_pk[0][0])[i] = 0;
