@@ -736,10 +736,19 @@ struct Rec12 {
         t1 = ((uint64_t)(r.z & ((1u << hb) - 1)) << 32) | r.y | ((uint64_t)((r.z >> hb) & 1) << 62);
     }
 };
-struct StoreRec12 {
+// two-word keys as 12-byte records (rec12) or whole keys: the format a uniform branch inside one
+// scatter loop (a loop instantiated per format kept both copies' invariants live, and the level
+// 2 of two-word keys spilled them, each reload waiting for the tile's prefetch loads)
+struct StoreW2 {
+    bool rec12;
     Rec12 rc;
     DEV void operator()(uint64_t* __restrict__ out, uint64_t dst, const uint64_t (&key)[2], uint32_t) const {
-        reinterpret_cast<uint3*>(out)[dst] = rc.enc(key[0], key[1]);
+        if (rec12) {
+            reinterpret_cast<uint3*>(out)[dst] = rc.enc(key[0], key[1]);
+        } else {
+            ks_store(out + dst * 2, key[0]);
+            ks_store(out + dst * 2 + 1, key[1]);
+        }
     }
 };
 
@@ -765,12 +774,14 @@ DEV void scatter_seg(const PartLds& l, uint32_t F, const Bin& bin, const Out& o,
             const uint4* h4 = reinterpret_cast<const uint4*>(l.hist);
             uint4* s4 = reinterpret_cast<uint4*>(l.start);
             uint32_t sum = 0;
+#pragma unroll 1
             for (uint32_t i = lo; i < hi; i++) {
                 const uint4 v = h4[i];
                 sum += v.x + v.y + v.z + v.w;
             }
             const uint32_t incl = wave_incl_sum(sum);
             uint32_t run = incl - sum;
+#pragma unroll 1
             for (uint32_t i = lo; i < hi; i++) {
                 const uint4 v = h4[i];
                 s4[i] = make_uint4(run, run + v.x, run + v.x + v.y, run + v.x + v.y + v.z);
@@ -780,9 +791,11 @@ DEV void scatter_seg(const PartLds& l, uint32_t F, const Bin& bin, const Out& o,
         } else {
             const uint32_t per = (F + 63) / 64, lo = min(F, lane * per), hi = min(F, lo + per);
             uint32_t sum = 0;
+#pragma unroll 1
             for (uint32_t i = lo; i < hi; i++) sum += l.hist[i];
             const uint32_t incl = wave_incl_sum(sum);
             uint32_t run = incl - sum;
+#pragma unroll 1
             for (uint32_t i = lo; i < hi; i++) {
                 l.start[i] = run;
                 run += l.hist[i];
@@ -800,6 +813,7 @@ DEV void scatter_seg(const PartLds& l, uint32_t F, const Bin& bin, const Out& o,
             for (int w = 0; w < W; w++) l.keys[slot * W + w] = tk[j][w];
         }
     bool spills = false;
+#pragma unroll 1
     for (uint32_t b = tid; b < F; b += NT) {
         const uint32_t st = l.start[b], h = l.hist[b];
         const uint64_t g = l.gbase[b] + l.lim[b];  // the bin's next destination
@@ -840,6 +854,7 @@ DEV void scatter_seg(const PartLds& l, uint32_t F, const Bin& bin, const Out& o,
         }
     };
     // two keys per thread per round, their LDS reads issued together
+#pragma unroll 1
     for (uint32_t i0 = tid; i0 < n; i0 += 2 * NT) {
         const uint32_t i1 = i0 + NT;
         const bool has1 = i1 < n;
@@ -1166,15 +1181,12 @@ __global__ __launch_bounds__(NT, scatter_waves(NT, k1_runw<W, NT>(), p1_out_word
                 auto pre = [&]() {  // after the rank atomics: load them
                     if (nxt) stage_word(t0 + TW, tid, npk, nbk);
                 };
-                if constexpr (OW == 2) {  // level 1 as 12-byte records (the kept Bloom levels, the table's)
-                    if (pb.rec12 & R12_P1) {
-                        scatter_seg<OW, RUNW, Bin, Out, NT>(l, F, bin, ob, tk, ok, out, mid,
-                                                            StoreRec12{Rec12{pb.r12_hb, pb.r12_xb1}}, pre);
-                        par ^= 1;
-                        continue;
-                    }
-                }
-                scatter_seg<OW, RUNW, Bin, Out, NT>(l, F, bin, ob, tk, ok, out, mid, StoreWords(), pre);
+                if constexpr (OW == 2)  // level 1 as 12-byte records (the kept Bloom levels, the table's)
+                    scatter_seg<OW, RUNW, Bin, Out, NT>(l, F, bin, ob, tk, ok, out, mid,
+                                                        StoreW2{(pb.rec12 & R12_P1) != 0, Rec12{pb.r12_hb, pb.r12_xb1}},
+                                                        pre);
+                else
+                    scatter_seg<OW, RUNW, Bin, Out, NT>(l, F, bin, ob, tk, ok, out, mid, StoreWords(), pre);
                 par ^= 1;
             } else {
                 scatter_tile<OW, RUNW, Bin, Out, NT>(l, F, bin, ob, tk, ok, out, NoMid());
@@ -1529,11 +1541,8 @@ __global__ __launch_bounds__(NT, scatter_waves(NT, run_w<W>(), W, 2048 / NT > 8 
             scatter_seg<W, RUNW, BinRegion, OutSeg, NT>(l, F, bin, o, tk, ok, pb.keys2, mid,
                                                         StoreRec6{xlo});
         } else if constexpr (W == 2) {
-            if (rout)
-                scatter_seg<W, RUNW, BinRegion, OutSeg, NT>(l, F, bin, o, tk, ok, pb.keys2, mid,
-                                                            StoreRec12{Rec12{pb.r12_hb, pb.r12_xb2}});
-            else
-                scatter_seg<W, RUNW, BinRegion, OutSeg, NT>(l, F, bin, o, tk, ok, pb.keys2, mid);
+            scatter_seg<W, RUNW, BinRegion, OutSeg, NT>(l, F, bin, o, tk, ok, pb.keys2, mid,
+                                                        StoreW2{rout, Rec12{pb.r12_hb, pb.r12_xb2}});
         } else {
             scatter_seg<W, RUNW, BinRegion, OutSeg, NT>(l, F, bin, o, tk, ok, pb.keys2, mid);
         }
