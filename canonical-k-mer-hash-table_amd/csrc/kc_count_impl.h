@@ -702,18 +702,6 @@ struct StoreRec6 {
         reinterpret_cast<uint16_t*>(q + 2)[dst & 1] = (uint16_t)((uint32_t)(key[0] >> 32) - xlo[b]);
     }
 };
-// the raw dwords of record p: lo | d-pair << 32 (decoded by rec6_key once the load is needed,
-// so a prefetch of the next items does not wait for its loads)
-DEV uint64_t rec6_raw(const uint64_t* __restrict__ keys, uint64_t p) {
-    const uint32_t* q = reinterpret_cast<const uint32_t*>(keys) + (p >> 1) * 3;
-    return ((uint64_t)q[2] << 32) | q[p & 1];
-}
-DEV uint64_t rec6_key(uint64_t raw, bool odd, uint32_t xlo) {
-    const uint32_t dd = (uint32_t)(raw >> 32);
-    const uint32_t d = odd ? dd >> 16 : dd & 0xFFFFu;
-    return ((uint64_t)(xlo + d) << 32) | (uint32_t)raw;
-}
-
 // pre(): called after the rank atomics (k_p1 issues the loads of its next tile's words there)
 // Level record of a two-word key (kc_internal.h PartBufs.rec12): table key (t0, t1) with
 // t0 = x << 32 | lo, t1 = key word 0 (2k - 64 bits) | TK_FLAG.  Three dwords {lo, t1 low, t1 bits
@@ -1577,7 +1565,8 @@ DEV uint32_t zero_byte_mask8(uint64_t x) {
 // Exclusive prefix of a level-3 workgroup's n <= MAX_SEG_GROUP segment fills (s_pre[0..n],
 // s_pre[n] = total), by the first wave: two fills per lane, one DPP scan (was a one-thread loop
 // of n dependent-looking loads, ~n HBM latencies at every workgroup's start)
-DEV void seg_prefix(uint32_t* s_pre, const uint32_t* __restrict__ fill, uint32_t n) {
+// s_pp (if given): the same prefix of the fills' record pairs, ceil(fill / 2) (k_p3's 6-byte records)
+DEV void seg_prefix(uint32_t* s_pre, const uint32_t* __restrict__ fill, uint32_t n, uint32_t* s_pp = nullptr) {
     if (threadIdx.x < 64) {
         const uint32_t j = 2 * threadIdx.x;
         const uint32_t a = j < n ? fill[j] : 0, b = j + 1 < n ? fill[j + 1] : 0;
@@ -1586,6 +1575,14 @@ DEV void seg_prefix(uint32_t* s_pre, const uint32_t* __restrict__ fill, uint32_t
         if (j < n) s_pre[j] = ex;
         if (j + 1 < n) s_pre[j + 1] = ex + a;
         if (threadIdx.x == 63) s_pre[n] = inc;
+        if (s_pp) {
+            const uint32_t pa = (a + 1) >> 1, pb = (b + 1) >> 1;
+            const uint32_t pinc = wave_incl_sum(pa + pb);
+            const uint32_t pex = pinc - (pa + pb);
+            if (j < n) s_pp[j] = pex;
+            if (j + 1 < n) s_pp[j + 1] = pex + pa;
+            if (threadIdx.x == 63) s_pp[n] = pinc;
+        }
     }
 }
 
@@ -1611,6 +1608,7 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
     constexpr int IW = CNT ? W + 1 : W;  // words per item
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ uint32_t s_pre[MAX_SEG_GROUP + 1];  // SEG: exclusive prefix of the B2 segment fills
+    __shared__ uint32_t s_pp[REC6 ? MAX_SEG_GROUP + 1 : 1];  // REC6: ... of their record pairs
     constexpr int S = BUCKET_WORDS / (W + 1);
     // keys loaded per thread before inserting (memory-level parallelism); 1024-thread
     // groups already keep 8 waves per SIMD in flight
@@ -1631,7 +1629,7 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
     // slice budget counts on)
     __shared__ uint64_t s_gst[SEG && CNT ? MAX_SEG_GROUP : 1];
     if constexpr (SEG) {
-        seg_prefix(s_pre, pb.hist2 + r * pb.B2, pb.B2);
+        seg_prefix(s_pre, pb.hist2 + r * pb.B2, pb.B2, REC6 ? s_pp : nullptr);
         if constexpr (CNT)
             if (pb.seg_start)
                 for (uint32_t g = threadIdx.x; g < pb.B2; g += NT) s_gst[g] = pb.seg_start[r * pb.B2 + g];
@@ -1738,23 +1736,6 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
                 add[q] = 1;
                 continue;
             }
-            if constexpr (REC6) {
-                // (loads only in range: the unconditional form of the two-word path measured 2 %
-                // slower here, profiles/r05_ab_load_merge.txt)
-                kk[q][0] = 0;
-                if (i < end) {
-                    while (nb <= i) {
-                        cs++;
-                        cb = nb;
-                        nb = s_pre[cs + 1];
-                    }
-                    const uint64_t p = (r * pb.B2 + cs) * pb.cap2 + (i - cb);
-                    kk[q][0] = rec6_raw(pb.keys2, p);
-                    ok |= (1u | (uint32_t)(p & 1) << 16) << q;  // valid, and (bit 16 + q) odd record
-                }
-                add[q] = 1;
-                continue;
-            }
             // every lane loads (past the end: a nearby item) into the same registers, its validity in
             // ok and its count masked where it is used: a value merged after a load made every
             // load wait for the earlier ones
@@ -1793,123 +1774,189 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
         }
     };
 
-    uint64_t kk[KB][W];
-    uint64_t add[KB];
-    uint32_t okm = 0, sg[KB];
-    if (start < vend) load_items(start, kk, add, okm, sg);
-    for (uint64_t base = start; base < vend; base += (uint64_t)KB * NT) {
-        // the next items' loads are issued before this batch's inserts
-        uint64_t nkk[KB][W];
-        uint64_t nadd[KB];
-        uint32_t nokm = 0, nsg[KB];
-        const uint64_t nbase = base + (uint64_t)KB * NT;
-        const bool more = W <= 2 && nbase < vend;  // W > 2: no spare registers
-        if (more) load_items(nbase, nkk, nadd, nokm, nsg);
-        if constexpr (REC6) {
+    // one key into the LDS region (tag probe, claim by CAS on word 0, count add); false: the
+    // region's probe bound was reached (counted as an overflow)
+    auto insert_one = [&](const uint64_t (&kw)[W], uint64_t a0) -> bool {
+        const uint64_t k0 = kw[0];
+        uint32_t b = bucket_in_region(k0, tv.R);
+        bool done = false;
+        {
+            constexpr uint32_t SMASK = (1u << S) - 1;
+            const uint32_t tag = slot_tag(k0);
+            const uint64_t bc = 0x0101010101010101ULL * tag;
+            for (int probe = 0; probe < 4 * BPR && !done;) {
+                const uint64_t tw = tg[b];
+                uint32_t m = zero_byte_mask8(tw ^ bc) & SMASK;
+                int slot = -1;
+                while (m) {  // candidates: usually none (new key) or exactly the key's slot
+                    const int sl = __builtin_ctz(m);
+                    m &= m - 1;
+                    bool eq = *lds_word(lt, b, sl * W) == k0;
 #pragma unroll
-            for (int q = 0; q < KB; q++) kk[q][0] = rec6_key(kk[q][0], (okm >> (16 + q)) & 1, xlo_r);
-        }
-        if constexpr (W == 2) {
-            if (r12) {
-                const Rec12 rc{pb.r12_hb, pb.r12_xb2};
-#pragma unroll
-                for (int q = 0; q < KB; q++) {
-                    const uint3 v = make_uint3((uint32_t)kk[q][0], (uint32_t)(kk[q][0] >> 32), (uint32_t)kk[q][1]);
-                    rc.dec(v, r12_reg ? xlo_r : sg[q] << pb.r12_xb2, kk[q][0], kk[q][1]);
-                }
-            }
-        }
-        bool pass[KB];
-#pragma unroll
-        for (int q = 0; q < KB; q++) {  // the gate reads of all KB items are issued together
-            pass[q] = (okm >> q) & 1;
-            if constexpr (GATE) {
-                const uint64_t t0 = kk[q][0];
-                if (bf.slice_blocks)
-                    pass[q] = pass[q] && block_gate(gs + (bloom_block(t0, bf.nblocks) - gblo) * 8, t0, bf.nh_gate);
-                else
-                    pass[q] = pass[q] && block_gate(bloom_block_ptr(bf, t0) + 8, t0, bf.nh_gate);
-            }
-            n_ins += pass[q];
-            if constexpr (CNT) {
-                add[q] &= CNT_MASK;
-                n_add += pass[q] ? add[q] : 0;
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < KB; q++) {
-            if (!pass[q]) continue;
-            const uint64_t k0 = kk[q][0];
-            uint32_t b = bucket_in_region(k0, tv.R);
-            bool done = false;
-            {
-                constexpr uint32_t SMASK = (1u << S) - 1;
-                const uint32_t tag = slot_tag(k0);
-                const uint64_t bc = 0x0101010101010101ULL * tag;
-                for (int probe = 0; probe < 4 * BPR && !done;) {
-                    const uint64_t tw = tg[b];
-                    uint32_t m = zero_byte_mask8(tw ^ bc) & SMASK;
-                    int slot = -1;
-                    while (m) {  // candidates: usually none (new key) or exactly the key's slot
-                        const int sl = __builtin_ctz(m);
-                        m &= m - 1;
-                        bool eq = *lds_word(lt, b, sl * W) == k0;
-#pragma unroll
-                        for (int w = 1; w < W; w++) eq &= *lds_word(lt, b, sl * W + w) == kk[q][w];
-                        if (eq) {
-                            slot = sl;
-                            break;
-                        }
+                    for (int w = 1; w < W; w++) eq &= *lds_word(lt, b, sl * W + w) == kw[w];
+                    if (eq) {
+                        slot = sl;
+                        break;
                     }
-                    uint64_t a = add[q];
-                    if (slot < 0) {
-                        const uint32_t em = zero_byte_mask8(tw) & SMASK;
-                        if (!em) {  // bucket full, key absent: next bucket
-                            b = (b + 1) & (BPR - 1);
-                            probe++;
-                            continue;
-                        }
-                        // claim the first untagged slot by its word 0; the tag is stored last, so
-                        // a tag match always finds the key's words published
-                        const int e = __builtin_ctz(em);
-                        const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long*>(lds_word(lt, b, e * W)),
-                                                       0ULL, (unsigned long long)k0);
-                        if (old == EMPTY) {
+                }
+                uint64_t a = a0;
+                if (slot < 0) {
+                    const uint32_t em = zero_byte_mask8(tw) & SMASK;
+                    if (!em) {  // bucket full, key absent: next bucket
+                        b = (b + 1) & (BPR - 1);
+                        probe++;
+                        continue;
+                    }
+                    // claim the first untagged slot by its word 0; the tag is stored last, so
+                    // a tag match always finds the key's words published
+                    const int e = __builtin_ctz(em);
+                    const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long*>(lds_word(lt, b, e * W)),
+                                                   0ULL, (unsigned long long)k0);
+                    if (old == EMPTY) {
 #pragma unroll
-                            for (int w = 1; w < W; w++)
-                                __hip_atomic_store(lds_word(lt, b, e * W + w), kk[q][w], __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-                            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                            __hip_atomic_store(reinterpret_cast<uint8_t*>(tg + b) + e, (uint8_t)tag, __ATOMIC_RELAXED,
+                        for (int w = 1; w < W; w++)
+                            __hip_atomic_store(lds_word(lt, b, e * W + w), kw[w], __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_WORKGROUP);
-                            if constexpr (W > 1) a += READY;  // the table format's published flag
-                            slot = e;
-                        } else if (W == 1 && old == k0) {
-                            slot = e;  // the same key, claimed an instant ago
-                        } else {
-                            probe++;  // claimed by another key (tag not yet stored): read again
-                            continue;
-                        }
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                        __hip_atomic_store(reinterpret_cast<uint8_t*>(tg + b) + e, (uint8_t)tag, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+                        if constexpr (W > 1) a += READY;  // the table format's published flag
+                        slot = e;
+                    } else if (W == 1 && old == k0) {
+                        slot = e;  // the same key, claimed an instant ago
+                    } else {
+                        probe++;  // claimed by another key (tag not yet stored): read again
+                        continue;
                     }
-                    atomicAdd(reinterpret_cast<unsigned long long*>(lds_word(lt, b, S * W + slot)),
-                              (unsigned long long)a);
-                    done = true;
+                }
+                atomicAdd(reinterpret_cast<unsigned long long*>(lds_word(lt, b, S * W + slot)),
+                          (unsigned long long)a);
+                done = true;
+            }
+        }
+
+        return done;
+    };
+
+    if constexpr (REC6) {
+        // 6-byte records by pairs: one 12-byte load gives two keys (the pair's three dwords
+        // {lo_even, lo_odd, d_even | d_odd << 16}, StoreRec6), KP pairs per thread and round with
+        // the next round's loads issued first: half the loads and rounds of one record per load.
+        // s_pp: exclusive prefix of the segments' pair counts; the last pair of an odd fill
+        // holds one record
+        constexpr int KP = GATE ? 2 : 4;  // (the gate's filter words: 4 pairs spill)
+        const uint32_t endp = s_pp[pb.B2];
+        uint32_t ps = 0, pcb = 0, pnb = s_pp[1], pfill = s_pre[1];
+        auto load_pairs = [&](uint32_t base, uint3 (&v)[KP], uint32_t& ok) {
+            ok = 0;
+#pragma unroll
+            for (int q = 0; q < KP; q++) {
+                const uint32_t j = base + threadIdx.x + (uint32_t)q * NT;
+                v[q] = make_uint3(0, 0, 0);
+                if (j < endp) {  // (loads only in range, as the one-record form)
+                    while (pnb <= j) {
+                        ps++;
+                        pcb = pnb;
+                        pnb = s_pp[ps + 1];
+                        pfill = s_pre[ps + 1] - s_pre[ps];
+                    }
+                    const uint64_t pp = ((r * pb.B2 + ps) * pb.cap2 >> 1) + (j - pcb);
+                    uint32_t w3[3];
+                    __builtin_memcpy(w3, reinterpret_cast<const uint32_t*>(pb.keys2) + pp * 3, 12);
+                    v[q] = make_uint3(w3[0], w3[1], w3[2]);
+                    ok |= (1u | (uint32_t)(2 * (j - pcb) + 1 < pfill) << 1) << (2 * q);
                 }
             }
-
-            if (!done) n_fail++;
-        }
-        if (more) {
-            okm = nokm;
+        };
+        uint3 cv[KP];
+        uint32_t cok = 0;
+        if (endp) load_pairs(0, cv, cok);
+        for (uint32_t base = 0; base < endp; base += (uint32_t)KP * NT) {
+            uint3 nv[KP];
+            uint32_t nok = 0;
+            const uint32_t nbase = base + (uint32_t)KP * NT;
+            if (nbase < endp) load_pairs(nbase, nv, nok);
+            uint64_t kp[2 * KP][1];
+            bool pass[2 * KP];
 #pragma unroll
-            for (int q = 0; q < KB; q++) {
-                add[q] = nadd[q];
-                sg[q] = nsg[q];
-#pragma unroll
-                for (int w = 0; w < W; w++) kk[q][w] = nkk[q][w];
+            for (int q = 0; q < KP; q++) {
+                kp[2 * q][0] = ((uint64_t)(xlo_r + (cv[q].z & 0xFFFFu)) << 32) | cv[q].x;
+                kp[2 * q + 1][0] = ((uint64_t)(xlo_r + (cv[q].z >> 16)) << 32) | cv[q].y;
             }
-        } else if (nbase < vend) {
-            load_items(nbase, kk, add, okm, sg);
+#pragma unroll
+            for (int q = 0; q < 2 * KP; q++) {  // the gate reads of all items are issued together
+                pass[q] = (cok >> q) & 1;
+                if constexpr (GATE) {
+                    const uint64_t t0 = kp[q][0];
+                    if (bf.slice_blocks)
+                        pass[q] = pass[q] && block_gate(gs + (bloom_block(t0, bf.nblocks) - gblo) * 8, t0, bf.nh_gate);
+                    else
+                        pass[q] = pass[q] && block_gate(bloom_block_ptr(bf, t0) + 8, t0, bf.nh_gate);
+                }
+                n_ins += pass[q];
+            }
+#pragma unroll
+            for (int q = 0; q < 2 * KP; q++)
+                if (pass[q] && !insert_one(kp[q], 1)) n_fail++;
+#pragma unroll
+            for (int q = 0; q < KP; q++) cv[q] = nv[q];
+            cok = nok;
+        }
+    } else {
+        uint64_t kk[KB][W];
+        uint64_t add[KB];
+        uint32_t okm = 0, sg[KB];
+        if (start < vend) load_items(start, kk, add, okm, sg);
+        for (uint64_t base = start; base < vend; base += (uint64_t)KB * NT) {
+            // the next items' loads are issued before this batch's inserts
+            uint64_t nkk[KB][W];
+            uint64_t nadd[KB];
+            uint32_t nokm = 0, nsg[KB];
+            const uint64_t nbase = base + (uint64_t)KB * NT;
+            const bool more = W <= 2 && nbase < vend;  // W > 2: no spare registers
+            if (more) load_items(nbase, nkk, nadd, nokm, nsg);
+            if constexpr (W == 2) {
+                if (r12) {
+                    const Rec12 rc{pb.r12_hb, pb.r12_xb2};
+    #pragma unroll
+                    for (int q = 0; q < KB; q++) {
+                        const uint3 v = make_uint3((uint32_t)kk[q][0], (uint32_t)(kk[q][0] >> 32), (uint32_t)kk[q][1]);
+                        rc.dec(v, r12_reg ? xlo_r : sg[q] << pb.r12_xb2, kk[q][0], kk[q][1]);
+                    }
+                }
+            }
+            bool pass[KB];
+    #pragma unroll
+            for (int q = 0; q < KB; q++) {  // the gate reads of all KB items are issued together
+                pass[q] = (okm >> q) & 1;
+                if constexpr (GATE) {
+                    const uint64_t t0 = kk[q][0];
+                    if (bf.slice_blocks)
+                        pass[q] = pass[q] && block_gate(gs + (bloom_block(t0, bf.nblocks) - gblo) * 8, t0, bf.nh_gate);
+                    else
+                        pass[q] = pass[q] && block_gate(bloom_block_ptr(bf, t0) + 8, t0, bf.nh_gate);
+                }
+                n_ins += pass[q];
+                if constexpr (CNT) {
+                    add[q] &= CNT_MASK;
+                    n_add += pass[q] ? add[q] : 0;
+                }
+            }
+    #pragma unroll
+            for (int q = 0; q < KB; q++)
+                if (pass[q] && !insert_one(kk[q], add[q])) n_fail++;
+            if (more) {
+                okm = nokm;
+    #pragma unroll
+                for (int q = 0; q < KB; q++) {
+                    add[q] = nadd[q];
+                    sg[q] = nsg[q];
+    #pragma unroll
+                    for (int w = 0; w < W; w++) kk[q][w] = nkk[q][w];
+                }
+            } else if (nbase < vend) {
+                load_items(nbase, kk, add, okm, sg);
+            }
         }
     }
     __syncthreads();
@@ -2069,6 +2116,7 @@ __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView b
             slow[q] = base + threadIdx.x + (uint64_t)q * NT < end && (cntw < 0 || t0[q] != EMPTY) &&
                       !block_gate(lf + (uint32_t)(bloom_block(t0[q], bf.nblocks) - blk0) * BF_BLOCK_WORDS + 8, t0[q],
                                   bf.nh);
+
             const uint64_t bal = __ballot(slow[q]);
             pre[q] = total;
             rank[q] = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
