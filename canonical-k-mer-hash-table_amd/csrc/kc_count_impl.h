@@ -182,37 +182,45 @@ DEV void block_insert(uint32_t* blk, uint64_t t0, int nh, BloomLocal& loc, bool 
     const uint64_t h = bmix(t0);
     uint32_t f1[8], f2[8];
     load8(blk + 8, f2);
+    load8(blk, f1);  // (with filter 2: one wait for the block's 64 bytes instead of two in turn)
     if (sb_all(f2, h, nh)) return;  // in the second filter already
-    load8(blk, f1);
-    int n = 0, s1 = 0, s2 = 0;
-    bool dup[MAX_NH];
+    // the key's positions as one bit mask per filter word (a position j >= 8 that repeats the bit
+    // of position j - 8 merges with it: counted once); n = distinct positions, s1 / s2 = those set
+    uint32_t pm[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-    for (int j = 0; j < MAX_NH; j++) {
-        dup[j] = j >= nh || (j >= 8 && sb_bit(h, j) == sb_bit(h, j - 8));
-        if (!dup[j]) {
-            n++;
-            s1 += (f1[j & 7] >> sb_bit(h, j)) & 1;
-            s2 += (f2[j & 7] >> sb_bit(h, j)) & 1;
-        }
+    for (int j = 0; j < MAX_NH; j++)
+        if (j < nh) pm[j & 7] |= 1u << sb_bit(h, j);
+    int n = 0, s1 = 0, s2 = 0;
+#pragma unroll
+    for (int w = 0; w < 8; w++) {
+        n += __popc(pm[w]);
+        s1 += __popc(pm[w] & f1[w]);
+        s2 += __popc(pm[w] & f2[w]);
     }
-    bool to_second = true;
-    if (s1 != n) {
+    // a filter's missing bits set by four 64-bit atomic ORs (word pairs; a pair with nothing to
+    // set ORs zero), issued back to back: one wait for all of them.  (One 32-bit atomic per
+    // position under its own branch waited for each return in turn.)  mine = bits this thread
+    // flipped, as MyAtomicBitArrayFT::set counts them
+    auto set_missing = [&](uint32_t* f, const uint32_t (&fw)[8]) {
+        uint64_t m[4], old[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            m[q] = (uint64_t)(pm[2 * q] & ~fw[2 * q]) | (uint64_t)(pm[2 * q + 1] & ~fw[2 * q + 1]) << 32;
+            old[q] = atomicOr(reinterpret_cast<unsigned long long*>(f) + q, (unsigned long long)m[q]);
+        }
         int mine = 0;
 #pragma unroll
-        for (int j = 0; j < MAX_NH; j++) {
-            const uint32_t m = 1u << sb_bit(h, j);
-            if (!dup[j] && !(f1[j & 7] & m)) mine += !(atomicOr(blk + (j & 7), m) & m);
-        }
+        for (int q = 0; q < 4; q++) mine += __popcll(m[q] & ~old[q]);
+        return mine;
+    };
+    bool to_second = true;
+    if (s1 != n) {
+        const int mine = set_missing(blk, f1);
         if (mine == n - s1 || (unique && mine > 0)) { loc.new_first++; to_second = false; }
         else loc.failed++;
     }
     if (to_second) {
-        int mine = 0;
-#pragma unroll
-        for (int j = 0; j < MAX_NH; j++) {
-            const uint32_t m = 1u << sb_bit(h, j);
-            if (!dup[j] && !(f2[j & 7] & m)) mine += !(atomicOr(blk + 8 + (j & 7), m) & m);
-        }
+        const int mine = set_missing(blk + 8, f2);
         if (unique || mine == n - s2) loc.new_second++;  // (a distinct key was not in filter 2 before)
     }
 }
