@@ -1643,7 +1643,7 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
                 for (uint32_t g = threadIdx.x; g < pb.B2; g += NT) s_gst[g] = pb.seg_start[r * pb.B2 + g];
         __syncthreads();
         start = 0;
-        end = s_pre[pb.B2];
+        end = __builtin_amdgcn_readfirstlane(s_pre[pb.B2]);  // (uniform: the round loop's branches are scalar)
     } else {
         start = pb.off2[r * pb.B2];
         end = pb.off2[(r + 1) * pb.B2];
@@ -1853,14 +1853,16 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
         // s_pp: exclusive prefix of the segments' pair counts; the last pair of an odd fill
         // holds one record
         constexpr int KP = GATE ? 2 : 4;  // (the gate's filter words: 4 pairs spill)
-        const uint32_t endp = s_pp[pb.B2];
+        const uint32_t endp = __builtin_amdgcn_readfirstlane(s_pp[pb.B2]);  // (uniform: scalar branches)
         uint32_t ps = 0, pcb = 0, pnb = s_pp[1], pfill = s_pre[1];
         auto load_pairs = [&](uint32_t base, uint3 (&v)[KP], uint32_t& ok) {
+            // the pairs' addresses first (the segment cursor's loop), then every load back to back
+            uint64_t pp[KP];
             ok = 0;
 #pragma unroll
             for (int q = 0; q < KP; q++) {
                 const uint32_t j = base + threadIdx.x + (uint32_t)q * NT;
-                v[q] = make_uint3(0, 0, 0);
+                pp[q] = 0;
                 if (j < endp) {  // (loads only in range, as the one-record form)
                     while (pnb <= j) {
                         ps++;
@@ -1868,12 +1870,17 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
                         pnb = s_pp[ps + 1];
                         pfill = s_pre[ps + 1] - s_pre[ps];
                     }
-                    const uint64_t pp = ((r * pb.B2 + ps) * pb.cap2 >> 1) + (j - pcb);
-                    uint32_t w3[3];
-                    __builtin_memcpy(w3, reinterpret_cast<const uint32_t*>(pb.keys2) + pp * 3, 12);
-                    v[q] = make_uint3(w3[0], w3[1], w3[2]);
+                    pp[q] = ((r * pb.B2 + ps) * pb.cap2 >> 1) + (j - pcb);
                     ok |= (1u | (uint32_t)(2 * (j - pcb) + 1 < pfill) << 1) << (2 * q);
                 }
+            }
+            // (every slot loads, a slot without a pair the buffer's first: a load under a branch
+            // was waited for inside it, where its registers merge with the other path's)
+#pragma unroll
+            for (int q = 0; q < KP; q++) {
+                uint32_t w3[3];
+                __builtin_memcpy(w3, reinterpret_cast<const uint32_t*>(pb.keys2) + pp[q] * 3, 12);
+                v[q] = make_uint3(w3[0], w3[1], w3[2]);
             }
         };
         uint3 cv[KP];
@@ -1882,8 +1889,9 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
         for (uint32_t base = 0; base < endp; base += (uint32_t)KP * NT) {
             uint3 nv[KP];
             uint32_t nok = 0;
-            const uint32_t nbase = base + (uint32_t)KP * NT;
-            if (nbase < endp) load_pairs(nbase, nv, nok);
+            // (the next round's loads unconditionally: past the end every slot reads the buffer's
+            // first pair, ok = 0; under a branch the loads were waited for as soon as issued)
+            load_pairs(base + (uint32_t)KP * NT, nv, nok);
             uint64_t kp[2 * KP][1];
             bool pass[2 * KP];
 #pragma unroll
@@ -1911,34 +1919,29 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
             cok = nok;
         }
     } else {
-        uint64_t kk[KB][W];
-        uint64_t add[KB];
-        uint32_t okm = 0, sg[KB];
-        if (start < vend) load_items(start, kk, add, okm, sg);
-        for (uint64_t base = start; base < vend; base += (uint64_t)KB * NT) {
-            // the next items' loads are issued before this batch's inserts
-            uint64_t nkk[KB][W];
-            uint64_t nadd[KB];
-            uint32_t nokm = 0, nsg[KB];
-            const uint64_t nbase = base + (uint64_t)KB * NT;
-            const bool more = W <= 2 && nbase < vend;  // W > 2: no spare registers
-            if (more) load_items(nbase, nkk, nadd, nokm, nsg);
+        struct Items {
+            uint64_t kk[KB][W];
+            uint64_t add[KB];
+            uint32_t okm, sg[KB];
+        };
+        // one round of KB items per thread: decode, gate, insert
+        auto round = [&](Items& it) {
             if constexpr (W == 2) {
                 if (r12) {
                     const Rec12 rc{pb.r12_hb, pb.r12_xb2};
-    #pragma unroll
+#pragma unroll
                     for (int q = 0; q < KB; q++) {
-                        const uint3 v = make_uint3((uint32_t)kk[q][0], (uint32_t)(kk[q][0] >> 32), (uint32_t)kk[q][1]);
-                        rc.dec(v, r12_reg ? xlo_r : sg[q] << pb.r12_xb2, kk[q][0], kk[q][1]);
+                        const uint3 v = make_uint3((uint32_t)it.kk[q][0], (uint32_t)(it.kk[q][0] >> 32), (uint32_t)it.kk[q][1]);
+                        rc.dec(v, r12_reg ? xlo_r : it.sg[q] << pb.r12_xb2, it.kk[q][0], it.kk[q][1]);
                     }
                 }
             }
             bool pass[KB];
-    #pragma unroll
+#pragma unroll
             for (int q = 0; q < KB; q++) {  // the gate reads of all KB items are issued together
-                pass[q] = (okm >> q) & 1;
+                pass[q] = (it.okm >> q) & 1;
                 if constexpr (GATE) {
-                    const uint64_t t0 = kk[q][0];
+                    const uint64_t t0 = it.kk[q][0];
                     if (bf.slice_blocks)
                         pass[q] = pass[q] && block_gate(gs + (bloom_block(t0, bf.nblocks) - gblo) * 8, t0, bf.nh_gate);
                     else
@@ -1946,24 +1949,34 @@ __global__ __launch_bounds__(P3_THREADS, P3_THREADS / 128) void k_p3(TableView t
                 }
                 n_ins += pass[q];
                 if constexpr (CNT) {
-                    add[q] &= CNT_MASK;
-                    n_add += pass[q] ? add[q] : 0;
+                    it.add[q] &= CNT_MASK;
+                    n_add += pass[q] ? it.add[q] : 0;
                 }
             }
-    #pragma unroll
+#pragma unroll
             for (int q = 0; q < KB; q++)
-                if (pass[q] && !insert_one(kk[q], add[q])) n_fail++;
-            if (more) {
-                okm = nokm;
-    #pragma unroll
-                for (int q = 0; q < KB; q++) {
-                    add[q] = nadd[q];
-                    sg[q] = nsg[q];
-    #pragma unroll
-                    for (int w = 0; w < W; w++) kk[q][w] = nkk[q][w];
-                }
-            } else if (nbase < vend) {
-                load_items(nbase, kk, add, okm, sg);
+                if (pass[q] && !insert_one(it.kk[q], it.add[q])) n_fail++;
+        };
+        constexpr uint64_t STEP = (uint64_t)KB * NT;
+        if constexpr (W <= 2) {
+            // ping-pong rounds: the next round's items load into the other buffer while this one is
+            // inserted (unconditionally: past the end a slot reads a nearby item, ok = 0).  Copying
+            // the prefetched items into the current buffer at each round's end made the compiler
+            // wait for the prefetch right after issuing it
+            Items ia, ib;
+            load_items(start, ia.kk, ia.add, ia.okm, ia.sg);
+            for (uint64_t base = start; base < vend; base += 2 * STEP) {
+                load_items(base + STEP, ib.kk, ib.add, ib.okm, ib.sg);
+                round(ia);
+                if (base + STEP >= vend) break;
+                load_items(base + 2 * STEP, ia.kk, ia.add, ia.okm, ia.sg);
+                round(ib);
+            }
+        } else {  // (W > 2: no spare registers for a second buffer)
+            Items ia;
+            for (uint64_t base = start; base < vend; base += STEP) {
+                load_items(base, ia.kk, ia.add, ia.okm, ia.sg);
+                round(ia);
             }
         }
     }
@@ -2036,7 +2049,7 @@ __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView b
         seg_prefix(s_pre, pb.hist2 + r * pb.B2, pb.B2);
         __syncthreads();
         start = 0;
-        end = s_pre[pb.B2];
+        end = __builtin_amdgcn_readfirstlane(s_pre[pb.B2]);  // (uniform: the round loop's branches are scalar)
     } else {
         start = pb.off2[r * pb.B2];
         end = pb.off2[(r + 1) * pb.B2];
@@ -2097,12 +2110,9 @@ __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView b
             w.cnt[q] = cntw >= 0 ? pb.keys2[ii * is + cntw] : 0;
         }
     };
-    Raw cur, nxt;
-    if (start < end) fetch(start, cur);
-    for (uint64_t base = start; base < end; base += (uint64_t)KB * NT) {
-        const uint64_t nbase = base + (uint64_t)KB * NT;
-        if (nbase < end) fetch(nbase, nxt);
-        uint64_t t0[KB];
+    // one round: KB items per thread, the fast path, then the wave's queue of slow items
+    auto round = [&](const Raw& cur, uint64_t base) {
+    uint64_t t0[KB];
         uint32_t two = 0;  // bit q: item q is a record of count >= 2
 #pragma unroll
         for (int q = 0; q < KB; q++) {
@@ -2121,10 +2131,14 @@ __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView b
         uint32_t pre[KB], rank[KB], total = 0;
 #pragma unroll
         for (int q = 0; q < KB; q++) {
-            slow[q] = base + threadIdx.x + (uint64_t)q * NT < end && (cntw < 0 || t0[q] != EMPTY) &&
-                      !block_gate(lf + (uint32_t)(bloom_block(t0[q], bf.nblocks) - blk0) * BF_BLOCK_WORDS + 8, t0[q],
-                                  bf.nh);
-
+            // (every slot reads its block, clamped into the region: no read under a branch, so
+            // the KB gate reads wait once together)
+            const uint32_t lb = (uint32_t)min(bloom_block(t0[q], bf.nblocks) - blk0, (uint64_t)bpr - 1);
+            slow[q] = !block_gate(lf + lb * BF_BLOCK_WORDS + 8, t0[q], bf.nh) &&
+                      base + threadIdx.x + (uint64_t)q * NT < end && (cntw < 0 || t0[q] != EMPTY);
+        }
+#pragma unroll
+        for (int q = 0; q < KB; q++) {  // (the ballots after all the gate reads)
             const uint64_t bal = __ballot(slow[q]);
             pre[q] = total;
             rank[q] = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
@@ -2146,7 +2160,20 @@ __global__ __launch_bounds__(B3_THREADS, B3_THREADS / 128) void k_b3(BloomView b
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // queue reads done before reuse
         }
-        cur = nxt;
+    };
+    // ping-pong rounds: the next round's items load into the other buffer while this one is
+    // processed (unconditionally: past the end a slot reads a nearby item and is not used).  A
+    // copy of the prefetched buffer into the current one at each round's end made the compiler
+    // wait for the prefetch right after issuing it
+    constexpr uint64_t STEP = (uint64_t)KB * NT;
+    Raw ra, rb;
+    fetch(start, ra);
+    for (uint64_t base = start; base < end; base += 2 * STEP) {
+        fetch(base + STEP, rb);
+        round(ra, base);
+        if (base + STEP >= end) break;
+        fetch(base + 2 * STEP, ra);
+        round(rb, base + STEP);
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < n4; i += NT) g4[i] = l4[i];
