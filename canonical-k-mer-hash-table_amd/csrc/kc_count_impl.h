@@ -760,7 +760,16 @@ DEV void scatter_seg(const PartLds& l, uint32_t F, const Bin& bin, const Out& o,
 #pragma unroll
     for (int j = 0; j < RUNW; j++) {
         const uint32_t b = bin(tk[j][0]);
-        pk[j] = ok[j] ? (b << 16) | atomicAdd(&l.hist[b], 1u) : ~0u;
+        if constexpr (W >= 2) {
+            // every slot issues its rank atomic (adding 0 where there is no key; a bin is in range
+            // for any key word), so the RUNW atomics go out back to back with one wait for their
+            // returns; an atomic under `if (ok)` was waited for inside the branch.  (One-word keys
+            // keep the branch: their level 1 has no registers left for RUNW returns in flight.)
+            const uint32_t rk = atomicAdd(&l.hist[b], ok[j] ? 1u : 0u);
+            pk[j] = ok[j] ? (b << 16) | rk : ~0u;
+        } else {
+            pk[j] = ok[j] ? (b << 16) | atomicAdd(&l.hist[b], 1u) : ~0u;
+        }
     }
     pre();
     __syncthreads();  // 1
