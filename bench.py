@@ -233,7 +233,10 @@ def cli_fullsize(job, args):
         out = os.path.join(td, "out.txt")
         share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
         cli_args = [str(args.k)] + fx["args"] + ["-t", str(max(3, min(share + 2, 64)))]
-        r = run_cli(fa, cli_args, out)
+        # a whole strong job's text (C4: ~60 GB) is digested on the device instead of written
+        # (--digest-only: kc_output_digest, the digest the fixture holds)
+        big = fx.get("whole_job", False)
+        r = run_cli(fa, cli_args, out, ["--digest-only"] if big else ())
         if r is None:
             return {"error": "CLI failed"}
         secs, write_s, wall, stdout = r
@@ -243,7 +246,17 @@ def cli_fullsize(job, args):
                "input_path": "device image" if "Input path: device image" in stdout else "host chunks",
                "path": "bin/kaarme on the whole workload's FASTA (page-cached file in TMPDIR): the reference's timer "
                        "lines include reading the file (parallel_parser.hpp:1230-1299,1544-1550)"}
-        if os.path.exists(dig):
+        m = re.search(r"Output digest: (\{.*\})", stdout)
+        if big and m:
+            import kaarme_amd as ka
+            got = json.loads(m.group(1))
+            rec["parity"] = {"match": ka.same_digest(got, fx["digest"]), "digest": got,
+                             "reference_case": f"tests/golden/fullsize.json {fx['name']}",
+                             "checker": "the CLI's --digest-only (kc_output_digest on the device) against the "
+                                        "fixture's whole-job digest"}
+            rec["sized_from_estimate"] = "Device table sized from the distinct estimate" in stdout
+            rec["path"] += "; --digest-only: the output digest instead of the file (write_s = its time)"
+        elif os.path.exists(dig):
             t0 = time.perf_counter()
             p = subprocess.run([dig, "lines", out], capture_output=True, text=True)
             if p.returncode == 0:
@@ -254,6 +267,48 @@ def cli_fullsize(job, args):
                                  "checker": "oracle/_ref/kc_digest lines (XXH64 per output line)",
                                  "digest_s": round(time.perf_counter() - t0, 2)}
     return rec
+
+
+def host_chunks_record(job, args, batch_mib=256, reps=3):
+    """The C-ABI path INTEGRATION.md section 2 tells a maintainer to bind: the
+    whole job through kc_count_chunk, one call per reference chunk (~10 MiB) straight from host
+    memory (a pageable array holding the file's bytes), the library's pinned double-buffered
+    stage (batch_mib MiB batches: the copy of batch i+1 overlaps the counting of batch i) and
+    H2D copies included, timed from the first call to kc_finish; the best of `reps` jobs after one
+    untimed job (pinned-stage allocation, kernel loading), digested against the fixture."""
+    import ctypes as C
+    import kaarme_amd as ka
+    fx = job.fixture
+    host = job.image.cpu().numpy()
+    base = host.ctypes.data
+    cfg = ka.Config(k=args.k, mode=2, table_slots=job.slots, min_abundance=fx["min_abundance"] if fx else 2,
+                    batch_bytes=batch_mib << 20)
+    kc = ka.KmerCounter(cfg)
+    try:
+        times = []
+        for rep in range(reps + 1):
+            kc.reset()
+            t0 = time.perf_counter()
+            for off, ln, bh in job.chunks:
+                kc._chk(kc.lib.kc_count_chunk(kc._ctx, C.c_void_p(base + off), ln, ka.FMT_FASTA, int(bh)),
+                        "kc_count_chunk")
+            st = kc.finish()
+            if rep:
+                times.append(time.perf_counter() - t0)
+        secs = min(times)
+        rec = {"value": st["windows"] / secs, "unit": "k-mers/s", "seconds": round(secs, 4),
+               "runs_s": [round(t, 4) for t in times], "statistic": f"best of {reps} after one untimed job",
+               "chunks": len(job.chunks), "batch_mib": batch_mib, "windows": st["windows"],
+               "path": "kc_count_chunk per reference chunk from pageable host memory -> the library's pinned "
+                       "double-buffered stage -> H2D -> tokenize + count (PCIe-inclusive; the C ABI's host-chunk "
+                       "entry point, include/kc_api.h, INTEGRATION.md section 2)"}
+        if fx is not None and fx.get("digest"):
+            got = kc.output_digest()
+            rec["parity"] = {"match": ka.same_digest(got, fx["digest"]), "digest": got,
+                             "reference_case": f"tests/golden/fullsize.json {fx['name']}"}
+        return rec
+    finally:
+        kc.close()
 
 
 def cpu_model():
@@ -408,7 +463,9 @@ def setup_job(args, env, image=None):
     # estimate -- C4 holds 1.0 G distinct k-mers in a -s 2.6e9 table, C5 1.5 G in -s 3.6e9, which as
     # 25 % headroom over -s take 83 / 192 GB of HBM for 35 / 86 GB of need)
     est_table = strong and not dist and not share and not args.s_table
-    if (strong and (share or est_table or (dist and world > 1))) or (dist and args.unique):
+    #  on one GPU the whole job's estimate runs inside the timed step: the
+    # counter is created with -s and every step sizes its table from the estimate (kc_size_table)
+    if (strong and (share or (dist and world > 1))) or (dist and args.unique):
         # (sharded Bloom jobs too: the rank's ungated local count holds all its distinct k-mers)
         # a rank's local table holds its own input's distinct k-mers, which its 1/G share of -s
         # does not bound: sized from a HyperLogLog estimate of them (kc_estimate_distinct_device,
@@ -442,7 +499,8 @@ def setup_job(args, env, image=None):
     workload = (f"{args.config}: synthetic {N} x {L} bp reads/GPU, k={k}, {tbl}" if not strong else
                 f"{args.config}: synthetic {args.reads} x {L} bp reads over {world} GPU(s), k={k}, {tbl} per GPU")
     if est_table:
-        workload += " (device table sized from the distinct estimate, 1.1 x HLL, not 1.25 x -s)"
+        workload += (" (device table sized from the distinct estimate, 1.1 x HLL, not 1.25 x -s; the estimate runs "
+                     "inside every timed step)")
     if share:
         workload = (f"{args.config} share 1/{share}: synthetic {N} x {L} bp reads (rank 0 of {args.reads} over "
                     f"{share} GPUs), k={k}, -m 2, local table from the distinct estimate, no exchange")
@@ -458,8 +516,8 @@ def setup_job(args, env, image=None):
     # (N > 1 strong: the owner table takes the local table's estimate-sized geometry, not the 1/G share
     # of -s -- the largest rank's distinct k-mers bound an owner's, about the job's 1/G, from above)
     tslots = slots
-    if share or est_table or (dist and world > 1 and strong and estimate):
-        tslots = estimate["local_slots"] if (share or est_table) else min(slots, estimate["local_slots"])
+    if share or (dist and world > 1 and strong and estimate):
+        tslots = estimate["local_slots"] if share else min(slots, estimate["local_slots"])
     cfg = ka.Config(k=k, mode=2, table_slots=tslots,
                     min_abundance=fx["min_abundance"] if fx else 2, batch_bytes=batch,
                     device=local, bf_enable=bool(args.unique), est_unique=args.unique)
@@ -472,8 +530,18 @@ def setup_job(args, env, image=None):
     else:
         counter = ka.KmerCounter(cfg)
 
+    est_log = []  # (estimate, slots, seconds) of every step that sized its table from the estimate
+
     def step():
         counter.reset()
+        if est_table:
+            # the whole job's distinct estimate (tokenizer + k_hll over every batch; the call waits
+            # for it) and the table sized from it, inside the step the line times
+            e0 = time.perf_counter()
+            est = counter.estimate_distinct_device(image.data_ptr(), chunks, ka.FMT_FASTA, stream.cuda_stream)
+            tab = min(windows_expected, int(1.1 * est) + (1 << 20))
+            counter.size_table(tab)
+            est_log.append((est, tab, time.perf_counter() - e0))
         if args.unique:  # Bloom pass, table sized 2 * new_in_second, counting pass behind the gate
             counter.bloom_device(image.data_ptr(), chunks, ka.FMT_FASTA, stream.cuda_stream)
             counter.bloom_finalize()
@@ -482,7 +550,8 @@ def setup_job(args, env, image=None):
 
     return argparse.Namespace(counter=counter, image=image, chunks=chunks, step=step, N=N, first=first, nbytes=nbytes,
                               slots=slots, strong=strong, windows_expected=windows_expected, tbl=tbl,
-                              workload=workload, fixture=fx, stream=stream, estimate=estimate, share=share)
+                              workload=workload, fixture=fx, stream=stream, estimate=estimate, share=share,
+                              est_log=est_log)
 
 
 def parity_record(job, k, dist=None):
@@ -734,12 +803,22 @@ def run_workload(args, env, image=None):
         out["xgmi"] = xgmi
     if job.estimate:
         out["local_table"] = job.estimate
+    if job.est_log:
+        timed = job.est_log[-args.steps:]
+        e, tab, _ = timed[-1]
+        out["local_table"] = {"distinct_estimate": int(e), "local_slots": tab, "in_timed_step": True,
+                              "ms": round(sum(x[2] for x in timed) / len(timed) * 1e3, 2),
+                              "method": "HyperLogLog, 2^14 registers (~0.8 % std. error) over the whole image "
+                                        "(kc_estimate_distinct_device), then kc_size_table(1.1 x estimate), in "
+                                        "every timed step (ms = its mean share of ms_per_step)"}
     if job.share:
         out["config"]["parallelism"] = f"one rank's share of hash-prefix shard x{job.share} (no exchange)"
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not job.share:
         out["cpu_baseline"] = cpu_baseline(args)
-    if world == 1 and not dist and args.cli_fullsize and not job.share and args.config in ("C2", "C3"):
+    if world == 1 and not dist and args.cli_fullsize and not job.share and args.config in ("C2", "C3", "C4"):
         out["cli_fullsize"] = cli_fullsize(job, args)
+    if world == 1 and not dist and args.host_chunks and not job.share and args.config == "C2":
+        out["c_abi_host_chunks"] = host_chunks_record(job, args)
     return out, image
 
 
@@ -866,12 +945,18 @@ def main():
                     help="at N=1 with the default C2: also time this workload on the one GPU ('c4' record: the "
                          "whole C4 job, the N=1 point of the strong-scaling curve the N > 1 lines time; 'none' = "
                          "skip)")
+    ap.add_argument("--quaternary", default="C5",
+                    help="at N=1 with the default C2: also time this workload on the one GPU ('c5' record: the "
+                         "whole long-read C5 job; 'none' = skip)")
+    ap.add_argument("--tertiary-cpu-sample-bases", type=int, default=50_000_000)
     ap.add_argument("--multi-secondary", default="C2",
                     help="at N > 1 with the default C4: also time this weak-scaling workload ('none' = skip)")
     ap.add_argument("--no-verify", dest="verify", action="store_false",
                     help="skip the parity digest against the reference's output (tests/golden/fullsize.json)")
     ap.add_argument("--no-cli-fullsize", dest="cli_fullsize", action="store_false",
                     help="skip the drop-in CLI on the whole C2 / C3 workload (cli_fullsize record)")
+    ap.add_argument("--no-host-chunks", dest="host_chunks", action="store_false",
+                    help="skip the C-ABI host-chunk record (kc_count_chunk over the C2 job's chunks from host memory)")
     ap.add_argument("--no-writer", dest="writer", action="store_false",
                     help="skip writing the timed job's output with kc_write (timed, and digested with --verify)")
     ap.add_argument("--share", type=int, default=0,
@@ -942,8 +1027,11 @@ def main():
         if args.secondary != "none":
             extra.append((args.secondary, dict(cpu_sample_bases=args.secondary_cpu_sample_bases)))
         if args.tertiary != "none":
-            # (no CPU baseline or compact figure: the C3 record carries the k = 51 baseline)
-            extra.append((args.tertiary, dict(no_cpu_baseline=True, compact=False)))
+            # (C4 -- the north star's "150 bp reads at k=51" -- with its own CPU
+            # baseline, the reference on a sample at C4's 30x coverage; no compact figure)
+            extra.append((args.tertiary, dict(cpu_sample_bases=args.tertiary_cpu_sample_bases, compact=False)))
+        if args.quaternary != "none":
+            extra.append((args.quaternary, dict(no_cpu_baseline=True, compact=False)))
     elif world > 1 and args.config == "C4" and args.multi_secondary != "none":
         extra.append((args.multi_secondary, {}))
     for name, over in extra:

@@ -169,6 +169,21 @@ struct kc_ctx {
     uint32_t defer_n = 0;      // batches of the current group whose segments wait
     uint64_t defer_syms = 0;   // the group's segment geometry is sized for batches of this bound
     uint64_t defer_groups = 0; // level-3 passes the deferral ran (kc_stats)
+    // super-k-mer routing (kc_route_superkmers_device): the pass-4 batches' parameters and the
+    // device cursors [0, 64) words per owner, [64, 128) windows per owner, [128] overflow flag
+    unsigned long long* d_skm = nullptr;
+    uint32_t skm_shards = 0;
+    int skm_m = 0;
+    uint64_t* skm_pk = nullptr;
+    uint32_t* skm_bk = nullptr;
+    uint64_t skm_cap = 0;
+    // windows per symbol of the batches being planned (1: tokenized input, where every symbol can
+    // end a window; a received super-k-mer stream carries k symbols of context per run)
+    double win_density = 1.0;
+    // a counting pass failed after some of its batches were counted (a deferred group whose level 3
+    // never ran, a failed launch): the table no longer matches the windows counted, so every call
+    // that counts or reads the table fails until kc_reset
+    std::string broken;
 
     // profiling: event quadruples {start, after gather, after tokenize, after count}
     bool profiling = false;
@@ -203,6 +218,12 @@ struct kc_ctx {
     do {                                                   \
         hipError_t _e = (expr);                            \
         if (_e != hipSuccess) return (ctx)->hipfail(_e, #expr); \
+    } while (0)
+
+// the calls that count into or read the table refuse a job a failed pass left incomplete
+#define JOB_OK(ctx)                                                                            \
+    do {                                                                                       \
+        if (!(ctx)->broken.empty()) return (ctx)->fail(KC_ERR_STATE, (ctx)->broken + " (kc_reset first)"); \
     } while (0)
 
 // ------------------------------------------------------------------------------
@@ -432,10 +453,11 @@ static PartPlan part_plan(const kc_ctx* c, uint64_t syms, bool seg, const PartGe
     if (seg) {
         auto capacity = [](double e) { return ((uint64_t)std::ceil(e + 8.0 * std::sqrt(e) + 32.0) + 7) / 8 * 8; };
         const uint64_t t1 = (uint64_t)p1_tile_max(c->W);  // k_p1<..., OutSeg> rounds block ranges to its tile
-        const uint64_t per1 = ((syms + p.nblk1 - 1) / p.nblk1 + t1 - 1) / t1 * t1;  // windows per level-1 block
+        const uint64_t per1 = ((syms + p.nblk1 - 1) / p.nblk1 + t1 - 1) / t1 * t1;  // symbols per level-1 block
         const uint64_t nseg = (p.nblk1 + p.B2 - 1) / p.B2;                           // level-1 segments per p2 block
-        p.cap1 = capacity((double)per1 / g.F1);
-        p.cap2 = capacity((double)nseg * per1 / g.F1 / g.F2);
+        const double d = c->win_density;  // windows per symbol (1 for tokenized input)
+        p.cap1 = capacity((double)per1 * d / g.F1);
+        p.cap2 = capacity((double)nseg * per1 * d / g.F1 / g.F2);
         if (const char* v = std::getenv("KC_SEG_CAP")) p.cap1 = p.cap2 = std::max<uint64_t>(1, std::strtoull(v, 0, 10));
         // the segment walks index a virtual run with 32-bit offsets
         if (nseg * p.cap1 >= (1ULL << 31) || (uint64_t)p.B2 * p.cap2 * slots >= (1ULL << 31)) p.cap1 = p.cap2 = 0;
@@ -443,16 +465,17 @@ static PartPlan part_plan(const kc_ctx* c, uint64_t syms, bool seg, const PartGe
     // the skew list of a segmented batch: {key words, count} records of keys past a segment's
     // end and of repeated windows (Bloom pass: plain keys), an eighth of the windows before the
     // batch falls back to the exact layout; its exact pipeline runs through the key buffers
+    const uint64_t wins = c->win_density < 1.0 ? (uint64_t)((double)syms * c->win_density) + 1024 : syms;
     if (p.cap1) {
-        p.spill_cap = std::max<uint64_t>(1 << 16, syms / 8);
+        p.spill_cap = std::max<uint64_t>(1 << 16, wins / 8);
         if (const char* v = std::getenv("KC_SPILL_CAP")) p.spill_cap = std::strtoull(v, 0, 10);  // tests
     }
     p.spill_words = p.spill_cap * (g.IW + 1);
-    p.need1 = std::max(std::max<uint64_t>(syms, (uint64_t)g.F1 * p.nblk1 * p.cap1) * g.IW, p.spill_words);
+    p.need1 = std::max(std::max<uint64_t>(wins, (uint64_t)g.F1 * p.nblk1 * p.cap1) * g.IW, p.spill_words);
     // one batch's level 2 in W-word items; a deferred group's slots in level-2 records (the exact
     // pipeline of a batch's tail, which writes W-word items, runs after its group's level 3)
     const uint64_t l2 = slots > 1 && rec2 ? (g.R * p.B2 * p.cap2 * slots * rec2 + 7) / 8 : g.R * p.B2 * p.cap2 * g.IW;
-    p.need2 = std::max(std::max<uint64_t>(syms * g.IW, l2), p.spill_words);
+    p.need2 = std::max(std::max<uint64_t>(wins * g.IW, l2), p.spill_words);
     // (the levels' record loads are 12 or 16 bytes wide whatever the record: a last 8- or
     // 12-byte record's load reads past it)
     p.need1 += 2;
@@ -642,15 +665,27 @@ static int run_deferred(kc_ctx* c, const PackedView& sv, uint64_t syms, int mode
     return KC_OK;
 }
 
+// pre: a symbol stream already in HBM (a received super-k-mer stream, kc_count_packed_device) of
+// `used` symbols instead of chunks to tokenize (src, nchunks and fmt unused)
 static int run_batch(kc_ctx* c, const uint8_t* src, uint64_t used, uint64_t nchunks, int fmt, int pass, hipStream_t s,
                      hipEvent_t ev_start = nullptr, hipEvent_t ev_gather = nullptr, bool keep = false,
-                     bool host_gate = false) {
+                     bool host_gate = false, const PackedView* pre = nullptr) {
     const uint64_t ntiles = used / TILE;
-    if (ntiles == 0) return KC_OK;
+    if (!pre && ntiles == 0) return KC_OK;
+    if (pre && used == 0) return KC_OK;
     if (pass == 3) {  // the distinct-count sketch (kc_estimate_distinct_device): tokenize + k_hll
         HIPCHK(c, launch_tokenize(src, ntiles, c->d_chunks, (int)nchunks, fmt, c->d_tiles, c->d_touts, c->d_tblk,
                                   PackedView{c->d_pk, c->d_bk}, used + nchunks, c->d_ctr, s));
         HIPCHK(c, launch_hll(PackedView{c->d_pk, c->d_bk}, c->cfg.k, c->W, c->d_ctr, c->d_hll, s));
+        return KC_OK;
+    }
+    if (pass == 4) {  // super-k-mer routing (kc_route_superkmers_device): tokenize + k_skm_route
+        const PackedView v{c->d_pk, c->d_bk};
+        HIPCHK(c, launch_tokenize(src, ntiles, c->d_chunks, (int)nchunks, fmt, c->d_tiles, c->d_touts, c->d_tblk, v,
+                                  used + nchunks, c->d_ctr, s));
+        HIPCHK(c, launch_skm_route(v, c->d_ctr, used + nchunks, c->cfg.k, c->skm_m, c->skm_shards, c->skm_pk,
+                                   c->skm_bk, c->skm_cap, c->d_skm, c->d_skm + SKM_MAX_SHARDS,
+                                   c->d_skm + 2 * SKM_MAX_SHARDS, s));
         return KC_OK;
     }
     std::array<hipEvent_t, 4> ev{ev_start, ev_gather, nullptr, nullptr};
@@ -664,9 +699,16 @@ static int run_batch(kc_ctx* c, const uint8_t* src, uint64_t used, uint64_t nchu
         ev[2] = c->get_event();
         ev[3] = c->get_event();
     }
-    const PackedView sv{c->d_pk, c->d_bk};
-    HIPCHK(c, launch_tokenize(src, ntiles, c->d_chunks, (int)nchunks, fmt, c->d_tiles, c->d_touts, c->d_tblk, sv,
-                              used + nchunks, c->d_ctr, s));
+    const PackedView sv = pre ? *pre : PackedView{c->d_pk, c->d_bk};
+    if (pre) {  // (the stream's length where the tokenizer would have left it)
+        HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)&c->d_ctr->stream_len, (int)(uint32_t)used, 1, s));
+        HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)((uint32_t*)&c->d_ctr->stream_len + 1), (int)(uint32_t)(used >> 32),
+                                    1, s));
+        nchunks = 0;
+    } else {
+        HIPCHK(c, launch_tokenize(src, ntiles, c->d_chunks, (int)nchunks, fmt, c->d_tiles, c->d_touts, c->d_tblk, sv,
+                                  used + nchunks, c->d_ctr, s));
+    }
     if (c->profiling) HIPCHK(c, hipEventRecord(ev[2], s));
     TableView tv = table_view(c);
     BloomView bv{c->d_bloom, c->bf_bits ? c->bf_bits - 1 : 0, c->nh, c->nh_gate, c->bloom_blocked,
@@ -970,17 +1012,8 @@ static int count_reused(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, s
 // per region.  The pass then runs partitioned when one sweep of the table per group beats the
 // direct inserts (use_partitioned's rule with the table's bytes spread over the group), e.g. C5's
 // one-GPU job, whose table is too large for a sweep per batch.  KC_DEFER=0: off.
+static int plan_deferral_nb(kc_ctx* c, uint64_t nb, uint64_t syms);
 static int plan_deferral(kc_ctx* c, const kc_chunk* chunks, size_t n) {
-    // KC_DEFER: 0 = off, N = groups of at most N batches (tests)
-    const char* kd = std::getenv("KC_DEFER");
-    const uint64_t kmax = kd ? std::strtoull(kd, nullptr, 10) : ~0ULL;
-    if (kmax == 0 || !c->nbuckets || !c->seg_ok) {
-        if (debug_on()) std::fprintf(stderr, "deferred level 3: off (knob %d, table %d, segmented levels %d)\n",
-                                     kmax != 0, c->nbuckets != 0, (int)c->seg_ok);
-        return KC_OK;
-    }
-    const PathKnob pk = insert_path_knob();
-    if (pk == PathKnob::Direct || pk == PathKnob::Exact) return KC_OK;
     uint64_t nb = 0, syms = 0, used = 0, cnt = 0;
     for (size_t i = 0; i <= n; i++) {
         const bool end = i == n;
@@ -996,6 +1029,20 @@ static int plan_deferral(kc_ctx* c, const kc_chunk* chunks, size_t n) {
         used += need;
         cnt++;
     }
+    return plan_deferral_nb(c, nb, syms);
+}
+// (nb batches of at most syms symbols each)
+static int plan_deferral_nb(kc_ctx* c, uint64_t nb, uint64_t syms) {
+    // KC_DEFER: 0 = off, N = groups of at most N batches (tests)
+    const char* kd = std::getenv("KC_DEFER");
+    const uint64_t kmax = kd ? std::strtoull(kd, nullptr, 10) : ~0ULL;
+    if (kmax == 0 || !c->nbuckets || !c->seg_ok) {
+        if (debug_on()) std::fprintf(stderr, "deferred level 3: off (knob %d, table %d, segmented levels %d)\n",
+                                     kmax != 0, c->nbuckets != 0, (int)c->seg_ok);
+        return KC_OK;
+    }
+    const PathKnob pk = insert_path_knob();
+    if (pk == PathKnob::Direct || pk == PathKnob::Exact) return KC_OK;
     if (nb < 2) return KC_OK;
     const PartPlan p = part_plan(c, syms, true, table_geo(c), 0, 1);
     if (p.cap1 == 0) {
@@ -1030,6 +1077,19 @@ static int plan_deferral(kc_ctx* c, const kc_chunk* chunks, size_t n) {
     return KC_OK;
 }
 
+// Every exit of a pass (an error inside it included) ends its deferral; an error that leaves a
+// group's batches counted without their level 3 marks the job broken
+struct DeferEnd {
+    kc_ctx* c;
+    ~DeferEnd() {
+        if (c->defer_on && c->defer_n > 0 && c->broken.empty())
+            c->broken = "a counting pass failed with " + std::to_string(c->defer_n) +
+                        " batch(es) of a deferred group not inserted: " + c->err;
+        c->defer_on = c->defer_last = false;
+        c->defer_n = 0;
+    }
+};
+
 static int device_pass(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, size_t n, int fmt, int pass,
                        hipStream_t s) {
     if (fmt != KC_FMT_FASTA && fmt != KC_FMT_FASTQ && fmt != KC_FMT_PLAIN) return c->fail(KC_ERR_ARG, "unknown format");
@@ -1041,17 +1101,21 @@ static int device_pass(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, si
     }
     std::vector<ChunkDesc> batch;
     uint64_t used = 0;
-    // one staging batch holds the whole image?
+    // one staging batch holds the whole image?  (every chunk is checked before any is counted: a
+    // pass either fails before its first batch or runs to its end)
     bool single = false;
     {
         uint64_t tot = 0, cnt = 0;
         for (size_t i = 0; i < n; i++)
             if (chunks[i].len) {
+                if (round_up(chunks[i].len, TILE) > c->batch_bytes)
+                    return c->fail(KC_ERR_ARG, "chunk larger than the staging batch");
                 tot += round_up(chunks[i].len, TILE);
                 cnt++;
             }
         single = cnt > 0 && tot <= c->batch_bytes && cnt <= c->max_chunks;
     }
+    DeferEnd defer_end{c};
     // level-1 reuse: the Bloom pass keeps its level-1 output if it is the job's only batch
     const bool keep = pass == 1 && c->bloom_batches == 0 && reuse_enabled() && single;
     // a counting pass of several batches defers level 3 (kc_ctx defer_*) when the segmented levels
@@ -1071,7 +1135,7 @@ static int device_pass(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, si
                                  hipMemcpyHostToDevice, s));
         HIPCHK(c, hipEventRecord(c->h_free[c->cur], s));
         hipEvent_t e0 = nullptr, e1 = nullptr;
-        const bool timed = c->profiling && pass != 3;  // (the sketch pass is not a timed batch)
+        const bool timed = c->profiling && pass != 3 && pass != 4;  // (the sketch / routing passes are not timed)
         if (timed) {
             e0 = c->get_event();
             e1 = c->get_event();
@@ -1115,7 +1179,6 @@ static int device_pass(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, si
     for (size_t i = 0; i < n; i++) {
         const uint64_t need = round_up(chunks[i].len, TILE);
         if (chunks[i].len == 0) continue;
-        if (need > c->batch_bytes) return c->fail(KC_ERR_ARG, "chunk larger than the staging batch");
         if (used + need > c->batch_bytes || batch.size() + 1 > c->max_chunks) {
             rc = launch();
             if (rc) return rc;
@@ -1132,7 +1195,6 @@ static int device_pass(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, si
     }
     last = true;
     rc = launch();
-    c->defer_on = false;
     if (rc) return rc;
     if (s != c->stream) {
         HIPCHK(c, hipEventRecord(c->xev, s));
@@ -1300,6 +1362,7 @@ void kc_destroy(kc_ctx* c) {
     hipFree(c->d_ctr);
     hipFree(c->d_sum);
     hipFree(c->d_hll);
+    hipFree(c->d_skm);
     hipFree(c->d_cwords);
     hipFree(c->d_csecond);
     hipFree(c->d_cstat);
@@ -1340,12 +1403,14 @@ void kc_destroy(kc_ctx* c) {
 
 int kc_bloom_chunk(kc_ctx* c, const uint8_t* buf, size_t len, int fmt, int bh) {
     if (!c) return KC_ERR_ARG;
+    JOB_OK(c);
     if (!c->cfg.bf_enable || c->bloom_final) return c->fail(KC_ERR_STATE, "bloom pass not active");
     return add_host_chunk(c, buf, len, fmt, bh, 1);
 }
 
 int kc_bloom_device(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, size_t n, int fmt, void* s) {
     if (!c || (!img && n) || (!chunks && n)) return KC_ERR_ARG;
+    JOB_OK(c);
     if (!c->cfg.bf_enable || c->bloom_final) return c->fail(KC_ERR_STATE, "bloom pass not active");
     return device_pass(c, img, chunks, n, fmt, 1, pick_stream(c, s));
 }
@@ -1411,12 +1476,14 @@ int kc_bloom_finalize(kc_ctx* c, uint64_t* new_in_second) {
 
 int kc_count_chunk(kc_ctx* c, const uint8_t* buf, size_t len, int fmt, int bh) {
     if (!c) return KC_ERR_ARG;
+    JOB_OK(c);
     if (!c->nbuckets) return c->fail(KC_ERR_STATE, "kc_bloom_finalize must precede the counting pass");
     return add_host_chunk(c, buf, len, fmt, bh, 0);
 }
 
 int kc_count_device(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, size_t n, int fmt, void* s) {
     if (!c || (!img && n) || (!chunks && n)) return KC_ERR_ARG;
+    JOB_OK(c);
     if (!c->nbuckets) return c->fail(KC_ERR_STATE, "kc_bloom_finalize must precede the counting pass");
     if (c->reuse_ok) {  // one chance: the first counting pass after the Bloom pass
         c->reuse_ok = false;
@@ -1452,6 +1519,140 @@ int kc_estimate_distinct_device(kc_ctx* c, const uint8_t* img, const kc_chunk* c
     if (e <= 2.5 * m && zeros) e = m * std::log(m / zeros);
     *estimate = e;
     return KC_OK;
+}
+
+int kc_size_table(kc_ctx* c, uint64_t slots) {
+    if (!c) return KC_ERR_ARG;
+    JOB_OK(c);
+    if (c->cfg.bf_enable) return c->fail(KC_ERR_STATE, "a Bloom job sizes its table from new_in_second");
+    if (!c->table_fresh || c->n_chunks) return c->fail(KC_ERR_STATE, "kc_size_table: the job has counted already");
+    int rc = flush_host(c);
+    if (rc) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipDeviceSynchronize());  // (the previous job's passes may still read the table)
+    const uint64_t phys = slots ? slots : c->cfg.table_slots;
+    // a table well below its allocation gives the memory back (the deferred level 3 sizes its
+    // groups from free HBM); the same size job after job keeps its allocation
+    const uint64_t want = std::max<uint64_t>(phys, 64) + std::max<uint64_t>(phys, 64) / 4;
+    const uint64_t bytes = (want + c->S - 1) / c->S * (BUCKET_WORDS * 8) + (uint64_t)BPR * BUCKET_WORDS * 8;
+    if (c->d_table && bytes * 4 < c->table_cap_bytes * 3) {
+        hipFree(c->d_table);
+        c->d_table = nullptr;
+        c->table_cap_bytes = 0;
+    }
+    return alloc_table(c, c->cfg.table_slots, 0, phys);  // (ensure_part re-plans the levels per batch)
+}
+
+int kc_route_superkmers_device(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, size_t n, int fmt,
+                               uint32_t nshards, int m, uint64_t* dev_pk, uint32_t* dev_bk, uint64_t cap_words,
+                               uint64_t* words, uint64_t* windows, void* sp) {
+    if (!c || !words || nshards == 0 || nshards > SKM_MAX_SHARDS || (!img && n) || (!chunks && n)) return KC_ERR_ARG;
+    if (cap_words && (!dev_pk || !dev_bk)) return KC_ERR_ARG;
+    JOB_OK(c);
+    const int mm = m ? m : std::min(SKM_DEFAULT_M, c->cfg.k);
+    if (mm < 1 || mm > 32 || mm > c->cfg.k) return c->fail(KC_ERR_ARG, "minimizer length must be in 1..min(32, k)");
+    hipStream_t s = pick_stream(c, sp);
+    const size_t nw = 2 * SKM_MAX_SHARDS + 16;
+    if (!c->d_skm && hipMalloc(&c->d_skm, nw * 8) != hipSuccess)
+        return c->fail(KC_ERR_NOMEM, "super-k-mer cursor allocation failed");
+    HIPCHK(c, hipMemsetAsync(c->d_skm, 0, nw * 8, s));
+    c->skm_shards = nshards;
+    c->skm_m = mm;
+    c->skm_pk = dev_pk;
+    c->skm_bk = dev_bk;
+    c->skm_cap = cap_words;
+    int rc = device_pass(c, img, chunks, n, fmt, 4, s);
+    if (rc) return rc;
+    std::vector<unsigned long long> h(nw);
+    HIPCHK(c, hipMemcpyAsync(h.data(), c->d_skm, nw * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    uint64_t worst = 0;
+    for (uint32_t o = 0; o < nshards; o++) {
+        words[o] = h[o];
+        if (windows) windows[o] = h[SKM_MAX_SHARDS + o];
+        worst = std::max<uint64_t>(worst, h[o]);
+    }
+    if (cap_words && h[2 * SKM_MAX_SHARDS])
+        return c->fail(KC_ERR_NOMEM, "super-k-mer buffer too small: " + std::to_string(worst) +
+                                         " words for the largest owner, capacity " + std::to_string(cap_words));
+    return KC_OK;
+}
+
+// A symbol stream in HBM (a received super-k-mer stream) through the pass's levels in batches of
+// about a staging batch's windows, cut at words whose first symbol is a break (no window spans a
+// cut), with the deferred level 3 of a counting pass over several batches.
+static int packed_pass(kc_ctx* c, const uint64_t* pk, const uint32_t* bk, uint64_t n_words, uint64_t windows, int pass,
+                       hipStream_t s) {
+    int rc = flush_host(c);  // keep order with staged host chunks
+    if (rc) return rc;
+    if (s != c->stream) {
+        HIPCHK(c, hipEventRecord(c->xev, c->stream));
+        HIPCHK(c, hipStreamWaitEvent(s, c->xev, 0));
+    }
+    if (n_words == 0) return KC_OK;
+    const double nsym = (double)n_words * 32.0;
+    const double dens = windows ? std::min(1.0, 1.15 * (double)windows / nsym + 1e-3) : 1.0;
+    const uint64_t lim = std::max<uint64_t>(1024, (uint64_t)((double)c->batch_bytes / dens) / 32);
+    std::vector<uint64_t> cuts{0};
+    std::vector<uint32_t> probe(4096);
+    while (n_words - cuts.back() > lim) {
+        uint64_t w = cuts.back() + lim;
+        bool found = false;
+        while (!found && w < n_words) {
+            const uint64_t m = std::min<uint64_t>(probe.size(), n_words - w);
+            HIPCHK(c, hipMemcpyAsync(probe.data(), bk + w, m * 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipStreamSynchronize(s));
+            uint64_t i = 0;
+            while (i < m && !(probe[i] >> 31)) i++;
+            w += i;
+            found = i < m;
+        }
+        if (!found) break;
+        cuts.push_back(w);
+    }
+    cuts.push_back(n_words);
+    const uint64_t nb = cuts.size() - 1;
+    uint64_t maxs = 0;
+    for (uint64_t i = 0; i < nb; i++) maxs = std::max<uint64_t>(maxs, (cuts[i + 1] - cuts[i]) * 32);
+    struct Density {
+        kc_ctx* c;
+        double d;
+        ~Density() { c->win_density = d; }
+    } restore{c, c->win_density};
+    c->win_density = dens;
+    DeferEnd defer_end{c};
+    c->defer_on = false;
+    c->defer_n = 0;
+    if (pass == 0 && nb >= 2 && (rc = plan_deferral_nb(c, nb, maxs))) return rc;
+    for (uint64_t i = 0; i < nb; i++) {
+        c->defer_last = i + 1 == nb;
+        const PackedView v{const_cast<uint64_t*>(pk) + cuts[i], const_cast<uint32_t*>(bk) + cuts[i]};
+        if ((rc = run_batch(c, nullptr, (cuts[i + 1] - cuts[i]) * 32, 0, 0, pass, s, nullptr, nullptr, false, nb == 1,
+                            &v)))
+            return rc;
+    }
+    if (s != c->stream) {
+        HIPCHK(c, hipEventRecord(c->xev, s));
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->xev, 0));
+    }
+    return KC_OK;
+}
+
+int kc_count_packed_device(kc_ctx* c, const uint64_t* pk, const uint32_t* bk, uint64_t n_words, uint64_t windows,
+                           void* sp) {
+    if (!c || (n_words && (!pk || !bk))) return KC_ERR_ARG;
+    JOB_OK(c);
+    if (!c->nbuckets) return c->fail(KC_ERR_STATE, "kc_bloom_finalize must precede the counting pass");
+    c->reuse_ok = false;  // (the Bloom pass's kept partitions are an image's)
+    return packed_pass(c, pk, bk, n_words, windows, 0, pick_stream(c, sp));
+}
+
+int kc_bloom_packed_device(kc_ctx* c, const uint64_t* pk, const uint32_t* bk, uint64_t n_words, uint64_t windows,
+                           void* sp) {
+    if (!c || (n_words && (!pk || !bk))) return KC_ERR_ARG;
+    JOB_OK(c);
+    if (!c->cfg.bf_enable || c->bloom_final) return c->fail(KC_ERR_STATE, "bloom pass not active");
+    return packed_pass(c, pk, bk, n_words, windows, 1, pick_stream(c, sp));
 }
 
 int kc_route_device(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, size_t n, int fmt, uint32_t nshards,
@@ -1521,6 +1722,7 @@ int kc_route_hint(kc_ctx* c, uint32_t nshards) {
 int kc_route_table_device(kc_ctx* c, uint32_t nshards, uint64_t* dev_out, uint64_t out_capacity, uint64_t* counts,
                           void* sp) {
     if (!c || !counts || nshards == 0 || nshards > 64) return KC_ERR_ARG;
+    JOB_OK(c);
     if (!c->nbuckets) return c->fail(KC_ERR_STATE, "no table");
     hipStream_t s = pick_stream(c, sp);
     int rc = flush_host(c);
@@ -1792,6 +1994,7 @@ int kc_insert_keys_device(kc_ctx* c, const uint64_t* keys, uint64_t n, void* sp)
 // the readers of the table (finish, dump, write, compact, ...): the staged work done and a
 // deferred reset carried out first
 static int sync_for_read(kc_ctx* c) {
+    JOB_OK(c);
     int rc = flush_host(c);
     if (rc) return rc;
     rc = materialize_zero(c, c->stream);  // a deferred reset is due before anyone reads the table
@@ -1811,6 +2014,7 @@ int kc_sync(kc_ctx* c) {
 }
 
 int kc_finish(kc_ctx* c, kc_stats* st) {
+    if (!c) return KC_ERR_ARG;
     int rc = sync_for_read(c);
     if (rc) return rc;
     DevCounters h;
@@ -1943,6 +2147,8 @@ int kc_reset(kc_ctx* c) {
     c->route_counts_kept = 0;
     c->defer_groups = 0;
     c->defer_n = 0;
+    c->defer_on = c->defer_last = false;
+    c->broken.clear();
     return KC_OK;
 }
 

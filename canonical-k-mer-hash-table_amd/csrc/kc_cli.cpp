@@ -52,8 +52,11 @@ struct Args {
     std::string gunzip_to;  // test hook: write the decompressed input there and exit (no GPU)
     // extensions, not in --help: --host-chunks stages host chunks instead of one
     // device image; --no-warmup skips the untimed warm-up pass; --readers N upload threads; --phases
-    // prints the counting pass's phase times on stderr
-    bool host_chunks = false, no_warmup = false, phases = false;
+    // prints the counting pass's phase times on stderr; --digest-only prints the output's digest
+    // (kc_output_digest) instead of writing it; --table-sizing auto|s|estimate: the device table from
+    // -s or from the input's distinct estimate (auto: the estimate when the -s table passes 16 GiB)
+    bool host_chunks = false, no_warmup = false, phases = false, digest_only = false;
+    int table_sizing = 0;  // --table-sizing auto (0) | s (1) | estimate (2)
     unsigned readers = 1;
 };
 
@@ -198,6 +201,7 @@ int parse(int argc, char** argv, Args* a) {
         if (o == "--host-chunks") { a->host_chunks = true; continue; }
         if (o == "--no-warmup") { a->no_warmup = true; continue; }
         if (o == "--phases") { a->phases = true; continue; }
+        if (o == "--digest-only") { a->digest_only = true; continue; }
         if (o.size() > 1 && o[0] == '-' && !(o.size() > 1 && std::isdigit((unsigned char)o[1]))) {
             std::string v;
             if (!next(&v)) return cli_error(kRequired, o + " requires an argument");
@@ -236,6 +240,11 @@ int parse(int argc, char** argv, Args* a) {
             } else if (o == "--device") {
                 if (!parse_int(v, &si) || si < 0) return cli_error(kConversion, "Could not convert: " + o + " = " + v);
                 a->device = (int)si;
+            } else if (o == "--table-sizing") {
+                if (v == "auto") a->table_sizing = 0;
+                else if (v == "s") a->table_sizing = 1;
+                else if (v == "estimate") a->table_sizing = 2;
+                else return cli_error(kValidation, o + ": Value " + v + " not in {auto, s, estimate}");
             } else if (o == "--readers") {
                 if (!parse_int(v, &si) || si < 1 || si > 16) return cli_error(kConversion, "Could not convert: " + o + " = " + v);
                 a->readers = (unsigned)si;
@@ -443,7 +452,11 @@ int main(int argc, char** argv) {
     }
     const std::string ext = ext_of(ext_path);
 
-    // ---- load the image (mmap, or a full gunzip)
+    // ---- load the image (mmap, or a full gunzip).  The reference's IO thread reads (and inflates)
+    // the file and cuts its chunks inside its timers (parallel_parser.hpp:1230-1299,1544-1550): the
+    // time of both is added to the first timer line below
+    using clk = std::chrono::high_resolution_clock;
+    const auto t_in0 = clk::now();
     const uint8_t* image = nullptr;
     uint64_t isize = 0;
     std::vector<uint8_t> gzbuf;
@@ -533,12 +546,18 @@ int main(int argc, char** argv) {
         return 1;
     }
 
+    const auto t_in1 = clk::now();  // (the input's bytes are in host memory: mapped, or inflated)
     kc_chunk* chunks = nullptr;
     uint64_t nch = 0;
     if (kc_plan_chunks(image, isize, (int)a.k, 0, fmt, &chunks, &nch) != KC_OK) {
         std::cerr << "chunk planning failed" << std::endl;
         return 1;
     }
+    const auto t_in2 = clk::now();
+    // (an uncompressed file is mapped lazily: its bytes are read by the timed upload, so only the
+    // planning counts; a gzip file is inflated here, which the reference does inside its timer)
+    const long long prep_us =
+        (long long)std::chrono::duration_cast<std::chrono::microseconds>(t_in2 - (gz ? t_in0 : t_in1)).count();
 
     kc_config cfg;
     std::memset(&cfg, 0, sizeof(cfg));
@@ -566,7 +585,6 @@ int main(int argc, char** argv) {
         kc_destroy(ctx);
         std::exit(1);
     };
-    using clk = std::chrono::high_resolution_clock;
     // The image goes to HBM once (--host-chunks: stage host chunks instead): both passes
     // then read it in place, and a Bloom job counts from the Bloom pass's partitions
     // (kc_api.h, partition reuse).  Its read is timed with the pass that needs it first,
@@ -637,7 +655,8 @@ int main(int argc, char** argv) {
         auto t1 = clk::now();
         std::cout << "New k-mers in second bloom filter " << nis << "\n";
         std::cout << "Time used to bloom filter k-mers: "
-                  << std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0).count() << " microseconds\n";
+                  << std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0).count() + prep_us
+                  << " microseconds\n";
     }
     std::cout << "Starting " << (a.mode == 0 ? "atomic flag basic" : "atomic variable pointer") << " hash table\n";
     const bool dbg = a.phases;  // phase times on stderr
@@ -645,6 +664,26 @@ int main(int argc, char** argv) {
         return (long long)std::chrono::duration_cast<std::chrono::microseconds>(y - x).count();
     };
     auto t0 = clk::now();
+    // A -s whose table would take a large share of HBM (C4's -s 2.6e9 asks for 83 GB at 25 %
+    // headroom; its 1.0 G distinct k-mers need 35 GB) is sized from the whole input's distinct
+    // estimate instead (kc_estimate_distinct_device + kc_size_table, inside the timer; -s stays
+    // the reference capacity for --strict-capacity), as bench.py's C4 / C5 lines are.  A table
+    // that still fills up (an estimate far below the truth) is counted again at -s.
+    const int kw = (int)(a.k / 32 + 1);
+    const double s_table_bytes = 1.25 * (double)a.slots / (double)(16 / (kw + 1)) * 128.0;
+    bool est_sized = false;
+    const bool want_est = a.table_sizing == 2 || (a.table_sizing == 0 && s_table_bytes > (double)(16ull << 30) && nch > 1);
+    if (staged && !loaded && !a.use_bf && want_est) {
+        load();
+        double est = 0;
+        if (d_img && kc_estimate_distinct_device(ctx, d_img, chunks, nch, fmt, nullptr, &est) == KC_OK) {
+            const double want = 1.1 * est + (double)(1 << 20);
+            if ((want < 0.8 * (double)a.slots || a.table_sizing == 2) && kc_size_table(ctx, (uint64_t)want) == KC_OK) {
+                est_sized = true;
+                if (dbg) std::cerr << "cli: table sized from the distinct estimate " << (uint64_t)est << "\n";
+            }
+        }
+    }
     // A large -s job counts the image's first half while the second half uploads (two counting
     // passes into one table: the second sweeps it once more, ~1.5 ms for C2's, against ~8 ms of
     // the upload hidden); a Bloom job's counting pass follows the Bloom pass, which read it all
@@ -688,7 +727,16 @@ int main(int argc, char** argv) {
     }
     }
     kc_stats stt;
-    if (kc_finish(ctx, &stt) != KC_OK) {
+    int frc = kc_finish(ctx, &stt);
+    if (frc == KC_ERR_TABLE_FULL && est_sized) {  // the estimate was too low: the -s table, counted again
+        std::cerr << "cli: the estimate-sized table filled up; counting again into the -s table\n";
+        if (kc_reset(ctx) != KC_OK || kc_size_table(ctx, 0) != KC_OK ||
+            kc_count_device(ctx, d_img, chunks, nch, fmt, nullptr) != KC_OK)
+            die("counting pass");
+        est_sized = false;
+        frc = kc_finish(ctx, &stt);
+    }
+    if (frc != KC_OK) {
         std::cout << "Hash table is full... Cannot handle this yet\n";
         die("counting pass");
     }
@@ -697,13 +745,28 @@ int main(int argc, char** argv) {
     // (functions_math.cpp:90); the device table keeps 25 % headroom over it
     const uint64_t ref_slots = kc_table_size_reference(a.use_bf ? 2 * bf_new_in_second : a.slots);
     std::cout << "Hash table size is: " << ref_slots << "\n";
-    if (a.min_abundance > 0) {
+    if (a.min_abundance > 0 && a.digest_only) {
+        // --digest-only (extension): the output's order-independent digest (kc_output_digest: lines,
+        // sum of T(c), sum and XOR of XXH64 per line) instead of the file -- C4's 60 GB of text
+        kc_digest dg;
+        if (kc_output_digest(ctx, &dg) != KC_OK) die("output digest");
+        char buf[200];
+        std::snprintf(buf, sizeof buf, "{\"lines\": %llu, \"count_sum\": %llu, \"hash_sum\": \"%016llx\", \"hash_xor\": \"%016llx\"}",
+                      (unsigned long long)dg.lines, (unsigned long long)dg.count_sum, (unsigned long long)dg.hash_sum,
+                      (unsigned long long)dg.hash_xor);
+        std::cout << "Output digest: " << buf << "\n";
+    } else if (a.min_abundance > 0) {
         std::cout << "Start writing k-mers in a file\n";
         if (kc_write(ctx, a.output.c_str()) != KC_OK) die("writing k-mers");
     }
     auto t2 = clk::now();
-    std::cout << "Time used to build hash table: " << std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0).count()
+    std::cout << "Time used to build hash table: "
+              << std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0).count() + (a.use_bf ? 0 : prep_us)
               << " microseconds\n";
+    std::cout << "Input read and chunked in " << prep_us << " microseconds (included in the first timer line)\n";
+    if (est_sized)
+        std::cout << "Device table sized from the distinct estimate (-s " << a.slots
+                  << " stays the reference capacity)\n";
     std::cout << "Time used to write k-mers in a file: "
               << std::chrono::duration_cast<std::chrono::microseconds>(t2 - t1).count() << " microseconds\n";
     std::cout << "Processed k-mers: " << stt.windows << " (inserted " << stt.inserted << ")\n";

@@ -2589,16 +2589,21 @@ template <int W, bool SEG, bool CNT = false, bool GATE = false>
 static hipError_t launch_p3(TableView t, DevCounters* ctr, PartBufs pb, const unsigned long long* gate, int fresh,
                             hipStream_t s, BloomView bf = BloomView{}) {
     size_t sm3 = (size_t)BPR * BUCKET_WORDS * 8 + (size_t)BPR * 8;
-    if (GATE) {
-        // the filter-2 slice goes to LDS if two workgroups still fit a CU (80 KiB each)
-        const uint64_t maxb = bf.nblocks / t.R + 2;
-        const size_t room = 80 * 1024 - sm3 - 1024;  // (static LDS: segment prefix, block sums)
-        bf.slice_blocks = maxb * 32 <= room ? (uint32_t)maxb : 0;
-        sm3 += (size_t)bf.slice_blocks * 32;
-    }
     auto p3 = k_p3<W, SEG, CNT, GATE>;
     if constexpr (W == 1 && SEG && !CNT)
         if (pb.rec6) p3 = k_p3<1, true, false, GATE, true>;
+    if (GATE) {
+        // the filter-2 slice goes to LDS if two workgroups still fit a CU (80 KiB each) beside the
+        // kernel's own static LDS (segment prefixes, block sums: its real size)
+        hipFuncAttributes fa{};
+        size_t stat = 2048;
+        if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(p3)) == hipSuccess) stat = fa.sharedSizeBytes;
+        const uint64_t maxb = bf.nblocks / t.R + 2;
+        const size_t used = sm3 + stat;
+        const size_t room = used < 80 * 1024 ? 80 * 1024 - used : 0;
+        bf.slice_blocks = maxb * 32 <= room ? (uint32_t)maxb : 0;
+        sm3 += (size_t)bf.slice_blocks * 32;
+    }
     if (SEG && pb.B2 > MAX_SEG_GROUP) return hipErrorInvalidValue;
     hipError_t e = set_smem(p3, sm3);
     if (e != hipSuccess) return e;
@@ -3174,47 +3179,78 @@ hipError_t WOps<W>::text_digest(TableView t, int count_mode, uint64_t a, int k, 
 
 // --------------------------------------------------------------------------------
 // k_hll<W>: HyperLogLog registers of a batch's distinct canonical k-mers, the estimate the
-// host sizes tables from (kc_estimate_distinct_device; the reference takes -s from its user,
-// main.cpp:134-154).  2^HLL_P registers in LDS: register = the top HLL_P bits of the table
-// key's word 0 (a bijective mix of the key; for W >= 2 of its last word and a hash of the
-// others), value = 1 + the leading zeros of its other bits; merged into the context's
-// registers with atomicMax.  Grid-stride over the batch's tiles, one tile per round.
-// 1024-thread workgroups: the 64 KiB of registers allow two workgroups per CU, and the
-// windows' symbol loads want the 8 waves per SIMD that two 256-thread ones left at 2.
+// host sizes tables from (kc_estimate_distinct_device + kc_size_table; the reference takes -s
+// from its user, main.cpp:134-154).  2^HLL_P registers in LDS: register = the top HLL_P bits of
+// the table key's word 0 (a bijective mix of the key; for W >= 2 of its last word and a hash of
+// the others), value = 1 + the leading zeros of its other bits; merged into the context's
+// registers with atomicMax.  Each workgroup takes one contiguous range of the stream and reads
+// its tiles' packed words from a double-buffered LDS stage (as k_p1): the next tile's words are
+// loaded while this tile's windows are hashed, so no window waits for HBM (round 6: the
+// grid-stride form read every run's words from HBM with dependent loads, 5.2 ms per C4 batch).
+// 1024-thread workgroups: the 64 KiB of registers allow two workgroups per CU.
 // --------------------------------------------------------------------------------
 constexpr int HLL_T = 1024;
+template <int W>
+constexpr int hll_stage_words() { return HLL_T * run_w<W>() / 32 + W + 3; }
+template <int W>
+constexpr size_t hll_smem() { return (size_t)HLL_M * 4 + (size_t)hll_stage_words<W>() * 24; }
 template <int W>
 __global__ __launch_bounds__(HLL_T) void k_hll(PackedView sv, int k, const DevCounters* __restrict__ ctr,
                                                uint32_t* __restrict__ regs, uint64_t pow5_k, uint64_t pow5_km1) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint32_t* r = reinterpret_cast<uint32_t*>(smem);
-    for (uint32_t i = threadIdx.x; i < HLL_M; i += HLL_T) r[i] = 0;
-    __syncthreads();
-    constexpr int RUNW = run_w<W>(), TW = HLL_T * RUNW;
+    constexpr int RUNW = run_w<W>(), TW = HLL_T * RUNW, SW = hll_stage_words<W>();
+    static_assert(SW <= HLL_T, "one stage word per thread");
+    uint64_t* st_pk = reinterpret_cast<uint64_t*>(smem + (size_t)HLL_M * 4);
+    uint32_t* st_bk = reinterpret_cast<uint32_t*>(st_pk + 2 * SW);
+    const int tid = threadIdx.x;
+    for (uint32_t i = tid; i < HLL_M; i += HLL_T) r[i] = 0;
     const uint64_t M = ctr->stream_len;
+    const uint64_t per = ((M + gridDim.x - 1) / gridDim.x + TW - 1) / TW * TW;
+    const uint64_t lo = min(M, (uint64_t)blockIdx.x * per), hi = min(M, lo + per);
+    const uint64_t wlim = M ? ((M - 1) >> 5) + 1 : 0;  // the last word run_windows may read
+    // tile t0 reads words (t0 >> 5) - W - 1 .. (t0 + TW) >> 5 (+1) of the stream (run_windows)
+    auto stage_word = [&](uint64_t ts, int i, uint64_t& pw, uint32_t& bw) {
+        const int64_t w = (int64_t)(ts >> 5) - (W + 1) + i;
+        const bool in = w >= 0 && (uint64_t)w <= wlim;
+        pw = in ? sv.pk[w] : 0;
+        bw = in ? sv.bk[w] : 0;
+    };
+    if (lo < hi && tid < SW) stage_word(lo, tid, st_pk[tid], st_bk[tid]);
+    __syncthreads();
     const RollConst rk = make_roll<W>(k, pow5_k, pow5_km1);
-    for (uint64_t t0 = (uint64_t)blockIdx.x * TW; t0 < M; t0 += (uint64_t)gridDim.x * TW) {
-        const uint64_t t1 = min(t0 + TW, M), r0 = t0 + (uint64_t)threadIdx.x * RUNW;
+    int par = 0;
+    for (uint64_t t0 = lo; t0 < hi; t0 += TW) {
+        const uint64_t t1 = min(t0 + TW, hi), r0 = t0 + (uint64_t)tid * RUNW;
+        const bool nxt = t0 + TW < hi && tid < SW;
+        uint64_t npk = 0;
+        uint32_t nbk = 0;
+        if (nxt) stage_word(t0 + TW, tid, npk, nbk);  // in flight while this tile is hashed
         if (r0 < t1)
-            run_windows<W, RUNW>(sv, r0, t1, rk,
-                                 [&](int, bool valid, const uint64_t (&fwd)[W], const uint64_t (&rc)[W]) {
-                if (!valid) return;
+            run_windows_src<W, RUNW>(PkStage{st_pk + par * SW, st_bk + par * SW, (int64_t)(t0 >> 5) - (W + 1)}, r0,
+                                     t1, rk, [&](int, bool valid, const uint64_t (&fwd)[W], const uint64_t (&rc)[W]) {
                 uint64_t key[W], tk[W];
                 canonical<W>(fwd, rc, key);
                 to_tkey<W>(key, tk);
                 const uint32_t j = (uint32_t)(tk[0] >> (64 - HLL_P));
                 const uint64_t rest = (tk[0] << HLL_P) | (1ULL << (HLL_P - 1));  // (<= 64 - HLL_P zeros)
-                atomicMax(&r[j], (uint32_t)__builtin_clzll(rest) + 1);
+                // (no branch: an invalid window merges 0, which changes nothing)
+                atomicMax(&r[j], valid ? (uint32_t)__builtin_clzll(rest) + 1 : 0u);
             });
+        if (nxt) {
+            st_pk[(par ^ 1) * SW + tid] = npk;
+            st_bk[(par ^ 1) * SW + tid] = nbk;
+        }
+        __syncthreads();
+        par ^= 1;
     }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < HLL_M; i += HLL_T)
+    for (uint32_t i = tid; i < HLL_M; i += HLL_T)
         if (r[i]) atomicMax(&regs[i], r[i]);
 }
 
 template <int W>
 hipError_t WOps<W>::hll(PackedView sym, int k, DevCounters* ctr, uint32_t* regs, hipStream_t s) {
-    const size_t sm = (size_t)HLL_M * 4;
+    const size_t sm = hll_smem<W>();
     hipError_t e = set_smem(k_hll<W>, sm);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_hll<W>, dim3(512), dim3(HLL_T), sm, s, sym, k, ctr, regs, pow5_mod54(k),

@@ -307,6 +307,15 @@ hipError_t launch_insert_counts_runs(const uint64_t* rec, const uint64_t* gstart
 constexpr int HLL_P = 14;
 constexpr uint32_t HLL_M = 1u << HLL_P;
 hipError_t launch_hll(PackedView sym, int k, int W, DevCounters* ctr, uint32_t* regs, hipStream_t s);
+// Super-k-mer routing of a tokenized batch to nshards owners by canonical minimizer (kc_skm.hip):
+// per owner a packed symbol stream (out_pk / out_bk regions of cap words), cursor[] = words used,
+// wins[] = windows routed, *ovf = 1 if a region overflowed
+constexpr uint32_t SKM_MAX_SHARDS = 64;
+constexpr int SKM_DEFAULT_M = 15;  // minimizer length (odd: no palindromic m-mers); min(15, k)
+constexpr uint64_t SKM_SEED = 0x5851F42D4C957F2DULL;  // the m-mer order h(x) = fmix64(x ^ SKM_SEED) >> 32
+hipError_t launch_skm_route(PackedView sv, const DevCounters* ctr, uint64_t sym_bound, int k, int m, uint32_t nshards,
+                            uint64_t* out_pk, uint32_t* out_bk, uint64_t cap, unsigned long long* cursor,
+                            unsigned long long* wins, unsigned long long* ovf, hipStream_t s);
 hipError_t launch_dump(TableView t, int count_mode, uint64_t min_abundance, uint64_t* out, DevCounters* ctr,
                        hipStream_t s);
 // GPU text formatting (kc_write): bytes of each TEXT_T-bucket block into block_bytes and

@@ -1,0 +1,290 @@
+// kc_skm.hip -- super-k-mer routing for the multi-GPU exchange.
+//
+// The owner of a canonical k-mer is a hash of its canonical minimizer: the smallest value of
+// h(canonical m-mer) over the k - m + 1 m-mers of the k-mer.  A k-mer and its reverse complement
+// hold the same canonical m-mers, so every occurrence of a canonical k-mer goes to one owner
+// (exact counts, as SURVEY 8e's hash-prefix owner), and consecutive windows of a read share their
+// minimizer -- and so their owner -- for ~(k - m + 2) / 2 windows on average.  A maximal run of r
+// consecutive valid windows with one owner (a super-k-mer) travels as its k - 1 + r symbols,
+// 2-bit packed, instead of r keys: ~1 byte per window at k = 51 against the 24-byte {key, count}
+// records of the pre-aggregated exchange (sharded.py), whose per-rank coverage at C4 / 8 ranks
+// gives ~0.4 distinct k-mers per window.
+//
+// Output: per owner, a symbol stream in the tokenizer's packed format (kc_internal.h PackedView:
+// pk[w] holds symbols 32w .. 32w + 31 at bits 62 - 2j, bk[w] their break flags at bit 31 - j).
+// Every super-k-mer is one break symbol followed by its k - 1 + r symbols, so the owner counts
+// the stream with the ordinary levels (kc_count_packed_device) and no window spans two
+// super-k-mers.  Each workgroup tile reserves a whole-word range per owner (one atomicAdd per
+// owner and tile, order free: counting is order-independent) and pads its tail with breaks.
+#include "kc_common.h"
+
+namespace kc {
+
+constexpr int SKM_T = 256;             // threads per workgroup
+constexpr int SKM_RUN = 16;            // window ends per thread
+constexpr int SKM_TP = SKM_T * SKM_RUN;  // window ends per tile
+constexpr int SKM_MAXW = MAX_K;        // most m-mers per window (k - m + 1 <= k)
+constexpr int SKM_STAGE = 2048;        // staged output words per tile (65 536 symbols)
+constexpr uint32_t SKM_BROKEN = 0xFFFFFFFFu;
+
+// h(canonical m-mer) in 32 bits, never SKM_BROKEN
+DEV uint32_t mmer_hash(uint64_t canon) {
+    const uint32_t h = (uint32_t)(fmix64(canon ^ SKM_SEED) >> 32);
+    return h == SKM_BROKEN ? SKM_BROKEN - 1 : h;
+}
+
+// 32 symbols starting at symbol s (s may be negative or unaligned; symbols before 0 read as 0)
+DEV uint64_t load32_at(const uint64_t* __restrict__ pk, int64_t s) {
+    const int64_t w = s >> 5;  // (arithmetic shift: floor)
+    const int o = (int)(s & 31);
+    const uint64_t a = w >= 0 ? pk[w] : 0, b = w + 1 >= 0 ? pk[w + 1] : 0;
+    return o ? (a << (2 * o)) | (b >> (64 - 2 * o)) : a;
+}
+
+// Write `len` symbols starting at input symbol `src` into the output at symbol `dst` (a break
+// symbol precedes them at dst - 1, set by the caller), OR-ing words into an LDS stage or, for
+// a tile whose output does not fit the stage, its global range.
+DEV void put_symbols(uint64_t* __restrict__ opk, const uint64_t* __restrict__ pk, int64_t src, uint64_t dst,
+                     uint64_t len) {
+    const uint64_t w0 = dst >> 5, w1 = (dst + len - 1) >> 5;
+    for (uint64_t w = w0; w <= w1; w++) {
+        const int64_t s0 = src + (int64_t)(w * 32) - (int64_t)dst;  // input symbol of output slot 32w
+        uint64_t v = load32_at(pk, s0);
+        // keep the output slots [dst, dst + len) of this word
+        const uint64_t lo = w * 32 < dst ? dst - w * 32 : 0;
+        const uint64_t hi = (w + 1) * 32 > dst + len ? dst + len - w * 32 : 32;
+        uint64_t m = (hi - lo == 32) ? ~0ULL : (((1ULL << (2 * (hi - lo))) - 1) << (2 * (32 - hi)));
+        v &= m;
+        atomicOr(reinterpret_cast<unsigned long long*>(opk + w), (unsigned long long)v);
+    }
+}
+
+// One workgroup per tile of SKM_TP window ends (grid-stride over tiles).
+//   out_pk / out_bk: nshards regions of cap words each; cursor[o]: words used in region o (grows
+//   past cap on overflow: the caller's retry size); wins[o]: windows routed to o; ovf: set when a
+//   region overflowed (nothing of that tile is written for that owner).
+__global__ __launch_bounds__(SKM_T) void k_skm_route(PackedView sv, const DevCounters* __restrict__ ctr, int k, int m,
+                                                     uint32_t nshards, uint64_t* __restrict__ out_pk,
+                                                     uint32_t* __restrict__ out_bk, uint64_t cap,
+                                                     unsigned long long* __restrict__ cursor,
+                                                     unsigned long long* __restrict__ wins,
+                                                     unsigned long long* __restrict__ ovf) {
+    __shared__ uint32_t s_h[SKM_TP + SKM_MAXW];
+    __shared__ uint8_t s_ow[SKM_TP];
+    __shared__ uint64_t s_pk[SKM_STAGE];
+    __shared__ uint32_t s_bk[SKM_STAGE];
+    __shared__ uint32_t s_cnt[SKM_MAX_SHARDS], s_win[SKM_MAX_SHARDS], s_lbase[SKM_MAX_SHARDS + 1];
+    __shared__ unsigned long long s_gbase[SKM_MAX_SHARDS];
+    __shared__ int s_direct;
+    const int tid = threadIdx.x;
+    const uint64_t M = ctr->stream_len;
+    const int w = k - m + 1;  // m-mers per window
+    const uint64_t mmask = m >= 32 ? ~0ULL : (1ULL << (2 * m)) - 1;
+    const int rsh = 64 - 2 * m;
+    const uint64_t ntiles = (M + SKM_TP - 1) / SKM_TP;
+    for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const uint64_t t0 = tile * SKM_TP, t1 = min(t0 + SKM_TP, M);
+        // 1. the hashes of the m-mers ending at t0 - w + 1 .. t1 - 1 (broken: a break symbol inside,
+        //    or the m-mer starts before the stream)
+        const int nh = (int)(t1 - t0) + w - 1;
+        for (int i = tid; i < nh; i += SKM_T) {
+            const int64_t q = (int64_t)t0 - (w - 1) + i;  // last symbol of the m-mer
+            const int64_t a = q - m + 1;
+            uint32_t h = SKM_BROKEN;
+            if (a >= 0) {
+                const uint64_t wa = (uint64_t)a >> 5, wq = (uint64_t)q >> 5;
+                uint32_t br = sv.bk[wa] & (0xFFFFFFFFu >> (a & 31));
+                if (wq != wa) br = br ? br : (sv.bk[wq] & (0xFFFFFFFFu << (31 - (q & 31))));
+                else br &= 0xFFFFFFFFu << (31 - (q & 31));
+                if (!br) {
+                    const uint64_t x = (load32_at(sv.pk, a) >> rsh) & mmask;  // m symbols, oldest first
+                    const uint64_t rc = (rev2(~x) >> rsh) & mmask;
+                    h = mmer_hash(x < rc ? x : rc);
+                }
+            }
+            s_h[i] = h;
+        }
+        if (tid < (int)nshards) {
+            s_cnt[tid] = 0;
+            s_win[tid] = 0;
+        }
+        if (tid == 0) s_direct = 0;
+        __syncthreads();
+        // 2. per window end: valid (no broken m-mer among its w) and the minimizer -> owner
+        const int j0 = tid * SKM_RUN;  // first window end of this thread (tile-relative)
+        uint8_t own[SKM_RUN];
+        {
+            // window end p = t0 + j covers the m-mers ending at p - w + 1 .. p, i.e. s_h[j .. j + w - 1]
+            uint32_t mn[SKM_RUN], mx[SKM_RUN];
+            if (w >= SKM_RUN) {
+                // window j covers s_h[j0 + j .. j0 + j + w - 1]: the part common to the thread's
+                // SKM_RUN windows [j0 + SKM_RUN - 1, j0 + w - 1], a left part [j0 + j, j0 + SKM_RUN - 2]
+                // (suffixes) and a right part [j0 + w, j0 + w + j - 1] (prefixes): w + 2 SKM_RUN reads
+                uint32_t cmn = SKM_BROKEN, cmx = 0;
+                for (int i = j0 + SKM_RUN - 1; i <= j0 + w - 1; i++) {
+                    const uint32_t h = i < nh ? s_h[i] : SKM_BROKEN;
+                    cmn = min(cmn, h);
+                    cmx = max(cmx, h);
+                }
+                uint32_t ln = SKM_BROKEN, lx = 0;
+#pragma unroll
+                for (int j = SKM_RUN - 1; j >= 0; j--) {
+                    if (j < SKM_RUN - 1) {
+                        const int i = j0 + j;
+                        const uint32_t h = i < nh ? s_h[i] : SKM_BROKEN;
+                        ln = min(ln, h);
+                        lx = max(lx, h);
+                    }
+                    mn[j] = min(ln, cmn);
+                    mx[j] = max(lx, cmx);
+                }
+                uint32_t rn = SKM_BROKEN, rx = 0;
+#pragma unroll
+                for (int j = 0; j < SKM_RUN; j++) {
+                    if (j > 0) {
+                        const int i = j0 + w + j - 1;
+                        const uint32_t h = i < nh ? s_h[i] : SKM_BROKEN;
+                        rn = min(rn, h);
+                        rx = max(rx, h);
+                    }
+                    mn[j] = min(mn[j], rn);
+                    mx[j] = max(mx[j], rx);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < SKM_RUN; j++) {
+                    uint32_t a = SKM_BROKEN, b = 0;
+                    for (int i = j0 + j; i < j0 + j + w; i++) {
+                        const uint32_t h = i < nh ? s_h[i] : SKM_BROKEN;
+                        a = min(a, h);
+                        b = max(b, h);
+                    }
+                    mn[j] = a;
+                    mx[j] = b;
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < SKM_RUN; j++) {
+                const bool valid = t0 + j0 + j < t1 && mx[j] != SKM_BROKEN;
+                own[j] = valid ? (uint8_t)(((uint64_t)mn[j] * nshards) >> 32) : 0xFF;
+                if (j0 + j < SKM_TP) s_ow[j0 + j] = own[j];
+            }
+        }
+        __syncthreads();
+        // 3. super-k-mer starts of this thread: run length, symbols (a break + k - 1 + r), local offset
+        const int tlen = (int)(t1 - t0);
+        uint32_t run[SKM_RUN], off[SKM_RUN];
+#pragma unroll
+        for (int j = 0; j < SKM_RUN; j++) {
+            run[j] = 0;
+            const int p = j0 + j;
+            if (p >= tlen || own[j] == 0xFF) continue;
+            if (p > 0 && s_ow[p - 1] == own[j]) continue;
+            int e = p + 1;
+            while (e < tlen && s_ow[e] == own[j]) e++;
+            run[j] = (uint32_t)(e - p);
+            off[j] = atomicAdd(&s_cnt[own[j]], (uint32_t)k + run[j]);
+            atomicAdd(&s_win[own[j]], run[j]);
+        }
+        __syncthreads();
+        // 4. whole-word ranges per owner: global (one atomicAdd each) and the LDS stage layout
+        if (tid == 0) {
+            uint32_t acc = 0;
+            for (uint32_t o = 0; o < nshards; o++) {
+                s_lbase[o] = acc;
+                acc += (s_cnt[o] + 31) / 32;
+            }
+            s_lbase[nshards] = acc;
+            s_direct = acc > SKM_STAGE;
+        }
+        if (tid < (int)nshards) {
+            const uint32_t nw = (s_cnt[tid] + 31) / 32;
+            unsigned long long g = ~0ULL;
+            if (nw) {
+                g = atomicAdd(&cursor[tid], (unsigned long long)nw);
+                atomicAdd(&wins[tid], (unsigned long long)s_win[tid]);
+                if (g + nw > cap) {
+                    atomicOr(ovf, 1ULL);
+                    g = ~0ULL;
+                }
+            }
+            s_gbase[tid] = g;
+        }
+        __syncthreads();
+        const bool direct = s_direct != 0;
+        const uint32_t tot = s_lbase[nshards];
+        if (!direct) {
+            for (uint32_t i = tid; i < tot; i += SKM_T) {
+                s_pk[i] = 0;
+                s_bk[i] = 0;
+            }
+        } else {
+            // (more than the stage holds: this tile ORs straight into its global ranges, zeroed first)
+            for (uint32_t o = 0; o < nshards; o++) {
+                const unsigned long long g = s_gbase[o];
+                if (g == ~0ULL) continue;
+                const uint32_t nw = (s_cnt[o] + 31) / 32;
+                for (uint32_t i = tid; i < nw; i += SKM_T) {
+                    out_pk[o * cap + g + i] = 0;
+                    out_bk[o * cap + g + i] = 0;
+                }
+            }
+            __threadfence();
+        }
+        __syncthreads();
+        // 5. the super-k-mers' symbols and separators; the tail of each owner's range: breaks
+#pragma unroll
+        for (int j = 0; j < SKM_RUN; j++) {
+            if (!run[j]) continue;
+            const uint32_t o = own[j];
+            const uint64_t d = (uint64_t)off[j] + 1;  // after the separator
+            const int64_t src = (int64_t)(t0 + j0 + j) - (k - 1);
+            const uint64_t len = (uint64_t)k - 1 + run[j];
+            if (!direct) {
+                const uint64_t base = (uint64_t)s_lbase[o] * 32;
+                atomicOr(&s_bk[(base + off[j]) >> 5], 0x80000000u >> ((base + off[j]) & 31));
+                put_symbols(s_pk, sv.pk, src, base + d, len);
+            } else if (s_gbase[o] != ~0ULL) {
+                const uint64_t base = (s_gbase[o] + o * cap) * 32;
+                atomicOr(&out_bk[(base + off[j]) >> 5], 0x80000000u >> ((base + off[j]) & 31));
+                put_symbols(out_pk, sv.pk, src, base + d, len);
+            }
+        }
+        if (tid < (int)nshards && s_cnt[tid] % 32) {
+            const uint32_t used = s_cnt[tid] % 32;  // the last word's padding symbols are breaks
+            const uint32_t pad = 0xFFFFFFFFu >> used;
+            const uint32_t lw = (s_cnt[tid] + 31) / 32 - 1;
+            if (!direct)
+                atomicOr(&s_bk[s_lbase[tid] + lw], pad);
+            else if (s_gbase[tid] != ~0ULL)
+                atomicOr(&out_bk[tid * cap + s_gbase[tid] + lw], pad);
+        }
+        __syncthreads();
+        // 6. staged tiles: copy each owner's words to its global range
+        if (!direct) {
+            for (uint32_t o = 0; o < nshards; o++) {
+                const unsigned long long g = s_gbase[o];
+                const uint32_t lb = s_lbase[o], nw = s_lbase[o + 1] - lb;
+                if (g == ~0ULL) continue;
+                for (uint32_t i = tid; i < nw; i += SKM_T) {
+                    out_pk[o * cap + g + i] = s_pk[lb + i];
+                    out_bk[o * cap + g + i] = s_bk[lb + i];
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+hipError_t launch_skm_route(PackedView sv, const DevCounters* ctr, uint64_t sym_bound, int k, int m, uint32_t nshards,
+                            uint64_t* out_pk, uint32_t* out_bk, uint64_t cap, unsigned long long* cursor,
+                            unsigned long long* wins, unsigned long long* ovf, hipStream_t s) {
+    if (nshards == 0 || nshards > SKM_MAX_SHARDS || m < 1 || m > 32 || m > k) return hipErrorInvalidValue;
+    const uint64_t tiles = (sym_bound + SKM_TP - 1) / SKM_TP;
+    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(tiles, 256 * 12));
+    hipLaunchKernelGGL(k_skm_route, dim3(grid), dim3(SKM_T), 0, s, sv, ctr, k, m, nshards, out_pk, out_bk, cap, cursor,
+                       wins, ovf);
+    return hipGetLastError();
+}
+
+}  // namespace kc

@@ -48,9 +48,9 @@ EXPORTS = (
     "kc_route_table_device", "kc_route_hint", "kc_insert_counts_device", "kc_clear_table", "kc_insert_counts_runs_device",
     "kc_xxh64", "kc_bloom_info", "kc_bloom_read", "kc_bloom_write", "kc_synth_skew_device",
     "kc_table_size_reference", "kc_bloom_get_device", "kc_bloom_merge_device", "kc_bloom_set_device",
-    "kc_bloom_estimate", "kc_compact", "kc_compact_dump", "kc_compact_lookup", "kc_compact_read",
+    "kc_bloom_estimate", "kc_compact", "kc_compact_dump", "kc_compact_lookup", "kc_compact_read", "kc_size_table",
     "kc_estimate_distinct_device", "kc_bloom_records_device", "kc_count_records_device", "kc_plan_chunks_device",
-    "kc_output_digest",
+    "kc_output_digest", "kc_route_superkmers_device", "kc_count_packed_device", "kc_bloom_packed_device",
 )
 
 
@@ -135,6 +135,11 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "kc_count_device": (I32, [P, P, ctypes.POINTER(kc_chunk), ctypes.c_size_t, I32, P]),
         "kc_estimate_distinct_device": (I32, [P, P, ctypes.POINTER(kc_chunk), ctypes.c_size_t, I32, P,
                                               ctypes.POINTER(ctypes.c_double)]),
+        "kc_size_table": (I32, [P, U64]),
+        "kc_route_superkmers_device": (I32, [P, P, ctypes.POINTER(kc_chunk), ctypes.c_size_t, I32, ctypes.c_uint32,
+                                             I32, P, P, U64, ctypes.POINTER(U64), ctypes.POINTER(U64), P]),
+        "kc_count_packed_device": (I32, [P, P, P, U64, U64, P]),
+        "kc_bloom_packed_device": (I32, [P, P, P, U64, U64, P]),
         "kc_sync": (I32, [P]),
         "kc_finish": (I32, [P, ctypes.POINTER(kc_stats)]),
         "kc_dump": (I32, [P, ctypes.POINTER(ctypes.POINTER(U64)), ctypes.POINTER(U64)]),
@@ -356,6 +361,42 @@ class KmerCounter:
                                                        ctypes.c_void_p(stream or None), ctypes.byref(est)),
                   "kc_estimate_distinct_device")
         return est.value
+
+    def size_table(self, slots: int):
+        """Size the table of the job about to be counted for `slots` k-mers (e.g. 1.1 x the distinct
+        estimate) instead of -s, which stays the job's reference capacity; 0 = back to -s
+        (kc_size_table: after create / reset, before the first counting pass)."""
+        self._chk(self.lib.kc_size_table(self._ctx, int(slots)), "kc_size_table")
+
+    def route_superkmers_device(self, dev_ptr: int, chunks, fmt: int, nshards: int, pk_ptr: int = 0, bk_ptr: int = 0,
+                                cap_words: int = 0, m: int = 0, stream: int = 0):
+        """Super-k-mers of a device image, per owner (canonical-minimizer owner, kc_api.h): region o of
+        pk / bk (cap_words words each, at o * cap_words) receives owner o's packed stream.  Returns
+        (words per owner, windows per owner); cap_words = 0 only sizes them.  Raises KcError
+        (KC_ERR_NOMEM) when a region is too small -- its .words holds the sizes needed."""
+        arr = self._chunk_array(chunks)
+        words = (ctypes.c_uint64 * nshards)()
+        wins = (ctypes.c_uint64 * nshards)()
+        rc = self.lib.kc_route_superkmers_device(self._ctx, ctypes.c_void_p(dev_ptr), arr, len(chunks), fmt, nshards, m,
+                                                 ctypes.c_void_p(pk_ptr or None), ctypes.c_void_p(bk_ptr or None),
+                                                 cap_words, words, wins, ctypes.c_void_p(stream or None))
+        if rc:
+            err = KcError(rc, f"kc_route_superkmers_device: {self.lib.kc_last_error(self._ctx).decode()}")
+            err.words = list(words)
+            raise err
+        return list(words), list(wins)
+
+    def count_packed_device(self, pk_ptr: int, bk_ptr: int, n_words: int, windows: int = 0, stream: int = 0):
+        """Counts the windows of a packed symbol stream in HBM (e.g. received super-k-mers)."""
+        self._chk(self.lib.kc_count_packed_device(self._ctx, ctypes.c_void_p(pk_ptr or None),
+                                                  ctypes.c_void_p(bk_ptr or None), n_words, windows,
+                                                  ctypes.c_void_p(stream or None)), "kc_count_packed_device")
+
+    def bloom_packed_device(self, pk_ptr: int, bk_ptr: int, n_words: int, windows: int = 0, stream: int = 0):
+        """Bloom pass 1 over a packed symbol stream in HBM."""
+        self._chk(self.lib.kc_bloom_packed_device(self._ctx, ctypes.c_void_p(pk_ptr or None),
+                                                  ctypes.c_void_p(bk_ptr or None), n_words, windows,
+                                                  ctypes.c_void_p(stream or None)), "kc_bloom_packed_device")
 
     def route_device(self, dev_ptr: int, chunks, fmt: int, nshards: int, out_ptr: int, out_capacity: int,
                      stream: int = 0) -> List[int]:

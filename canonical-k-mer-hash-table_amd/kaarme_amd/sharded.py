@@ -67,23 +67,26 @@ def chunk_words_default() -> int:
 
 
 def exchange(dist, keys, counts: Sequence[int], W: int, group=None, chunk_words: int = 0,
-             with_counts: bool = False, verify: bool = True):
+             with_counts: bool = False, verify: bool = True, extra: int = 0):
     """All-to-all of owner-grouped items of W int64 words each.  keys: int64 tensor
     holding sum(counts)*W words (group d = the items for rank d, in rank order).
     Returns (received items, n received[, items received from each rank]); the items
     from rank s follow those of s-1.  verify: the senders' per-group word sums travel
-    beside the items and must equal the sums of the groups received (else RuntimeError)."""
+    beside the items and must equal the sums of the groups received (else RuntimeError).
+    extra: words of slack after the received items (readable, unspecified)."""
     import torch
 
     chunk_words = chunk_words or chunk_words_default()
     dev = keys.device
     world = len(counts)
     if world == 1:  # nothing leaves the rank
+        if extra and keys.numel() < int(counts[0]) * W + extra:
+            keys = torch.cat([keys[: int(counts[0]) * W], keys.new_zeros(extra)])
         return (keys, int(counts[0]), [int(counts[0])]) if with_counts else (keys, int(counts[0]))
     if _host_staged(dist, group, keys):
         # gloo moves host tensors only: the items cross through host memory (tests with several
         # ranks on one GPU; RCCL moves device memory directly)
-        res = exchange(dist, keys.cpu(), counts, W, group, chunk_words, True, verify)
+        res = exchange(dist, keys.cpu(), counts, W, group, chunk_words, True, verify, extra)
         out = res[0].to(dev)
         return (out, res[1], res[2]) if with_counts else (out, res[1])
     sw = [int(c) * W for c in counts]
@@ -102,7 +105,7 @@ def exchange(dist, keys, counts: Sequence[int], W: int, group=None, chunk_words:
     rh = recv_head.view(world, -1).cpu().tolist()
     recv = [int(r[0]) for r in rh]
     total = sum(recv)
-    out = torch.empty(max(1, total * W), dtype=torch.int64, device=dev)
+    out = torch.empty(max(1, total * W + extra), dtype=torch.int64, device=dev)
     rw = [r * W for r in recv]
     ro = [sum(rw[:d]) for d in range(world)]
     big = torch.tensor([max(sw + rw + [0])], dtype=torch.int64, device=dev)
@@ -191,13 +194,31 @@ def batch_groups(chunks, batch_bytes: int):
 
 class DeviceEngine:
     """The HIP engine of one rank: a local table counting the rank's input and an owner
-    table holding the merged counts of the k-mers this rank owns."""
+    table holding the merged counts of the k-mers this rank owns.  superkmers: no local table --
+    a routing context (tokenizer + kc_route_superkmers_device) and the owner table, which counts
+    the super-k-mer streams the rank receives (kc_count_packed_device)."""
 
-    def __init__(self, cfg: Config, local_slots: int = 0, world: int = 1):
+    def __init__(self, cfg: Config, local_slots: int = 0, world: int = 1, superkmers: bool = False):
         import dataclasses
 
         self.cfg = cfg  # the owner table: this rank's share of -s
         self.world = world
+        self.superkmers = superkmers
+        self._skm_cap = 0
+        self._spk = self._sbk = None
+        if superkmers:
+            # (the routing context's own table is a stub: it never counts)
+            self.kc = KmerCounter(dataclasses.replace(cfg, bf_enable=False, table_slots=1 << 16))
+            self.same_geometry = False
+            self.owner = None
+            self._agg = None
+            self._agg_slots = 0
+            self._uniq, self._nuniq = None, 0
+            self.W = words_for_k(cfg.k)
+            self.device = "cuda"
+            self._buf = None
+            self._rec = None
+            return
         # the local table must hold every distinct k-mer of this rank's input, which the
         # owner share does not bound (a rank sees ~all k-mers of the genome at low
         # per-rank coverage): local_slots, e.g. min(-s total, this rank's windows).  With the
@@ -283,6 +304,54 @@ class DeviceEngine:
         else:
             self.owner_table().insert_counts_device(recs.data_ptr(), n, stream)
 
+    # -- super-k-mer exchange (kc_route_superkmers_device / kc_count_packed_device)
+    def _skm_alloc(self, parts: int, need: int):
+        import torch
+
+        cap = (int(need * 1.1) + 64) // 2 * 2
+        self._spk = torch.empty(parts * cap + 2, dtype=torch.int64, device="cuda")
+        self._sbk = torch.empty(parts * cap + 2, dtype=torch.int32, device="cuda")
+        self._skm_cap = cap
+
+    def skm_route(self, dev_ptr: int, chunks, fmt: int, parts: int, stream: int = 0):
+        """The image's super-k-mers per owner, as contiguous send buffers in rank order: (pk words
+        int64, bk words as int64 pairs, words per owner (even: an odd group gets a pad word of
+        breaks), windows per owner).  The regions are sized by a dry run the first time and grow
+        when a route reports them too small."""
+        import torch
+
+        from . import KcError
+
+        for attempt in range(2):
+            if self._skm_cap == 0:
+                need, _ = self.kc.route_superkmers_device(dev_ptr, chunks, fmt, parts, stream=stream)
+                self._skm_alloc(parts, max(need))
+            try:
+                words, wins = self.kc.route_superkmers_device(dev_ptr, chunks, fmt, parts, self._spk.data_ptr(),
+                                                              self._sbk.data_ptr(), self._skm_cap, stream=stream)
+                break
+            except KcError as e:
+                if attempt or getattr(e, "words", None) is None:
+                    raise
+                self._skm_alloc(parts, max(e.words))
+        cap = self._skm_cap
+        pks, bks, even = [], [], []
+        for o in range(parts):
+            n = int(words[o])
+            pks.append(self._spk[o * cap: o * cap + n])
+            bks.append(self._sbk[o * cap: o * cap + n])
+            if n % 2:  # (a pad word: no symbol, every position a break)
+                pks.append(self._spk.new_zeros(1))
+                bks.append(self._sbk.new_full((1,), -1))
+            even.append(n + n % 2)
+        return torch.cat(pks), torch.cat(bks).view(torch.int64), even, [int(w) for w in wins]
+
+    def count_packed(self, pk, bk, n_words: int, windows: int, stream: int = 0):
+        self.owner_table().count_packed_device(pk.data_ptr(), bk.data_ptr(), n_words, windows, stream)
+
+    def bloom_packed(self, pk, bk, n_words: int, windows: int, stream: int = 0):
+        self.owner_table().bloom_packed_device(pk.data_ptr(), bk.data_ptr(), n_words, windows, stream)
+
     # -- owner-sharded Bloom filter: the rank's ungated local count, then the owner's two
     # passes over the {key, count} records it receives
     def bloom(self, dev_ptr: int, chunks, fmt: int, stream: int = 0):
@@ -338,20 +407,29 @@ class DeviceEngine:
 class ShardedCounter:
     """KmerCounter-compatible front end whose table is sharded over the process group."""
 
-    def __init__(self, cfg: Config, dist, engine=None, group=None, local_slots: int = 0):
+    def __init__(self, cfg: Config, dist, engine=None, group=None, local_slots: int = 0, exchange: str = "records"):
         """cfg.table_slots = this rank's owner share of -s, also the local table's size
         unless local_slots is larger.  local_slots must bound the distinct k-mers of this
         rank's own input: when each rank holds a small share of a large genome (strong
-        scaling, e.g. C4), pass min(-s total, this rank's windows)."""
+        scaling, e.g. C4), pass min(-s total, this rank's windows).
+        exchange: "records" (every rank counts its input locally; the table's {key, count} records
+        go to their owners at the merge) or "superkmers" (every counting / Bloom pass routes the
+        input's super-k-mers to their canonical-minimizer owners, which count them: no local table;
+        collective per pass)."""
+        if exchange not in ("records", "superkmers"):
+            raise ValueError(f"exchange must be 'records' or 'superkmers', not {exchange!r}")
         self.cfg = cfg
         self.dist = dist
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.W = words_for_k(cfg.k)
+        self.mode = exchange
         if engine is None:
-            engine = DeviceEngine(cfg, local_slots, self.world)
+            engine = DeviceEngine(cfg, local_slots, self.world, superkmers=exchange == "superkmers")
         self.engine = engine
+        self._in_windows = 0  # super-k-mers: the windows this rank routed (its input's)
+        self._skm_recv = None  # super-k-mers: the Bloom pass's received streams (its counting pass reuses them)
         self.device = getattr(self.engine, "device", "cpu")
         self._pending = False
         self._stream = 0
@@ -365,8 +443,64 @@ class ShardedCounter:
                        "merges": 0}
         self._profiling = False
 
+    def _skm_exchange(self, dev_ptr: int, chunks, fmt: int, stream: int):
+        """Route this rank's image as super-k-mers and exchange them (two all-to-alls: the pk words
+        and the bk words; the windows per owner beside them): (pk, bk int32, words, windows) received."""
+        import time
+
+        import torch
+
+        with _on_stream(self.device, stream):
+            tr = time.perf_counter()
+            spk, sbk, words, wins = self.engine.skm_route(dev_ptr, chunks, fmt, self.world, stream)
+            self.xstats["route_s"] += time.perf_counter() - tr
+            self._in_windows += sum(wins)
+            t0 = time.perf_counter()
+            rpk, n, per_rank = exchange(self.dist, spk, words, 1, self.group, with_counts=True, extra=2)
+            rbk, n2 = exchange(self.dist, sbk, [w // 2 for w in words], 1, self.group, extra=1)
+            if 2 * n2 != n:
+                raise RuntimeError(f"super-k-mer exchange: {n} pk words but {2 * n2} bk words received")
+            if self.world > 1:
+                dev = "cpu" if self.dist.get_backend(self.group) == "gloo" else spk.device
+                wt = torch.tensor(wins, dtype=torch.int64, device=dev)
+                rt = torch.empty_like(wt)
+                self.dist.all_to_all_single(rt, wt, group=self.group)
+                windows = int(rt.sum().item())
+            else:
+                windows = sum(wins)
+            self.xstats["exchange_s"] += time.perf_counter() - t0
+            self.xstats["bytes_sent"] += sum(w for d, w in enumerate(words) if d != self.rank) * 12
+            self.xstats["bytes_recv"] += sum(w for d, w in enumerate(per_rank) if d != self.rank) * 12
+            self.xstats["merges"] += 1
+        return rpk, rbk.view(torch.int32), n, windows
+
+    def _skm_count(self, recv, stream: int):
+        import time
+
+        pk, bk, n, windows = recv
+        with _on_stream(self.device, stream):
+            ti = time.perf_counter()
+            self.engine.count_packed(pk, bk, n, windows, stream)
+            if self._profiling and self.device == "cuda":
+                import torch
+
+                torch.cuda.synchronize()
+                self.xstats["insert_s"] += time.perf_counter() - ti
+        self._inflight = [pk, bk]  # the receive buffers must outlive the count
+
     # the counting pass over a device image (chunks from kaarme_amd.plan_chunks): local
     def count_device(self, dev_ptr: int, chunks: List[Tuple[int, int, int]], fmt: int, stream: int = 0):
+        if self.mode == "superkmers":  # (collective)
+            if self.cfg.bf_enable:
+                if self._skm_recv is None or self._bloom_input != (dev_ptr, tuple(map(tuple, chunks)), fmt):
+                    raise ValueError("a sharded Bloom job counts the input of its Bloom pass (bloom_device, "
+                                     "bloom_finalize, count_device over the same image and chunks)")
+                self._skm_count(self._skm_recv, stream)
+                self._skm_recv = None
+            else:
+                self._skm_count(self._skm_exchange(dev_ptr, chunks, fmt, stream), stream)
+            self._stream = stream
+            return
         if self.cfg.bf_enable:
             # the owners counted the Bloom pass's input behind their gates (bloom_finalize): the
             # counting pass must present that input again (the reference reads the file twice)
@@ -415,10 +549,20 @@ class ShardedCounter:
         self._inflight = [recv]  # the receive buffer must outlive the insert
         self._pending = False
 
-    # the Bloom pass over a device image: this rank's ungated local count
+    # the Bloom pass over a device image: this rank's ungated local count (super-k-mers: the owners'
+    # Bloom pass 1 over the streams they receive, collective)
     def bloom_device(self, dev_ptr: int, chunks: List[Tuple[int, int, int]], fmt: int, stream: int = 0):
         if not self.cfg.bf_enable:
             raise ValueError("bloom_device needs Config(bf_enable=True)")
+        if self.mode == "superkmers":
+            recv = self._skm_exchange(dev_ptr, chunks, fmt, stream)
+            pk, bk, n, windows = recv
+            with _on_stream(self.device, stream):
+                self.engine.bloom_packed(pk, bk, n, windows, stream)
+            self._skm_recv = recv
+            self._bloom_input = (dev_ptr, tuple(map(tuple, chunks)), fmt)
+            self._stream = stream
+            return
         self.engine.bloom(dev_ptr, chunks, fmt, stream)
         self._bloom_input = (dev_ptr, tuple(map(tuple, chunks)), fmt)
         self._stream = stream
@@ -432,6 +576,14 @@ class ShardedCounter:
         import torch
 
         stream = self._stream if stream is None else stream
+        if self.mode == "superkmers":  # every owner holds all occurrences of its k-mers: its own pass 1
+            with _on_stream(self.device, stream):
+                nis = self.engine.owner_bloom_finalize()
+                tot = torch.tensor([int(nis)], dtype=torch.int64, device=self.device if self.device == "cuda" else "cpu")
+                if self.world > 1:
+                    self.dist.all_reduce(tot, group=self.group)
+            self._pending = False
+            return int(tot.item())
         with _on_stream(self.device, stream):
             recs, counts = self.engine.route_table(self.world, stream)
             self.engine.clear_local()
@@ -462,7 +614,7 @@ class ShardedCounter:
 
     def _local_owner(self) -> bool:
         """One rank, no Bloom filter: the local table is the owner table (merge moves nothing)."""
-        return self.world == 1 and not self.cfg.bf_enable
+        return self.world == 1 and not self.cfg.bf_enable and self.mode == "records"
 
     def reset(self):
         self.engine.reset()
@@ -470,6 +622,8 @@ class ShardedCounter:
         self._inflight = []
         self._bloom_input = None
         self._counted = False
+        self._in_windows = 0
+        self._skm_recv = None
 
     def sync(self):
         """Completes the job: the (collective) merge if counts are pending, then waits."""
@@ -487,10 +641,13 @@ class ShardedCounter:
             self.kc.profile(enable)
 
     def timing(self) -> dict:
-        """Local counting batches (+ the table routing) plus the merge insert (count_ms)."""
+        """Local counting batches (+ the table routing) plus the merge insert (count_ms); super-k-mers:
+        the owner's batches (the routing passes are not timed)."""
         a = self.engine.kc.timing()
         if self._local_owner():
             return dict(a)
+        if self.mode == "superkmers":
+            return dict(self.kc.timing())
         b = self.kc.timing()
         out = dict(a)
         out["count_ms"] = a["count_ms"] + b["count_ms"]
@@ -499,6 +656,12 @@ class ShardedCounter:
     def finish(self) -> dict:
         """Stats of the owner table; windows / chunks / bytes are this rank's input."""
         self.sync()
+        if self.mode == "superkmers":  # (no local table: the windows are the ones this rank routed)
+            st = dict(self.kc.finish())
+            st["owner_windows"] = st["windows"]
+            st["windows"] = self._in_windows
+            st["local_distinct"] = 0
+            return st
         local = self.engine.kc.finish()
         own = local if self._local_owner() else self.kc.finish()
         st = dict(own)

@@ -155,6 +155,16 @@ int kc_count_device(kc_ctx* ctx, const uint8_t* dev_image, const kc_chunk* chunk
  * the same k can run it (its table size does not matter). */
 int kc_estimate_distinct_device(kc_ctx* ctx, const uint8_t* dev_image, const kc_chunk* chunks, size_t n_chunks,
                                 int fmt, void* hip_stream, double* estimate);
+/* Size the device table of the job about to be counted (after kc_create or kc_reset, before
+ * its first counting pass; no Bloom filter): `slots` k-mers with the usual 25 % headroom,
+ * e.g. 1.1 x kc_estimate_distinct_device, instead of -s (kc_config.table_slots), which stays
+ * the job's reference capacity (KC_STRICT_CAPACITY: kc_finish fails past next_prime3mod4(-s)).
+ * 0 = back to -s.
+ * A table much smaller than its allocation gets a new one (the memory goes back to the
+ * deferred level 3).  Replaces nothing in the reference, whose table is -s slots
+ * (parallel_parser.hpp:1192-1196): -s 2.6e9 for C4's 1.0 G distinct k-mers takes 83 GB of
+ * HBM at 25 % headroom, the estimate 35 GB. */
+int kc_size_table(kc_ctx* ctx, uint64_t slots);
 /* Wait for all work enqueued on the context. */
 int kc_sync(kc_ctx* ctx);
 
@@ -168,6 +178,30 @@ int kc_sync(kc_ctx* ctx);
 int kc_route_device(kc_ctx* ctx, const uint8_t* dev_image, const kc_chunk* chunks, size_t n_chunks, int fmt,
                     uint32_t nshards, uint64_t* dev_out, uint64_t out_capacity, uint64_t* counts, void* hip_stream);
 int kc_insert_keys_device(kc_ctx* ctx, const uint64_t* dev_keys, uint64_t n_keys, void* hip_stream);
+
+/* Super-k-mer sharding (the multi-GPU exchange of kaarme_amd.sharded): the owner of
+ * a canonical k-mer is a hash of its canonical minimizer (the least h(canonical m-mer) over its
+ * k - m + 1 m-mers; m = 0: min(15, k)), the same for both strands, so every occurrence of a k-mer
+ * has one owner and the owners' counts are exact.  kc_route_superkmers_device tokenizes a device
+ * image (any number of staging batches) and writes, per owner o < nshards (<= 64), the maximal runs
+ * of consecutive windows with owner o ("super-k-mers": a break symbol + the run's k - 1 + r symbols)
+ * as a packed symbol stream -- pk words of 32 2-bit symbols, bk words of their break flags (bit 31 =
+ * the word's first symbol), the tokenizer's layout -- into region o of dev_pk / dev_bk (cap_words
+ * words per region, region o at o * cap_words); words[o] = words written (or needed), windows[o] =
+ * windows routed.  cap_words = 0: a dry run that only sizes the regions; a region too small fails
+ * with KC_ERR_NOMEM and words[] holding the sizes needed.  The caller exchanges region o with
+ * rank o (all-to-all), and each owner counts what it received with kc_count_packed_device (or runs
+ * its Bloom pass 1 over it with kc_bloom_packed_device, then kc_bloom_finalize and the counting
+ * pass): the concatenated streams of every sender, n_words words, readable for n_words + 2 words;
+ * `windows` = the windows they hold (sizes the partition levels; 0 = unknown).  Replaces the
+ * reference's one shared table (kmer_hash_table.cpp:2207-2567) with one table per owner. */
+int kc_route_superkmers_device(kc_ctx* ctx, const uint8_t* dev_image, const kc_chunk* chunks, size_t n_chunks,
+                               int fmt, uint32_t nshards, int m, uint64_t* dev_pk, uint32_t* dev_bk,
+                               uint64_t cap_words, uint64_t* words, uint64_t* windows, void* hip_stream);
+int kc_count_packed_device(kc_ctx* ctx, const uint64_t* dev_pk, const uint32_t* dev_bk, uint64_t n_words,
+                           uint64_t windows, void* hip_stream);
+int kc_bloom_packed_device(kc_ctx* ctx, const uint64_t* dev_pk, const uint32_t* dev_bk, uint64_t n_words,
+                           uint64_t windows, void* hip_stream);
 
 /* Pre-aggregated sharding (the multi-GPU path of kaarme_amd.sharded): every rank counts
  * its own input into its own table, then kc_route_table_device writes the table's

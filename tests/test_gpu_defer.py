@@ -100,3 +100,68 @@ def test_deferred_level3_twice_on_one_context(tmp_path, monkeypatch):
             groups.append(st["deferred_level3"])
             assert kc.output_digest() == text_digest(str(out))
     assert groups[0] == groups[1] >= 2  # (groups of 3 batches: the same groups in both jobs)
+
+
+@pytest.mark.parametrize("k", [31, 51, 127])
+def test_deferred_level3_behind_the_bloom_gate(k, tmp_path, monkeypatch):
+    """A Bloom job (-b, mode 2 with the gate at level 3) whose counting pass spans several staging
+    batches defers its level 3 behind the gate: the k-mers seen twice or more are the
+    oracle's exactly (the filter only gates) and a count-1 line is a true singleton, with and without
+    the deferral."""
+    monkeypatch.setenv("KC_INSERT_PATH", "partitioned")
+    monkeypatch.setenv("KC_DEFER", "2")
+    img, host, path = _image(tmp_path)
+    chunks = ka.plan_chunks(host, k, ka.FMT_FASTA, 200_000)
+
+    def job():
+        cfg = ka.Config(k=k, mode=2, min_abundance=1, bf_enable=True, est_unique=2_000_000, fpr=0.01,
+                        batch_bytes=400 << 10)
+        with ka.KmerCounter(cfg) as kc:
+            kc.bloom_device(img.data_ptr(), chunks, ka.FMT_FASTA)
+            kc.bloom_finalize()
+            kc.count_device(img.data_ptr(), chunks, ka.FMT_FASTA)
+            return kc.lines(), kc.finish()
+
+    lines, st = job()
+    assert st["deferred_level3"] >= 1
+    out = tmp_path / "oracle.txt"
+    oracle_count(path, k, ["-a", "1", "-c", "200000"], out)
+    exact = dict(l.split() for l in open(out).read().splitlines())
+    want2 = sorted(f"{km} {c}" for km, c in exact.items() if int(c) >= 2)
+    monkeypatch.setenv("KC_DEFER", "0")
+    lines0, st0 = job()
+    assert st0["deferred_level3"] == 0
+    # (Bloom pass 1 is order-dependent for false positives, as the reference's insertion_process with
+    # several workers: the singletons that pass the gate may differ between two jobs, so each job is
+    # checked on its own)
+    for got in (lines, lines0):
+        assert sorted(l for l in got if int(l.rsplit(" ", 1)[1]) >= 2) == want2
+        assert all(exact.get(l.split()[0]) == "1" for l in got if l.endswith(" 1"))
+
+
+def test_failed_pass_leaves_no_deferred_group(tmp_path, monkeypatch):
+    """a counting pass whose later chunk does not fit a staging batch fails before it
+    counts anything (the chunks are checked first), and the context stays usable: host chunks counted
+    next on the same context give the oracle's counts for exactly those bytes."""
+    monkeypatch.setenv("KC_INSERT_PATH", "partitioned")
+    monkeypatch.setenv("KC_DEFER", "2")
+    img, host, path = _image(tmp_path)
+    k = 31
+    chunks = ka.plan_chunks(host, k, ka.FMT_FASTA, 200_000)
+    bad = list(chunks)
+    off, _, bh = bad[-1]
+    bad[-1] = (off, 2 << 20, bh)  # larger than the 400 KiB stage (the bytes are never read)
+    with ka.KmerCounter(ka.Config(k=k, mode=2, min_abundance=1, table_slots=4_000_000,
+                                  batch_bytes=400 << 10)) as kc:
+        with pytest.raises(ka.KcError, match="larger than the staging batch"):
+            kc.count_device(img.data_ptr(), bad, ka.FMT_FASTA)
+        first = host[chunks[0][0]:chunks[0][0] + chunks[0][1]]
+        kc.count_chunk(first, ka.FMT_FASTA, bool(chunks[0][2]))
+        st = kc.finish()
+        assert st["deferred_level3"] == 0
+        lines = kc.lines()
+    part = tmp_path / "first.fasta"
+    part.write_bytes(first)
+    out = tmp_path / "oracle.txt"
+    oracle_count(str(part), k, ["-a", "1"], out)
+    assert sorted_digest_lines(lines) == sorted_digest_file(out)

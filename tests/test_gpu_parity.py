@@ -729,3 +729,70 @@ def test_cli_overlapped_upload_equals_one_pass(tmp_path):
         kc.finish()
         want = kc.output_digest()
     assert ka.same_digest(text_digest(str(out)), want)
+
+
+@pytest.mark.parametrize("sizing", ["estimate", "auto"])
+def test_cli_table_sized_from_estimate(sizing, tmp_path):
+    """the CLI sizes a large -s job's table from the input's distinct estimate
+    (kc_estimate_distinct_device + kc_size_table inside its timer; auto: when the -s table would pass
+    16 GiB) and --digest-only prints the output digest; both equal the oracle's output."""
+    n, L = 200_000, 150
+    p = tmp_path / "reads.fasta"
+    subprocess.run([GEN, str(p), str(n), str(L), "2000000", "-s", "11", "-e", "0.001"], check=True)
+    out = tmp_path / "out.txt"
+    # auto: an -s whose 25 %-headroom table is > 16 GiB (k = 51: 5 slots per 128-byte bucket)
+    s = "4000000" if sizing == "estimate" else "800000000"
+    r = subprocess.run([CLI, str(p), "51", "-m", "2", "-s", s, "-a", "1", "-t", "3", "-o", str(out),
+                        "--table-sizing", sizing], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "sized from the distinct estimate" in r.stdout, r.stdout[-2000:]
+    exp = tmp_path / "exp.txt"
+    oracle_count(str(p), 51, ["-a", "1"], exp)
+    assert ka.same_digest(text_digest(str(out)), text_digest(str(exp)))
+    r2 = subprocess.run([CLI, str(p), "51", "-m", "2", "-s", s, "-a", "1", "-t", "3", "-o", str(out),
+                         "--table-sizing", sizing, "--digest-only"], capture_output=True, text=True)
+    assert r2.returncode == 0, r2.stdout[-3000:] + r2.stderr[-3000:]
+    import json
+    import re
+    got = json.loads(re.search(r"Output digest: (\{.*\})", r2.stdout).group(1))
+    assert ka.same_digest(got, text_digest(str(exp)))
+
+
+def test_size_table_from_estimate(tmp_path):
+    """kc_size_table: a job's table sized from its distinct estimate instead of -s (two jobs on one
+    context, as bench.py's C4 / C5 steps), the counts equal the oracle's; refused once the job has
+    counted and for a Bloom job."""
+    import torch
+    n, L = 20_000, 150
+    p = tmp_path / "reads.fasta"
+    subprocess.run([GEN, str(p), str(n), str(L), "400000", "-s", "3", "-e", "0.002"], check=True)
+    host = open(p, "rb").read()
+    img = torch.frombuffer(bytearray(host), dtype=torch.uint8).cuda()
+    k = 51
+    chunks = ka.plan_chunks(host, k, ka.FMT_FASTA, 300_000)
+    exp = tmp_path / "exp.txt"
+    oracle_count(str(p), k, ["-a", "1"], exp)
+    want = text_digest(str(exp))
+    with ka.KmerCounter(ka.Config(k=k, mode=2, min_abundance=1, table_slots=400_000_000,
+                                  batch_bytes=1 << 20)) as kc:
+        big = None
+        for _ in range(2):
+            kc.reset()
+            est = kc.estimate_distinct_device(img.data_ptr(), chunks, ka.FMT_FASTA)
+            assert abs(est - want["lines"]) < 0.05 * want["lines"], (est, want["lines"])
+            kc.size_table(int(1.1 * est) + 4096)
+            kc.count_device(img.data_ptr(), chunks, ka.FMT_FASTA)
+            st = kc.finish()
+            assert st["table_slots"] < 400_000_000 // 100
+            assert ka.same_digest(kc.output_digest(), want)
+            with pytest.raises(ka.KcError, match="counted already"):
+                kc.size_table(1 << 20)
+        kc.reset()
+        kc.size_table(0)  # back to -s
+        kc.count_device(img.data_ptr(), chunks, ka.FMT_FASTA)
+        big = kc.finish()
+        assert big["table_slots"] >= 400_000_000
+        assert ka.same_digest(kc.output_digest(), want)
+    with ka.KmerCounter(ka.Config(k=k, mode=2, bf_enable=True, est_unique=100_000)) as kb:
+        with pytest.raises(ka.KcError, match="Bloom"):
+            kb.size_table(1 << 20)

@@ -76,6 +76,9 @@ class _Table:
     def sync(self):
         pass
 
+    def finish(self):
+        return {"windows": sum(self.table.values()), "distinct": len(self.table)}
+
     def output_digest(self):
         """kc_output_digest of this table's lines (T(c) = c mod 65536, -m 0; a = 1)."""
         from conftest import lines_digest
@@ -180,6 +183,43 @@ class NumpyEngine:
     def owner_table(self):
         return self.owner
 
+    # -- super-k-mer exchange (DeviceEngine.skm_route / count_packed / bloom_packed): the host
+    # router of tests/skm_model.py, the device stream format both ways
+    def skm_route(self, dev_ptr, chunks, fmt, parts, stream=0):
+        import skm_model as sm
+        seqs = [line for off, ln, _ in chunks for line in self.lines[off:off + ln]]
+        routed = sm.route(seqs, self.k, parts)
+        pks, bks, words, wins = [], [], [], []
+        for o in range(parts):
+            pk, bk = sm.pack(routed[o]) if routed[o] else (np.zeros(0, np.uint64), np.zeros(0, np.uint32))
+            if len(pk) % 2:
+                pk = np.concatenate([pk, np.zeros(1, np.uint64)])
+                bk = np.concatenate([bk, np.full(1, 0xFFFFFFFF, np.uint32)])
+            pks.append(pk)
+            bks.append(bk)
+            words.append(len(pk))
+            wins.append(sum(len(x) - self.k + 1 for x in routed[o]))
+        pk = np.concatenate(pks) if pks else np.zeros(0, np.uint64)
+        bk = np.concatenate(bks) if bks else np.zeros(0, np.uint32)
+        return (torch.from_numpy(pk.view(np.int64).copy()), torch.from_numpy(bk.view(np.int64).copy()), words, wins)
+
+    def _packed_kmers(self, pk, bk, n):
+        import skm_model as sm
+        seqs = sm.unpack(pk[:n].numpy().view(np.uint64), bk[:n].numpy().view(np.uint32))
+        return [km for x in seqs for km in canonical_windows(x, self.k)]
+
+    def count_packed(self, pk, bk, n, windows, stream=0):
+        kms = self._packed_kmers(pk, bk, n)
+        assert len(kms) == windows
+        if self.bf:  # behind the owner's gate
+            kms = [km for km in kms
+                   if self._has(bloom_positions(to_words(km, self.W), self.NBLOCKS, self.NH)[: self.NH_GATE], 8)]
+        self.owner.table.update(kms)
+
+    def bloom_packed(self, pk, bk, n, windows, stream=0):
+        for km in self._packed_kmers(pk, bk, n):
+            self._insert(to_words(km, self.W))
+
     def reset(self):
         self.kc.table.clear()
         self.owner.table.clear()
@@ -241,6 +281,67 @@ def _worker(rank, world, port, k, reads, outdir, rounds):
             json.dump(sc.output_digest(), f)
     finally:
         dist.destroy_process_group()
+
+
+def _skm_worker(rank, world, port, k, reads, outdir, bf):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        eng = NumpyEngine(k, reads, bf=bf)
+        cfg = Config(k=k, mode=2, bf_enable=bf, est_unique=1000) if bf else Config(k=k, mode=0)
+        sc = ShardedCounter(cfg, dist, engine=eng, exchange="superkmers")
+        per = (len(reads) + world - 1) // world
+        lo, hi = rank * per, min(len(reads), (rank + 1) * per)
+        out = {}
+        for job in range(2):  # two jobs on one counter, as bench.py's steps
+            sc.reset()
+            if bf:
+                sc.bloom_device(0, [(lo, hi - lo, 0)], 2)
+                out["nis"] = sc.bloom_finalize()
+            sc.count_device(0, [(lo, hi - lo, 0)], 2)
+            sc.sync()
+            st = sc.finish()
+            out["windows"] = st["windows"]
+            out["owner"] = dict(eng.owner.table)
+            if not bf:
+                out["digest"] = sc.output_digest()
+        out["sent"] = sc.xstats["bytes_sent"]
+        with open(os.path.join(outdir, f"shard{rank}.json"), "w") as f:
+            json.dump(out, f)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("k,world,bf", [(21, 2, False), (33, 3, False), (51, 2, True)])
+def test_sharded_superkmers(tmp_path, k, world, bf):
+    """The super-k-mer exchange: every rank routes its reads' super-k-mers to
+    their canonical-minimizer owners (two all-to-alls of packed words) and each owner counts what it
+    receives -- no local table.  The owners are disjoint, their union is the single-process count
+    (and, with the Bloom filter, exact for every k-mer seen twice, count-1 only for true singletons),
+    each rank reports its own input's windows, and the combined digest is the whole job's."""
+    reads = make_reads(60, 90, seed=k + world)
+    mp.spawn(_skm_worker, args=(world, _free_port(), k, reads, str(tmp_path), bf), nprocs=world, join=True)
+    shards = [json.load(open(tmp_path / f"shard{r}.json")) for r in range(world)]
+    truth = collections.Counter(km for r in reads for km in canonical_windows(r, k))
+    union = collections.Counter()
+    for a in range(world):
+        for b in range(a + 1, world):
+            assert not (set(shards[a]["owner"]) & set(shards[b]["owner"]))
+        union.update(shards[a]["owner"])
+    per = (len(reads) + world - 1) // world
+    for r in range(world):
+        assert shards[r]["windows"] == sum(len(canonical_windows(x, k)) for x in reads[r * per:(r + 1) * per])
+    assert any(s["sent"] > 0 for s in shards)
+    if bf:
+        assert {km: c for km, c in union.items() if truth[km] >= 2} == {km: c for km, c in truth.items() if c >= 2}
+        assert all(truth[km] == 1 == c for km, c in union.items() if truth[km] < 2)
+        assert all(s["nis"] == shards[0]["nis"] for s in shards)
+    else:
+        assert union == truth
+        from conftest import lines_digest
+        want = lines_digest(f"{km} {c & 0xFFFF}" for km, c in truth.items())
+        assert all(s["digest"] == want for s in shards)
 
 
 @pytest.mark.parametrize("k", [5, 21, 33, 51])
