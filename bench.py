@@ -403,6 +403,13 @@ def fixture_case(args, share=0, first=0, count=None):
     return None
 
 
+def gpu_free(torch, args, world):
+    """Free HBM this rank may plan with: all of it, or its 1/world share when --rehearse-one-gpu
+    puts every rank on one GPU (the ranks size their buffers concurrently)."""
+    free, _ = torch.cuda.mem_get_info()
+    return free // world if getattr(args, "rehearse_one_gpu", False) else free
+
+
 def setup_job(args, env, image=None):
     """The counting job one bench step runs: the device image (generated in HBM unless given),
     the reference chunk table, the counter with the bench's table and staging geometry, and
@@ -451,7 +458,7 @@ def setup_job(args, env, image=None):
         # (0.45 x free / (28 W + 4)) stays as a floor: every recorded configuration ran with it
         # (C5 at full size takes the exact layout, whose buffers need less).  Batches stay
         # within the 2 GiB measured on the device (C4 at full size: 2.06 GB).
-        free, _ = torch.cuda.mem_get_info()
+        free = gpu_free(torch, args, world)
         want = 1.25 * (slots if slots else 2 * (args.unique or 0))
         table = int(want / (16 // (W + 1))) * 128
         fit = int(0.85 * max(0, free - nbytes - table)) // (21 * W + 3)
@@ -463,9 +470,19 @@ def setup_job(args, env, image=None):
     # estimate -- C4 holds 1.0 G distinct k-mers in a -s 2.6e9 table, C5 1.5 G in -s 3.6e9, which as
     # 25 % headroom over -s take 83 / 192 GB of HBM for 35 / 86 GB of need)
     est_table = strong and not dist and not share and not args.s_table
+    # N > 1: the exchange.  "superkmers": each rank routes its reads' super-k-mers
+    # to their canonical-minimizer owners, which count them (no local table, no estimate); "records":
+    # each rank counts locally and its table's {key, count} records go to their owners.  auto: super-
+    # k-mers for the strong presets and Bloom jobs (C4 / 8 ranks: ~1.3 B per window against ~10 B of
+    # records), records for a weak job without the filter (C2: each rank's reads cover the genome 30x,
+    # so its 86 M distinct k-mers x 16 B undercut 1.2 G windows of super-k-mers)
+    xmode = args.exchange
+    if xmode == "auto":
+        xmode = "superkmers" if (strong or args.unique) else "records"
+    skm = bool(dist) and world > 1 and xmode == "superkmers"
     #  on one GPU the whole job's estimate runs inside the timed step: the
     # counter is created with -s and every step sizes its table from the estimate (kc_size_table)
-    if (strong and (share or (dist and world > 1))) or (dist and args.unique):
+    if not skm and ((strong and (share or (dist and world > 1))) or (dist and args.unique)):
         # (sharded Bloom jobs too: the rank's ungated local count holds all its distinct k-mers)
         # a rank's local table holds its own input's distinct k-mers, which its 1/G share of -s
         # does not bound: sized from a HyperLogLog estimate of them (kc_estimate_distinct_device,
@@ -485,14 +502,23 @@ def setup_job(args, env, image=None):
         estimate = {"distinct_estimate": int(est), "local_slots": local_slots,
                     "ms": round((time.perf_counter() - e0) * 1e3, 1),
                     "method": "HyperLogLog, 2^14 registers (~0.8 % std. error); local table = 1.1 x estimate"}
-    if dist and world > 1 and not args.batch_mib:
+    if skm and not args.batch_mib:
+        # a rank holds its owner table (its 1/G share of -s, or of 2 x -u with the filter) and the
+        # super-k-mer buffers (sent, a contiguous copy, received: ~0.5 B per image byte each)
+        from kaarme_amd.sharded import owner_share
+        osl = owner_share(slots or 2 * (args.unique or 0), world) if (slots or args.unique) else windows_expected
+        per_table = int(1.25 * osl / (16 // (W + 1))) * 128
+        free = gpu_free(torch, args, world)
+        fit = int(0.85 * max(0, free - per_table - 2 * nbytes)) // (21 * W + 3)
+        batch = min(batch, max(64 << 20, min(fit, 1 << 31)) // 4096 * 4096)
+    elif dist and world > 1 and not args.batch_mib:
         # a rank also holds its owner table (the local table's geometry, sharded.DeviceEngine) and
         # the merge's record buffers (send x 1.25 + receive: W + 1 words per distinct k-mer of its
         # input) beside the local count's partition buffers: the batch takes what is left
         lsl = estimate["local_slots"] if estimate else min(slots or windows_expected, windows_expected)
         per_table = int(1.25 * (lsl if estimate else max(slots or 0, lsl)) / (16 // (W + 1))) * 128
         recs = int(2.25 * lsl * (W + 1) * 8)
-        free, _ = torch.cuda.mem_get_info()  # (the image is already allocated)
+        free = gpu_free(torch, args, world)  # (the image is already allocated)
         fit = int(0.85 * max(0, free - 2 * per_table - recs)) // (21 * W + 3)
         batch = min(batch, max(64 << 20, min(fit, 1 << 31)) // 4096 * 4096)
     tbl =" ".join(["-m", "2"] + table_args(slots, args.unique))
@@ -518,6 +544,9 @@ def setup_job(args, env, image=None):
     tslots = slots
     if share or (dist and world > 1 and strong and estimate):
         tslots = estimate["local_slots"] if share else min(slots, estimate["local_slots"])
+    if skm and slots:  # (every rank owns ~1/G of the distinct k-mers: its share of -s, + 8 sigma)
+        from kaarme_amd.sharded import owner_share
+        tslots = owner_share(slots, world)
     cfg = ka.Config(k=k, mode=2, table_slots=tslots,
                     min_abundance=fx["min_abundance"] if fx else 2, batch_bytes=batch,
                     device=local, bf_enable=bool(args.unique), est_unique=args.unique)
@@ -526,7 +555,7 @@ def setup_job(args, env, image=None):
         local_slots = 0
         if strong or args.unique:
             local_slots = estimate["local_slots"] if estimate else min(args.slots or 0, windows_expected)
-        counter = ShardedCounter(cfg, dist, local_slots=local_slots)
+        counter = ShardedCounter(cfg, dist, local_slots=local_slots, exchange=xmode)
     else:
         counter = ka.KmerCounter(cfg)
 
@@ -551,7 +580,7 @@ def setup_job(args, env, image=None):
     return argparse.Namespace(counter=counter, image=image, chunks=chunks, step=step, N=N, first=first, nbytes=nbytes,
                               slots=slots, strong=strong, windows_expected=windows_expected, tbl=tbl,
                               workload=workload, fixture=fx, stream=stream, estimate=estimate, share=share,
-                              est_log=est_log)
+                              est_log=est_log, exchange=xmode if dist else None)
 
 
 def parity_record(job, k, dist=None):
@@ -672,10 +701,21 @@ def run_workload(args, env, image=None):
                 "exchange_ms_per_step": round(xsec / args.steps * 1e3, 3),
                 "gbs_per_rank": round(sent / max(xsec, 1e-9) / 1e9, 2), "peak_gbs_per_gpu": 7 * 153,
                 "route_ms_per_step": round(rsec / args.steps * 1e3, 3),
-                "owner_insert_ms_per_step": round(isec / args.steps * 1e3, 3),
+                "owner_insert_ms_per_step": round(isec / args.steps * 1e3, 3), "exchange": job.exchange,
                 "note": "max over ranks; the all-to-all of {key, count} records incl. its count/sum headers; "
                         "route = the local table as owner-grouped records (host waits for its counts), "
                         "owner insert = the received records into the owner table (waited for)"}
+        if job.exchange == "superkmers":
+            # bytes per rank of the super-k-mer exchange at G ranks, from this run's words per window:
+            # every rank sends (G - 1) / G of its windows' super-k-mers, 12 bytes per 32 symbols
+            bpw = sent / args.steps / max(1, windows_expected) * world / max(1, world - 1)
+            total_w = args.reads * (L - k + 1) if strong else windows_expected * world
+            xgmi["bytes_per_window_sent"] = round(bpw, 4)
+            xgmi["model_sent_bytes_per_rank"] = {str(G): int(total_w / G * bpw * (G - 1) / G) for G in (2, 4, 8)}
+            xgmi["note"] = ("max over ranks; two all-to-alls (packed symbol words, break words) of the canonical-"
+                            "minimizer super-k-mers + their count/sum headers; route = tokenizer + k_skm_route + the "
+                            "send buffers; owner insert = kc_count_packed_device of the received streams (waited "
+                            "for); model = the job's windows / G x bytes_per_window_sent x (G - 1) / G")
     st = counter.finish()  # raises on table overflow
     if rank == 0:
         log(f"{args.config}: {args.steps} steps in {elapsed:.3f} s; parity / writer records")
@@ -726,6 +766,11 @@ def run_workload(args, env, image=None):
     # the roofline window is the tokenizer + the counting pass of a batch (the
     # input bytes sym_B are read by the tokenizer, so its time is inside the window that A counts)
     count_ms = (tm["tokenize_ms"] + tm["count_ms"]) / launches
+    if job.est_log:
+        # the strong presets' distinct estimate (tokenizer + k_hll, whose tokenized batches the counting
+        # pass reads) is part of every batch's window: its wall time per batch (host waits included)
+        timed = job.est_log[-args.steps:]
+        count_ms += sum(x[2] for x in timed) / len(timed) * 1e3 / per_step
     units_per_step = per_step
     if args.unique:
         # Bloom configs: the unit is one Bloom pass + one counting pass over
@@ -760,7 +805,9 @@ def run_workload(args, env, image=None):
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": kname,
                 "kernel_ms": round(count_ms, 4), "algorithmic_bytes_per_launch": int(bytes_per_launch),
-                "window": "tokenizer + counting pass (HIP events on the pass's stream)"}
+                "window": "tokenizer + counting pass (HIP events on the pass's stream)" + (
+                    "; + the distinct estimate (tokenizer + k_hll, wall time per batch) whose tokenized batches the "
+                    "counting pass reads" if job.est_log else "")}
     if args.unique:
         roofline["with_filter_rmw"] = {"achieved": round(bytes_rmw / (count_ms * 1e-3) / 1e9, 2),
                                        "frac": round(bytes_rmw / (count_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
@@ -964,6 +1011,9 @@ def main():
                          "table sized from the distinct estimate; no exchange)")
     ap.add_argument("--s-table", action="store_true",
                     help="strong presets on one GPU: size the table from -s (1.25 x) instead of the distinct estimate")
+    ap.add_argument("--exchange", default="auto", choices=("auto", "records", "superkmers"),
+                    help="N > 1: the sharded exchange (auto: super-k-mers for strong presets and Bloom jobs, "
+                         "records for weak ones)")
     ap.add_argument("--force-sharded", action="store_true",
                     help="use the sharded (RCCL) path even at one rank (testing)")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),

@@ -177,6 +177,19 @@ struct kc_ctx {
     uint64_t* skm_pk = nullptr;
     uint32_t* skm_bk = nullptr;
     uint64_t skm_cap = 0;
+    // kc_estimate_distinct_device keeps its tokenized batches for the next counting pass over the
+    // same image, chunks and format (kept_*): keep_pk / keep_bk hold batch i's stream at word kept[i].first
+    uint64_t* keep_pk = nullptr;
+    uint32_t* keep_bk = nullptr;
+    uint64_t keep_cap = 0, keep_woff = 0;  // words allocated / used
+    bool keep_target = false;              // the estimate pass writes its streams there
+    bool kept_valid = false;
+    const uint8_t* kept_img = nullptr;
+    int kept_fmt = -1;
+    std::vector<kc_chunk> kept_chunks;
+    std::vector<std::pair<uint64_t, uint64_t>> kept;  // per batch: first word, symbol bound
+    uint64_t* d_kept_len = nullptr;                    // per batch: the stream length the tokenizer left
+    uint64_t kept_len_cap = 0;
     // windows per symbol of the batches being planned (1: tokenized input, where every symbol can
     // end a window; a received super-k-mer stream carries k symbols of context per run)
     double win_density = 1.0;
@@ -666,17 +679,31 @@ static int run_deferred(kc_ctx* c, const PackedView& sv, uint64_t syms, int mode
 }
 
 // pre: a symbol stream already in HBM (a received super-k-mer stream, kc_count_packed_device) of
-// `used` symbols instead of chunks to tokenize (src, nchunks and fmt unused)
+// `used` symbols instead of chunks to tokenize (src, nchunks and fmt unused); pre_len: the device
+// word holding its actual length when `used` only bounds it (a batch the estimate pass tokenized)
 static int run_batch(kc_ctx* c, const uint8_t* src, uint64_t used, uint64_t nchunks, int fmt, int pass, hipStream_t s,
                      hipEvent_t ev_start = nullptr, hipEvent_t ev_gather = nullptr, bool keep = false,
-                     bool host_gate = false, const PackedView* pre = nullptr) {
+                     bool host_gate = false, const PackedView* pre = nullptr, const uint64_t* pre_len = nullptr) {
     const uint64_t ntiles = used / TILE;
     if (!pre && ntiles == 0) return KC_OK;
     if (pre && used == 0) return KC_OK;
     if (pass == 3) {  // the distinct-count sketch (kc_estimate_distinct_device): tokenize + k_hll
-        HIPCHK(c, launch_tokenize(src, ntiles, c->d_chunks, (int)nchunks, fmt, c->d_tiles, c->d_touts, c->d_tblk,
-                                  PackedView{c->d_pk, c->d_bk}, used + nchunks, c->d_ctr, s));
-        HIPCHK(c, launch_hll(PackedView{c->d_pk, c->d_bk}, c->cfg.k, c->W, c->d_ctr, c->d_hll, s));
+        PackedView v{c->d_pk, c->d_bk};
+        const uint64_t words = (used + nchunks) / 32 + 4;
+        const bool kept = c->keep_target && c->keep_woff + words <= c->keep_cap && c->kept.size() < c->kept_len_cap;
+        if (kept) {  // (kept for the counting pass)
+            v = PackedView{c->keep_pk + c->keep_woff, c->keep_bk + c->keep_woff};
+            c->kept.emplace_back(c->keep_woff, used + nchunks);
+            c->keep_woff += words;
+        } else {
+            c->keep_target = false;
+        }
+        HIPCHK(c, launch_tokenize(src, ntiles, c->d_chunks, (int)nchunks, fmt, c->d_tiles, c->d_touts, c->d_tblk, v,
+                                  used + nchunks, c->d_ctr, s));
+        if (kept)  // the batch's stream length (the tokenizer's, below the bound)
+            HIPCHK(c, hipMemcpyAsync(c->d_kept_len + c->kept.size() - 1, &c->d_ctr->stream_len, 8,
+                                     hipMemcpyDeviceToDevice, s));
+        HIPCHK(c, launch_hll(v, c->cfg.k, c->W, c->d_ctr, c->d_hll, s));
         return KC_OK;
     }
     if (pass == 4) {  // super-k-mer routing (kc_route_superkmers_device): tokenize + k_skm_route
@@ -701,9 +728,13 @@ static int run_batch(kc_ctx* c, const uint8_t* src, uint64_t used, uint64_t nchu
     }
     const PackedView sv = pre ? *pre : PackedView{c->d_pk, c->d_bk};
     if (pre) {  // (the stream's length where the tokenizer would have left it)
-        HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)&c->d_ctr->stream_len, (int)(uint32_t)used, 1, s));
-        HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)((uint32_t*)&c->d_ctr->stream_len + 1), (int)(uint32_t)(used >> 32),
-                                    1, s));
+        if (pre_len) {
+            HIPCHK(c, hipMemcpyAsync(&c->d_ctr->stream_len, pre_len, 8, hipMemcpyDeviceToDevice, s));
+        } else {
+            HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)&c->d_ctr->stream_len, (int)(uint32_t)used, 1, s));
+            HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)((uint32_t*)&c->d_ctr->stream_len + 1),
+                                        (int)(uint32_t)(used >> 32), 1, s));
+        }
         nchunks = 0;
     } else {
         HIPCHK(c, launch_tokenize(src, ntiles, c->d_chunks, (int)nchunks, fmt, c->d_tiles, c->d_touts, c->d_tblk, sv,
@@ -1118,6 +1149,17 @@ static int device_pass(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, si
     DeferEnd defer_end{c};
     // level-1 reuse: the Bloom pass keeps its level-1 output if it is the job's only batch
     const bool keep = pass == 1 && c->bloom_batches == 0 && reuse_enabled() && single;
+    // the estimate pass's tokenized batches (kc_estimate_distinct_device), if this counting pass reads
+    // the same image, chunks and format: used once, then dropped
+    bool use_kept = false;
+    if (c->kept_valid && pass == 0 && img == c->kept_img && fmt == c->kept_fmt && n == c->kept_chunks.size()) {
+        use_kept = true;
+        for (size_t i = 0; i < n && use_kept; i++)
+            use_kept = chunks[i].off == c->kept_chunks[i].off && chunks[i].len == c->kept_chunks[i].len &&
+                       chunks[i].broken_header == c->kept_chunks[i].broken_header;
+    }
+    if (pass != 3) c->kept_valid = false;
+    size_t kept_i = 0;
     // a counting pass of several batches defers level 3 (kc_ctx defer_*) when the segmented levels
     // run and HBM holds at least two batches' level-2 segments beside everything else
     c->defer_on = false;
@@ -1162,7 +1204,15 @@ static int device_pass(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, si
         // image; the batches of a larger image keep the device gate (kc_api.h: kc_count_device)
         // -- or a deferred pass, which reads each batch's flags
         c->defer_last = last;
-        int r = run_batch(c, img, used, batch.size(), fmt, pass, s, e0, e1, keep, single);
+        int r;
+        if (use_kept && kept_i < c->kept.size()) {
+            const PackedView kv{c->keep_pk + c->kept[kept_i].first, c->keep_bk + c->kept[kept_i].first};
+            r = run_batch(c, img, c->kept[kept_i].second, 0, fmt, pass, s, e0, e1, keep, single, &kv,
+                          c->d_kept_len + kept_i);
+            kept_i++;
+        } else {
+            r = run_batch(c, img, used, batch.size(), fmt, pass, s, e0, e1, keep, single);
+        }
         if (keep) HIPCHK(c, hipStreamWaitEvent(s, c->aev[1], 0));  // (before an error return, too)
         if (r) return r;
         if (keep && c->reuse_kept) {
@@ -1363,6 +1413,9 @@ void kc_destroy(kc_ctx* c) {
     hipFree(c->d_sum);
     hipFree(c->d_hll);
     hipFree(c->d_skm);
+    hipFree(c->keep_pk);
+    hipFree(c->keep_bk);
+    hipFree(c->d_kept_len);
     hipFree(c->d_cwords);
     hipFree(c->d_csecond);
     hipFree(c->d_cstat);
@@ -1501,8 +1554,39 @@ int kc_estimate_distinct_device(kc_ctx* c, const uint8_t* img, const kc_chunk* c
     if (!c->d_hll && hipMalloc(&c->d_hll, HLL_M * 4) != hipSuccess)
         return c->fail(KC_ERR_NOMEM, "sketch allocation failed");
     HIPCHK(c, hipMemsetAsync(c->d_hll, 0, HLL_M * 4, s));
+    // the tokenized batches are kept for the counting pass when they take < 1/8 of the free HBM
+    c->kept_valid = false;
+    c->kept.clear();
+    c->keep_woff = 0;
+    c->keep_target = false;
+    {
+        uint64_t words = 64;
+        for (size_t i = 0; i < n; i++) words += (round_up(chunks[i].len, TILE) + 1) / 32 + 5;
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) == hipSuccess) {
+            if (words > c->keep_cap && (double)words * 12 < (double)(fr + c->keep_cap * 12) / 8) {
+                hipFree(c->keep_pk);
+                hipFree(c->keep_bk);
+                c->keep_pk = nullptr;
+                c->keep_bk = nullptr;
+                c->keep_cap = 0;
+                if (hipMalloc(&c->keep_pk, words * 8) == hipSuccess && hipMalloc(&c->keep_bk, words * 4) == hipSuccess)
+                    c->keep_cap = words;
+            }
+            if (!c->d_kept_len && hipMalloc(&c->d_kept_len, 8192 * 8) == hipSuccess) c->kept_len_cap = 8192;
+            c->keep_target = c->keep_cap >= words && c->kept_len_cap > 0;
+        }
+    }
     int rc = device_pass(c, img, chunks, n, fmt, 3, s);
+    const bool kept = c->keep_target;
+    c->keep_target = false;
     if (rc) return rc;
+    if (kept) {
+        c->kept_valid = true;
+        c->kept_img = img;
+        c->kept_fmt = fmt;
+        c->kept_chunks.assign(chunks, chunks + n);
+    }
     std::vector<uint32_t> reg(HLL_M);
     HIPCHK(c, hipMemcpyAsync(reg.data(), c->d_hll, HLL_M * 4, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
@@ -2149,6 +2233,7 @@ int kc_reset(kc_ctx* c) {
     c->defer_n = 0;
     c->defer_on = c->defer_last = false;
     c->broken.clear();
+    c->kept_valid = false;
     return KC_OK;
 }
 

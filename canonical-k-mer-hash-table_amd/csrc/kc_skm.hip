@@ -1,7 +1,7 @@
 // kc_skm.hip -- super-k-mer routing for the multi-GPU exchange.
 //
 // The owner of a canonical k-mer is a hash of its canonical minimizer: the smallest value of
-// h(canonical m-mer) over the k - m + 1 m-mers of the k-mer.  A k-mer and its reverse complement
+// h(canonical m-mer) over the k - m + 1 m-mers of the k-mer, mixed again (skm_owner).  A k-mer and its reverse complement
 // hold the same canonical m-mers, so every occurrence of a canonical k-mer goes to one owner
 // (exact counts, as SURVEY 8e's hash-prefix owner), and consecutive windows of a read share their
 // minimizer -- and so their owner -- for ~(k - m + 2) / 2 windows on average.  A maximal run of r
@@ -31,6 +31,18 @@ constexpr uint32_t SKM_BROKEN = 0xFFFFFFFFu;
 DEV uint32_t mmer_hash(uint64_t canon) {
     const uint32_t h = (uint32_t)(fmix64(canon ^ SKM_SEED) >> 32);
     return h == SKM_BROKEN ? SKM_BROKEN - 1 : h;
+}
+
+// the owner of a minimizer value: the minimum of w uniform hashes is small, so it is mixed again
+// (murmur3's fmix32) before the multiply-shift onto the owners
+DEV uint32_t skm_owner(uint32_t minh, uint32_t nshards) {
+    uint32_t h = minh;
+    h ^= h >> 16;
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+    h *= 0xC2B2AE35u;
+    h ^= h >> 16;
+    return (uint32_t)(((uint64_t)h * nshards) >> 32);
 }
 
 // 32 symbols starting at symbol s (s may be negative or unaligned; symbols before 0 read as 0)
@@ -166,7 +178,7 @@ __global__ __launch_bounds__(SKM_T) void k_skm_route(PackedView sv, const DevCou
 #pragma unroll
             for (int j = 0; j < SKM_RUN; j++) {
                 const bool valid = t0 + j0 + j < t1 && mx[j] != SKM_BROKEN;
-                own[j] = valid ? (uint8_t)(((uint64_t)mn[j] * nshards) >> 32) : 0xFF;
+                own[j] = valid ? (uint8_t)skm_owner(mn[j], nshards) : 0xFF;
                 if (j0 + j < SKM_TP) s_ow[j0 + j] = own[j];
             }
         }

@@ -152,7 +152,10 @@ int kc_count_device(kc_ctx* ctx, const uint8_t* dev_image, const kc_chunk* chunk
  * (~0.8 % standard error), so a caller can size a table (kc_config.table_slots) before
  * counting, e.g. a rank's local table in a sharded job.  Counts nothing and leaves the
  * table alone; the call waits for its work (the estimate is a host value).  Any context of
- * the same k can run it (its table size does not matter). */
+ * the same k can run it (its table size does not matter).  When HBM allows, the context keeps
+ * the tokenized batches (3/8 byte per input byte) for its next kc_count_device over the same
+ * image pointer, chunk table and format, which then skips its tokenizer: the caller must not
+ * change the image's bytes in between (kc_reset or any other pass drops them). */
 int kc_estimate_distinct_device(kc_ctx* ctx, const uint8_t* dev_image, const kc_chunk* chunks, size_t n_chunks,
                                 int fmt, void* hip_stream, double* estimate);
 /* Size the device table of the job about to be counted (after kc_create or kc_reset, before

@@ -17,10 +17,11 @@ import os
 import sys
 from collections import defaultdict
 
-# the roofline window: the tokenizer + the counting pass (+ the reuse checksum beside them)
+# the roofline window: the tokenizer + the counting pass (+ the reuse checksum beside them; the
+# distinct estimate of the strong presets, whose tokenized batches the counting pass reads)
 COUNT_PASS = ("k_p1<", "k_p2<", "k_p2f<", "k_p3<", "k_b3<", "k_bf3<", "k_bprobe<", "k_scanA", "k_scanB", "k_scanC",
               "k_count<", "k_tile_map", "k_tile_summary", "k_tscan_block", "k_tscan_top", "k_zero_edges", "k_emit",
-              "k_checksum")
+              "k_checksum", "k_hll<", "k_skm_route")
 # FETCH_SIZE / WRITE_SIZE unit: 1023.99998 bytes per unit measured in r01_v5 against
 # k_gather's WRITE_SIZE for a known byte count (k_gather no longer exists: the tokenizer
 # reads device images in place), i.e. the counters are in KiB.

@@ -3,8 +3,9 @@ infrastructure: the canonical-minimizer owner of every window of a sequence, the
 stream format (kc_internal.h PackedView) both ways, and a host router that produces the same
 per-owner streams the device kernel does (up to the order of the super-k-mers).
 
-owner(window) = (min over its k - m + 1 m-mers of h(canonical m-mer)) * G >> 32, with
-h(x) = fmix64(x ^ SKM_SEED) >> 32 (0xFFFFFFFF -> 0xFFFFFFFE), m = min(15, k) by default.
+owner(window) = fmix32(min over its k - m + 1 m-mers of h(canonical m-mer)) * G >> 32, with
+h(x) = fmix64(x ^ SKM_SEED) >> 32 (0xFFFFFFFF -> 0xFFFFFFFE), m = min(15, k) by default (the
+minimum of many uniform hashes is small: mixed again before it picks an owner).
 """
 import numpy as np
 
@@ -47,6 +48,16 @@ def mmer_hashes(codes, m):
     return np.where(bad, BROKEN, h).astype(np.uint64)
 
 
+def fmix32(h):
+    h = h.astype(np.uint64) & np.uint64(0xFFFFFFFF)
+    h ^= h >> np.uint64(16)
+    h = (h * np.uint64(0x85EBCA6B)) & np.uint64(0xFFFFFFFF)
+    h ^= h >> np.uint64(13)
+    h = (h * np.uint64(0xC2B2AE35)) & np.uint64(0xFFFFFFFF)
+    h ^= h >> np.uint64(16)
+    return h
+
+
 def window_owners(codes, k, G, m=0):
     """Owner of the window ending at every position p >= k - 1 (index p - k + 1), -1 if invalid."""
     m = m or min(DEFAULT_M, k)
@@ -56,7 +67,7 @@ def window_owners(codes, k, G, m=0):
         return np.zeros(0, dtype=np.int64)
     hw = np.lib.stride_tricks.sliding_window_view(h, w)
     mn, mx = hw.min(axis=1), hw.max(axis=1)
-    own = ((mn * np.uint64(G)) >> np.uint64(32)).astype(np.int64)
+    own = ((fmix32(mn) * np.uint64(G)) >> np.uint64(32)).astype(np.int64)
     return np.where(mx == BROKEN, -1, own)
 
 

@@ -89,6 +89,9 @@ def test_two_rank_line_rehearsed_on_one_gpu_matches_one_gpu():
     d2 = _json_line(p2.stdout)
     assert d2["n_gpus"] == 2 and d2["scaling"] == "strong" and d2["config"]["workload"].startswith("C4")
     assert "xgmi" in d2 and d2["xgmi"]["sent_bytes_per_step_per_rank"] > 0 and "c2" in d2
+    # (the strong line takes the super-k-mer exchange: bytes per window sent and the G = 2/4/8 model)
+    assert d2["xgmi"]["exchange"] == "superkmers" and set(d2["xgmi"]["model_sent_bytes_per_rank"]) == {"2", "4", "8"}
+    assert 0.2 < d2["xgmi"]["bytes_per_window_sent"] < 3.0
     p1 = subprocess.run([sys.executable, BENCH, "--config", "C4"] + common, capture_output=True, text=True,
                         timeout=300, env=_env())
     assert p1.returncode == 0, p1.stderr[-3000:]

@@ -2,7 +2,9 @@
 gloo (the device tensors of the exchange cross through host memory; on a node the same code
 runs over RCCL).  Every rank runs ShardedCounter with the HIP DeviceEngine on its share of the
 reference chunks (every other chunk): the Bloom pass and the filter combine (-b), the local
-count, the pre-aggregated merge (kc_route_table_device -> all-to-all -> kc_insert_counts_*).
+count, the pre-aggregated merge (kc_route_table_device -> all-to-all -> kc_insert_counts_*) -- or the
+super-k-mer exchange (kc_route_superkmers_device -> two all-to-alls -> kc_count_packed_device, and
+the owners' own Bloom passes over what they receive).
 The union of the owners' outputs must equal the reference's output on the whole input
 (tests/golden/cases.json); the reference's single shared table is kmer_hash_table.cpp:2207.
 """
@@ -46,7 +48,7 @@ def _options(args):
     return o
 
 
-def _rank(rank, world, port, path, k, args, out_dir):
+def _rank(rank, world, port, path, k, args, out_dir, exchange="records"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch
     import torch.distributed as dist
@@ -63,7 +65,7 @@ def _rank(rank, world, port, path, k, args, out_dir):
     img = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
     cfg = ka.Config(k=k, mode=o["mode"], table_slots=o["slots"] or (1 << 20), bf_enable=o["bf"],
                     est_unique=o["u"], fpr=o["fpr"], min_abundance=o["a"])
-    sc = ShardedCounter(cfg, dist)
+    sc = ShardedCounter(cfg, dist, exchange=exchange)
     stream = torch.cuda.current_stream().cuda_stream
     if o["bf"]:
         sc.bloom_device(img.data_ptr(), mine, ka.FMT_FASTA, stream)
@@ -82,15 +84,16 @@ def _rank(rank, world, port, path, k, args, out_dir):
 
 
 @pytest.mark.timeout(300)
+@pytest.mark.parametrize("exchange", ["records", "superkmers"])
 @pytest.mark.parametrize("name,k,args", PICK, ids=[f"{n}-k{k}" for n, k, _ in PICK])
-def test_two_processes_equal_the_reference(name, k, args, golden_input, tmp_path):
+def test_two_processes_equal_the_reference(name, k, args, exchange, golden_input, tmp_path):
     import torch.multiprocessing as mp
 
     import kaarme_amd as ka
 
     case = CASES[(name, k, args)]
     path = golden_input(name)
-    mp.start_processes(_rank, args=(2, _free_port(), path, k, args, str(tmp_path)), nprocs=2, join=True,
+    mp.start_processes(_rank, args=(2, _free_port(), path, k, args, str(tmp_path), exchange), nprocs=2, join=True,
                        start_method="spawn")
     recs = [np.load(tmp_path / f"r{r}.npy") for r in range(2)]
     keys = [set(map(tuple, r[:, :-1].tolist())) for r in recs]

@@ -59,6 +59,8 @@ def test_superkmers_match_the_model(k, G, tmp_path):
         w = sum(len(s) - k + 1 for s in got)
         assert w == wins[o] == sum(len(s) - k + 1 for s in model[o]), o
         total += w
+        if not got:
+            continue
         # the same windows: the oracle's counts over the device's and the model's super-k-mers
         a, b = tmp_path / f"dev{o}.txt", tmp_path / f"mod{o}.txt"
         a.write_text("".join(s + "\n" for s in got))

@@ -31,6 +31,17 @@ def test_owner_is_strand_symmetric():
             assert (a == b[::-1]).all() and (a >= 0).all() and (a < G).all()
 
 
+def test_owners_are_balanced():
+    """Every owner gets about 1/G of the windows (the minimizer value is mixed before it picks an
+    owner: its raw value, a minimum of many hashes, is small)."""
+    rng = np.random.default_rng(4)
+    seq = "".join("ACGT"[x] for x in rng.integers(0, 4, 200_000))
+    for k, G in ((31, 3), (51, 8)):
+        own = sm.window_owners(sm.CODE[np.frombuffer(seq.encode(), np.uint8)], k, G)
+        share = np.bincount(own, minlength=G) / len(own)
+        assert share.min() > 0.5 / G and share.max() < 1.5 / G, share
+
+
 def test_superkmers_cover_every_window_once():
     rng = np.random.default_rng(3)
     seqs = _seqs(200, rng, 10, 400)
