@@ -706,16 +706,28 @@ def run_workload(args, env, image=None):
                         "route = the local table as owner-grouped records (host waits for its counts), "
                         "owner insert = the received records into the owner table (waited for)"}
         if job.exchange == "superkmers":
-            # bytes per rank of the super-k-mer exchange at G ranks, from this run's words per window:
-            # every rank sends (G - 1) / G of its windows' super-k-mers, 12 bytes per 32 symbols
+            # bytes per rank of the super-k-mer exchange at G ranks, from this run's bytes per window: a run
+            # of r windows costs k + r symbols (12 bytes per 32); runs of one owner merge consecutive
+            # super-k-mers, r_G = r_1 G / (G - 1), so r_1 follows from this run's r_world; every rank sends
+            # (G - 1) / G of its 1/G of the job's windows
             bpw = sent / args.steps / max(1, windows_expected) * world / max(1, world - 1)
+            spw = bpw / (12 / 32)
+            r1 = k / max(spw - 1, 1e-6) * (world - 1) / world
             total_w = args.reads * (L - k + 1) if strong else windows_expected * world
+
+            def bpw_at(G):
+                r = r1 * G / (G - 1)
+                return (k + r) / r * 12 / 32
+
             xgmi["bytes_per_window_sent"] = round(bpw, 4)
-            xgmi["model_sent_bytes_per_rank"] = {str(G): int(total_w / G * bpw * (G - 1) / G) for G in (2, 4, 8)}
+            xgmi["superkmer_windows_per_run"] = round(r1, 2)
+            xgmi["model_sent_bytes_per_rank"] = {str(G): int(total_w / G * bpw_at(G) * (G - 1) / G) for G in (2, 4, 8)}
+            xgmi["records_design_bytes_per_rank"] = "~10.8 GB at G = 8 for C4 (DESIGN 4; round 5's exchange)"
             xgmi["note"] = ("max over ranks; two all-to-alls (packed symbol words, break words) of the canonical-"
                             "minimizer super-k-mers + their count/sum headers; route = tokenizer + k_skm_route + the "
                             "send buffers; owner insert = kc_count_packed_device of the received streams (waited "
-                            "for); model = the job's windows / G x bytes_per_window_sent x (G - 1) / G")
+                            "for); model = the job's windows / G x the bytes per window at G (superkmer_windows_per_run, runs of one owner "
+                            "merging G / (G - 1) super-k-mers) x (G - 1) / G")
     st = counter.finish()  # raises on table overflow
     if rank == 0:
         log(f"{args.config}: {args.steps} steps in {elapsed:.3f} s; parity / writer records")

@@ -189,7 +189,9 @@ struct kc_ctx {
     std::vector<kc_chunk> kept_chunks;
     std::vector<std::pair<uint64_t, uint64_t>> kept;  // per batch: first word, symbol bound
     uint64_t* d_kept_len = nullptr;                    // per batch: the stream length the tokenizer left
+    uint64_t* d_kept_win = nullptr;                    // per batch: the estimate pass's windows so far
     uint64_t kept_len_cap = 0;
+    double kept_density = 1.0;                         // the kept batches' largest windows per symbol
     // windows per symbol of the batches being planned (1: tokenized input, where every symbol can
     // end a window; a received super-k-mer stream carries k symbols of context per run)
     double win_density = 1.0;
@@ -704,6 +706,9 @@ static int run_batch(kc_ctx* c, const uint8_t* src, uint64_t used, uint64_t nchu
             HIPCHK(c, hipMemcpyAsync(c->d_kept_len + c->kept.size() - 1, &c->d_ctr->stream_len, 8,
                                      hipMemcpyDeviceToDevice, s));
         HIPCHK(c, launch_hll(v, c->cfg.k, c->W, c->d_ctr, c->d_hll, s));
+        if (kept)  // the windows so far (the batch's: the difference to the previous batch's)
+            HIPCHK(c, hipMemcpyAsync(c->d_kept_win + c->kept.size() - 1, &c->d_ctr->est_windows, 8,
+                                     hipMemcpyDeviceToDevice, s));
         return KC_OK;
     }
     if (pass == 4) {  // super-k-mer routing (kc_route_superkmers_device): tokenize + k_skm_route
@@ -1160,6 +1165,13 @@ static int device_pass(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, si
     }
     if (pass != 3) c->kept_valid = false;
     size_t kept_i = 0;
+    // (a pass over kept batches sizes its partition levels for their windows per symbol)
+    struct Density {
+        kc_ctx* c;
+        double d;
+        ~Density() { c->win_density = d; }
+    } restore_density{c, c->win_density};
+    if (use_kept) c->win_density = c->kept_density;
     // a counting pass of several batches defers level 3 (kc_ctx defer_*) when the segmented levels
     // run and HBM holds at least two batches' level-2 segments beside everything else
     c->defer_on = false;
@@ -1416,6 +1428,7 @@ void kc_destroy(kc_ctx* c) {
     hipFree(c->keep_pk);
     hipFree(c->keep_bk);
     hipFree(c->d_kept_len);
+    hipFree(c->d_kept_win);
     hipFree(c->d_cwords);
     hipFree(c->d_csecond);
     hipFree(c->d_cstat);
@@ -1573,15 +1586,31 @@ int kc_estimate_distinct_device(kc_ctx* c, const uint8_t* img, const kc_chunk* c
                 if (hipMalloc(&c->keep_pk, words * 8) == hipSuccess && hipMalloc(&c->keep_bk, words * 4) == hipSuccess)
                     c->keep_cap = words;
             }
-            if (!c->d_kept_len && hipMalloc(&c->d_kept_len, 8192 * 8) == hipSuccess) c->kept_len_cap = 8192;
+            if (!c->d_kept_len && hipMalloc(&c->d_kept_len, 8192 * 8) == hipSuccess &&
+                hipMalloc(&c->d_kept_win, 8192 * 8) == hipSuccess)
+                c->kept_len_cap = 8192;
             c->keep_target = c->keep_cap >= words && c->kept_len_cap > 0;
         }
     }
+    HIPCHK(c, hipMemsetAsync(&c->d_ctr->est_windows, 0, 8, s));
     int rc = device_pass(c, img, chunks, n, fmt, 3, s);
     const bool kept = c->keep_target;
     c->keep_target = false;
     if (rc) return rc;
     if (kept) {
+        // the kept batches' windows per symbol: the counting pass sizes its segments for them (a batch
+        // of 150 bp reads holds 0.62 windows per symbol at k = 51; sized per symbol, C4's deferred
+        // level-2 slots were 2.1 x its records and a pass took two groups)
+        std::vector<uint64_t> wins(c->kept.size()), lens(c->kept.size());
+        HIPCHK(c, hipMemcpyAsync(wins.data(), c->d_kept_win, wins.size() * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(lens.data(), c->d_kept_len, lens.size() * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        double d = 0;
+        for (size_t i = 0; i < wins.size(); i++) {
+            const uint64_t w = wins[i] - (i ? wins[i - 1] : 0);
+            d = std::max(d, (double)w / (double)std::max<uint64_t>(1, lens[i]));
+        }
+        c->kept_density = std::min(1.0, d * 1.02 + 0.005);
         c->kept_valid = true;
         c->kept_img = img;
         c->kept_fmt = fmt;

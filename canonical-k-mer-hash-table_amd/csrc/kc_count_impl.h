@@ -3220,6 +3220,7 @@ __global__ __launch_bounds__(HLL_T) void k_hll(PackedView sv, int k, const DevCo
     __syncthreads();
     const RollConst rk = make_roll<W>(k, pow5_k, pow5_km1);
     int par = 0;
+    uint32_t nwin = 0;
     for (uint64_t t0 = lo; t0 < hi; t0 += TW) {
         const uint64_t t1 = min(t0 + TW, hi), r0 = t0 + (uint64_t)tid * RUNW;
         const bool nxt = t0 + TW < hi && tid < SW;
@@ -3229,6 +3230,7 @@ __global__ __launch_bounds__(HLL_T) void k_hll(PackedView sv, int k, const DevCo
         if (r0 < t1)
             run_windows_src<W, RUNW>(PkStage{st_pk + par * SW, st_bk + par * SW, (int64_t)(t0 >> 5) - (W + 1)}, r0,
                                      t1, rk, [&](int, bool valid, const uint64_t (&fwd)[W], const uint64_t (&rc)[W]) {
+                nwin += valid;
                 uint64_t key[W], tk[W];
                 canonical<W>(fwd, rc, key);
                 to_tkey<W>(key, tk);
@@ -3246,6 +3248,7 @@ __global__ __launch_bounds__(HLL_T) void k_hll(PackedView sv, int k, const DevCo
     }
     for (uint32_t i = tid; i < HLL_M; i += HLL_T)
         if (r[i]) atomicMax(&regs[i], r[i]);
+    block_add4(nwin, 0, 0, 0, &const_cast<DevCounters*>(ctr)->est_windows, nullptr, nullptr, nullptr);
 }
 
 template <int W>

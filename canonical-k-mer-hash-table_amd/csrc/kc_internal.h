@@ -80,6 +80,9 @@ struct DevCounters {
     unsigned long long heavy;           uint64_t _p16[15];
     // deferred level 3: a batch's part_overflow held aside while the group's level 3 runs
     unsigned long long held_overflow;   uint64_t _p19[15];
+    // the distinct estimate's pass: valid windows (sizes the partition levels of the counting pass that
+    // reads its tokenized batches)
+    unsigned long long est_windows;     uint64_t _p20[15];
 };
 
 // The symbol stream: 32 symbols per word, symbol j of word w at bits 62-2j of pk[w]

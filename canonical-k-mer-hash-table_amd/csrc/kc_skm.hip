@@ -20,11 +20,12 @@
 
 namespace kc {
 
-constexpr int SKM_T = 256;             // threads per workgroup
-constexpr int SKM_RUN = 16;            // window ends per thread
+constexpr int SKM_T = 512;             // threads per workgroup
+constexpr int SKM_RUN = 8;             // window ends per thread
 constexpr int SKM_TP = SKM_T * SKM_RUN;  // window ends per tile
 constexpr int SKM_MAXW = MAX_K;        // most m-mers per window (k - m + 1 <= k)
-constexpr int SKM_STAGE = 2048;        // staged output words per tile (65 536 symbols)
+constexpr int SKM_STAGE = 1024;        // staged output words per tile (32 768 symbols)
+constexpr int SKM_IN = (SKM_TP + SKM_MAXW) / 32 + 4;  // staged input words per tile
 constexpr uint32_t SKM_BROKEN = 0xFFFFFFFFu;
 
 // h(canonical m-mer) in 32 bits, never SKM_BROKEN
@@ -45,23 +46,27 @@ DEV uint32_t skm_owner(uint32_t minh, uint32_t nshards) {
     return (uint32_t)(((uint64_t)h * nshards) >> 32);
 }
 
-// 32 symbols starting at symbol s (s may be negative or unaligned; symbols before 0 read as 0)
-DEV uint64_t load32_at(const uint64_t* __restrict__ pk, int64_t s) {
-    const int64_t w = s >> 5;  // (arithmetic shift: floor)
+// 32 symbols starting at symbol s of the tile's staged input words (word wlo of the stream at
+// stage index 0; s >= 32 wlo)
+DEV uint64_t load32_at(const uint64_t* __restrict__ st, int64_t wlo, int64_t s) {
+    const int64_t w = (s >> 5) - wlo;  // (arithmetic shift: floor)
     const int o = (int)(s & 31);
-    const uint64_t a = w >= 0 ? pk[w] : 0, b = w + 1 >= 0 ? pk[w + 1] : 0;
+    const uint64_t a = st[w], b = st[w + 1];
     return o ? (a << (2 * o)) | (b >> (64 - 2 * o)) : a;
 }
 
 // Write `len` symbols starting at input symbol `src` into the output at symbol `dst` (a break
 // symbol precedes them at dst - 1, set by the caller), OR-ing words into an LDS stage or, for
 // a tile whose output does not fit the stage, its global range.
-DEV void put_symbols(uint64_t* __restrict__ opk, const uint64_t* __restrict__ pk, int64_t src, uint64_t dst,
-                     uint64_t len) {
+DEV void put_symbols(uint64_t* __restrict__ opk, const uint64_t* __restrict__ st, int64_t wlo, int64_t src,
+                     uint64_t dst, uint64_t len) {
     const uint64_t w0 = dst >> 5, w1 = (dst + len - 1) >> 5;
     for (uint64_t w = w0; w <= w1; w++) {
-        const int64_t s0 = src + (int64_t)(w * 32) - (int64_t)dst;  // input symbol of output slot 32w
-        uint64_t v = load32_at(pk, s0);
+        // input symbol of output slot 32w (before src for the first word: those slots are masked off,
+        // and the stage holds a word before src's)
+        const int64_t s0 = max(src + (int64_t)(w * 32) - (int64_t)dst, (int64_t)(wlo * 32));
+        uint64_t v = load32_at(st, wlo, s0);
+        if (src + (int64_t)(w * 32) - (int64_t)dst < s0) v >>= 2 * (s0 - (src + (int64_t)(w * 32) - (int64_t)dst));
         // keep the output slots [dst, dst + len) of this word
         const uint64_t lo = w * 32 < dst ? dst - w * 32 : 0;
         const uint64_t hi = (w + 1) * 32 > dst + len ? dst + len - w * 32 : 32;
@@ -81,81 +86,96 @@ __global__ __launch_bounds__(SKM_T) void k_skm_route(PackedView sv, const DevCou
                                                      unsigned long long* __restrict__ cursor,
                                                      unsigned long long* __restrict__ wins,
                                                      unsigned long long* __restrict__ ovf) {
-    __shared__ uint32_t s_h[SKM_TP + SKM_MAXW];
+    // s_u: the m-mer hashes (steps 1-2), then each window end's run length and offset (steps 3-5)
+    constexpr int NU = (SKM_TP + SKM_MAXW) > (SKM_TP * 3 / 2) ? (SKM_TP + SKM_MAXW) : (SKM_TP * 3 / 2);
+    __shared__ uint32_t s_u[NU];
+    uint32_t* s_h = s_u;
+    uint32_t* s_off = s_u;                                          // [SKM_TP]
+    uint16_t* s_run = reinterpret_cast<uint16_t*>(s_u + SKM_TP);   // [SKM_TP]
+    __shared__ uint64_t s_ipk[SKM_IN + 1];  // the tile's input words (symbols t0 - k + 1 .. t1)
+    __shared__ uint32_t s_ibk[SKM_IN + 1];
     __shared__ uint8_t s_ow[SKM_TP];
     __shared__ uint64_t s_pk[SKM_STAGE];
     __shared__ uint32_t s_bk[SKM_STAGE];
     __shared__ uint32_t s_cnt[SKM_MAX_SHARDS], s_win[SKM_MAX_SHARDS], s_lbase[SKM_MAX_SHARDS + 1];
     __shared__ unsigned long long s_gbase[SKM_MAX_SHARDS];
     __shared__ int s_direct;
+    __shared__ uint32_t s_wmin[SKM_T / 64];
     const int tid = threadIdx.x;
     const uint64_t M = ctr->stream_len;
     const int w = k - m + 1;  // m-mers per window
     const uint64_t mmask = m >= 32 ? ~0ULL : (1ULL << (2 * m)) - 1;
     const int rsh = 64 - 2 * m;
     const uint64_t ntiles = (M + SKM_TP - 1) / SKM_TP;
+    const int j0 = tid * SKM_RUN;  // first window end of this thread (tile-relative)
     for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const uint64_t t0 = tile * SKM_TP, t1 = min(t0 + SKM_TP, M);
+        const int tlen = (int)(t1 - t0);
+        // 0. the tile's input words into LDS: symbols t0 - k + 1 .. t1 (+ one word: 32-symbol loads)
+        const int64_t wlo = ((int64_t)t0 - (k - 1)) >> 5;
+        const int nin = (int)((int64_t)((t1 - 1) >> 5) + 2 - wlo);
+        for (int i = tid; i < nin; i += SKM_T) {
+            const int64_t gw = wlo + i;
+            const bool in = gw >= 0 && (uint64_t)gw <= ((M - 1) >> 5) + 1;
+            s_ipk[i] = in ? sv.pk[gw] : 0;
+            s_ibk[i] = in ? sv.bk[gw] : 0xFFFFFFFFu;
+        }
+        if (tid < (int)nshards) {
+            s_cnt[tid] = 0;
+            s_win[tid] = 0;
+        }
+        __syncthreads();
         // 1. the hashes of the m-mers ending at t0 - w + 1 .. t1 - 1 (broken: a break symbol inside,
         //    or the m-mer starts before the stream)
-        const int nh = (int)(t1 - t0) + w - 1;
+        const int nh = tlen + w - 1;
         for (int i = tid; i < nh; i += SKM_T) {
             const int64_t q = (int64_t)t0 - (w - 1) + i;  // last symbol of the m-mer
             const int64_t a = q - m + 1;
             uint32_t h = SKM_BROKEN;
             if (a >= 0) {
-                const uint64_t wa = (uint64_t)a >> 5, wq = (uint64_t)q >> 5;
-                uint32_t br = sv.bk[wa] & (0xFFFFFFFFu >> (a & 31));
-                if (wq != wa) br = br ? br : (sv.bk[wq] & (0xFFFFFFFFu << (31 - (q & 31))));
+                const int64_t wa = (a >> 5) - wlo, wq = (q >> 5) - wlo;
+                uint32_t br = s_ibk[wa] & (0xFFFFFFFFu >> (a & 31));
+                if (wq != wa) br = br ? br : (s_ibk[wq] & (0xFFFFFFFFu << (31 - (q & 31))));
                 else br &= 0xFFFFFFFFu << (31 - (q & 31));
                 if (!br) {
-                    const uint64_t x = (load32_at(sv.pk, a) >> rsh) & mmask;  // m symbols, oldest first
+                    const uint64_t x = (load32_at(s_ipk, wlo, a) >> rsh) & mmask;  // m symbols, oldest first
                     const uint64_t rc = (rev2(~x) >> rsh) & mmask;
                     h = mmer_hash(x < rc ? x : rc);
                 }
             }
             s_h[i] = h;
         }
-        if (tid < (int)nshards) {
-            s_cnt[tid] = 0;
-            s_win[tid] = 0;
-        }
-        if (tid == 0) s_direct = 0;
         __syncthreads();
-        // 2. per window end: valid (no broken m-mer among its w) and the minimizer -> owner
-        const int j0 = tid * SKM_RUN;  // first window end of this thread (tile-relative)
-        uint8_t own[SKM_RUN];
+        // 2. per window end: valid (no broken m-mer among its w) and the minimizer -> owner.  Window j
+        //    covers s_h[j0 + j .. j0 + j + w - 1]: for w >= SKM_RUN the part common to the thread's
+        //    SKM_RUN windows [j0 + SKM_RUN - 1, j0 + w - 1], a left part [j0 + j, j0 + SKM_RUN - 2]
+        //    (suffixes) and a right part [j0 + w, j0 + w + j - 1] (prefixes): w + 2 SKM_RUN reads
         {
-            // window end p = t0 + j covers the m-mers ending at p - w + 1 .. p, i.e. s_h[j .. j + w - 1]
+            auto hv = [&](int i) { return i < nh ? s_h[i] : SKM_BROKEN; };
             uint32_t mn[SKM_RUN], mx[SKM_RUN];
             if (w >= SKM_RUN) {
-                // window j covers s_h[j0 + j .. j0 + j + w - 1]: the part common to the thread's
-                // SKM_RUN windows [j0 + SKM_RUN - 1, j0 + w - 1], a left part [j0 + j, j0 + SKM_RUN - 2]
-                // (suffixes) and a right part [j0 + w, j0 + w + j - 1] (prefixes): w + 2 SKM_RUN reads
                 uint32_t cmn = SKM_BROKEN, cmx = 0;
                 for (int i = j0 + SKM_RUN - 1; i <= j0 + w - 1; i++) {
-                    const uint32_t h = i < nh ? s_h[i] : SKM_BROKEN;
+                    const uint32_t h = hv(i);
                     cmn = min(cmn, h);
                     cmx = max(cmx, h);
                 }
-                uint32_t ln = SKM_BROKEN, lx = 0;
+                uint32_t ln = cmn, lx = cmx;
 #pragma unroll
                 for (int j = SKM_RUN - 1; j >= 0; j--) {
                     if (j < SKM_RUN - 1) {
-                        const int i = j0 + j;
-                        const uint32_t h = i < nh ? s_h[i] : SKM_BROKEN;
+                        const uint32_t h = hv(j0 + j);
                         ln = min(ln, h);
                         lx = max(lx, h);
                     }
-                    mn[j] = min(ln, cmn);
-                    mx[j] = max(lx, cmx);
+                    mn[j] = ln;
+                    mx[j] = lx;
                 }
                 uint32_t rn = SKM_BROKEN, rx = 0;
 #pragma unroll
                 for (int j = 0; j < SKM_RUN; j++) {
                     if (j > 0) {
-                        const int i = j0 + w + j - 1;
-                        const uint32_t h = i < nh ? s_h[i] : SKM_BROKEN;
+                        const uint32_t h = hv(j0 + w + j - 1);
                         rn = min(rn, h);
                         rx = max(rx, h);
                     }
@@ -167,7 +187,7 @@ __global__ __launch_bounds__(SKM_T) void k_skm_route(PackedView sv, const DevCou
                 for (int j = 0; j < SKM_RUN; j++) {
                     uint32_t a = SKM_BROKEN, b = 0;
                     for (int i = j0 + j; i < j0 + j + w; i++) {
-                        const uint32_t h = i < nh ? s_h[i] : SKM_BROKEN;
+                        const uint32_t h = hv(i);
                         a = min(a, h);
                         b = max(b, h);
                     }
@@ -175,28 +195,55 @@ __global__ __launch_bounds__(SKM_T) void k_skm_route(PackedView sv, const DevCou
                     mx[j] = b;
                 }
             }
+            __syncthreads();  // (s_h is read no more: its space holds the runs below)
 #pragma unroll
             for (int j = 0; j < SKM_RUN; j++) {
-                const bool valid = t0 + j0 + j < t1 && mx[j] != SKM_BROKEN;
-                own[j] = valid ? (uint8_t)skm_owner(mn[j], nshards) : 0xFF;
-                if (j0 + j < SKM_TP) s_ow[j0 + j] = own[j];
+                const bool valid = j0 + j < tlen && mx[j] != SKM_BROKEN;
+                s_ow[j0 + j] = valid ? (uint8_t)skm_owner(mn[j], nshards) : 0xFF;
             }
         }
         __syncthreads();
-        // 3. super-k-mer starts of this thread: run length, symbols (a break + k - 1 + r), local offset
-        const int tlen = (int)(t1 - t0);
-        uint32_t run[SKM_RUN], off[SKM_RUN];
+        // 3. super-k-mer starts: run length, symbols (a break + k - 1 + r), offset in the owner's range.
+        //    A run ends at the next boundary (a position whose owner differs from its predecessor's, or
+        //    the tile's end): the thread's first boundary, then a suffix minimum of those over the
+        //    threads (wave shuffles + one LDS pass over the waves), so every run length is O(1)
+        {
+            uint32_t bmask = 0;  // bit j: window end j0 + j is a boundary
+            uint8_t prev = j0 == 0 ? 0xFE : (j0 - 1 < tlen ? s_ow[j0 - 1] : 0xFF);
 #pragma unroll
-        for (int j = 0; j < SKM_RUN; j++) {
-            run[j] = 0;
-            const int p = j0 + j;
-            if (p >= tlen || own[j] == 0xFF) continue;
-            if (p > 0 && s_ow[p - 1] == own[j]) continue;
-            int e = p + 1;
-            while (e < tlen && s_ow[e] == own[j]) e++;
-            run[j] = (uint32_t)(e - p);
-            off[j] = atomicAdd(&s_cnt[own[j]], (uint32_t)k + run[j]);
-            atomicAdd(&s_win[own[j]], run[j]);
+            for (int j = 0; j < SKM_RUN; j++) {
+                const uint8_t o = j0 + j < tlen ? s_ow[j0 + j] : 0xFF;
+                if (o != prev || j0 + j >= tlen) bmask |= 1u << j;
+                prev = o;
+            }
+            uint32_t fb = bmask ? (uint32_t)(j0 + __builtin_ctz(bmask)) : (uint32_t)SKM_TP;
+            // suffix minimum over the threads after this one: within the wave by shuffles, then the waves'
+            const int lane = tid & 63, wv = tid >> 6;
+            uint32_t sfx = fb;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t o = __shfl_down(sfx, d, 64);
+                if (lane + d < 64) sfx = min(sfx, o);
+            }
+            if (lane == 0) s_wmin[wv] = sfx;
+            __syncthreads();
+            uint32_t after = __shfl_down(sfx, 1, 64);  // the suffix minimum from the next thread
+            if (lane == 63) after = SKM_TP;
+            for (int v = wv + 1; v < SKM_T / 64; v++) after = min(after, s_wmin[v]);
+#pragma unroll
+            for (int j = 0; j < SKM_RUN; j++) {
+                const int p = j0 + j;
+                uint32_t r = 0;
+                if ((bmask >> j) & 1 && p < tlen && s_ow[p] != 0xFF) {
+                    const uint32_t later = bmask & ~((2u << j) - 1);  // boundaries after p in this thread
+                    const uint32_t e = min(later ? (uint32_t)(j0 + __builtin_ctz(later)) : after, (uint32_t)tlen);
+                    const uint32_t o = s_ow[p];
+                    r = e - (uint32_t)p;
+                    s_off[p] = atomicAdd(&s_cnt[o], (uint32_t)k + r);
+                    atomicAdd(&s_win[o], r);
+                }
+                s_run[p] = (uint16_t)r;
+            }
         }
         __syncthreads();
         // 4. whole-word ranges per owner: global (one atomicAdd each) and the LDS stage layout
@@ -245,21 +292,23 @@ __global__ __launch_bounds__(SKM_T) void k_skm_route(PackedView sv, const DevCou
         }
         __syncthreads();
         // 5. the super-k-mers' symbols and separators; the tail of each owner's range: breaks
-#pragma unroll
+#pragma unroll 1
         for (int j = 0; j < SKM_RUN; j++) {
-            if (!run[j]) continue;
-            const uint32_t o = own[j];
-            const uint64_t d = (uint64_t)off[j] + 1;  // after the separator
-            const int64_t src = (int64_t)(t0 + j0 + j) - (k - 1);
-            const uint64_t len = (uint64_t)k - 1 + run[j];
+            const int p = j0 + j;
+            const uint32_t r = s_run[p];
+            if (!r) continue;
+            const uint32_t o = s_ow[p], off = s_off[p];
+            const uint64_t d = (uint64_t)off + 1;  // after the separator
+            const int64_t src = (int64_t)(t0 + p) - (k - 1);
+            const uint64_t len = (uint64_t)k - 1 + r;
             if (!direct) {
                 const uint64_t base = (uint64_t)s_lbase[o] * 32;
-                atomicOr(&s_bk[(base + off[j]) >> 5], 0x80000000u >> ((base + off[j]) & 31));
-                put_symbols(s_pk, sv.pk, src, base + d, len);
+                atomicOr(&s_bk[(base + off) >> 5], 0x80000000u >> ((base + off) & 31));
+                put_symbols(s_pk, s_ipk, wlo, src, base + d, len);
             } else if (s_gbase[o] != ~0ULL) {
                 const uint64_t base = (s_gbase[o] + o * cap) * 32;
-                atomicOr(&out_bk[(base + off[j]) >> 5], 0x80000000u >> ((base + off[j]) & 31));
-                put_symbols(out_pk, sv.pk, src, base + d, len);
+                atomicOr(&out_bk[(base + off) >> 5], 0x80000000u >> ((base + off) & 31));
+                put_symbols(out_pk, s_ipk, wlo, src, base + d, len);
             }
         }
         if (tid < (int)nshards && s_cnt[tid] % 32) {
@@ -293,7 +342,7 @@ hipError_t launch_skm_route(PackedView sv, const DevCounters* ctr, uint64_t sym_
                             unsigned long long* wins, unsigned long long* ovf, hipStream_t s) {
     if (nshards == 0 || nshards > SKM_MAX_SHARDS || m < 1 || m > 32 || m > k) return hipErrorInvalidValue;
     const uint64_t tiles = (sym_bound + SKM_TP - 1) / SKM_TP;
-    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(tiles, 256 * 12));
+    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(tiles, 256 * 16));
     hipLaunchKernelGGL(k_skm_route, dim3(grid), dim3(SKM_T), 0, s, sv, ctr, k, m, nshards, out_pk, out_bk, cap, cursor,
                        wins, ovf);
     return hipGetLastError();
