@@ -476,7 +476,7 @@ def setup_job(args, env, image=None):
     # k-mers for the strong presets and Bloom jobs (C4 / 8 ranks: ~1.3 B per window against ~10 B of
     # records), records for a weak job without the filter (C2: each rank's reads cover the genome 30x,
     # so its 86 M distinct k-mers x 16 B undercut 1.2 G windows of super-k-mers)
-    xmode = args.exchange
+    xmode = getattr(args, "exchange", "auto")
     if xmode == "auto":
         xmode = "superkmers" if (strong or args.unique) else "records"
     skm = bool(dist) and world > 1 and xmode == "superkmers"
