@@ -167,6 +167,8 @@ struct kc_ctx {
     bool defer_last = false;   // the batch being launched is the pass's last
     uint32_t defer_g = 0;      // batches per group
     uint32_t defer_n = 0;      // batches of the current group whose segments wait
+    uint64_t skew_prev = 0;    // the group's skew list after its last batch (entries, of them records of
+    uint64_t heavy_prev = 0;   // repeated windows): what a batch that overflows leaves to insert
     uint64_t defer_syms = 0;   // the group's segment geometry is sized for batches of this bound
     uint64_t defer_groups = 0; // level-3 passes the deferral ran (kc_stats)
     // super-k-mer routing (kc_route_superkmers_device): the pass-4 batches' parameters and the
@@ -455,7 +457,7 @@ struct PartPlan {
     uint64_t spill_cap, spill_words, need1, need2;
 };
 static PartPlan part_plan(const kc_ctx* c, uint64_t syms, bool seg, const PartGeo& g, uint32_t bins1, uint32_t slots,
-                          uint64_t rec2 = 0) {
+                          uint64_t rec2 = 0, bool tight = false) {
     PartPlan p{};
     const uint64_t tile = (uint64_t)COUNT_THREADS * run_width(c->W);
     p.nblk1 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(2048, (syms + tile - 1) / tile));
@@ -466,7 +468,13 @@ static PartPlan part_plan(const kc_ctx* c, uint64_t syms, bool seg, const PartGe
     p.n2 = g.R * p.B2 * slots;
     p.nbs = (std::max(p.n1, p.n2) + 4095) / 4096 + 2;
     if (seg) {
-        auto capacity = [](double e) { return ((uint64_t)std::ceil(e + 8.0 * std::sqrt(e) + 32.0) + 7) / 8 * 8; };
+        // tight (a deferred pass): e + 3.5 sigma + 8.  Its keys past a segment's end (a few segments
+        // in 10^4 overflow, by a few keys) join the group's skew list, which is inserted once after
+        // the group's level 3 (run_deferred), so the slots of more batches fit beside the table (C5
+        // on one GPU: 54.2 -> 43.4 GB per batch, groups of 2 -> 3).  (At 3 sigma, C5's ~54 K spilled
+        // keys per batch touched ~100 K regions per group in the list's level 3: 12 ms per job.)
+        const double sd = tight ? 3.5 : 8.0, add = tight ? 8.0 : 32.0;
+        auto capacity = [&](double e) { return ((uint64_t)std::ceil(e + sd * std::sqrt(e) + add) + 7) / 8 * 8; };
         const uint64_t t1 = (uint64_t)p1_tile_max(c->W);  // k_p1<..., OutSeg> rounds block ranges to its tile
         const uint64_t per1 = ((syms + p.nblk1 - 1) / p.nblk1 + t1 - 1) / t1 * t1;  // symbols per level-1 block
         const uint64_t nseg = (p.nblk1 + p.B2 - 1) / p.B2;                           // level-1 segments per p2 block
@@ -482,7 +490,8 @@ static PartPlan part_plan(const kc_ctx* c, uint64_t syms, bool seg, const PartGe
     // batch falls back to the exact layout; its exact pipeline runs through the key buffers
     const uint64_t wins = c->win_density < 1.0 ? (uint64_t)((double)syms * c->win_density) + 1024 : syms;
     if (p.cap1) {
-        p.spill_cap = std::max<uint64_t>(1 << 16, wins / 8);
+        // (a deferred pass's list takes its group's few spilled keys: a sixteenth)
+        p.spill_cap = std::max<uint64_t>(1 << 16, wins / (tight ? 16 : 8));
         if (const char* v = std::getenv("KC_SPILL_CAP")) p.spill_cap = std::strtoull(v, 0, 10);  // tests
     }
     p.spill_words = p.spill_cap * (g.IW + 1);
@@ -501,7 +510,7 @@ static PartPlan part_plan(const kc_ctx* c, uint64_t syms, bool seg, const PartGe
 // Partition buffers for a batch of up to `syms` symbols (lazily grown): part_plan's sizes
 static int ensure_part_geo(kc_ctx* c, uint64_t syms, bool seg, const PartGeo& g, PartBufs& pb, PartCap& cap,
                            uint32_t bins1 = 0, uint32_t slots = 1, uint64_t rec2 = 0) {
-    const PartPlan p = part_plan(c, syms, seg, g, bins1, slots, rec2);
+    const PartPlan p = part_plan(c, syms, seg, g, bins1, slots, rec2, slots > 1);
     const uint64_t n1 = p.n1, n2 = p.n2, nbs = p.nbs;
     if (n1 > cap.h1) {
         hipFree(pb.hist1);
@@ -633,6 +642,13 @@ static int tail_needed(kc_ctx* c, hipStream_t s, bool* need) {
     return KC_OK;
 }
 
+// a device counter set from the host, in stream order
+static hipError_t set_dev_u64(unsigned long long* p, uint64_t v, hipStream_t s) {
+    hipError_t e = hipMemsetD32Async((hipDeviceptr_t)p, (int)(uint32_t)v, 1, s);
+    if (e == hipSuccess) e = hipMemsetD32Async((hipDeviceptr_t)((uint32_t*)p + 1), (int)(uint32_t)(v >> 32), 1, s);
+    return e;
+}
+
 // The level-3 pass of the deferred group (run_deferred): the waiting batches' segments, slots of
 // batches that did not fill the group zeroed first (their fills are a previous group's)
 static int flush_deferred(kc_ctx* c, const PackedView& sv, uint64_t syms, int mode, const TableView& tv,
@@ -664,17 +680,37 @@ static int run_deferred(kc_ctx* c, const PackedView& sv, uint64_t syms, int mode
     PartBufs pb = c->pb;
     pb.b2t = c->defer_g * pb.B2;
     pb.b2off = c->defer_n * pb.B2;
+    pb.keep_skew = c->defer_n > 0;  // (the group's skew list so far stays)
     HIPCHK(c, launch_count_partitioned(sv, syms, c->cfg.k, mode, tv, bv, c->d_ctr, pb, c->table_fresh, s, PH_L12));
     c->defer_n++;
-    unsigned long long f[2] = {0, 0};
+    unsigned long long f[3] = {0, 0, 0};
     HIPCHK(c, hipMemcpyAsync(&f[0], &c->d_ctr->part_overflow, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipMemcpyAsync(&f[1], &c->d_ctr->spill_n, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(&f[2], &c->d_ctr->heavy_n, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
-    const bool tail = f[0] != 0 || f[1] != 0;
-    if (!tail && c->defer_n < c->defer_g && !c->defer_last) return KC_OK;
-    int rc = flush_deferred(c, sv, syms, mode, tv, bv, pb, s, f[0] != 0);
+    const bool overflowed = f[0] != 0;
+    // a skew list alone does not end the group: the next batch appends to it
+    if (!overflowed && c->defer_n < c->defer_g && !c->defer_last) {
+        c->skew_prev = f[1];
+        c->heavy_prev = f[2];
+        return KC_OK;
+    }
+    int rc = flush_deferred(c, sv, syms, mode, tv, bv, pb, s, overflowed);
     if (rc) return rc;
-    if (tail)
+    if (overflowed && c->skew_prev) {
+        // this batch is redone by the exact pipeline (its tail); the list's first skew_prev entries
+        // are the group's earlier batches' and are inserted first, with the overflow flag held
+        HIPCHK(c, launch_hold_overflow(c->d_ctr, 0, s));
+        HIPCHK(c, set_dev_u64(&c->d_ctr->spill_n, c->skew_prev, s));
+        HIPCHK(c, set_dev_u64(&c->d_ctr->heavy_n, c->heavy_prev, s));
+        HIPCHK(c, launch_count_partitioned(sv, syms, c->cfg.k, mode, tv, bv, c->d_ctr, c->pb, c->table_fresh, s,
+                                           PH_TAIL));
+        HIPCHK(c, set_dev_u64(&c->d_ctr->spill_n, 0, s));
+        HIPCHK(c, set_dev_u64(&c->d_ctr->heavy_n, 0, s));
+        HIPCHK(c, launch_hold_overflow(c->d_ctr, 1, s));
+    }
+    c->skew_prev = c->heavy_prev = 0;
+    if (overflowed || f[1] != 0)
         HIPCHK(c, launch_count_partitioned(sv, syms, c->cfg.k, mode, tv, bv, c->d_ctr, c->pb, c->table_fresh, s,
                                            PH_TAIL));
     return KC_OK;
@@ -1043,7 +1079,7 @@ static int count_reused(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, s
 // The deferred level 3's group size for a counting pass over chunks (device_pass splits them into
 // batches of batch_bytes / max_chunks): the batches' largest symbol bound fixes the segment
 // geometry of every slot (part_plan, level-2 records of level2_record_bytes); a group takes as many
-// batches as 85 % of the HBM left beside the level-1 buffers and the skew list (free + the
+// batches as 90 % of the HBM left beside the level-1 buffers and the skew list (free + the
 // partition buffers held now, less 2 GiB) holds level-2 slots for, at most MAX_SEG_GROUP segments
 // per region.  The pass then runs partitioned when one sweep of the table per group beats the
 // direct inserts (use_partitioned's rule with the table's bytes spread over the group), e.g. C5's
@@ -1080,7 +1116,7 @@ static int plan_deferral_nb(kc_ctx* c, uint64_t nb, uint64_t syms) {
     const PathKnob pk = insert_path_knob();
     if (pk == PathKnob::Direct || pk == PathKnob::Exact) return KC_OK;
     if (nb < 2) return KC_OK;
-    const PartPlan p = part_plan(c, syms, true, table_geo(c), 0, 1);
+    const PartPlan p = part_plan(c, syms, true, table_geo(c), 0, 1, 0, true);
     if (p.cap1 == 0) {
         if (debug_on()) std::fprintf(stderr, "deferred level 3: off (exact layout for this batch size)\n");
         return KC_OK;
@@ -1091,7 +1127,7 @@ static int plan_deferral_nb(kc_ctx* c, uint64_t nb, uint64_t syms) {
     HIPCHK(c, hipMemGetInfo(&fr, &tot));
     const double held = (double)(c->k1_words + c->k2_words + c->spill_words) * 8.0;
     const double fixed = (double)(std::max(p.need1, c->k1_words) + std::max(p.spill_words, c->spill_words)) * 8.0;
-    const double avail = 0.85 * ((double)fr + held - fixed) - (double)(2ull << 30);
+    const double avail = 0.9 * ((double)fr + held - fixed) - (double)(2ull << 30);
     uint64_t g = avail > 0 ? (uint64_t)(avail / slot_bytes) : 0;
     g = std::min<uint64_t>({g, kmax, nb, MAX_SEG_GROUP / std::max<uint32_t>(1, p.B2),
                             ((1ULL << 31) - 1) / ((uint64_t)p.B2 * p.cap2)});
@@ -1123,6 +1159,7 @@ struct DeferEnd {
                         " batch(es) of a deferred group not inserted: " + c->err;
         c->defer_on = c->defer_last = false;
         c->defer_n = 0;
+        c->skew_prev = c->heavy_prev = 0;
     }
 };
 
@@ -1176,6 +1213,7 @@ static int device_pass(kc_ctx* c, const uint8_t* img, const kc_chunk* chunks, si
     // run and HBM holds at least two batches' level-2 segments beside everything else
     c->defer_on = false;
     c->defer_n = 0;
+    c->skew_prev = c->heavy_prev = 0;
     if (pass == 0 && !single) {
         rc = plan_deferral(c, chunks, n);
         if (rc) return rc;
@@ -1736,6 +1774,7 @@ static int packed_pass(kc_ctx* c, const uint64_t* pk, const uint32_t* bk, uint64
     DeferEnd defer_end{c};
     c->defer_on = false;
     c->defer_n = 0;
+    c->skew_prev = c->heavy_prev = 0;
     if (pass == 0 && nb >= 2 && (rc = plan_deferral_nb(c, nb, maxs))) return rc;
     for (uint64_t i = 0; i < nb; i++) {
         c->defer_last = i + 1 == nb;
@@ -2260,6 +2299,7 @@ int kc_reset(kc_ctx* c) {
     c->route_counts_kept = 0;
     c->defer_groups = 0;
     c->defer_n = 0;
+    c->skew_prev = c->heavy_prev = 0;
     c->defer_on = c->defer_last = false;
     c->broken.clear();
     c->kept_valid = false;

@@ -760,7 +760,7 @@ DEV void scatter_seg(const PartLds& l, uint32_t F, const Bin& bin, const Out& o,
 #pragma unroll
     for (int j = 0; j < RUNW; j++) {
         const uint32_t b = bin(tk[j][0]);
-        if constexpr (W >= 2) {
+        if constexpr (W >= 1) {
             // every slot issues its rank atomic (adding 0 where there is no key; a bin is in range
             // for any key word), so the RUNW atomics go out back to back with one wait for their
             // returns; an atomic under `if (ok)` was waited for inside the branch.  (One-word keys
@@ -2781,7 +2781,7 @@ static hipError_t launch_part_w(PackedView sym, int k, TableView t, BloomView bf
         if ((e = launch_p3<W, true, false, GATE3>(t, ctr, p3, nullptr, fresh, s, bf)) != hipSuccess) return e;
     }
     if (phase & (PH_MAIN | PH_L12)) {
-    hipLaunchKernelGGL(k_batch_begin, dim3(1), dim3(1), 0, s, ctr);
+    if (!pb.keep_skew) hipLaunchKernelGGL(k_batch_begin, dim3(1), dim3(1), 0, s, ctr);
     const uint64_t pk = pow5_mod54(k), pkm1 = pow5_mod54(k - 1);
     auto k1 = k_p1<W, MODE, true, BinRegion, OutSeg, scatter_threads<W>()>;
     // Short level-1 runs (fewer than 8 keys per bin and tile: big tables, C4 shares) leave

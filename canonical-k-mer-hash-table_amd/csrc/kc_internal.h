@@ -143,6 +143,9 @@ struct PartBufs {
     // B2 and no offset, one batch); the deferred level 3 runs with B2 = b2t.
     uint32_t b2t;
     uint32_t b2off;
+    // a later batch of a deferred group: its skew-list entries go after the group's earlier
+    // batches' (the list is inserted once, after the group's level 3: kc_api.cpp run_deferred)
+    uint32_t keep_skew;
 };
 constexpr int R12_P1 = 1, R12_IN = 2, R12_OUT = 4, R12_L2 = 8;
 // R12_REG: the records are in the table's own geometry (the counting pass's levels): a bin's

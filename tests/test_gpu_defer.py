@@ -71,11 +71,38 @@ def test_deferred_level3_with_batch_tails(k, spill, tmp_path, monkeypatch):
     monkeypatch.setenv("KC_SPILL_CAP", "64" if spill == "full" else str(1 << 24))
     img, host, path = _image(tmp_path, n=6000)
     lines, st, _ = _count(img, host, k, 4_000_000, 300 << 10)
+    nb = -(-len(host) // (300 << 10))
     if spill == "full":
         assert st["part_fallbacks"] >= 1
     else:
         assert st["spilled"] > 0
+        # a skew list does not end a group: its batches append to one list, inserted after the
+        # group's level 3
+        assert st["deferred_level3"] < nb, (st["deferred_level3"], nb)
     assert st["deferred_level3"] >= 1
+    out = tmp_path / "oracle.txt"
+    oracle_count(path, k, ["-a", "1", "-c", "200000"], out)
+    assert sorted_digest_lines(lines) == sorted_digest_file(out)
+
+
+@pytest.mark.parametrize("k", [31, 51])
+def test_deferred_group_overflow_after_earlier_skew_lists(k, tmp_path, monkeypatch):
+    """The group's skew list holds its earlier batches' entries when a later batch overflows it: those
+    entries are inserted after the group's level 3 and the overflowing batch is redone on the exact
+    layout (run_deferred).  The list's capacity is 1.5 batches' worth of entries, so the second batch
+    of a group overflows it."""
+    monkeypatch.setenv("KC_INSERT_PATH", "partitioned")
+    monkeypatch.setenv("KC_SEG_CAP", "8")
+    monkeypatch.setenv("KC_DEFER", "3")
+    img, host, path = _image(tmp_path, n=6000)
+    nb = -(-len(host) // (300 << 10))
+    monkeypatch.setenv("KC_SPILL_CAP", str(1 << 24))
+    _, st0, _ = _count(img, host, k, 4_000_000, 300 << 10)
+    per_batch = (st0["spilled"] + st0["heavy_records"]) / nb
+    assert per_batch > 100
+    monkeypatch.setenv("KC_SPILL_CAP", str(int(per_batch * 1.5)))
+    lines, st, _ = _count(img, host, k, 4_000_000, 300 << 10)
+    assert st["part_fallbacks"] >= 1
     out = tmp_path / "oracle.txt"
     oracle_count(path, k, ["-a", "1", "-c", "200000"], out)
     assert sorted_digest_lines(lines) == sorted_digest_file(out)
