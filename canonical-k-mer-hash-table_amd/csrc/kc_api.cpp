@@ -1668,7 +1668,7 @@ int kc_estimate_distinct_device(kc_ctx* c, const uint8_t* img, const kc_chunk* c
     const double m = HLL_M, alpha = 0.7213 / (1.0 + 1.079 / m);
     double e = alpha * m * m / sum;
     if (e <= 2.5 * m && zeros) e = m * std::log(m / zeros);
-    *estimate = e;
+    *estimate = std::ldexp(e, hll_sample_bits(c->W));  // (k_hll_s: the sample's estimate)
     return KC_OK;
 }
 

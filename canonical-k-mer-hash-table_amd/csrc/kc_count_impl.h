@@ -3251,14 +3251,137 @@ __global__ __launch_bounds__(HLL_T) void k_hll(PackedView sv, int k, const DevCo
     block_add4(nwin, 0, 0, 0, &const_cast<DevCounters*>(ctr)->est_windows, nullptr, nullptr, nullptr);
 }
 
+// k_hll_s<W> (W <= 4): the same registers over a 2^-HLL_SB sample of the distinct canonical k-mers.
+// Every window's canonical key is formed (the rolling extraction) and a cheap strand-symmetric
+// hash of it (one 32-bit multiply of its folded halves) picks 1 in 2^HLL_SB distinct keys; only
+// those take the table-key mix (the side hash's fmix64s and tmix: 3 to 7 64-bit multiplies) and
+// the register update.  A sampled key joins its wave's ring of HLL_Q keys in LDS (ballot + mbcnt
+// positions), and whenever 64 wait, every lane of the wave hashes one of them: the expensive half
+// runs with all lanes busy on 1/8 of the windows (the unsampled kernel ran it on every window).
+// The host scales the estimate by 2^HLL_SB (kc_estimate_distinct_device).  One 1024-thread
+// workgroup per CU (registers 64 KiB + rings 16 waves x HLL_Q x W words + the stage).
+constexpr int HLL_Q = 128;  // ring entries per wave (a window step adds at most 64)
+// windows per thread and run: the run's start (the break scan and the first window's reverse
+// complement, O(W)) is paid once per KC_HLL_RUNW windows
+#ifndef KC_HLL_RUNW
+#define KC_HLL_RUNW 24
+#endif
+constexpr int HLL_RUNW = KC_HLL_RUNW;
+template <int W>
+constexpr int hll_s_stage_words() { return HLL_T * HLL_RUNW / 32 + W + 3; }
+template <int W>
+constexpr size_t hll_s_smem() {
+    return (size_t)HLL_M * 4 + (size_t)hll_s_stage_words<W>() * 24 + (size_t)(HLL_T / 64) * HLL_Q * W * 8;
+}
+template <int W>
+__global__ __launch_bounds__(HLL_T) void k_hll_s(PackedView sv, int k, const DevCounters* __restrict__ ctr,
+                                                 uint32_t* __restrict__ regs, uint64_t pow5_k, uint64_t pow5_km1) {
+    static_assert(hll_sample_bits(W) > 0, "sampled keys of up to four words");
+    constexpr int SB = hll_sample_bits(W);
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint32_t* r = reinterpret_cast<uint32_t*>(smem);
+    constexpr int RUNW = HLL_RUNW, TW = HLL_T * RUNW, SW = hll_s_stage_words<W>();
+    static_assert(SW <= HLL_T, "one stage word per thread");
+    uint64_t* st_pk = reinterpret_cast<uint64_t*>(smem + (size_t)HLL_M * 4);
+    uint32_t* st_bk = reinterpret_cast<uint32_t*>(st_pk + 2 * SW);
+    const int tid = threadIdx.x, lane = tid & 63;
+    uint64_t* ring = reinterpret_cast<uint64_t*>(smem + (size_t)HLL_M * 4 + (size_t)SW * 24) +
+                     (size_t)(tid >> 6) * HLL_Q * W;
+    for (uint32_t i = tid; i < HLL_M; i += HLL_T) r[i] = 0;
+    const uint64_t M = ctr->stream_len;
+    const uint64_t per = ((M + gridDim.x - 1) / gridDim.x + TW - 1) / TW * TW;
+    const uint64_t lo = min(M, (uint64_t)blockIdx.x * per), hi = min(M, lo + per);
+    const uint64_t wlim = M ? ((M - 1) >> 5) + 1 : 0;
+    auto stage_word = [&](uint64_t ts, int i, uint64_t& pw, uint32_t& bw) {
+        const int64_t w = (int64_t)(ts >> 5) - (W + 1) + i;
+        const bool in = w >= 0 && (uint64_t)w <= wlim;
+        pw = in ? sv.pk[w] : 0;
+        bw = in ? sv.bk[w] : 0;
+    };
+    if (lo < hi && tid < SW) stage_word(lo, tid, st_pk[tid], st_bk[tid]);
+    __syncthreads();
+    const RollConst rk = make_roll<W>(k, pow5_k, pow5_km1);
+    // ring [head, tail) of the wave's sampled keys (wave-uniform counters)
+    uint32_t head = 0, tail = 0;
+    // `n` (<= 64) keys from the ring's head, one per lane: the table-key mix and the register
+    auto drain = [&](uint32_t n) {
+        __builtin_amdgcn_wave_barrier();  // (the ring's stores of other lanes first)
+        if (lane < (int)n) {
+            const uint32_t e = (head + lane) & (HLL_Q - 1);
+            uint64_t key[W], tk[W];
+#pragma unroll
+            for (int w = 0; w < W; w++) key[w] = ring[e * W + w];
+            to_tkey<W>(key, tk);
+            const uint32_t j = (uint32_t)(tk[0] >> (64 - HLL_P));
+            const uint64_t rest = (tk[0] << HLL_P) | (1ULL << (HLL_P - 1));
+            atomicMax(&r[j], (uint32_t)__builtin_clzll(rest) + 1);
+        }
+        head += n;
+    };
+    int par = 0;
+    uint32_t nwin = 0;
+    for (uint64_t t0 = lo; t0 < hi; t0 += TW) {
+        const uint64_t t1 = min(t0 + TW, hi), r0 = t0 + (uint64_t)tid * RUNW;
+        const bool nxt = t0 + TW < hi && tid < SW;
+        uint64_t npk = 0;
+        uint32_t nbk = 0;
+        if (nxt) stage_word(t0 + TW, tid, npk, nbk);
+        // (a thread past the tile's end still takes part in the wave's ballots: run_windows_src
+        // reports its windows invalid)
+        run_windows_src<W, RUNW>(PkStage{st_pk + par * SW, st_bk + par * SW, (int64_t)(t0 >> 5) - (W + 1)},
+                                 r0 < t1 ? r0 : t1, t1, rk,
+                                 [&](int, bool valid, const uint64_t (&fwd)[W], const uint64_t (&rc)[W]) {
+            nwin += valid;
+            uint64_t key[W];
+            canonical<W>(fwd, rc, key);
+            uint32_t x = (uint32_t)key[W - 1] ^ __builtin_rotateleft32((uint32_t)(key[W - 1] >> 32), 13);
+#pragma unroll
+            for (int w = 0; w + 1 < W; w++)
+                x ^= __builtin_rotateleft32((uint32_t)key[w], 5 + 7 * w) ^
+                     __builtin_rotateleft32((uint32_t)(key[w] >> 32), 19 + 3 * w);
+            const bool take = valid && ((x * 0x9E3779B1u) >> (32 - SB)) == 0;
+            const uint64_t m = __ballot(take);
+            if (take) {
+                const uint32_t e = (tail + lane_rank(m)) & (HLL_Q - 1);
+#pragma unroll
+                for (int w = 0; w < W; w++) ring[e * W + w] = key[w];
+            }
+            tail += (uint32_t)__popcll(m);
+            if (tail - head >= 64) drain(64);
+        });
+        if (nxt) {
+            st_pk[(par ^ 1) * SW + tid] = npk;
+            st_bk[(par ^ 1) * SW + tid] = nbk;
+        }
+        __syncthreads();
+        par ^= 1;
+    }
+    drain(tail - head);
+    __syncthreads();
+    for (uint32_t i = tid; i < HLL_M; i += HLL_T)
+        if (r[i]) atomicMax(&regs[i], r[i]);
+    block_add4(nwin, 0, 0, 0, &const_cast<DevCounters*>(ctr)->est_windows, nullptr, nullptr, nullptr);
+}
+
 template <int W>
 hipError_t WOps<W>::hll(PackedView sym, int k, DevCounters* ctr, uint32_t* regs, hipStream_t s) {
-    const size_t sm = hll_smem<W>();
-    hipError_t e = set_smem(k_hll<W>, sm);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_hll<W>, dim3(512), dim3(HLL_T), sm, s, sym, k, ctr, regs, pow5_mod54(k),
-                       pow5_mod54(k - 1));
-    return hipGetLastError();
+    if constexpr (hll_sample_bits(W) > 0) {
+        const size_t sm = hll_s_smem<W>();
+        hipError_t e = set_smem(k_hll_s<W>, sm);
+        if (e != hipSuccess) return e;
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        hipLaunchKernelGGL(k_hll_s<W>, dim3((unsigned)std::max(1, cus)), dim3(HLL_T), sm, s, sym, k, ctr, regs,
+                           pow5_mod54(k), pow5_mod54(k - 1));
+        return hipGetLastError();
+    } else {
+        const size_t sm = hll_smem<W>();
+        hipError_t e = set_smem(k_hll<W>, sm);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_hll<W>, dim3(512), dim3(HLL_T), sm, s, sym, k, ctr, regs, pow5_mod54(k),
+                           pow5_mod54(k - 1));
+        return hipGetLastError();
+    }
 }
 
 }  // namespace kc

@@ -312,6 +312,9 @@ hipError_t launch_insert_counts_runs(const uint64_t* rec, const uint64_t* gstart
 // HyperLogLog registers of the distinct-count estimate (kc_count_impl.h k_hll)
 constexpr int HLL_P = 14;
 constexpr uint32_t HLL_M = 1u << HLL_P;
+// k_hll of keys up to four words hashes a 2^-HLL_SB sample of the distinct k-mers (a cheap
+// strand-symmetric hash of the canonical key picks them): the estimate is 2^HLL_SB x the sample's
+constexpr int hll_sample_bits(int W) { return W <= 4 ? 3 : 0; }
 hipError_t launch_hll(PackedView sym, int k, int W, DevCounters* ctr, uint32_t* regs, hipStream_t s);
 // Super-k-mer routing of a tokenized batch to nshards owners by canonical minimizer (kc_skm.hip):
 // per owner a packed symbol stream (out_pk / out_bk regions of cap words), cursor[] = words used,

@@ -12,5 +12,5 @@ for w in 1 2 3 4 5 6 7 8 9 10 11 12 13 14 15; do
 done
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o lib_ab/libkc_$NAME.so $P/build/kc_tokenize.o $P/build/kc_util.o \
-    $P/build/kc_count.o $B/kc_count_w*.o $P/build/kc_compact_w*.o $P/build/kc_api.o -lpthread
+    $P/build/kc_count.o $P/build/kc_skm.o $B/kc_count_w*.o $P/build/kc_compact_w*.o $P/build/kc_api.o -lpthread
 echo lib_ab/libkc_$NAME.so

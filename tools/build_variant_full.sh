@@ -10,6 +10,7 @@ H=/opt/rocm/bin/hipcc
 $H $HIPFLAGS -c $P/csrc/kc_tokenize.hip -o $B/kc_tokenize.o &
 $H $HIPFLAGS -c $P/csrc/kc_util.hip -o $B/kc_util.o &
 $H $HIPFLAGS -c $P/csrc/kc_count.hip -o $B/kc_count.o &
+$H $HIPFLAGS -c $P/csrc/kc_skm.hip -o $B/kc_skm.o &
 $H $HIPFLAGS -x hip -c $P/csrc/kc_api.cpp -o $B/kc_api.o &
 wait
 for w in 1 2 3 4 5 6 7 8 9 10 11 12 13 14 15; do
