@@ -760,7 +760,7 @@ DEV void scatter_seg(const PartLds& l, uint32_t F, const Bin& bin, const Out& o,
 #pragma unroll
     for (int j = 0; j < RUNW; j++) {
         const uint32_t b = bin(tk[j][0]);
-        if constexpr (W >= 1) {
+        if constexpr (W >= 2) {
             // every slot issues its rank atomic (adding 0 where there is no key; a bin is in range
             // for any key word), so the RUNW atomics go out back to back with one wait for their
             // returns; an atomic under `if (ok)` was waited for inside the branch.  (One-word keys
