@@ -149,7 +149,10 @@ int kc_count_device(kc_ctx* ctx, const uint8_t* dev_image, const kc_chunk* chunk
 /* Distinct-count estimate of a device image (no reference counterpart: Kaarme takes the
  * table size from its user, -s, main.cpp:134-154, or from the Bloom pass, main.cpp:454): the
  * canonical k-mers of the image's windows into a HyperLogLog sketch of 2^14 registers
- * (~0.8 % standard error), so a caller can size a table (kc_config.table_slots) before
+ * (~0.8 % standard error; for k <= 128 over a 1/8 sample of the distinct k-mers picked by a
+ * strand-symmetric hash, the estimate scaled by 8, whose sampling error is far smaller for
+ * the millions of k-mers it is meant for and ~9 % at a thousand), so a caller can size a
+ * table (kc_config.table_slots) before
  * counting, e.g. a rank's local table in a sharded job.  Counts nothing and leaves the
  * table alone; the call waits for its work (the estimate is a host value).  Any context of
  * the same k can run it (its table size does not matter).  When HBM allows, the context keeps
