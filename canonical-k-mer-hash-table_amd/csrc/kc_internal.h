@@ -321,7 +321,8 @@ hipError_t launch_hll(PackedView sym, int k, int W, DevCounters* ctr, uint32_t* 
 // wins[] = windows routed, *ovf = 1 if a region overflowed
 constexpr uint32_t SKM_MAX_SHARDS = 64;
 constexpr int SKM_DEFAULT_M = 15;  // minimizer length (odd: no palindromic m-mers); min(15, k)
-constexpr uint64_t SKM_SEED = 0x5851F42D4C957F2DULL;  // the m-mer order h(x) = fmix64(x ^ SKM_SEED) >> 32
+// the m-mer order: h(x) = fmix32(lo32(x) ^ hi32(x) * SKM_FOLD ^ SKM_SEED32) (a bijection for m <= 16)
+constexpr uint32_t SKM_SEED32 = 0x4C957F2Du, SKM_FOLD = 0x9E3779B1u;
 hipError_t launch_skm_route(PackedView sv, const DevCounters* ctr, uint64_t sym_bound, int k, int m, uint32_t nshards,
                             uint64_t* out_pk, uint32_t* out_bk, uint64_t cap, unsigned long long* cursor,
                             unsigned long long* wins, unsigned long long* ovf, hipStream_t s);

@@ -28,22 +28,26 @@ constexpr int SKM_STAGE = 1024;        // staged output words per tile (32 768 s
 constexpr int SKM_IN = (SKM_TP + SKM_MAXW) / 32 + 4;  // staged input words per tile
 constexpr uint32_t SKM_BROKEN = 0xFFFFFFFFu;
 
-// h(canonical m-mer) in 32 bits, never SKM_BROKEN
+DEV uint32_t fmix32(uint32_t h) {  // murmur3's finalizer (a bijection)
+    h ^= h >> 16;
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+    h *= 0xC2B2AE35u;
+    h ^= h >> 16;
+    return h;
+}
+// h(canonical m-mer) in 32 bits, never SKM_BROKEN: two 32-bit multiplies (a 64-bit fmix64 took
+// six of the kernel's per-position multiplies; m <= 16 m-mers fit the low word, so distinct m-mers
+// keep distinct hashes)
 DEV uint32_t mmer_hash(uint64_t canon) {
-    const uint32_t h = (uint32_t)(fmix64(canon ^ SKM_SEED) >> 32);
+    const uint32_t h = fmix32((uint32_t)canon ^ (uint32_t)(canon >> 32) * SKM_FOLD ^ SKM_SEED32);
     return h == SKM_BROKEN ? SKM_BROKEN - 1 : h;
 }
 
 // the owner of a minimizer value: the minimum of w uniform hashes is small, so it is mixed again
 // (murmur3's fmix32) before the multiply-shift onto the owners
 DEV uint32_t skm_owner(uint32_t minh, uint32_t nshards) {
-    uint32_t h = minh;
-    h ^= h >> 16;
-    h *= 0x85EBCA6Bu;
-    h ^= h >> 13;
-    h *= 0xC2B2AE35u;
-    h ^= h >> 16;
-    return (uint32_t)(((uint64_t)h * nshards) >> 32);
+    return (uint32_t)(((uint64_t)fmix32(minh ^ 0x9E3779B9u) * nshards) >> 32);
 }
 
 // 32 symbols starting at symbol s of the tile's staged input words (word wlo of the stream at
@@ -100,6 +104,8 @@ __global__ __launch_bounds__(SKM_T) void k_skm_route(PackedView sv, const DevCou
     __shared__ uint32_t s_cnt[SKM_MAX_SHARDS], s_win[SKM_MAX_SHARDS], s_lbase[SKM_MAX_SHARDS + 1];
     __shared__ unsigned long long s_gbase[SKM_MAX_SHARDS];
     __shared__ int s_direct;
+    __shared__ uint16_t s_starts[SKM_TP];  // the tile's super-k-mer starts (step 3), in any order
+    __shared__ uint32_t s_nstart, s_wtot[SKM_T / 64];
     __shared__ uint32_t s_wmin[SKM_T / 64];
     const int tid = threadIdx.x;
     const uint64_t M = ctr->stream_len;
@@ -108,6 +114,11 @@ __global__ __launch_bounds__(SKM_T) void k_skm_route(PackedView sv, const DevCou
     const int rsh = 64 - 2 * m;
     const uint64_t ntiles = (M + SKM_TP - 1) / SKM_TP;
     const int j0 = tid * SKM_RUN;  // first window end of this thread (tile-relative)
+    // (step 1's layout of the m-mer hashes: row i % SKM_RUN, column i / SKM_RUN; the row pitch is 8
+    // words past a multiple of the 64 banks, so a wave's 8 x 8 writes of step 1 hit 64 banks too)
+    constexpr int HP = ((SKM_TP + SKM_MAXW) / SKM_RUN + 1 + 63) / 64 * 64 + 8;
+    static_assert(SKM_RUN == 8 && HP * SKM_RUN <= NU, "the interleaved hashes fit s_u");
+    auto hix = [](int i) { return (i & (SKM_RUN - 1)) * HP + (i >> 3); };
     for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const uint64_t t0 = tile * SKM_TP, t1 = min(t0 + SKM_TP, M);
         const int tlen = (int)(t1 - t0);
@@ -126,9 +137,14 @@ __global__ __launch_bounds__(SKM_T) void k_skm_route(PackedView sv, const DevCou
         }
         __syncthreads();
         // 1. the hashes of the m-mers ending at t0 - w + 1 .. t1 - 1 (broken: a break symbol inside,
-        //    or the m-mer starts before the stream)
+        //    or the m-mer starts before the stream).  Thread t rolls the SKM_RUN consecutive m-mers
+        //    8t .. 8t + 7 (one extraction, then a symbol each); the rest (the w - 1 past the tile's
+        //    SKM_TP) one by one.  m-mer i sits at s_h[hix(i)]: the SKM_RUN m-mers of a thread in SKM_RUN
+        //    rows, so that the lanes of a wave touch consecutive words here and in step 2 (a thread's
+        //    m-mers side by side put the lanes 8 words apart: 8-way LDS bank conflicts, 20 % of the
+        //    kernel's cycles)
         const int nh = tlen + w - 1;
-        for (int i = tid; i < nh; i += SKM_T) {
+        auto mmer_at = [&](int i) {  // one m-mer from scratch
             const int64_t q = (int64_t)t0 - (w - 1) + i;  // last symbol of the m-mer
             const int64_t a = q - m + 1;
             uint32_t h = SKM_BROKEN;
@@ -143,7 +159,49 @@ __global__ __launch_bounds__(SKM_T) void k_skm_route(PackedView sv, const DevCou
                     h = mmer_hash(x < rc ? x : rc);
                 }
             }
-            s_h[i] = h;
+            return h;
+        };
+        {
+            const int i0 = j0;  // this thread's first m-mer
+            if (i0 < nh) {
+                const int64_t q0 = (int64_t)t0 - (w - 1) + i0, a0 = q0 - m + 1;
+                // consecutive non-break symbols ending at q0 (capped at m; none before the stream)
+                int since = 0;
+                if (q0 >= 0) {
+                    const int64_t wq = (q0 >> 5) - wlo;
+                    const uint32_t mq = s_ibk[wq] & (0xFFFFFFFFu << (31 - (q0 & 31)));
+                    if (mq) {
+                        since = (int)(q0 & 31) - (31 - __builtin_ctz(mq));
+                    } else {
+                        const uint32_t mp = wq > 0 ? s_ibk[wq - 1] : 0xFFFFFFFFu;
+                        since = (int)(q0 & 31) + 1 + (mp ? 31 - (31 - __builtin_ctz(mp)) : 32);
+                    }
+                    since = (int)min((int64_t)min(since, m), q0 + 1);
+                }
+                uint64_t x = 0, rc = 0;
+                if (a0 >= -32) {  // (a stage word exists before the stream's first)
+                    x = (load32_at(s_ipk, wlo, a0) >> rsh) & mmask;
+                    rc = (rev2(~x) >> rsh) & mmask;
+                }
+                s_h[hix(i0)] = since >= m ? mmer_hash(x < rc ? x : rc) : SKM_BROKEN;
+                // the next SKM_RUN - 1 symbols and their break bits
+                const int64_t q1 = q0 + 1;
+                const uint64_t ins = load32_at(s_ipk, wlo, q1);
+                const int64_t wb = (q1 >> 5) - wlo;
+                const int ob = (int)(q1 & 31);
+                const uint32_t inb = ob ? (s_ibk[wb] << ob) | (s_ibk[wb + 1] >> (32 - ob)) : s_ibk[wb];
+                const int rcs = 2 * (m - 1);
+#pragma unroll
+                for (int j = 1; j < SKM_RUN; j++) {
+                    const uint32_t c = (uint32_t)(ins >> (62 - 2 * (j - 1))) & 3;
+                    const bool brk = (inb >> (31 - (j - 1))) & 1;
+                    since = brk ? 0 : min(since + 1, m);
+                    x = ((x << 2) | c) & mmask;
+                    rc = (rc >> 2) | ((uint64_t)(3 - c) << rcs);
+                    if (i0 + j < nh) s_h[hix(i0 + j)] = since >= m ? mmer_hash(x < rc ? x : rc) : SKM_BROKEN;
+                }
+            }
+            for (int i = SKM_TP + tid; i < nh; i += SKM_T) s_h[hix(i)] = mmer_at(i);
         }
         __syncthreads();
         // 2. per window end: valid (no broken m-mer among its w) and the minimizer -> owner.  Window j
@@ -151,7 +209,7 @@ __global__ __launch_bounds__(SKM_T) void k_skm_route(PackedView sv, const DevCou
         //    SKM_RUN windows [j0 + SKM_RUN - 1, j0 + w - 1], a left part [j0 + j, j0 + SKM_RUN - 2]
         //    (suffixes) and a right part [j0 + w, j0 + w + j - 1] (prefixes): w + 2 SKM_RUN reads
         {
-            auto hv = [&](int i) { return i < nh ? s_h[i] : SKM_BROKEN; };
+            auto hv = [&](int i) { return i < nh ? s_h[hix(i)] : SKM_BROKEN; };
             uint32_t mn[SKM_RUN], mx[SKM_RUN];
             if (w >= SKM_RUN) {
                 uint32_t cmn = SKM_BROKEN, cmx = 0;
@@ -230,6 +288,7 @@ __global__ __launch_bounds__(SKM_T) void k_skm_route(PackedView sv, const DevCou
             uint32_t after = __shfl_down(sfx, 1, 64);  // the suffix minimum from the next thread
             if (lane == 63) after = SKM_TP;
             for (int v = wv + 1; v < SKM_T / 64; v++) after = min(after, s_wmin[v]);
+            uint32_t smask = 0;  // bit j: a super-k-mer starts at window end j0 + j
 #pragma unroll
             for (int j = 0; j < SKM_RUN; j++) {
                 const int p = j0 + j;
@@ -237,13 +296,28 @@ __global__ __launch_bounds__(SKM_T) void k_skm_route(PackedView sv, const DevCou
                 if ((bmask >> j) & 1 && p < tlen && s_ow[p] != 0xFF) {
                     const uint32_t later = bmask & ~((2u << j) - 1);  // boundaries after p in this thread
                     const uint32_t e = min(later ? (uint32_t)(j0 + __builtin_ctz(later)) : after, (uint32_t)tlen);
-                    const uint32_t o = s_ow[p];
                     r = e - (uint32_t)p;
-                    s_off[p] = atomicAdd(&s_cnt[o], (uint32_t)k + r);
-                    atomicAdd(&s_win[o], r);
+                    smask |= 1u << j;
                 }
                 s_run[p] = (uint16_t)r;
             }
+            // the tile's list of starts: a block scan of the threads' counts (no per-start atomics
+            // under a branch: each of a thread's 8 slots had waited for its own LDS atomic)
+            const uint32_t cnt = (uint32_t)__builtin_popcount(smask), incl = wave_incl_sum(cnt);
+            if (lane == 63) s_wtot[wv] = incl;
+            __syncthreads();
+            uint32_t at = incl - cnt;
+            for (int v = 0; v < wv; v++) at += s_wtot[v];
+            if (tid == SKM_T - 1) s_nstart = at + cnt;
+            for (uint32_t mk = smask; mk; mk &= mk - 1) s_starts[at++] = (uint16_t)(j0 + __builtin_ctz(mk));
+        }
+        __syncthreads();
+        // each start's offset in its owner's range (order free: counting does not depend on it)
+        for (uint32_t i = tid; i < s_nstart; i += SKM_T) {
+            const int p = s_starts[i];
+            const uint32_t o = s_ow[p], r = s_run[p];
+            s_off[p] = atomicAdd(&s_cnt[o], (uint32_t)k + r);
+            atomicAdd(&s_win[o], r);
         }
         __syncthreads();
         // 4. whole-word ranges per owner: global (one atomicAdd each) and the LDS stage layout
@@ -291,12 +365,14 @@ __global__ __launch_bounds__(SKM_T) void k_skm_route(PackedView sv, const DevCou
             __threadfence();
         }
         __syncthreads();
-        // 5. the super-k-mers' symbols and separators; the tail of each owner's range: breaks
+        // 5. the super-k-mers' symbols and separators, one start per thread from the tile's list (a
+        //    thread's own 8 window ends held ~0.4 starts: each of the 8 slots ran the symbol copy for
+        //    the few lanes with a start there); the tail of each owner's range: breaks
+        const uint32_t nst = s_nstart;
 #pragma unroll 1
-        for (int j = 0; j < SKM_RUN; j++) {
-            const int p = j0 + j;
+        for (uint32_t i = tid; i < nst; i += SKM_T) {
+            const int p = s_starts[i];
             const uint32_t r = s_run[p];
-            if (!r) continue;
             const uint32_t o = s_ow[p], off = s_off[p];
             const uint64_t d = (uint64_t)off + 1;  // after the separator
             const int64_t src = (int64_t)(t0 + p) - (k - 1);

@@ -4,12 +4,13 @@ stream format (kc_internal.h PackedView) both ways, and a host router that produ
 per-owner streams the device kernel does (up to the order of the super-k-mers).
 
 owner(window) = fmix32(min over its k - m + 1 m-mers of h(canonical m-mer)) * G >> 32, with
-h(x) = fmix64(x ^ SKM_SEED) >> 32 (0xFFFFFFFF -> 0xFFFFFFFE), m = min(15, k) by default (the
+h(x) = fmix32(lo32(x) ^ hi32(x) * SKM_FOLD ^ SKM_SEED32) (0xFFFFFFFF -> 0xFFFFFFFE), m = min(15, k) by default (the
 minimum of many uniform hashes is small: mixed again before it picks an owner).
 """
 import numpy as np
 
-SKM_SEED = 0x5851F42D4C957F2D
+SKM_SEED32 = 0x4C957F2D
+SKM_FOLD = 0x9E3779B1
 BROKEN = 0xFFFFFFFF
 DEFAULT_M = 15
 
@@ -17,17 +18,6 @@ CODE = np.full(256, 4, dtype=np.uint8)
 for _i, _c in enumerate("ACGT"):
     CODE[ord(_c)] = _i
     CODE[ord(_c.lower())] = _i
-
-
-def fmix64(x):
-    x = x.astype(np.uint64, copy=True)
-    with np.errstate(over="ignore"):
-        x ^= x >> np.uint64(33)
-        x *= np.uint64(0xFF51AFD7ED558CCD)
-        x ^= x >> np.uint64(33)
-        x *= np.uint64(0xC4CEB9FE1A85EC53)
-        x ^= x >> np.uint64(33)
-    return x
 
 
 def mmer_hashes(codes, m):
@@ -43,7 +33,9 @@ def mmer_hashes(codes, m):
     fwd = (c << sh).sum(axis=1, dtype=np.uint64)
     rc = ((np.uint64(3) - c[:, ::-1]) << sh).sum(axis=1, dtype=np.uint64)
     canon = np.minimum(fwd, rc)
-    h = fmix64(canon ^ np.uint64(SKM_SEED)) >> np.uint64(32)
+    m32 = np.uint64(0xFFFFFFFF)
+    x = (canon & m32) ^ (((canon >> np.uint64(32)) * np.uint64(SKM_FOLD)) & m32) ^ np.uint64(SKM_SEED32)
+    h = fmix32(x)
     h = np.where(h == BROKEN, BROKEN - 1, h)
     return np.where(bad, BROKEN, h).astype(np.uint64)
 
@@ -67,7 +59,7 @@ def window_owners(codes, k, G, m=0):
         return np.zeros(0, dtype=np.int64)
     hw = np.lib.stride_tricks.sliding_window_view(h, w)
     mn, mx = hw.min(axis=1), hw.max(axis=1)
-    own = ((fmix32(mn) * np.uint64(G)) >> np.uint64(32)).astype(np.int64)
+    own = ((fmix32(mn ^ np.uint64(0x9E3779B9)) * np.uint64(G)) >> np.uint64(32)).astype(np.int64)
     return np.where(mx == BROKEN, -1, own)
 
 
