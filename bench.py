@@ -874,7 +874,7 @@ def run_workload(args, env, image=None):
         out["config"]["parallelism"] = f"one rank's share of hash-prefix shard x{job.share} (no exchange)"
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not job.share:
         out["cpu_baseline"] = cpu_baseline(args)
-    if world == 1 and not dist and args.cli_fullsize and not job.share and args.config in ("C2", "C3", "C4"):
+    if world == 1 and not dist and args.cli_fullsize and not job.share and args.config in ("C2", "C3", "C4", "C5"):
         out["cli_fullsize"] = cli_fullsize(job, args)
     if world == 1 and not dist and args.host_chunks and not job.share and args.config == "C2":
         out["c_abi_host_chunks"] = host_chunks_record(job, args)
@@ -1013,7 +1013,7 @@ def main():
     ap.add_argument("--no-verify", dest="verify", action="store_false",
                     help="skip the parity digest against the reference's output (tests/golden/fullsize.json)")
     ap.add_argument("--no-cli-fullsize", dest="cli_fullsize", action="store_false",
-                    help="skip the drop-in CLI on the whole C2 / C3 workload (cli_fullsize record)")
+                    help="skip the drop-in CLI on the whole workload's file (cli_fullsize record; C2 / C3 / C4 / C5)")
     ap.add_argument("--no-host-chunks", dest="host_chunks", action="store_false",
                     help="skip the C-ABI host-chunk record (kc_count_chunk over the C2 job's chunks from host memory)")
     ap.add_argument("--no-writer", dest="writer", action="store_false",
