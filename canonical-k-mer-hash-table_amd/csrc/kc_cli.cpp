@@ -629,6 +629,15 @@ int main(int argc, char** argv) {
         if (force) unsetenv("KC_INSERT_PATH");
         if (!a.use_bf && kc_reset(ctx) != KC_OK) die("reset after warm-up");
     }
+    // A -s whose table would take a large share of HBM is sized from the input's distinct estimate
+    // inside the timer (below).  Its -s table, allocated by kc_create, is given back first (untimed
+    // setup, as the reference's table allocation): beside C5's 192 GB -s table the 10 GB upload
+    // crawled at 1.7 GB/s (5.8 s; 0.35 s beside a 96 GB table, profiles/r06_cli_c5_phases.txt)
+    const int kw = (int)(a.k / 32 + 1);
+    const double s_table_bytes = 1.25 * (double)a.slots / (double)(16 / (kw + 1)) * 128.0;
+    const bool want_est = a.table_sizing == 2 || (a.table_sizing == 0 && s_table_bytes > (double)(16ull << 30) && nch > 1);
+    bool s_table_dropped = false;
+    if (staged && !a.use_bf && want_est) s_table_dropped = kc_size_table(ctx, 1u << 20) == KC_OK;
     uint8_t* d_img = nullptr;
     bool loaded = false;
     auto load = [&]() {
@@ -669,10 +678,7 @@ int main(int argc, char** argv) {
     // estimate instead (kc_estimate_distinct_device + kc_size_table, inside the timer; -s stays
     // the reference capacity for --strict-capacity), as bench.py's C4 / C5 lines are.  A table
     // that still fills up (an estimate far below the truth) is counted again at -s.
-    const int kw = (int)(a.k / 32 + 1);
-    const double s_table_bytes = 1.25 * (double)a.slots / (double)(16 / (kw + 1)) * 128.0;
     bool est_sized = false;
-    const bool want_est = a.table_sizing == 2 || (a.table_sizing == 0 && s_table_bytes > (double)(16ull << 30) && nch > 1);
     if (staged && !loaded && !a.use_bf && want_est) {
         load();
         double est = 0;
@@ -684,6 +690,7 @@ int main(int argc, char** argv) {
             }
         }
     }
+    if (s_table_dropped && !est_sized && kc_size_table(ctx, 0) != KC_OK) die("sizing the -s table");
     // A large -s job counts the image's first half while the second half uploads (two counting
     // passes into one table: the second sweeps it once more, ~1.5 ms for C2's, against ~8 ms of
     // the upload hidden); a Bloom job's counting pass follows the Bloom pass, which read it all

@@ -1,24 +1,29 @@
-"""The drop-in CLI on the whole 16 GB C4 file with 1 / 2 / 4 / 8 upload readers (--readers): its
-timer line (file read + chunking + estimate + count) and its stdout's phase lines, to pick the
-reader count for big inputs.  Not a test; run on a GPU box: python3 -u tests/cli_readers_probe.py"""
+"""The drop-in CLI on a whole strong workload's file (C4: 16 GB, k = 51, -s 2.6e9; C5: 10 GB,
+k = 127, -s 3.6e9) with several upload reader counts (--readers), its timer lines and its phase
+lines (--phases, stderr).  Not a test; run on a GPU box:
+    python3 -u tests/cli_readers_probe.py [C4|C5] [readers ...]"""
 import os
+import subprocess
 import sys
 import tempfile
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "canonical-k-mer-hash-table_amd"))
 import torch  # noqa: E402
 
-import bench  # noqa: E402
 import kaarme_amd as ka  # noqa: E402
 
+cfg = sys.argv[1] if len(sys.argv) > 1 and sys.argv[1].startswith("C") else "C4"
+readers = [int(x) for x in sys.argv[2 if len(sys.argv) > 1 and sys.argv[1].startswith("C") else 1:]] or [1, 2, 4, 8]
+N, L, k, s = (100_000_000, 150, 51, "2600000000") if cfg == "C4" else (1_000_000, 10_000, 127, "3600000000")
+s = os.environ.get("PROBE_S", s)  # (diagnosis: a smaller -s, i.e. a smaller table allocated at kc_create)
 lib = ka.load_library()
-N, L = 100_000_000, 150
 nb = lib.kc_synth_bytes(0, N, L, 0)
 img = torch.empty(nb, dtype=torch.uint8, device="cuda")
 assert lib.kc_synth_device(img.data_ptr(), 0, N, 42, 500_000_000, L, 0, 0.001, 0.0, 0) == 0
 torch.cuda.synchronize()
+cli = os.path.join(ROOT, "canonical-k-mer-hash-table_amd", "bin", "kaarme")
 with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
     fa = os.path.join(td, "input.fasta")
     with open(fa, "wb") as f:
@@ -28,12 +33,11 @@ with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
     with open(fa, "rb") as f:
         while f.read(1 << 24):
             pass
-    for rd in [int(x) for x in (sys.argv[1:] or ["1", "2", "4", "8"])]:
-        r = bench.run_cli(fa, ["51", "-m", "2", "-s", "2600000000", "-a", "1", "-t", "18"], os.path.join(td, "o.txt"),
-                          ["--digest-only", "--readers", str(rd)])
-        if r is None:
-            print("readers", rd, "failed", flush=True)
-            continue
-        secs, write_s, wall, out = r
-        lines = [l for l in out.splitlines() if "Time used" in l or "Input" in l or "digest" in l.lower()]
-        print("readers", rd, "build_s", round(secs, 3), "wall", round(wall, 2), "|", " | ".join(lines)[:600], flush=True)
+    for rd in readers:
+        t0 = time.perf_counter()
+        p = subprocess.run([cli, fa, str(k), "-m", "2", "-s", s, "-a", "1", "-t", "18", "-o", os.path.join(td, "o.txt"),
+                            "--digest-only", "--phases", "--readers", str(rd)], capture_output=True, text=True)
+        wall = time.perf_counter() - t0
+        keep = [l for l in (p.stdout + p.stderr).splitlines() if l.strip()]
+        print(f"== {cfg} readers {rd} rc {p.returncode} wall {wall:.2f}", flush=True)
+        print("\n".join(keep[-40:]), flush=True)
